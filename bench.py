@@ -1,0 +1,144 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: the rocm-gpu-test pod's in-pod workload step.
+
+BASELINE.json metric: "cluster-create->GPU-pod-Running sec; in-pod bf16 GEMM
+TFLOPS at 1/2/4/8 MI355X". The cluster-create half needs docker + kind + a GPU
+host (see ``bench/e2e.py``); this script measures the in-pod half exactly as the
+pod runs it, one process per GPU:
+
+  step (per rank) = G x bf16 GEMM C = A . B^T  (M=N=K=8192, hand-written gfx950
+                    MFMA kernel, kgs.ops.gemm_nt)
+                  + an RCCL all-reduce of a gradient bucket (default 64 MiB
+                    fp32) on a separate HIP stream, overlapped with the GEMMs
+                    (the data-parallel gradient-sync pattern; skipped at N=1)
+
+Timing: W untimed warmup steps, then K steps bracketed by barrier +
+torch.cuda.synchronize() on both sides; the MAX over ranks is reported.
+value = aggregate GEMM TFLOP/s over all N GPUs (weak scaling: per-GPU work is
+fixed). Synthetic U[-1,1) operands (random data, not zeros: DVFS reads zeros
+fast, cdna_hip_programming.md rule 25).
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
+        torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--m", type=int, default=8192)
+    ap.add_argument("--n", type=int, default=8192)
+    ap.add_argument("--k", type=int, default=8192)
+    ap.add_argument("--gemms-per-step", type=int, default=4)
+    ap.add_argument("--allreduce-mb", type=float, default=64.0, help="gradient bucket all-reduced per step (MiB)")
+    ap.add_argument("--no-overlap", action="store_true", help="run the all-reduce after the GEMMs, same stream")
+    ap.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt), untimed part")
+    ap.add_argument("--verify", action="store_true", help="check one GEMM against fp32 torch before timing")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    import torch
+    import torch.distributed as dist
+
+    from kgs.models.gemm_workload import GemmWorkload
+    from kgs.parallel import dist as kdist
+
+    ctx = kdist.init_from_env(expected_world=args.gpus)
+    rank, world = ctx.rank, ctx.world_size
+    dev = ctx.device
+
+    wl = GemmWorkload(
+        m=args.m,
+        n=args.n,
+        k=args.k,
+        gemms_per_step=args.gemms_per_step,
+        allreduce_bytes=int(args.allreduce_mb * (1 << 20)) if world > 1 else 0,
+        overlap=not args.no_overlap,
+        device=dev,
+        group=ctx.group,
+        seed=1234 + rank,
+    )
+    if args.verify:
+        err = wl.verify()
+        if rank == 0:
+            print(f"[bench] verify rel err {err:.3e}", file=sys.stderr)
+        if err > 2e-2:
+            raise SystemExit(f"GEMM verification failed: rel err {err}")
+
+    for _ in range(args.warmup):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    kdist.barrier(ctx)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    torch.cuda.synchronize(dev)
+    kdist.barrier(ctx)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+
+    elapsed_max = kdist.max_over_ranks(ctx, elapsed)
+    ms_per_step = elapsed_max / max(1, args.steps) * 1e3
+    flops_per_step = wl.flops_per_step()
+    per_gpu_tflops = flops_per_step / (ms_per_step * 1e-3) / 1e12
+    total_tflops = per_gpu_tflops * world
+
+    extra = {}
+    if args.compare_torch:
+        extra["torch_matmul_tflops_per_gpu"] = round(wl.torch_reference_tflops(), 1)
+
+    if rank == 0:
+        out = {
+            "metric": "in-pod bf16 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 MFMA GEMM + RCCL grad all-reduce)",
+            "value": round(total_tflops, 2),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(total_tflops / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
+            "dtype": "bf16",
+            "data": "synthetic U[-1,1) operands, random-init",
+            "config": {
+                "model": "rocm-gpu-test in-pod workload: bf16 GEMM C=A.B^T (kgs gfx950 MFMA kernel)",
+                "global_batch": args.gemms_per_step * world,
+                "seq_len": args.m,
+                "parallelism": f"dp{world}",
+                "m": args.m,
+                "n": args.n,
+                "k": args.k,
+                "gemms_per_step_per_gpu": args.gemms_per_step,
+                "allreduce_mb": args.allreduce_mb if world > 1 else 0,
+                "allreduce_overlap": not args.no_overlap,
+            },
+            "per_gpu_tflops": round(per_gpu_tflops, 2),
+            "gemm_path": wl.path_name(),
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    kdist.shutdown(ctx)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""GEMM sweep on one MI355X: kgs HIP kernel vs torch.matmul (hipBLASLt).
+
+Interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24), random
+U[-1,1) operands (rule 25). Prints one JSON line per shape and writes
+gpurun_out/gemm_sweep.json.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from kgs.ops import gemm_nt  # noqa: E402
+
+
+def time_fn(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="4096,8192")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--out", default="gpurun_out/gemm_sweep.json")
+    a = ap.parse_args()
+    res = []
+    for s in a.shapes.split(","):
+        dims = [int(x) for x in s.split("x")]
+        M, N, K = (dims * 3)[:3] if len(dims) == 1 else dims
+        A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
+        B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        C2 = torch.empty_like(C)
+        ours = lambda: gemm_nt(A, B, out=C)  # noqa: E731
+        ref = lambda: torch.matmul(A, B.T, out=C2)  # noqa: E731
+        for f in (ours, ref):
+            for _ in range(3):
+                f()
+        torch.cuda.synchronize()
+        t_ours, t_ref = [], []
+        for _ in range(a.rounds):
+            t_ours.append(time_fn(ours, a.iters))
+            t_ref.append(time_fn(ref, a.iters))
+        err = ((C.float() - C2.float()).abs().max() / C2.float().abs().max()).item()
+        fl = 2.0 * M * N * K
+        r = {
+            "shape": [M, N, K],
+            "kgs_tflops_median": round(fl / (sorted(t_ours)[len(t_ours) // 2] * 1e-3) / 1e12, 1),
+            "kgs_tflops_best": round(fl / (min(t_ours) * 1e-3) / 1e12, 1),
+            "hipblaslt_tflops_median": round(fl / (sorted(t_ref)[len(t_ref) // 2] * 1e-3) / 1e12, 1),
+            "hipblaslt_tflops_best": round(fl / (min(t_ref) * 1e-3) / 1e12, 1),
+            "rel_err_vs_hipblaslt": err,
+        }
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

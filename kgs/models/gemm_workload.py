@@ -1,0 +1,95 @@
+"""The rocm-gpu-test pod's compute workload: bf16 MFMA GEMMs + RCCL gradient sync.
+
+One :class:`GemmWorkload` per rank (one process per GPU). A step is
+``gemms_per_step`` GEMMs ``C = A . B^T`` on the hand-written gfx950 kernel
+(:func:`kgs.ops.gemm_nt`) plus, when the pod holds more than one GPU, an RCCL
+all-reduce of a gradient-sized bucket on its own HIP stream so the collective
+overlaps the MFMA work (the data-parallel pattern; xGMI traffic while the
+matrix cores run).
+
+Replaces the reference's ``echo Hello from fake ROCm GPU node``
+(pods/rocm-gpu-test-pod.yaml:9).
+"""
+from __future__ import annotations
+
+import torch
+
+
+class GemmWorkload:
+    def __init__(self, m=8192, n=8192, k=8192, gemms_per_step=4, allreduce_bytes=0, overlap=True,
+                 device=None, group=None, seed=0, backend="kgs"):
+        self.m, self.n, self.k = m, n, k
+        self.g = gemms_per_step
+        self.device = torch.device(device) if device is not None else torch.device("cuda")
+        self.group = group
+        self.overlap = overlap
+        self.backend = backend
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+        # U[-1, 1) operands: random data (zeros inflate TFLOPS via DVFS)
+        self.a = (torch.rand((m, k), generator=gen, device=self.device) * 2 - 1).to(torch.bfloat16)
+        self.b = (torch.rand((n, k), generator=gen, device=self.device) * 2 - 1).to(torch.bfloat16)
+        self.c = [torch.empty((m, n), dtype=torch.bfloat16, device=self.device) for _ in range(2)]
+        self.bucket = None
+        if allreduce_bytes > 0:
+            self.bucket = torch.rand(allreduce_bytes // 4, generator=gen, device=self.device)
+            self.comm_stream = torch.cuda.Stream(device=self.device)
+        if backend == "kgs":
+            from kgs.ops import gemm_nt
+
+            self._gemm = lambda i: gemm_nt(self.a, self.b, out=self.c[i & 1])
+        else:
+            self._gemm = lambda i: torch.matmul(self.a, self.b.T, out=self.c[i & 1])
+
+    def flops_per_step(self) -> float:
+        return 2.0 * self.m * self.n * self.k * self.g
+
+    def path_name(self) -> str:
+        if self.backend != "kgs":
+            return "torch.matmul"
+        from kgs.ops import fast_path_ok
+
+        return "kgs gemm_nt_256 (8-phase LDS-DMA pipeline)" if fast_path_ok(self.a, self.b, self.c[0]) else \
+            "kgs gemm_nt_generic"
+
+    def _allreduce(self):
+        import torch.distributed as dist
+
+        dist.all_reduce(self.bucket, group=self.group)
+
+    def step(self) -> None:
+        cur = torch.cuda.current_stream(self.device)
+        if self.bucket is not None and self.overlap:
+            self.comm_stream.wait_stream(cur)
+            with torch.cuda.stream(self.comm_stream):
+                self._allreduce()
+        for i in range(self.g):
+            self._gemm(i)
+        if self.bucket is not None:
+            if self.overlap:
+                cur.wait_stream(self.comm_stream)
+            else:
+                self._allreduce()
+
+    @torch.no_grad()
+    def verify(self, rows: int = 256) -> float:
+        """Relative max error of one GEMM's first ``rows`` rows vs fp32 torch."""
+        self._gemm(0)
+        ref = self.a[:rows].float() @ self.b.float().T
+        got = self.c[0][:rows].float()
+        return ((got - ref).abs().max() / ref.abs().max()).item()
+
+    def torch_reference_tflops(self, iters: int = 10) -> float:
+        """hipBLASLt (torch.matmul) TFLOP/s on the same operands, for comparison."""
+        out = torch.empty_like(self.c[0])
+        for _ in range(3):
+            torch.matmul(self.a, self.b.T, out=out)
+        torch.cuda.synchronize(self.device)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            torch.matmul(self.a, self.b.T, out=out)
+        e.record()
+        torch.cuda.synchronize(self.device)
+        ms = s.elapsed_time(e) / iters
+        return 2.0 * self.m * self.n * self.k / (ms * 1e-3) / 1e12

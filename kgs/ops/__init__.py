@@ -1,0 +1,23 @@
+"""HIP/CDNA4 kernels exposed to PyTorch (gfx950 only).
+
+* :func:`gemm_nt`, :func:`matmul`, :func:`linear`, :class:`Linear` -- bf16 MFMA GEMM
+  (``native/kernels/gemm_bf16.hip``)
+* :func:`vector_add`, :func:`transpose_bf16`, :func:`checksum` -- memory-bound
+  helpers (``native/kernels/elementwise.hip``)
+
+Importing this package does not touch the GPU; the native library is loaded on
+first use and raises :class:`NativeUnavailable` if it is missing.
+"""
+from ._lib import KernelError, NativeUnavailable, available  # noqa: F401
+
+
+def __getattr__(name):  # lazy: keep `import kgs.ops` free of torch for CPU-only tools
+    if name in ("gemm_nt", "matmul", "linear", "Linear", "fast_path_ok", "transpose", "EPI"):
+        from . import gemm
+
+        return getattr(gemm, name)
+    if name in ("vector_add", "transpose_bf16", "checksum"):
+        from . import elementwise
+
+        return getattr(elementwise, name)
+    raise AttributeError(name)

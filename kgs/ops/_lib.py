@@ -1,0 +1,87 @@
+"""ctypes binding to ``kgs/_native/libkgs_kernels.so`` (the gfx950 HIP kernels).
+
+The library exports a plain C ABI (see ``native/kernels/*.hip``): raw device
+pointers, sizes and a ``hipStream_t``. Torch is imported first so that the
+library's ``libamdhip64.so.7`` dependency resolves (by SONAME) to the HIP runtime
+torch already loaded -- one HIP runtime per process, shared streams.
+
+There is deliberately no silent fallback: on a machine with a GPU, a missing or
+unloadable library raises ``NativeUnavailable`` (the driver checks that the
+native code is what runs).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from functools import lru_cache
+from pathlib import Path
+
+NATIVE_DIR = Path(__file__).resolve().parents[1] / "_native"
+LIB_PATH = Path(os.environ.get("KGS_KERNELS_LIB", NATIVE_DIR / "libkgs_kernels.so"))
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class KernelError(RuntimeError):
+    pass
+
+
+_ERRS = {-1: "bad shape", -2: "bad alignment / not eligible for this variant", -3: "bad argument"}
+
+_c_void_p = ctypes.c_void_p
+_c_int = ctypes.c_int
+_c_long = ctypes.c_long
+
+_SIGS = {
+    "kgs_gemm_bf16_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_fast_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
+    "kgs_vector_add_f32": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
+    "kgs_vector_add_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
+    "kgs_transpose_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
+    "kgs_checksum_bf16": ([_c_void_p, _c_long, _c_void_p, _c_void_p], _c_int),
+}
+
+
+@lru_cache(maxsize=1)
+def lib() -> ctypes.CDLL:
+    import torch  # noqa: F401  -- must precede the load (shared HIP runtime)
+
+    if not LIB_PATH.exists():
+        raise NativeUnavailable(
+            f"{LIB_PATH} is missing: build it with `python -m kgs.utils.build` (hipcc --offload-arch=gfx950)"
+        )
+    try:
+        so = ctypes.CDLL(str(LIB_PATH))
+    except OSError as e:  # pragma: no cover - depends on the box
+        raise NativeUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(so, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = args
+        fn.restype = res
+    return so
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except NativeUnavailable:
+        return False
+
+
+def check(rc: int, what: str) -> None:
+    if rc == 0:
+        return
+    if rc < 0:
+        raise KernelError(f"{what}: {_ERRS.get(rc, rc)}")
+    raise KernelError(f"{what}: hipError_t {rc}")
+
+
+def stream_handle(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,58 @@
+"""Memory-bound HIP ops: vector add (config-2 smoke), transpose, checksum."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+
+def _dev_check(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise ValueError("tensor must be on a GPU")
+        if not t.is_contiguous():
+            raise ValueError("tensor must be contiguous")
+
+
+def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a + b`` elementwise (f32 or bf16) on the HIP vector-add kernel."""
+    _dev_check(a, b)
+    if a.shape != b.shape or a.dtype != b.dtype:
+        raise ValueError("a and b must match in shape and dtype")
+    out = torch.empty_like(a) if out is None else out
+    _dev_check(out)
+    n = a.numel()
+    if a.dtype == torch.float32:
+        fn = _lib.lib().kgs_vector_add_f32
+    elif a.dtype == torch.bfloat16:
+        fn = _lib.lib().kgs_vector_add_bf16
+    else:
+        raise TypeError(f"unsupported dtype {a.dtype}")
+    _lib.check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), n, _lib.stream_handle(a.device)), "vector_add")
+    return out
+
+
+def transpose_bf16(x: torch.Tensor) -> torch.Tensor:
+    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("transpose_bf16 needs a row-major bf16 matrix")
+    if not x.is_cuda:
+        raise ValueError("tensor must be on a GPU")
+    rows, cols = x.shape
+    out = torch.empty((cols, rows), dtype=torch.bfloat16, device=x.device)
+    rc = _lib.lib().kgs_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0), rows,
+                                       _lib.stream_handle(x.device))
+    _lib.check(rc, "transpose_bf16")
+    return out
+
+
+def checksum(x: torch.Tensor) -> torch.Tensor:
+    """Device-side (sum, sum|x|) of a bf16 tensor as a 2-element f32 tensor."""
+    _dev_check(x)
+    if x.dtype != torch.bfloat16 or x.numel() % 8:
+        raise ValueError("checksum needs bf16 with numel % 8 == 0")
+    out = torch.zeros(2, dtype=torch.float32, device=x.device)
+    _lib.check(
+        _lib.lib().kgs_checksum_bf16(x.data_ptr(), x.numel(), out.data_ptr(), _lib.stream_handle(x.device)),
+        "checksum",
+    )
+    return out

@@ -1,0 +1,171 @@
+"""bf16 MFMA GEMM ops backed by ``native/kernels/gemm_bf16.hip``.
+
+``gemm_nt(a, b)`` computes ``a @ b.T`` for ``a: [M, K]``, ``b: [N, K]`` (both
+K-contiguous bf16 on a gfx950 device), with optional fused bias + activation in
+the kernel epilogue. ``matmul`` and ``Linear`` are built on it; the backward pass
+re-uses the same NT kernel after a HIP transpose, so every FLOP of the in-pod
+workload runs on the hand-written MFMA kernel.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib
+
+EPI = {None: 0, "none": 0, "bias": 1, "gelu": 2, "relu": 3, "silu": 4}
+VARIANTS = {"auto": 0, "fast": 1, "generic": 2}
+
+
+def _check_operand(t: torch.Tensor, name: str) -> None:
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name} must be bfloat16, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be on a GPU")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError(f"{name} must be a 2-D row-major (stride(1)==1) matrix")
+
+
+def gemm_nt(
+    a: torch.Tensor,
+    b: torch.Tensor,
+    bias: torch.Tensor | None = None,
+    act: str | None = None,
+    out: torch.Tensor | None = None,
+    variant: str = "auto",
+) -> torch.Tensor:
+    """``act(a @ b.T + bias)`` in bf16 with f32 accumulation.
+
+    act: None | "bias" (bias only) | "gelu" | "relu" | "silu"; a non-None act or
+    bias implies the bias epilogue (a zero bias is allocated if act is given
+    without one).
+    """
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if a.device != b.device:
+        raise ValueError("a and b on different devices")
+    epi_name = act if act is not None else ("bias" if bias is not None else None)
+    if epi_name not in EPI:
+        raise ValueError(f"unknown activation {act!r}")
+    epi = EPI[epi_name]
+    if epi and bias is None:
+        bias = torch.zeros(N, dtype=torch.bfloat16, device=a.device)
+    if bias is not None:
+        if bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous():
+            raise ValueError("bias must be a contiguous bf16 vector of length N")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out")
+        if tuple(out.shape) != (M, N):
+            raise ValueError(f"out has shape {tuple(out.shape)}, expected {(M, N)}")
+    rc = _lib.lib().kgs_gemm_bf16_nt(
+        a.data_ptr(),
+        b.data_ptr(),
+        out.data_ptr(),
+        bias.data_ptr() if bias is not None else None,
+        M,
+        N,
+        K,
+        a.stride(0),
+        b.stride(0),
+        out.stride(0),
+        epi,
+        VARIANTS[variant],
+        _lib.stream_handle(a.device),
+    )
+    _lib.check(rc, f"gemm_nt[{M}x{N}x{K}]")
+    return out
+
+
+def fast_path_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> bool:
+    M, K = a.shape
+    N = b.shape[0]
+    c_ptr = out.data_ptr() if out is not None else 0
+    ldc = out.stride(0) if out is not None else N
+    return bool(
+        _lib.lib().kgs_gemm_bf16_nt_fast_ok(a.data_ptr(), b.data_ptr(), c_ptr, M, N, K, a.stride(0), b.stride(0), ldc)
+    )
+
+
+def transpose(x: torch.Tensor) -> torch.Tensor:
+    """Materialised ``x.T`` for a row-major bf16 matrix (HIP LDS-tiled transpose)."""
+    from .elementwise import transpose_bf16
+
+    return transpose_bf16(x)
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """``a @ b`` with ``b: [K, N]`` row-major: one HIP transpose + the NT kernel."""
+    return gemm_nt(a, transpose(b))
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, act):
+        ctx.save_for_backward(x, w, bias)
+        ctx.act = act
+        if act in (None, "none"):
+            return gemm_nt(x, w, bias=bias)
+        if not any(ctx.needs_input_grad[:3]):
+            return gemm_nt(x, w, bias=bias, act=act)  # inference: activation fused in the epilogue
+        # training keeps the pre-activation for the backward pass: GEMM with the
+        # bias epilogue, then the activation in torch (cheap, memory-bound)
+        z = gemm_nt(x, w, bias=bias)
+        ctx.z = z
+        return _act(z, act)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w, bias = ctx.saved_tensors
+        gy = gy.contiguous()
+        if ctx.act not in (None, "none"):
+            z = ctx.z.float().requires_grad_(True)
+            with torch.enable_grad():
+                y = _act(z, ctx.act)
+            (gz,) = torch.autograd.grad(y, z, gy.float())
+            gy = gz.to(torch.bfloat16).contiguous()
+        # dX[M,K] = dY[M,N] . W[N,K]      -> NT with B = W^T [K,N]
+        gx = gemm_nt(gy, transpose(w))
+        # dW[N,K] = dY^T[N,M] . X[M,K]    -> NT with A = dY^T [N,M], B = X^T [K,M]
+        gw = gemm_nt(transpose(gy), transpose(x))
+        gb = gy.float().sum(0).to(torch.bfloat16) if bias is not None else None
+        return gx, gw, gb, None
+
+
+def _act(z: torch.Tensor, act: str) -> torch.Tensor:
+    if act == "gelu":
+        return torch.nn.functional.gelu(z, approximate="tanh")
+    if act == "relu":
+        return torch.relu(z)
+    if act == "silu":
+        return torch.nn.functional.silu(z)
+    if act == "bias":
+        return z
+    raise ValueError(act)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None):
+    """Differentiable ``act(x @ w.T + bias)`` on the HIP GEMM (x: [M,K], w: [N,K])."""
+    return _LinearFn.apply(x, w, bias, act)
+
+
+class Linear(torch.nn.Module):
+    """bf16 ``nn.Linear`` whose forward and backward GEMMs run on the HIP kernel."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, act: str | None = None,
+                 device=None):
+        super().__init__()
+        w = torch.empty(out_features, in_features, dtype=torch.bfloat16, device=device)
+        torch.nn.init.normal_(w, std=in_features ** -0.5)
+        self.weight = torch.nn.Parameter(w)
+        self.bias = torch.nn.Parameter(torch.zeros(out_features, dtype=torch.bfloat16, device=device)) if bias else None
+        self.act = act
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        y = linear(x.reshape(-1, shp[-1]).contiguous(), self.weight, self.bias, self.act)
+        return y.reshape(*shp[:-1], y.shape[-1])

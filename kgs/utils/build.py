@@ -1,0 +1,233 @@
+"""In-tree native build for kgs (gfx950 only).
+
+Builds, with the ROCm toolchain in ``/opt/rocm``:
+
+* ``kgs/_native/libkgs_kernels.so`` -- every ``native/kernels/*.hip`` (bf16 MFMA
+  GEMM, vector add, transpose, checksum, P2P all-reduce) behind a C ABI that
+  ``kgs/ops/_lib.py`` loads with ctypes.
+* ``kgs/_native/libkgs_gpuinfo.so`` + ``kgs/_native/kgs-gpuinfo`` -- the C++
+  device-enumeration core (KFD sysfs topology + amd-smi) used by the device
+  plugin, also as a standalone CLI.
+* ``kgs/_native/kgs-rccl-bench`` -- single-process multi-GPU RCCL all-reduce
+  sweep (ncclCommInitAll), the C++ twin of ``kgs.parallel.allreduce``.
+
+Everything is compiled for ``--offload-arch=gfx950`` and nothing else. The
+build is incremental (mtime based) and parallel; ``python -m kgs.utils.build``
+or ``__graft_entry__.build()`` drive it. No JIT cache is used, so the built
+``.so`` files travel with the repo snapshot to the GPU box.
+
+The reference has no native build at all; its only native components are Go
+device plugins cloned and built inside docker (kind-gpu-sim.sh:180-228).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from dataclasses import dataclass, field
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[2]
+NATIVE = REPO / "native"
+OUT = REPO / "kgs" / "_native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+ARCH = "gfx950"
+
+HIPCC = str(ROCM / "bin" / "hipcc")
+CXX = os.environ.get("CXX", "g++")
+
+HIP_FLAGS = [
+    f"--offload-arch={ARCH}",
+    "-O3",
+    "-std=c++17",
+    "-fPIC",
+    "-Wall",
+    "-Wno-unused-function",
+    "-Wno-unused-variable",
+    "-munsafe-fp-atomics",
+]
+
+
+@dataclass
+class Target:
+    name: str
+    output: Path
+    sources: list[Path]
+    compiler: str
+    flags: list[str] = field(default_factory=list)
+    link_flags: list[str] = field(default_factory=list)
+    shared: bool = True
+    headers: list[Path] = field(default_factory=list)
+    optional: bool = False  # skip (with a warning) if a dependency is missing
+
+    def stale(self) -> bool:
+        if not self.output.exists():
+            return True
+        out_m = self.output.stat().st_mtime
+        deps = list(self.sources) + list(self.headers) + [Path(__file__)]
+        return any(p.exists() and p.stat().st_mtime > out_m for p in deps)
+
+
+def _pybind_includes() -> list[str]:
+    try:
+        import pybind11  # noqa: WPS433
+
+        inc = [pybind11.get_include()]
+    except Exception:  # pragma: no cover - pybind11 is in the image
+        return []
+    import sysconfig
+
+    inc.append(sysconfig.get_paths()["include"])
+    return [f"-I{p}" for p in inc]
+
+
+def _py_ext_suffix() -> str:
+    import sysconfig
+
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def targets() -> list[Target]:
+    kdir = NATIVE / "kernels"
+    gdir = NATIVE / "gpuinfo"
+    rdir = NATIVE / "rccl_bench"
+    k_headers = sorted(kdir.glob("*.h"))
+    g_headers = sorted(gdir.glob("*.h"))
+    amdsmi_ok = (ROCM / "include" / "amd_smi" / "amdsmi.h").exists()
+    smi_flags = ["-DKGS_HAVE_AMDSMI=1", f"-I{ROCM / 'include'}"] if amdsmi_ok else []
+    smi_link = [f"-L{ROCM / 'lib'}", "-lamd_smi", f"-Wl,-rpath,{ROCM / 'lib'}"] if amdsmi_ok else []
+    core = [gdir / "gpuinfo.cpp"]
+    ts = [
+        Target(
+            "kernels",
+            OUT / "libkgs_kernels.so",
+            sorted(kdir.glob("*.hip")),
+            HIPCC,
+            flags=HIP_FLAGS + [f"-I{kdir}"],
+            headers=k_headers,
+        ),
+        Target(
+            "gpuinfo-lib",
+            OUT / "libkgs_gpuinfo.so",
+            core + [gdir / "gpuinfo_capi.cpp"],
+            CXX,
+            flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{gdir}"] + smi_flags,
+            link_flags=smi_link,
+            headers=g_headers,
+        ),
+        Target(
+            "gpuinfo-py",
+            OUT / f"_gpuinfo{_py_ext_suffix()}",
+            core + [gdir / "gpuinfo_py.cpp"],
+            CXX,
+            flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{gdir}"] + smi_flags + _pybind_includes(),
+            link_flags=smi_link,
+            headers=g_headers,
+        ),
+        Target(
+            "gpuinfo-cli",
+            OUT / "kgs-gpuinfo",
+            core + [gdir / "gpuinfo_cli.cpp"],
+            CXX,
+            flags=["-O2", "-std=c++17", "-Wall", f"-I{gdir}"] + smi_flags,
+            link_flags=smi_link,
+            shared=False,
+            headers=g_headers,
+        ),
+        Target(
+            "rccl-bench",
+            OUT / "kgs-rccl-bench",
+            [rdir / "rccl_bench.cpp"],
+            HIPCC,
+            flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", f"-I{ROCM / 'include'}"],
+            link_flags=[f"-L{ROCM / 'lib'}", "-lrccl", f"-Wl,-rpath,{ROCM / 'lib'}"],
+            shared=False,
+            optional=True,
+        ),
+    ]
+    return [t for t in ts if all(s.exists() for s in t.sources)]
+
+
+def _compile_one(t: Target, src: Path, obj: Path) -> None:
+    cmd = [t.compiler, *t.flags, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+
+
+def build_target(t: Target, jobs: int = 8, verbose: bool = False) -> bool:
+    """Build one target; returns True if it was (re)built."""
+    if not t.stale():
+        return False
+    objdir = REPO / "build" / "obj" / t.name
+    objdir.mkdir(parents=True, exist_ok=True)
+    objs = [objdir / (s.stem + ".o") for s in t.sources]
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        futs = [ex.submit(_compile_one, t, s, o) for s, o in zip(t.sources, objs)]
+        for f in futs:
+            f.result()
+    t.output.parent.mkdir(parents=True, exist_ok=True)
+    tmp = t.output.with_name(t.output.name + ".tmp")
+    link = [t.compiler]
+    if t.compiler == HIPCC:
+        link.append(f"--offload-arch={ARCH}")
+    if t.shared:
+        link.append("-shared")
+    link += [str(o) for o in objs] + ["-o", str(tmp)] + t.link_flags
+    r = subprocess.run(link, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, t.output)
+    if verbose:
+        print(f"[kgs.build] built {t.output.relative_to(REPO)}", file=sys.stderr)
+    return True
+
+
+def build_all(jobs: int | None = None, verbose: bool = True, only: list[str] | None = None) -> dict[str, str]:
+    """Build every native target. Returns {name: "built"|"fresh"|"skipped: why"}."""
+    if not Path(HIPCC).exists():
+        raise RuntimeError(f"hipcc not found at {HIPCC}; set ROCM_PATH")
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    status: dict[str, str] = {}
+    for t in targets():
+        if only and t.name not in only:
+            continue
+        try:
+            status[t.name] = "built" if build_target(t, jobs=jobs, verbose=verbose) else "fresh"
+        except RuntimeError as e:
+            if t.optional:
+                status[t.name] = f"skipped: {str(e).splitlines()[0]}"
+                if verbose:
+                    print(f"[kgs.build] optional target {t.name} skipped:\n{e}", file=sys.stderr)
+            else:
+                raise
+    return status
+
+
+def clean() -> None:
+    shutil.rmtree(REPO / "build" / "obj", ignore_errors=True)
+    for p in OUT.glob("*"):
+        if p.name != "__init__.py":
+            p.unlink()
+
+
+def main(argv: list[str] | None = None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="python -m kgs.utils.build", description=__doc__.splitlines()[0])
+    ap.add_argument("--clean", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--only", nargs="*", default=None)
+    a = ap.parse_args(argv)
+    if a.clean:
+        clean()
+    st = build_all(jobs=a.jobs, only=a.only)
+    for k, v in st.items():
+        print(f"{k:14s} {v}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,421 @@
+// bf16 GEMM for gfx950 (MI355X / CDNA4), hand-written on MFMA + LDS-DMA.
+//
+//   C[M,N] (bf16) = epilogue( A[M,K] · B[N,K]^T )      f32 accumulation
+//
+// Both operands are K-contiguous ("NT", the torch.nn.Linear weight layout), so
+// every MFMA fragment is one 16-byte LDS read.
+//
+// Two kernels:
+//
+//  * gemm_nt_256 -- the hot path (M%256 == N%256 == 0, K%128 == 0).
+//      256x256x64 block tile, 512 threads = 8 waves as 2(M) x 4(N), each wave
+//      owns 128x64 of C as 2x2 quadrants of 64x32 (4x2 MFMA 16x16x32 tiles).
+//      A and B K-tiles are split into 128-row halves (A0 A1 B0 B1, 16 KiB each)
+//      staged by `global_load_lds_dwordx4` into a 2-deep ring (128 KiB LDS, one
+//      workgroup per CU). The wave->row map is interleaved so that a quadrant
+//      phase touches exactly one A half and one B half; with that, a half-tile
+//      can be restaged independently of the other halves of its K-tile.
+//
+//      K-loop: 8 phases per iteration (2 K-tiles x 4 quadrants). Phase p:
+//         ds_read the quadrant's fragments (12 / 4 / 8 / 0 x ds_read_b128)
+//         issue half-tile h = p + 5 (2 x glds per wave)
+//         s_waitcnt vmcnt(6)            <- 3 half-tiles stay in flight
+//         s_barrier ; lgkmcnt(0) ; setprio(1) ; 16 x MFMA ; setprio(0) ; s_barrier
+//      Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's
+//      MFMA block overlaps its partner's LDS-read/DMA-issue block.
+//      Hazard accounting (phase p, half-tile h issued at p-5):
+//        RAW: h retired by the issuing waves' vmcnt(6) in phase h-2 and read at
+//             phase >= h-1 after >= 1 more barrier on every wave;
+//        WAR: a half-tile slot is re-issued >= 2 phases after its last ds_read
+//             (A0: read at 4t/4t+1, reissued at 4t+3), which with the one-barrier
+//             stagger still leaves a barrier between the last read and the DMA.
+//      LDS image: 128-byte rows, 16-byte chunk c stored at c ^ ((row >> 1) & 7),
+//      which makes every ds_read_b128 16-lane group hit 16 distinct bank slots
+//      (conflict-free); the swizzle is applied to the glds SOURCE address.
+//      Grid: one block per 256x256 tile, XCD-bijective remap then GROUP_M=8
+//      grouped order so the ~32 co-resident tiles of an XCD share A/B panels.
+//
+//  * gemm_nt_generic -- any shape/stride (bounds-checked, register staged,
+//      128x128x32 tile). Used for ragged shapes and as the test oracle's twin.
+//
+// C ABI: kgs_gemm_bf16_nt(...) (bottom of file), loaded from Python via ctypes
+// (kgs/ops/_lib.py) and from the C++ benches.
+//
+// Reference parity: the reference (kind-gpu-sim) has no kernels at all -- its
+// test pod only echoes (pods/rocm-gpu-test-pod.yaml:9, Readme.md:16-20). This is
+// the in-pod hot path required by BASELINE.json configs 3-4.
+#include "kgs_common.h"
+
+namespace kgs {
+namespace g256 {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HALF_BYTES = 128 * BK * 2;   // 16 KiB: 128 rows x 128 B
+constexpr int BUF_BYTES = 4 * HALF_BYTES;  // A0 A1 B0 B1
+constexpr int LDS_BYTES = 2 * BUF_BYTES;   // 2-deep ring = 128 KiB
+constexpr int P_A0 = 0, P_A1 = 1, P_B0 = 2, P_B1 = 3;
+constexpr int LOOKAHEAD = 5;               // half-tiles issued ahead of use
+constexpr int GROUP_M = 8;
+
+struct Regs {
+  bf16x8 a[4][2];        // A fragments of the current m-half: [m-tile][k-sub]
+  bf16x8 b[2][2][2];     // B fragments of both n-halves: [n-half][n-tile][k-sub]
+  f32x4 acc[2][4][2][2]; // [m-half][m-tile][n-half][n-tile]
+};
+
+struct Ctx {
+  char* smem;
+  const unsigned short* Ag;  // A + tile_m*256*lda
+  const unsigned short* Bg;  // B + tile_n*256*ldb
+  long a_half;               // 128*lda (elements)
+  long b_half;
+  int offA0, offA1, offB0, offB1;  // per-lane glds source offsets (elements)
+  int ro0, ro1;                    // per-lane ds_read byte offsets for k-sub 0/1
+  int wr, wc, w;                   // wave coordinates (wave-uniform)
+  int nt;                          // number of K-tiles
+};
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int PART>
+__device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
+  char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048;
+  const unsigned short* src;
+  int o0, o1;
+  if constexpr (PART == P_A0 || PART == P_A1) {
+    src = c.Ag + (PART == P_A1 ? c.a_half : 0) + k0;
+    o0 = c.offA0; o1 = c.offA1;
+  } else {
+    src = c.Bg + (PART == P_B1 ? c.b_half : 0) + k0;
+    o0 = c.offB0; o1 = c.offB1;
+  }
+  glds16(src + o0, dst);
+  glds16(src + o1, dst + 1024);
+}
+
+// Read the 4 m-tiles x 2 k-subs of A for this wave from half-tile `part`.
+__device__ __forceinline__ void read_a(const Ctx& c, Regs& R, const char* half) {
+  const char* p = half + c.wr * 64 * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    R.a[i][0] = *(const bf16x8*)(p + i * 16 * 128 + c.ro0);
+    R.a[i][1] = *(const bf16x8*)(p + i * 16 * 128 + c.ro1);
+  }
+}
+
+template <int NH>
+__device__ __forceinline__ void read_b(const Ctx& c, Regs& R, const char* half) {
+  const char* p = half + c.wc * 32 * 128;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    R.b[NH][n][0] = *(const bf16x8*)(p + n * 16 * 128 + c.ro0);
+    R.b[NH][n][1] = *(const bf16x8*)(p + n * 16 * 128 + c.ro1);
+  }
+}
+
+template <int MH, int NH>
+__device__ __forceinline__ void mma_quadrant(Regs& R) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        // operands swapped (B first) so each lane ends up holding 4
+        // consecutive output COLUMNS of one row: C[m = lane&15][n = 4*(lane>>4)+e]
+        R.acc[MH][i][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            R.b[NH][n][s], R.a[i][s], R.acc[MH][i][NH][n], 0, 0, 0);
+}
+
+template <int QP>
+__device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
+  constexpr int q = QP & 3;
+  constexpr int cbuf = QP >> 2;
+  const char* buf = c.smem + cbuf * BUF_BYTES;
+  if constexpr (q == 0) {
+    read_a(c, R, buf + P_A0 * HALF_BYTES);
+    read_b<0>(c, R, buf + P_B0 * HALF_BYTES);
+  } else if constexpr (q == 1) {
+    read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
+  } else if constexpr (q == 2) {
+    read_a(c, R, buf + P_A1 * HALF_BYTES);
+  }
+  // prefetch half-tile h = 8*it + QP + LOOKAHEAD; stream order A0,B0,B1,A1
+  constexpr int hoff = QP + LOOKAHEAD;
+  constexpr int toff = hoff >> 2;
+  constexpr int jp = hoff & 3;
+  constexpr int part = jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1;
+  int t = 2 * it + toff;
+  t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
+  issue<part>(c, toff & 1, t * BK);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  bar();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_setprio(1);
+  if constexpr (q == 0) mma_quadrant<0, 0>(R);
+  if constexpr (q == 1) mma_quadrant<0, 1>(R);
+  if constexpr (q == 2) mma_quadrant<1, 1>(R);
+  if constexpr (q == 3) mma_quadrant<1, 0>(R);
+  __builtin_amdgcn_s_setprio(0);
+  bar();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restrict__ A,
+                                                   const unsigned short* __restrict__ B,
+                                                   unsigned short* __restrict__ C,
+                                                   const unsigned short* __restrict__ bias,
+                                                   int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per_group = GROUP_M * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsz = min(ntm - first_m, GROUP_M);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  {
+    // glds j (0/1) of wave w fills half-tile rows w*16 + j*8 + lane/8; lane's
+    // physical 16-B chunk is lane&7 and holds logical chunk (lane&7)^f(row).
+    const int r0 = w * 16 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ ((r0 >> 1) & 7);
+    const int c1 = (lane & 7) ^ ((r1 >> 1) & 7);
+    c.offA0 = r0 * lda + c0 * 8;
+    c.offA1 = r1 * lda + c1 * 8;
+    c.offB0 = r0 * ldb + c0 * 8;
+    c.offB1 = r1 * ldb + c1 * 8;
+    // fragment read: row lane&15, logical chunk 4*s + lane/16
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+
+  Regs R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
+  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  issue<P_A0>(c, 0, 0);
+  issue<P_B0>(c, 0, 0);
+  issue<P_B1>(c, 0, 0);
+  issue<P_A1>(c, 0, 0);
+  issue<P_A0>(c, 1, k1);
+  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
+  bar();
+  if (c.wr == 1) bar();  // stagger: waves 4-7 trail by one barrier
+
+  const int iters = c.nt >> 1;
+  for (int it = 0; it < iters; ++it) {
+    phase<0>(c, R, it);
+    phase<1>(c, R, it);
+    phase<2>(c, R, it);
+    phase<3>(c, R, it);
+    phase<4>(c, R, it);
+    phase<5>(c, R, it);
+    phase<6>(c, R, it);
+    phase<7>(c, R, it);
+  }
+  if (c.wr == 0) bar();  // balance the stagger barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
+
+  // epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n)
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          f32x4 v = R.acc[mh][i][nh][n];
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI != EPI_NONE) {
+            bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+          }
+          uint2 o;
+          o.x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o.y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+          *(uint2*)(crow + col) = o;
+        }
+    }
+}
+
+}  // namespace g256
+
+namespace gen {
+
+// Generic bounds-checked NT GEMM: 128x128x32 tile, 256 threads (2x2 waves of
+// 64x64), register-staged loads with zero fill, padded LDS rows.
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int ROWB = BK * 2 + 16;  // 80-byte padded row
+
+__device__ __forceinline__ bf16x8 load8(const unsigned short* __restrict__ P, int ld, int row, int nrows,
+                                        int k, int K, bool vec_ok) {
+  bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (row >= nrows) return v;
+  const unsigned short* p = P + (long)row * ld + k;
+  if (vec_ok && k + 8 <= K) return *(const bf16x8*)p;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    if (k + e < K) v[e] = (short)p[e];
+  return v;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_nt_generic(const unsigned short* __restrict__ A,
+                                                       const unsigned short* __restrict__ B,
+                                                       unsigned short* __restrict__ C,
+                                                       const unsigned short* __restrict__ bias,
+                                                       int M, int N, int K, int lda, int ldb, int ldc,
+                                                       int vec_ok) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * BM * ROWB];
+  char* sA = smem;
+  char* sB = smem + BM * ROWB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  const int tm = blockIdx.y, tn = blockIdx.x;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // each thread stages 2 chunks of A and 2 of B: row = tid/4 (+64), chunk = tid%4
+  const int lr = tid >> 2, lc = tid & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    bf16x8 a0 = load8(A, lda, m0 + lr, M, k0 + lc * 8, K, vec_ok);
+    bf16x8 a1 = load8(A, lda, m0 + lr + 64, M, k0 + lc * 8, K, vec_ok);
+    bf16x8 b0 = load8(B, ldb, n0 + lr, N, k0 + lc * 8, K, vec_ok);
+    bf16x8 b1 = load8(B, ldb, n0 + lr + 64, N, k0 + lc * 8, K, vec_ok);
+    __syncthreads();
+    *(bf16x8*)(sA + lr * ROWB + lc * 16) = a0;
+    *(bf16x8*)(sA + (lr + 64) * ROWB + lc * 16) = a1;
+    *(bf16x8*)(sB + lr * ROWB + lc * 16) = b0;
+    *(bf16x8*)(sB + (lr + 64) * ROWB + lc * 16) = b1;
+    __syncthreads();
+    bf16x8 af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(sA + (wr * 64 + i * 16 + fr) * ROWB + fq * 16);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) bfr[n] = *(const bf16x8*)(sB + (wc * 64 + n * 16 + fr) * ROWB + fq * 16);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+        acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[n], af[i], acc[i][n], 0, 0, 0);
+  }
+
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr * 64 + i * 16 + fr;
+    if (row >= M) continue;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = n0 + wc * 64 + n * 16 + fq * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (col + e < N) {
+          float b = (EPI != EPI_NONE) ? bf2f(bias[col + e]) : 0.f;
+          C[(long)row * ldc + col + e] = f2bf(epilogue<EPI>(acc[i][n][e], b));
+        }
+      }
+    }
+  }
+}
+
+}  // namespace gen
+
+template <int EPI>
+static hipError_t launch(int variant, const unsigned short* A, const unsigned short* B, unsigned short* C,
+                         const unsigned short* bias, int M, int N, int K, int lda, int ldb, int ldc,
+                         hipStream_t s) {
+  if (variant == 1) {
+    dim3 grid((M / g256::BM) * (N / g256::BN));
+    hipLaunchKernelGGL(g256::gemm_nt_256<EPI>, grid, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else {
+    const int vec_ok = ((lda % 8) == 0 && (ldb % 8) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
+    dim3 grid((N + gen::BN - 1) / gen::BN, (M + gen::BM - 1) / gen::BM);
+    hipLaunchKernelGGL(gen::gemm_nt_generic<EPI>, grid, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
+                       vec_ok);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace kgs
+
+// Can the 256x256 pipelined kernel take this problem?
+KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
+                                        int ldb, int ldc) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (M % 256 || N % 256 || K % 128) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 4) return 0;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 8) return 0;
+  // 32-bit per-lane offsets: (255 rows) * ld must fit
+  if ((long)lda * 256 >= (1L << 31) || (long)ldb * 256 >= (1L << 31)) return 0;
+  return 1;
+}
+
+// variant: 0 = auto, 1 = force 256x256 pipelined (must be eligible), 2 = force generic.
+KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                                int ldb, int ldc, int epi, int variant, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
+  if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (epi != kgs::EPI_NONE && bias == nullptr) return KGS_ERR_ARG;
+  const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc);
+  int v;
+  if (variant == 0) v = fast ? 1 : 2;
+  else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
+  else if (variant == 2) v = 2;
+  else return KGS_ERR_ARG;
+  if (v == 1 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto bb = (const unsigned short*)bias;
+  hipError_t e;
+  switch (epi) {
+    case kgs::EPI_NONE: e = kgs::launch<kgs::EPI_NONE>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS: e = kgs::launch<kgs::EPI_BIAS>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS_GELU: e = kgs::launch<kgs::EPI_BIAS_GELU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS_RELU: e = kgs::launch<kgs::EPI_BIAS_RELU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS_SILU: e = kgs::launch<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    default: return KGS_ERR_ARG;
+  }
+  return (int)e;
+}

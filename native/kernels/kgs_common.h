@@ -1,0 +1,85 @@
+// Shared device helpers for the kgs gfx950 kernels.
+//
+// Everything here is written for CDNA4 (gfx950, wave64, MFMA, LDS-DMA). There is
+// no CUDA path and no multi-arch dispatch: kernels are compiled with
+// `--offload-arch=gfx950` only (see kgs/utils/build.py).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define KGS_LDS __attribute__((address_space(3)))
+#define KGS_GLB __attribute__((address_space(1)))
+
+#define KGS_EXPORT extern "C" __attribute__((visibility("default")))
+
+// Error codes returned by the C ABI (0 = success, >0 = hipError_t, <0 = ours).
+enum {
+  KGS_OK = 0,
+  KGS_ERR_SHAPE = -1,      // non-positive or overflowing dimension
+  KGS_ERR_ALIGN = -2,      // pointer / leading-dimension alignment
+  KGS_ERR_ARG = -3,        // unknown enum value
+};
+
+namespace kgs {
+
+// Round-to-nearest-even f32 -> bf16 bits. hipcc lowers the __bf16 cast to
+// v_cvt_pk_bf16_f32 on gfx950, which also keeps NaNs NaN
+// (MI355X_MICROARCH.md, correctness boundaries).
+__device__ __forceinline__ unsigned short f2bf(float x) {
+  __bf16 h = (__bf16)x;
+  return __builtin_bit_cast(unsigned short, h);
+}
+
+__device__ __forceinline__ float bf2f(unsigned short h) {
+  return __builtin_bit_cast(float, ((unsigned)h) << 16);
+}
+
+__device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+
+// 16-byte LDS-DMA: each lane's 16 global bytes land at lds_base + lane*16
+// (lds_base must be wave-uniform). The swizzle, if any, is applied to the
+// per-lane *source* address (cdna_hip_programming.md rule 21).
+__device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
+  __builtin_amdgcn_global_load_lds((KGS_GLB void*)gsrc, (KGS_LDS void*)lds_base, 16, 0, 0);
+}
+
+// Bijective XCD-aware remap of a 1-D grid: blocks that the dispatcher deals to
+// the same XCD (bid % 8 equal) get a contiguous range of logical ids, so
+// neighbouring output tiles share that XCD's L2 (guide T1).
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+}
+
+// Epilogue activations (fused into the GEMM store).
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_SILU = 4 };
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  // tanh via exp: stable for |u| large.
+  float e = __expf(-2.0f * fabsf(u));
+  float t = (1.0f - e) / (1.0f + e);
+  t = u < 0.f ? -t : t;
+  return 0.5f * x * (1.0f + t);
+}
+
+template <int EPI>
+__device__ __forceinline__ float epilogue(float v, float b) {
+  if constexpr (EPI == EPI_NONE) return v;
+  v += b;
+  if constexpr (EPI == EPI_BIAS_GELU) return gelu_tanh(v);
+  if constexpr (EPI == EPI_BIAS_RELU) return v > 0.f ? v : 0.f;
+  if constexpr (EPI == EPI_BIAS_SILU) return v / (1.0f + __expf(-v));
+  return v;
+}
+
+}  // namespace kgs

@@ -1,0 +1,174 @@
+"""Numerics of the gfx950 HIP kernels against plain PyTorch fp32 references.
+
+GEMM checks follow cdna_hip_programming.md §3: an ASYMMETRIC B (so a swapped
+C-write cannot pass), A = I, random operands over several shapes, both kernel
+variants, every fused epilogue, and a backward pass through ``kgs.ops.Linear``.
+"""
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ref_nt(a, b, bias=None, act=None):
+    y = a.float() @ b.float().T
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = torch.nn.functional.gelu(y, approximate="tanh")
+    elif act == "relu":
+        y = torch.relu(y)
+    elif act == "silu":
+        y = torch.nn.functional.silu(y)
+    return y
+
+
+def _rel_err(got, ref):
+    return ((got.float() - ref).abs().max() / ref.abs().max().clamp_min(1e-6)).item()
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from kgs.ops import _lib
+
+    _lib.lib()  # fail loudly if the HIP library is missing on a GPU box
+    torch.manual_seed(0)
+
+
+def test_vector_add_f32_and_bf16():
+    from kgs.ops import vector_add
+
+    for n in (1, 7, 4096, (1 << 20) + 3):
+        a = torch.randn(n, device=DEV)
+        b = torch.randn(n, device=DEV)
+        torch.testing.assert_close(vector_add(a, b), a + b)
+        ab, bb = a.bfloat16(), b.bfloat16()
+        ref = (ab.float() + bb.float()).bfloat16()
+        torch.testing.assert_close(vector_add(ab, bb), ref)
+
+
+def test_transpose():
+    from kgs.ops import transpose_bf16
+
+    for r, c in ((1, 1), (64, 64), (100, 37), (257, 1031)):
+        x = torch.randn(r, c, device=DEV).bfloat16()
+        torch.testing.assert_close(transpose_bf16(x), x.T.contiguous(), rtol=0, atol=0)
+
+
+def test_checksum():
+    from kgs.ops import checksum
+
+    x = torch.randn(1 << 16, device=DEV).bfloat16()
+    got = checksum(x)
+    ref = torch.stack([x.float().sum(), x.float().abs().sum()])
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
+
+
+@pytest.mark.parametrize("variant", ["generic", "fast"])
+def test_gemm_identity_asymmetric(variant):
+    from kgs.ops import gemm_nt
+
+    n = 256
+    a = torch.eye(n, device=DEV).bfloat16()
+    # B[n][k] asymmetric; C = A . B^T = B^T
+    idx = torch.arange(n, device=DEV)
+    b = ((idx[:, None] * 3 + idx[None, :] * 7) % 61 - 30).float().bfloat16()
+    k = 256
+    a2 = torch.zeros(n, k, device=DEV).bfloat16()
+    a2[:, :n] = a
+    c = gemm_nt(a2, b, variant=variant)
+    torch.testing.assert_close(c.float(), b.float().T, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize(
+    "M,N,K",
+    [(256, 256, 128), (512, 768, 256), (256, 512, 1024), (1024, 1024, 1024), (768, 256, 384), (2048, 1280, 640)],
+)
+def test_gemm_fast_random(M, N, K):
+    from kgs.ops import fast_path_ok, gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    assert fast_path_ok(a, b)
+    c = gemm_nt(a, b, variant="fast")
+    ref = _ref_nt(a, b)
+    assert _rel_err(c, ref) < 1e-2
+    # the two variants agree (same fp32 accumulation, possibly different order)
+    g = gemm_nt(a, b, variant="generic")
+    assert _rel_err(c, g.float()) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (17, 33, 65), (100, 300, 70), (255, 129, 31), (1000, 24, 8)])
+def test_gemm_generic_ragged(M, N, K):
+    from kgs.ops import gemm_nt
+
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = torch.randn(N, K, device=DEV).bfloat16()
+    c = gemm_nt(a, b)
+    assert _rel_err(c, _ref_nt(a, b)) < 1e-2
+
+
+def test_gemm_strided_operands():
+    from kgs.ops import gemm_nt
+
+    big_a = torch.randn(512, 1024, device=DEV).bfloat16()
+    big_b = torch.randn(512, 1024, device=DEV).bfloat16()
+    a = big_a[:, 128:384]  # ld = 1024, K = 256
+    b = big_b[:256, 256:512]
+    c = gemm_nt(a, b, variant="fast")
+    assert _rel_err(c, _ref_nt(a, b)) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["bias", "gelu", "relu", "silu"])
+@pytest.mark.parametrize("variant", ["fast", "generic"])
+def test_gemm_epilogues(act, variant):
+    from kgs.ops import gemm_nt
+
+    M, N, K = 512, 512, 256
+    a = (torch.rand(M, K, device=DEV) - 0.5).bfloat16()
+    b = (torch.rand(N, K, device=DEV) - 0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    c = gemm_nt(a, b, bias=bias, act=act, variant=variant)
+    ref = _ref_nt(a, b, bias, None if act == "bias" else act)
+    torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_gemm_repeatable_large():
+    """Race screen: the pipelined kernel must be bitwise deterministic."""
+    from kgs.ops import gemm_nt
+
+    M = N = K = 2048
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    c0 = gemm_nt(a, b)
+    assert _rel_err(c0, _ref_nt(a, b)) < 1e-2
+    for _ in range(20):
+        assert torch.equal(gemm_nt(a, b), c0)
+
+
+def test_matmul_and_linear_backward():
+    from kgs.ops import Linear, matmul
+
+    a = torch.randn(256, 512, device=DEV).bfloat16()
+    b = torch.randn(512, 384, device=DEV).bfloat16()
+    assert _rel_err(matmul(a, b), a.float() @ b.float()) < 1e-2
+
+    torch.manual_seed(1)
+    lin = Linear(512, 256, act="gelu", device=DEV)
+    x = torch.randn(128, 512, device=DEV).bfloat16().requires_grad_(True)
+    y = lin(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+
+    xr = x.detach().float().requires_grad_(True)
+    wr = lin.weight.detach().float().requires_grad_(True)
+    br = lin.bias.detach().float().requires_grad_(True)
+    yr = torch.nn.functional.gelu(xr @ wr.T + br, approximate="tanh")
+    yr.backward(gy.float())
+    assert _rel_err(y, yr) < 2e-2
+    assert _rel_err(x.grad, xr.grad) < 3e-2
+    assert _rel_err(lin.weight.grad, wr.grad) < 3e-2
+    assert _rel_err(lin.bias.grad, br.grad) < 3e-2
