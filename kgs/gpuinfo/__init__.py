@@ -1,0 +1,158 @@
+"""Python view of the native GPU enumeration core (``native/gpuinfo``).
+
+``discover(root)`` returns a :class:`Topology` built by the C++ core
+(pybind11 module ``kgs._native._gpuinfo``; ctypes over
+``libkgs_gpuinfo.so`` as a second path). There is no pure-Python parser: the
+device plugin and CLI always see what the native core sees.
+
+The reference has no discovery at all -- it writes a constant capacity of 2
+into each worker's status (kind-gpu-sim.sh:113).
+"""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+from dataclasses import dataclass, field
+from functools import lru_cache
+from pathlib import Path
+
+NATIVE_DIR = Path(__file__).resolve().parents[1] / "_native"
+XGMI = 11
+PCIE = 2
+
+
+class GpuInfoUnavailable(RuntimeError):
+    pass
+
+
+@dataclass
+class Link:
+    to_node: int
+    type: int
+    weight: int = 0
+    max_bandwidth_mbs: int = 0
+
+    @property
+    def is_xgmi(self) -> bool:
+        return self.type == XGMI
+
+
+@dataclass
+class Gpu:
+    index: int
+    node_id: int
+    render_minor: int
+    bdf: str = ""
+    gpu_id: int = 0
+    unique_id: str = "0"
+    hive_id: str = "0"
+    gfx_arch: str = ""
+    gfx_target_version: int = 0
+    vendor_id: int = 0
+    device_id: int = 0
+    simd_count: int = 0
+    cu_count: int = 0
+    num_xcc: int = 0
+    lds_kb: int = 0
+    wave_size: int = 0
+    max_clock_mhz: int = 0
+    vram_bytes: int = 0
+    numa_node: int = -1
+    uuid: str = ""
+    properties_readable: bool = True
+    render_node_present: bool = False
+    healthy: bool = False
+    health_reason: str = ""
+    links: list = field(default_factory=list)
+
+    @property
+    def device_id_str(self) -> str:
+        """Stable kubelet device ID: the PCI address when known, else the node id."""
+        return self.bdf if self.bdf and self.bdf != "0000:00:00.0" else f"kfd-node-{self.node_id}"
+
+    @property
+    def render_path(self) -> str:
+        return f"/dev/dri/renderD{self.render_minor}"
+
+    def xgmi_peers(self) -> set:
+        return {lk.to_node for lk in self.links if lk.is_xgmi}
+
+
+@dataclass
+class Topology:
+    root: str
+    kfd_present: bool
+    topology_present: bool
+    amdsmi_used: bool
+    cpu_nodes: int
+    gpus: list
+    warnings: list
+
+    def by_node(self) -> dict:
+        return {g.node_id: g for g in self.gpus}
+
+    def xgmi_connected(self, a: Gpu, b: Gpu) -> bool:
+        return b.node_id in a.xgmi_peers() or a.node_id in b.xgmi_peers()
+
+    @property
+    def healthy_gpus(self) -> list:
+        return [g for g in self.gpus if g.healthy]
+
+
+def _parse(js: str) -> Topology:
+    d = json.loads(js)
+    gpus = []
+    for g in d["gpus"]:
+        links = [Link(**lk) for lk in g.pop("links")]
+        gpus.append(Gpu(links=links, **g))
+    return Topology(
+        root=d["root"], kfd_present=d["kfd_present"], topology_present=d["topology_present"],
+        amdsmi_used=d["amdsmi_used"], cpu_nodes=d["cpu_nodes"], gpus=gpus, warnings=d["warnings"],
+    )
+
+
+@lru_cache(maxsize=1)
+def _backend():
+    try:
+        from kgs._native import _gpuinfo  # type: ignore
+
+        return ("pybind", _gpuinfo)
+    except ImportError:
+        pass
+    so = NATIVE_DIR / "libkgs_gpuinfo.so"
+    if so.exists():
+        lib = ctypes.CDLL(str(so))
+        lib.kgs_gpuinfo_discover_json.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_long]
+        lib.kgs_gpuinfo_discover_json.restype = ctypes.c_long
+        return ("ctypes", lib)
+    raise GpuInfoUnavailable(
+        f"native gpuinfo core not built ({NATIVE_DIR}); run `python -m kgs.utils.build`"
+    )
+
+
+def backend_name() -> str:
+    return _backend()[0]
+
+
+def discover_json(root: str = "/", use_amdsmi: bool = True) -> str:
+    kind, mod = _backend()
+    if kind == "pybind":
+        return mod.discover_json(str(root), use_amdsmi)
+    n = mod.kgs_gpuinfo_discover_json(str(root).encode(), int(use_amdsmi), None, 0)
+    buf = ctypes.create_string_buffer(n + 1)
+    mod.kgs_gpuinfo_discover_json(str(root).encode(), int(use_amdsmi), buf, n + 1)
+    return buf.value.decode()
+
+
+def discover(root: str | os.PathLike = "/", use_amdsmi: bool = True) -> Topology:
+    return _parse(discover_json(str(root), use_amdsmi))
+
+
+def health(root: str, node_id: int, render_minor: int) -> tuple:
+    kind, mod = _backend()
+    if kind == "pybind":
+        return tuple(mod.health(str(root), node_id, render_minor))
+    t = discover(root, use_amdsmi=False)
+    g = t.by_node().get(node_id)
+    return (bool(g and g.healthy), g.health_reason if g else "KFD node gone")
