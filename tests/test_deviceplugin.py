@@ -1,0 +1,245 @@
+"""Device plugin (T2 of SURVEY.md §4): real gRPC over unix sockets against a
+fake kubelet, on a fake 8 x MI355X sysfs tree and on the captured box tree."""
+import os
+import tempfile
+import threading
+import time
+
+import grpc
+import pytest
+
+from kgs.deviceplugin import api
+from kgs.deviceplugin.fake_kubelet import FakeKubelet
+from kgs.deviceplugin.server import AmdGpuDevicePlugin, FakeSource, RealSource, load_partition
+from kgs.gpuinfo.fake import make_fake_mi355x, remove_gpu_device, restore_gpu_device
+
+FIXTURE_BOX = os.path.join(os.path.dirname(__file__), "fixtures", "kfd_box1")
+
+
+@pytest.fixture
+def short_tmp():
+    # unix socket paths must stay < 108 bytes
+    d = tempfile.mkdtemp(prefix="kgs", dir="/tmp")
+    yield d
+    import shutil
+
+    shutil.rmtree(d, ignore_errors=True)
+
+
+@pytest.fixture
+def host8(short_tmp):
+    return str(make_fake_mi355x(os.path.join(short_tmp, "host")))
+
+
+@pytest.fixture
+def cluster(short_tmp, host8):
+    dpdir = os.path.join(short_tmp, "dp")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    src = RealSource(host8, use_amdsmi=False)
+    plug = AmdGpuDevicePlugin(src, plugin_dir=dpdir, health_interval=0.1)
+    plug.start()
+    plug.register()
+    plug.notify()
+    assert kub.wait(lambda: bool(kub.device_lists))
+    yield kub, plug, src, host8
+    plug.stop()
+    kub.stop()
+
+
+def test_register_and_list_and_watch(cluster):
+    kub, plug, src, _ = cluster
+    reg = kub.registrations[-1]
+    assert reg.version == "v1beta1"
+    assert reg.resource_name == "amd.com/gpu"
+    assert reg.endpoint == "kgs-amdgpu.sock"
+    assert reg.options.get_preferred_allocation_available
+    assert kub.options.get_preferred_allocation_available and not kub.options.pre_start_required
+    devs = kub.latest_devices()
+    assert len(devs) == 8 and kub.capacity() == 8
+    assert all(h == "Healthy" for _, h, _ in devs)
+    # NUMA topology hints: 4 GPUs per socket
+    assert sorted(n[0] for _, _, n in devs) == [0, 0, 0, 0, 1, 1, 1, 1]
+
+
+def test_allocate_gives_kfd_and_render_nodes(cluster):
+    kub, plug, src, host = cluster
+    ids = [d.id for d in src.devices()][:2]
+    resp = kub.allocate(ids)
+    c = resp.container_responses[0]
+    paths = [(s.container_path, s.host_path, s.permissions) for s in c.devices]
+    assert paths[0] == ("/dev/kfd", "/dev/kfd", "rw")
+    assert ("/dev/dri/renderD128", "/dev/dri/renderD128", "rw") in paths
+    assert ("/dev/dri/renderD136", "/dev/dri/renderD136", "rw") in paths
+    assert len(paths) == 3
+    assert c.envs["KGS_RENDER_MINORS"] == "128,136"
+    assert c.annotations["kgs.amd.com/gpus"] == ",".join(ids)
+    for _, h, _ in paths:
+        assert os.path.exists(os.path.join(host, h.lstrip("/")))
+
+
+def test_allocate_unknown_device_rejected(cluster):
+    kub, *_ = cluster
+    with pytest.raises(grpc.RpcError) as ei:
+        kub.allocate(["0000:ff:00.0"])
+    assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+
+
+def test_health_flip_streams_unhealthy_then_recovers(cluster):
+    kub, plug, src, host = cluster
+    n0 = len(kub.device_lists)
+    remove_gpu_device(host, 144)
+    assert plug.health_tick()
+    assert kub.wait(lambda: len(kub.device_lists) > n0)
+    devs = dict((i, h) for i, h, _ in kub.latest_devices())
+    sick = [d.id for d in src.devices() if d.render_minor == 144][0]
+    assert devs[sick] == "Unhealthy" and kub.capacity() == 7
+    with pytest.raises(grpc.RpcError) as ei:
+        kub.allocate([sick])
+    assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+    n1 = len(kub.device_lists)
+    restore_gpu_device(host, 144)
+    assert plug.health_tick()
+    assert kub.wait(lambda: len(kub.device_lists) > n1)
+    assert kub.capacity() == 8
+    assert not plug.health_tick()  # no change -> no update
+
+
+def test_kfd_loss_marks_all_unhealthy(cluster):
+    kub, plug, src, host = cluster
+    os.unlink(os.path.join(host, "dev/kfd"))
+    n0 = len(kub.device_lists)
+    assert plug.health_tick()
+    assert kub.wait(lambda: len(kub.device_lists) > n0)
+    assert kub.capacity() == 0
+
+
+def test_preferred_allocation_packs_numa(cluster):
+    kub, plug, src, _ = cluster
+    ids = [d.id for d in src.devices()]
+    # 4 GPUs from all 8: one socket
+    got = kub.preferred(ids, [], 4)
+    numas = {d.numa for d in src.devices() if d.id in got}
+    assert len(got) == 4 and len(numas) == 1
+    # must-include a socket-1 GPU -> the rest come from socket 1
+    got = kub.preferred(ids, [ids[5]], 4)
+    assert ids[5] in got and {d.numa for d in src.devices() if d.id in got} == {1}
+    got = kub.preferred(ids, [], 8)
+    assert sorted(got) == sorted(ids)
+
+
+def test_kubelet_restart_reregisters(short_tmp, host8):
+    dpdir = os.path.join(short_tmp, "dp")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    plug = AmdGpuDevicePlugin(RealSource(host8, use_amdsmi=False), plugin_dir=dpdir, health_interval=0.2)
+    t = threading.Thread(target=plug.serve_forever, kwargs={"poll": 0.05}, daemon=True)
+    t.start()
+    try:
+        assert kub.wait(lambda: len(kub.registrations) == 1 and bool(kub.device_lists), timeout=15)
+        kub.restart()
+        assert kub.wait(lambda: len(kub.registrations) >= 2, timeout=15)
+        assert kub.wait(lambda: kub.capacity() == 8, timeout=15)
+        deadline = time.monotonic() + 10
+        while plug.registrations < 2 and time.monotonic() < deadline:
+            time.sleep(0.05)
+        assert plug.registrations >= 2
+    finally:
+        plug.stop()
+        t.join(timeout=10)
+        kub.stop()
+
+
+def test_partition_filtering(short_tmp, host8):
+    import json
+
+    pf = os.path.join(short_tmp, "gpus.json")
+    with open(pf, "w") as f:
+        json.dump({"nodes": {"c-worker": [128, 136, 144, 152], "c-worker2": [160, 168, 176, 184],
+                             "c-worker3": []}}, f)
+    a = load_partition(pf, "c-worker")
+    b = load_partition(pf, "c-worker2")
+    assert a == {128, 136, 144, 152} and b == {160, 168, 176, 184}
+    assert load_partition(pf, "c-worker3") == set()
+    assert load_partition(pf, "unknown-node") == set()
+    assert load_partition(None, "x") is None
+    src = RealSource(host8, a, use_amdsmi=False)
+    assert [d.render_minor for d in src.devices()] == [128, 136, 144, 152]
+    os.environ["KGS_ALLOWED_RENDER_MINORS"] = "184"
+    try:
+        assert load_partition(pf, "c-worker") == {184}
+    finally:
+        del os.environ["KGS_ALLOWED_RENDER_MINORS"]
+
+
+def test_captured_box_tree():
+    src = RealSource(FIXTURE_BOX, use_amdsmi=False)
+    devs = src.devices()
+    assert len(devs) == 1
+    d = devs[0]
+    assert d.render_minor == 144 and d.id == "0000:5a:00.0" and d.healthy
+    assert d.meta["gfx"] == "gfx950" and d.meta["cus"] == 256 and d.meta["vram_gib"] == 288.0
+
+
+def test_fake_source_plugin(short_tmp):
+    dpdir = os.path.join(short_tmp, "dp")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    src = FakeSource(2)
+    plug = AmdGpuDevicePlugin(src, plugin_dir=dpdir)
+    plug.start()
+    plug.register()
+    plug.notify()
+    try:
+        assert kub.wait(lambda: kub.capacity() == 2)
+        r = kub.allocate(["fake-amdgpu-0"])
+        assert len(r.container_responses[0].devices) == 0
+        assert r.container_responses[0].envs["KGS_FAKE_GPUS"] == "fake-amdgpu-0"
+        n = len(kub.device_lists)
+        src.set_unhealthy("fake-amdgpu-1")
+        assert plug.health_tick()
+        assert kub.wait(lambda: len(kub.device_lists) > n)
+        assert kub.capacity() == 1
+    finally:
+        plug.stop()
+        kub.stop()
+
+
+def test_register_rejects_wrong_version(short_tmp):
+    dpdir = os.path.join(short_tmp, "dp")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    try:
+        with grpc.insecure_channel(f"unix://{kub.sock}") as ch:
+            stub = ch.unary_unary(api.method_path("Registration", "Register"),
+                                  request_serializer=api.RegisterRequest.SerializeToString,
+                                  response_deserializer=api.Empty.FromString)
+            with pytest.raises(grpc.RpcError):
+                stub(api.RegisterRequest(version="v1alpha", endpoint="x", resource_name="amd.com/gpu"), timeout=5)
+    finally:
+        kub.stop()
+
+
+def test_self_test_cli(host8, capsys):
+    from kgs.deviceplugin.__main__ import main
+
+    rc = main(["--self-test", "--dev-root", host8, "--no-amdsmi", "--partition-file", "/nonexistent"])
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    assert '"capacity": 8' in out and '"paths_exist": true' in out
+
+
+def test_serve_forever_stops_promptly(short_tmp, host8):
+    dpdir = os.path.join(short_tmp, "dp")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    plug = AmdGpuDevicePlugin(RealSource(host8, use_amdsmi=False), plugin_dir=dpdir)
+    t = threading.Thread(target=plug.serve_forever, kwargs={"poll": 0.05}, daemon=True)
+    t.start()
+    assert kub.wait(lambda: bool(kub.device_lists), timeout=15)
+    t0 = time.monotonic()
+    plug.stop()
+    t.join(timeout=10)
+    assert not t.is_alive() and time.monotonic() - t0 < 10
+    assert not os.path.exists(plug.socket_path)
+    kub.stop()
