@@ -1,0 +1,128 @@
+"""``kgs`` command line -- drop-in for ``kind-gpu-sim.sh``.
+
+  kgs create [rocm] [--registry-port=N] [--cluster-name=S] [--runtime=docker|podman]
+                    [--workers=N] [--gpu-partition=all-on-first|split] [--fake-gpus=N]
+                    [--fake-mode=patch|plugin] [--timings-json=F] [--dry-run] [--keep-on-fail]
+  kgs delete [--cluster-name=S]
+  kgs load   --image-name=IMG [--cluster-name=S]
+  kgs status [--json]
+  kgs bench  [e2e options]          create -> gpu-rocm-test Running, per-phase JSON
+  kgs images [--workload] [--plugin] build the in-tree images
+
+Flags are accepted in both ``--k=v`` and ``--k v`` form and anywhere on the line
+(the reference scans all argv for its three flags, kind-gpu-sim.sh:31-43). Unlike
+the reference, an unknown flag is an error, and the GPU type is a real
+positional (Q1). Usage errors exit 1, as ``usage()`` does (kind-gpu-sim.sh:364-367).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+
+from . import config as C
+
+VERBS = ("create", "delete", "load", "status", "bench", "images")
+
+
+class _Parser(argparse.ArgumentParser):
+    def error(self, message):  # exit 1 like the reference's usage()
+        self.print_usage(sys.stderr)
+        print(f"{self.prog}: error: {message}", file=sys.stderr)
+        raise SystemExit(1)
+
+
+def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
+    ap = _Parser(prog=prog, description="MI355X-native kind GPU provisioner (kind-gpu-sim compatible)",
+                 usage=C.USAGE.format(prog=prog))
+    ap.add_argument("verb", nargs="?", choices=VERBS)
+    ap.add_argument("gpu_type", nargs="?", default="rocm")
+    ap.add_argument("--registry-port", type=int, default=C.DEFAULT_REGISTRY_PORT)
+    ap.add_argument("--cluster-name", default=C.DEFAULT_CLUSTER_NAME)
+    ap.add_argument("--image-name", default=C.DEFAULT_IMAGE_NAME)
+    ap.add_argument("--runtime", choices=("docker", "podman"), default=None)
+    ap.add_argument("--workers", type=int, default=C.DEFAULT_WORKERS)
+    ap.add_argument("--gpu-partition", choices=("all-on-first", "split"), default="all-on-first")
+    ap.add_argument("--fake-gpus", type=int, default=None,
+                    help="force the simulated path with N amd.com/gpu per worker (reference default: 2)")
+    ap.add_argument("--fake-mode", choices=("patch", "plugin"), default="patch",
+                    help="fake capacity via node-status patch (reference) or via the plugin's fake source")
+    ap.add_argument("--registry-bind", default="127.0.0.1")
+    ap.add_argument("--kind-node-image", default=None)
+    ap.add_argument("--plugin-image", default=None, help="use a prebuilt device-plugin image")
+    ap.add_argument("--skip-build", action="store_true")
+    ap.add_argument("--ready-timeout", type=int, default=C.PLUGIN_READY_TIMEOUT_S)
+    ap.add_argument("--timings-json", default=None)
+    ap.add_argument("--dev-root", default="/", help="host root for GPU discovery (tests)")
+    ap.add_argument("--dry-run", action="store_true", help="print the command plan, change nothing")
+    ap.add_argument("--keep-on-fail", action="store_true")
+    ap.add_argument("--json", action="store_true")
+    # bench/images options
+    ap.add_argument("--gpus", type=int, default=1, help="bench: amd.com/gpu requested by the test pod")
+    ap.add_argument("--pod-timeout", type=int, default=C.TEST_POD_READY_TIMEOUT_S)
+    ap.add_argument("--keep", action="store_true", help="bench: keep the cluster afterwards")
+    ap.add_argument("--workload-image", default=None)
+    ap.add_argument("--workload", action="store_true")
+    ap.add_argument("--plugin", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    return ap
+
+
+def settings_from(a) -> C.Settings:
+    return C.Settings(
+        registry_port=a.registry_port, cluster_name=a.cluster_name, image_name=a.image_name, runtime=a.runtime,
+        workers=a.workers, gpu_partition=a.gpu_partition, fake_gpus=a.fake_gpus, fake_mode=a.fake_mode,
+        registry_bind=a.registry_bind, kind_node_image=a.kind_node_image, dry_run=a.dry_run,
+        keep_on_fail=a.keep_on_fail, skip_build=a.skip_build, timings_json=a.timings_json,
+        plugin_image=a.plugin_image, ready_timeout_s=a.ready_timeout, dev_root=a.dev_root,
+    )
+
+
+def main(argv=None, prog: str = "kgs") -> int:
+    ap = build_parser(prog)
+    a = ap.parse_intermixed_args(argv)
+    logging.basicConfig(level=logging.DEBUG if a.verbose else logging.INFO, format="%(message)s",
+                        stream=sys.stderr)
+    if a.verb is None:
+        print(C.USAGE.format(prog=prog), file=sys.stderr)
+        return 1
+    from .cluster import Provisioner, ProvisionError
+    from .runtime import RuntimeNotFound
+    from .utils.proc import CommandError
+
+    s = settings_from(a)
+    p = Provisioner(s)
+    try:
+        if a.verb == "create":
+            return p.create(a.gpu_type)
+        if a.verb == "delete":
+            return p.delete()
+        if a.verb == "load":
+            return p.load()
+        if a.verb == "status":
+            return p.status(as_json=a.json)
+        if a.verb == "bench":
+            from .e2e import run_e2e
+
+            return run_e2e(p, gpus=a.gpus, pod_timeout=a.pod_timeout, keep=a.keep,
+                           workload_image=a.workload_image)
+        if a.verb == "images":
+            from .images import build_images
+
+            return build_images(p, workload=a.workload or not a.plugin, plugin=a.plugin or not a.workload)
+    except (ProvisionError, RuntimeNotFound) as e:
+        print(str(e), file=sys.stderr)
+        return 1
+    except CommandError as e:
+        print(f"ERROR: {e}", file=sys.stderr)
+        if e.stderr:
+            print(e.stderr.rstrip(), file=sys.stderr)
+        return 1
+    finally:
+        if s.dry_run and p.runner.plan:
+            import shlex
+
+            print("# command plan:", file=sys.stderr)
+            for step in p.runner.plan:
+                print("  " + shlex.join(step["argv"]) + ("  <<stdin" if "stdin" in step else ""), file=sys.stderr)
+    return 1

@@ -17,9 +17,10 @@ import os
 import signal
 import sys
 import tempfile
+import threading
 
 from . import api
-from .server import AmdGpuDevicePlugin, FakeSource, RealSource, load_partition
+from .server import AmdGpuDevicePlugin, FakeSource, RealSource, load_partition, mark_ready
 
 
 def _args(argv=None):
@@ -32,6 +33,7 @@ def _args(argv=None):
     ap.add_argument("--fake-gpus", type=int, default=int(os.environ.get("KGS_FAKE_GPUS", "0") or 0))
     ap.add_argument("--health-interval", type=float, default=float(os.environ.get("KGS_HEALTH_INTERVAL", "5")))
     ap.add_argument("--no-amdsmi", action="store_true")
+    ap.add_argument("--ready-file", default=os.environ.get("KGS_READY_FILE", "/tmp/kgs-dp-ready"))
     ap.add_argument("--self-test", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -82,7 +84,21 @@ def main(argv=None) -> int:
     src = make_source(a)
     logging.getLogger("kgs.deviceplugin").info(
         "node=%s devices=%s", a.node_name, [(d.id, d.render_minor, d.healthy) for d in src.devices()])
-    plug = AmdGpuDevicePlugin(src, a.resource, plugin_dir=a.plugin_dir, health_interval=a.health_interval)
+    stop = threading.Event()
+    if not src.devices() and a.fake_gpus <= 0:
+        # A GPU-labelled worker that owns no GPU (all-on-first partition, or a
+        # CPU-only host using the reference's patched fake capacity): registering
+        # an empty amd.com/gpu list would make the kubelet zero the capacity, so
+        # stay idle (and Ready) instead.
+        logging.getLogger("kgs.deviceplugin").info("no GPUs for this node; idle (not registering)")
+        mark_ready(a.ready_file, {"state": "idle", "devices": 0})
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+        signal.signal(signal.SIGINT, lambda *_: stop.set())
+        while not stop.wait(3600):
+            pass
+        return 0
+    plug = AmdGpuDevicePlugin(src, a.resource, plugin_dir=a.plugin_dir, health_interval=a.health_interval,
+                              ready_file=a.ready_file)
 
     def _term(signum, frame):
         plug.stop()

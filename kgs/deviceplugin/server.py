@@ -157,11 +157,23 @@ def load_partition(path: str | None, node_name: str | None) -> set | None:
     return None
 
 
+def mark_ready(path: str | None, status: dict) -> None:
+    """Readiness file for the DaemonSet probe (registered, or idle by design)."""
+    if not path:
+        return
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        json.dump(status, f)
+    os.replace(tmp, path)
+
+
 # ------------------------------------------------------------------- plugin --
 class AmdGpuDevicePlugin:
     def __init__(self, source, resource_name: str = RESOURCE_NAME, plugin_dir: str = api.DEVICE_PLUGIN_PATH,
-                 socket_name: str = SOCKET_NAME, health_interval: float = 5.0, kubelet_socket: str | None = None):
+                 socket_name: str = SOCKET_NAME, health_interval: float = 5.0, kubelet_socket: str | None = None,
+                 ready_file: str | None = None):
         self.source = source
+        self.ready_file = ready_file
         self.resource_name = resource_name
         self.plugin_dir = plugin_dir
         self.socket_name = socket_name
@@ -347,6 +359,8 @@ class AmdGpuDevicePlugin:
             try:
                 self.register()
                 self.notify()
+                mark_ready(self.ready_file, {"state": "registered", "resource": self.resource_name,
+                                             "devices": len(self.source.devices())})
                 return
             except grpc.RpcError as e:
                 log.warning("kubelet registration failed (%s); retrying in %.1fs", e.code() if hasattr(e, "code")

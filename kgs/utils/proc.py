@@ -62,7 +62,7 @@ class Runner:
         if input is not None:
             entry["stdin"] = input
         self.plan.append(entry)
-        if self.echo or self.dry_run:
+        if self.echo:
             log.info("+ %s%s", shlex.join(argv), "  <<stdin" if input is not None else "")
         if self.dry_run:
             out = ""

@@ -1,0 +1,107 @@
+"""gpu-rocm-test pod entrypoint (replaces ``echo Hello from fake ROCm GPU node``).
+
+pods/rocm-gpu-test-pod.yaml runs ``python3 -m kgs.workload.entrypoint --pod``:
+
+1. If the pod got no real GPU (CPU-only host, fake capacity -- BASELINE config 1)
+   print the reference's line ``Hello from fake ROCm GPU node``
+   (pods/rocm-gpu-test-pod.yaml:9) and hold.
+2. Otherwise list the allocated GPUs (native gpuinfo core: the render nodes the
+   device plugin passed in), then start one worker process per GPU with
+   ``torch.distributed.run`` -- vector add, bf16 MFMA GEMM, RCCL all-reduce
+   sweep (:mod:`kgs.workload.worker`) -- and print one JSON result line.
+3. ``--pod`` keeps the container Running afterwards (``sleep 3600`` in the
+   reference) so ``kubectl logs`` / ``kubectl wait`` behave the same.
+
+The parent never initialises the GPU itself: it counts render nodes and spawns
+the workers as children (no exec from a GPU-initialised process).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+HELLO_FAKE = "Hello from fake ROCm GPU node"
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def allocated_gpus() -> list:
+    """GPUs visible in this container (the device plugin only passes the
+    allocated render nodes, so this is exactly the pod's allocation)."""
+    if os.environ.get("KGS_FAKE_GPUS"):
+        return []
+    if not os.path.exists("/dev/kfd"):
+        return []
+    try:
+        from kgs import gpuinfo
+
+        topo = gpuinfo.discover("/", use_amdsmi=False)
+        return [g for g in topo.gpus if g.render_node_present and g.healthy]
+    except Exception:
+        return []
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="kgs-workload")
+    ap.add_argument("--pod", action="store_true", help="hold the container after the run (sleep)")
+    ap.add_argument("--hold", type=int, default=3600)
+    ap.add_argument("--gemm-size", type=int, default=8192)
+    ap.add_argument("--gemm-iters", type=int, default=20)
+    ap.add_argument("--allreduce-sizes", default="")
+    ap.add_argument("--nproc", type=int, default=0, help="override the GPU count")
+    ap.add_argument("--json-out", default=None)
+    ap.add_argument("--timeout", type=int, default=1200)
+    a = ap.parse_args(argv)
+
+    gpus = allocated_gpus()
+    n = a.nproc or len(gpus)
+    result: dict = {"mode": "fake" if n == 0 else "gpu", "n_gpus": n, "t_start": time.time()}
+    if n == 0:
+        print(HELLO_FAKE, flush=True)
+    else:
+        print(f"kgs workload: {n} GPU(s) allocated", flush=True)
+        for g in gpus:
+            print(f"  renderD{g.render_minor} {g.bdf} {g.gfx_arch} {g.cu_count} CUs {g.num_xcc} XCDs "
+                  f"{g.vram_bytes / 2**30:.0f} GiB numa{g.numa_node}", flush=True)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        env = dict(os.environ)
+        env["PYTHONPATH"] = root + (":" + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "kgs.workload.worker",
+               "--gemm-size", str(a.gemm_size), "--gemm-iters", str(a.gemm_iters)]
+        if a.allreduce_sizes:
+            cmd += ["--allreduce-sizes", a.allreduce_sizes]
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
+        sys.stderr.write(p.stderr[-4000:])
+        for line in p.stdout.splitlines():
+            if line.startswith("KGS_RESULT "):
+                result.update(json.loads(line[len("KGS_RESULT "):]))
+            else:
+                print(line, flush=True)
+        result["worker_rc"] = p.returncode
+    result["t_end"] = time.time()
+    line = json.dumps(result)
+    print(line, flush=True)
+    if a.json_out:
+        with open(a.json_out, "w") as f:
+            f.write(line + "\n")
+    rc = 0 if result.get("worker_rc", 0) == 0 and result.get("all_ok", True) else 1
+    if a.pod:
+        time.sleep(a.hold)
+    return rc
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
