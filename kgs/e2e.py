@@ -1,0 +1,73 @@
+"""``kgs bench``: the headline metric -- cluster create -> GPU pod Running.
+
+Phases (all in one PhaseTimer, written to ``--timings-json``):
+  create phases (kgs.cluster.Provisioner.create)
+  pod-apply       kubectl apply the gpu-rocm-test pod (N x amd.com/gpu)
+  pod-running     kubectl wait --for=jsonpath={.status.phase}=Running
+  pod-ready       kubectl wait --for=condition=Ready
+and the headline ``create_to_running_s`` = start of create .. pod Running. The
+pod's own result line (GEMM TFLOPS, all-reduce busBW) is parsed from its logs
+when it has finished its run.
+
+Mirrors the reference CI (rocm-ci.yaml:28-39: create, kubectl create pod,
+kubectl wait Ready --timeout=60s, kubectl logs), timed phase by phase. Needs a
+docker/podman + kind + kubectl host; none exists in the build container or on
+the gpurun boxes, so the e2e number is produced by this tool on such a host
+(BASELINE.md says which numbers were measured where).
+"""
+from __future__ import annotations
+
+import json
+import time
+
+from . import config as C
+from . import manifests
+
+
+def workload_image(p) -> str:
+    rt = p.ensure_runtime()
+    repo = f"{C.WORKLOAD_IMAGE_REPO}:{C.WORKLOAD_IMAGE_TAG}"
+    return f"localhost/{repo}" if rt.name == "podman" else f"{p.s.registry_host}/{repo}"
+
+
+def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, keep: bool = False,
+            workload_image: str | None = None, pod_command: list | None = None) -> int:
+    t = p.timer
+    t_start = time.perf_counter()
+    p.create("rocm")
+    image = workload_image or globals()["workload_image"](p)
+    if p.ensure_runtime().name == "podman" and not workload_image:
+        with t.phase("workload-image-load"):
+            p.rt.load_into_kind(image, p.s.cluster_name)
+    pod =manifests.gpu_test_pod(image, gpus=gpus, command=pod_command)
+    name = pod["metadata"]["name"]
+    result = {}
+    try:
+        with t.phase("pod-apply"):
+            p.kubectl("apply", "-f", "-", input=manifests.dump(pod))
+        with t.phase("pod-running"):
+            p.kubectl("wait", "--for=jsonpath={.status.phase}=Running", f"pod/{name}", f"--timeout={pod_timeout}s")
+        running_s = time.perf_counter() - t_start
+        with t.phase("pod-ready"):
+            p.kubectl("wait", "--for=condition=Ready", f"pod/{name}", f"--timeout={pod_timeout}s")
+        with t.phase("pod-logs"):
+            deadline = time.monotonic() + (600 if not p.runner.dry_run else 0)
+            while True:
+                r = p.kubectl("logs", f"pod/{name}", check=False, mutating=False)
+                for line in r.stdout.splitlines():
+                    if line.startswith("{") and '"mode"' in line:
+                        result = json.loads(line)
+                if result or time.monotonic() > deadline:
+                    break
+                time.sleep(2)
+        t.meta.update(create_to_running_s=round(running_s, 4), gpus_requested=gpus, pod_result=result)
+    finally:
+        t.write(p.s.timings_json)
+        if not keep and not p.runner.dry_run:
+            p.delete()
+    summary = {"metric": "cluster-create->GPU-pod-Running", "value": t.meta.get("create_to_running_s"),
+               "unit": "s", "gpus": gpus, "fake": p.fake, "phases": {ph["phase"]: ph["seconds"] for ph in t.phases}}
+    if result.get("gemm_tflops_total"):
+        summary["in_pod_gemm_tflops"] = result["gemm_tflops_total"]
+    p.out(json.dumps(summary))
+    return 0

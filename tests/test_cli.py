@@ -1,0 +1,310 @@
+"""T1: the CLI against stateful fake kind/kubectl/docker/podman
+binaries on PATH. Asserts the reference's observable contract (§2.2) and the
+deliberate fixes (Q1-Q15)."""
+import json
+import os
+import stat
+import sys
+
+import pytest
+import yaml
+
+from kgs import config as C
+from kgs.cli import main
+from kgs.gpuinfo.fake import make_fake_mi355x
+
+FAKE_TOOL = os.path.join(os.path.dirname(__file__), "fakebin", "fake_tool.py")
+
+
+@pytest.fixture
+def world(tmp_path, monkeypatch):
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    os.chmod(FAKE_TOOL, os.stat(FAKE_TOOL).st_mode | stat.S_IEXEC | stat.S_IXGRP | stat.S_IXOTH)
+    for tool in ("kind", "kubectl", "docker", "podman", "systemctl"):
+        (bindir / tool).symlink_to(FAKE_TOOL)
+    py_dir = os.path.dirname(sys.executable)
+    monkeypatch.setenv("PATH", f"{bindir}:{py_dir}:/usr/bin:/bin")
+    monkeypatch.setenv("KGS_FAKE_STATE", str(tmp_path / "state.json"))
+    monkeypatch.setenv("KGS_FAKE_LOG", str(tmp_path / "log.jsonl"))
+    monkeypatch.delenv("KGS_FAKE_FAIL", raising=False)
+    work = tmp_path / "work"
+    work.mkdir()
+    monkeypatch.chdir(work)
+    empty_root = tmp_path / "nogpu"
+    empty_root.mkdir()
+
+    class W:
+        path = tmp_path
+        cwd = work
+        nogpu = str(empty_root)
+
+        @staticmethod
+        def state():
+            p = tmp_path / "state.json"
+            return json.loads(p.read_text()) if p.exists() else {}
+
+        @staticmethod
+        def log():
+            p = tmp_path / "log.jsonl"
+            return [json.loads(x) for x in p.read_text().splitlines()] if p.exists() else []
+
+        @staticmethod
+        def calls(tool, *prefix):
+            return [e["argv"] for e in W.log() if e["tool"] == tool and e["argv"][: len(prefix)] == list(prefix)]
+
+        @staticmethod
+        def kubectl_calls(*prefix):
+            out = []
+            for e in W.log():
+                if e["tool"] != "kubectl":
+                    continue
+                a = e["argv"]
+                if a[:1] == ["--context"]:
+                    a = a[2:]
+                if a[: len(prefix)] == list(prefix):
+                    out.append((a, e["stdin"]))
+            return out
+
+    return W
+
+
+def run(*args):
+    return main(list(args))
+
+
+def test_create_fake_path_matches_reference_contract(world, capsys):
+    rc = run("create", "--dev-root", world.nogpu)
+    out = capsys.readouterr().out
+    assert rc == 0
+    assert "Simulated GPU Kind cluster is ready for 'rocm'!" in out
+    st = world.state()
+    # registry: name, restart policy, port mapping bound to localhost (Q4), on the kind network
+    reg = st["containers"]["kind-registry"]
+    assert reg["running"] and "--restart=always" in reg["args"]
+    assert "127.0.0.1:5000:5000" in reg["args"] and reg["image"] == C.REGISTRY_IMAGE
+    assert "kind" in reg["networks"]
+    cl = st["clusters"]["kind-gpu-sim"]
+    assert sorted(cl["nodes"]) == ["kind-gpu-sim-control-plane", "kind-gpu-sim-worker", "kind-gpu-sim-worker2"]
+    for n in ("kind-gpu-sim-worker", "kind-gpu-sim-worker2"):
+        node = cl["nodes"][n]
+        assert node["labels"] == {"hardware-type": "gpu", "node-role.kubernetes.io/worker": "",
+                                  "rocm.amd.com/gpu.present": "true"}
+        assert node["taints"] == ["gpu=true:NoSchedule"]
+        assert node["capacity"] == {"amd.com/gpu": "2"}  # kind-gpu-sim.sh:113
+    cp = cl["nodes"]["kind-gpu-sim-control-plane"]
+    assert cp["labels"] == {} and cp["taints"] == []
+    kinds = [o["kind"] for o in cl["objects"]]
+    assert kinds == ["ConfigMap", "DaemonSet"]
+    cm = cl["objects"][0]
+    assert cm["metadata"] == {"name": "local-registry-hosting", "namespace": "kube-public"}
+    assert 'host: "localhost:5000"' in cm["data"]["localRegistryHosting.v1"]
+    ds = cl["objects"][1]
+    assert ds["metadata"] == {"name": "amdgpu-device-plugin-daemonset", "namespace": "kube-system"}
+    tpl = ds["spec"]["template"]
+    assert tpl["metadata"]["labels"] == {"app": "amdgpu-device-plugin"}
+    assert tpl["spec"]["nodeSelector"] == {"hardware-type": "gpu"}
+    assert tpl["spec"]["tolerations"] == [{"key": "gpu", "operator": "Equal", "value": "true",
+                                           "effect": "NoSchedule"}]
+    ctr = tpl["spec"]["containers"][0]
+    assert ctr["name"] == "amdgpu-dp-ds" and ctr["image"] == "localhost:5000/amdgpu-dp:dev"
+    assert ctr["securityContext"] == {"privileged": True} and ctr["imagePullPolicy"] == "IfNotPresent"
+    mounts = {m["mountPath"] for m in ctr["volumeMounts"]}
+    assert {"/var/lib/kubelet/device-plugins", "/dev", "/sys", "/etc/kgs"} <= mounts  # Q7 fixed
+    assert "localhost:5000/amdgpu-dp:dev" in st["registry_images"]
+    # kind config: config_path + bind-mounted hosts.toml (Q2/Q3), 1 CP + 2 workers
+    cfg = yaml.safe_load((world.cwd / "kind-config.yaml").read_text())
+    assert cfg["kind"] == "Cluster" and cfg["apiVersion"] == "kind.x-k8s.io/v1alpha4"
+    assert [n["role"] for n in cfg["nodes"]] == ["control-plane", "worker", "worker"]
+    assert 'config_path = "/etc/containerd/certs.d"' in cfg["containerdConfigPatches"][0]
+    hosts = world.cwd / ".kgs" / "kind-gpu-sim" / "certs.d" / "localhost:5000" / "hosts.toml"
+    assert hosts.read_text() == '[host."http://kind-registry:5000"]\n  capabilities = ["pull", "resolve"]\n'
+    # no per-node docker exec / SIGHUP (Q2), labels + taint batched in one call each
+    assert world.calls("docker", "exec") == []
+    assert len(world.kubectl_calls("label")) == 1 and len(world.kubectl_calls("taint")) == 1
+    # no GPU passthrough mounts on a CPU-only host
+    assert all(m["containerPath"] not in ("/dev/kfd",) for n in cfg["nodes"] for m in n.get("extraMounts", []))
+
+
+def test_create_real_gpus_all_on_first(world, tmp_path, capsys):
+    host = make_fake_mi355x(tmp_path / "host8")
+    rc = run("create", "rocm", "--dev-root", str(host), "--timings-json", str(tmp_path / "t.json"))
+    out = capsys.readouterr().out
+    assert rc == 0, out
+    assert "8 amd.com/gpu advertised" in out
+    cfg = yaml.safe_load((world.cwd / "kind-config.yaml").read_text())
+    w1, w2 = cfg["nodes"][1], cfg["nodes"][2]
+    w1_paths = [m["containerPath"] for m in w1["extraMounts"]]
+    assert "/dev/kfd" in w1_paths and sum(p.startswith("/dev/dri/renderD") for p in w1_paths) == 8
+    assert "/dev/kfd" not in [m["containerPath"] for m in w2["extraMounts"]]
+    part = json.loads((world.cwd / ".kgs" / "kind-gpu-sim" / "gpus.json").read_text())
+    assert part["nodes"]["kind-gpu-sim-worker"] == [128 + 8 * i for i in range(8)]
+    assert part["nodes"]["kind-gpu-sim-worker2"] == []
+    st = world.state()["clusters"]["kind-gpu-sim"]
+    # capacity comes from the plugin (kubelet-managed), never from a status patch (H5)
+    assert world.kubectl_calls("patch") == []
+    assert st["nodes"]["kind-gpu-sim-worker"]["allocatable"] == {"amd.com/gpu": "8"}
+    assert st["nodes"]["kind-gpu-sim-worker"]["labels"]["kgs.amd.com/gpu-partition"] == "8"
+    t = json.loads((tmp_path / "t.json").read_text())
+    names = [p["phase"] for p in t["phases"]]
+    assert names == ["runtime", "discover", "registry", "kind-config", "kind-create", "registry-network", "nodes",
+                     "registry-configmap", "plugin-image", "plugin-deploy", "plugin-ready", "capacity"]
+    assert t["fake"] is False and all(p["ok"] for p in t["phases"])
+
+
+def test_create_split_partition(world, tmp_path):
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--dev-root", str(host), "--gpu-partition", "split") == 0
+    part = json.loads((world.cwd / ".kgs" / "kind-gpu-sim" / "gpus.json").read_text())["nodes"]
+    assert part["kind-gpu-sim-worker"] == [128, 136, 144, 152]  # NUMA 0
+    assert part["kind-gpu-sim-worker2"] == [160, 168, 176, 184]  # NUMA 1
+    st = world.state()["clusters"]["kind-gpu-sim"]["nodes"]
+    assert st["kind-gpu-sim-worker"]["allocatable"] == {"amd.com/gpu": "4"}
+    assert st["kind-gpu-sim-worker2"]["allocatable"] == {"amd.com/gpu": "4"}
+
+
+def test_create_is_idempotent(world, capsys):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    assert run("create", "--dev-root", world.nogpu) == 0
+    out = capsys.readouterr().out
+    assert "Registry 'kind-registry' already running." in out
+    assert "already exists; reconciling" in out
+    assert len(world.calls("kind", "create", "cluster")) == 1  # Q15
+    assert len(world.calls("docker", "run")) == 1
+
+
+def test_delete_then_delete_again(world, capsys):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    assert run("delete") == 0
+    st = world.state()
+    assert st["clusters"] == {} and "kind-registry" not in st["containers"]
+    capsys.readouterr()
+    assert run("delete") == 0
+    out = capsys.readouterr().out
+    assert "Kind cluster 'kind-gpu-sim' does not exist. Skipping delete." in out
+    assert "No running container named 'kind-registry' to stop." in out
+    assert "No container named 'kind-registry' to remove." in out
+    assert not (world.cwd / ".kgs" / "kind-gpu-sim").exists()
+
+
+def test_load_docker_and_podman(world):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    assert run("load", "--image-name=myimg:1") == 0
+    assert world.calls("kind", "load", "docker-image") == [["load", "docker-image", "myimg:1", "--name",
+                                                             "kind-gpu-sim"]]
+    assert run("load", "--image-name", "myimg:2", "--runtime", "podman") == 0
+    saves = world.calls("podman", "save")
+    assert saves and saves[0][1] == "myimg:2"
+    archive = saves[0][saves[0].index("-o") + 1]
+    assert archive != "/tmp/image.tar" and not os.path.exists(archive)  # Q9: private, removed
+    assert world.calls("kind", "load", "image-archive")[0][2] == archive
+
+
+def test_load_requires_image(world, capsys):
+    assert run("load") == 1
+    assert "--image-name" in capsys.readouterr().err
+
+
+def test_usage_and_bad_verbs(world, capsys):
+    assert run() == 1
+    assert "Usage:" in capsys.readouterr().err
+    with pytest.raises(SystemExit) as e:
+        run("frobnicate")
+    assert e.value.code == 1
+    assert run("create", "nvidia", "--dev-root", world.nogpu) == 1
+    assert "Unknown GPU type: nvidia" in capsys.readouterr().err
+    with pytest.raises(SystemExit) as e:
+        run("create", "--no-such-flag")
+    assert e.value.code == 1
+
+
+def test_flags_anywhere_both_forms(world):
+    # Q1: flags before the verb, `=` and space forms; gpu type stays positional
+    assert run("--cluster-name=foo", "create", "--registry-port", "5001", "rocm", "--dev-root", world.nogpu) == 0
+    st = world.state()
+    assert "foo" in st["clusters"]
+    assert "127.0.0.1:5001:5000" in st["containers"]["kind-registry"]["args"]
+    cm = st["clusters"]["foo"]["objects"][0]
+    assert 'host: "localhost:5001"' in cm["data"]["localRegistryHosting.v1"]
+    assert (world.cwd / ".kgs" / "foo" / "certs.d" / "localhost:5001" / "hosts.toml").exists()
+    assert all(a[1] == "kind-foo" for a in world.calls("kubectl"))
+
+
+def test_plugin_not_ready_rolls_back(world, monkeypatch, capsys):
+    monkeypatch.setenv("KGS_FAKE_FAIL", "plugin-ready")
+    assert run("create", "--dev-root", world.nogpu) == 1
+    assert "ERROR: ROCm plugin pods not ready in time" in capsys.readouterr().err
+    assert world.state()["clusters"] == {}
+    assert run("create", "--dev-root", world.nogpu, "--keep-on-fail") == 1
+    assert "kind-gpu-sim" in world.state()["clusters"]
+
+
+def test_kind_create_failure_exit_1(world, monkeypatch, capsys):
+    monkeypatch.setenv("KGS_FAKE_FAIL", "kind-create")
+    assert run("create", "--dev-root", world.nogpu) == 1
+    assert "failed to create cluster" in capsys.readouterr().err
+
+
+def test_podman_runtime(world):
+    assert run("create", "--runtime", "podman", "--dev-root", world.nogpu) == 0
+    build = [e for e in world.log() if e["tool"] == "podman" and e["argv"][0] == "build"][0]
+    assert build["env"]["KIND_EXPERIMENTAL_PROVIDER"] == "podman"
+    assert build["env"]["BUILDAH_FORMAT"] == "docker"
+    ds = world.state()["clusters"]["kind-gpu-sim"]["objects"][1]
+    assert ds["spec"]["template"]["spec"]["containers"][0]["image"] == "localhost/amdgpu-dp:dev"
+    assert world.calls("kind", "load", "image-archive")
+    assert world.calls("podman", "push") == []
+
+
+def test_docker_preferred_when_both_present(world):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    assert world.calls("docker", "run") and not world.calls("podman", "run")  # Q14
+
+
+def test_fake_mode_plugin(world):
+    assert run("create", "--fake-gpus", "3", "--fake-mode", "plugin") == 0
+    assert world.kubectl_calls("patch") == []
+    nodes = world.state()["clusters"]["kind-gpu-sim"]["nodes"]
+    assert nodes["kind-gpu-sim-worker"]["allocatable"] == {"amd.com/gpu": "3"}
+    ds = world.state()["clusters"]["kind-gpu-sim"]["objects"][1]
+    env = {e["name"]: e.get("value") for e in ds["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env["KGS_FAKE_GPUS"] == "3"
+
+
+def test_dry_run_executes_nothing(world, capsys):
+    assert run("create", "--dry-run", "--dev-root", world.nogpu) == 0
+    assert world.log() == []
+    err = capsys.readouterr().err
+    assert "kind create cluster --name kind-gpu-sim" in err
+    assert not (world.cwd / "kind-config.yaml").exists()
+
+
+def test_status(world, capsys):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    capsys.readouterr()
+    assert run("status", "--json") == 0
+    info = json.loads(capsys.readouterr().out)
+    assert info["exists"] and info["allocatable"] == {"kind-gpu-sim-worker": 2, "kind-gpu-sim-worker2": 2}
+
+
+def test_bench_e2e(world, tmp_path, capsys):
+    rc = run("bench", "--dev-root", world.nogpu, "--timings-json", str(tmp_path / "e2e.json"))
+    assert rc == 0
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith('{"metric"')]
+    summary = json.loads(lines[-1])
+    assert summary["metric"] == "cluster-create->GPU-pod-Running" and summary["value"] > 0
+    t = json.loads((tmp_path / "e2e.json").read_text())
+    assert [p["phase"] for p in t["phases"]][-4:] == ["pod-apply", "pod-running", "pod-ready", "pod-logs"]
+    assert t["pod_result"]["mode"] == "fake"
+    pod = [o for o in world.log() if o["tool"] == "kubectl" and "apply" in o["argv"] and o["stdin"]
+           and "kind: Pod" in o["stdin"]]
+    doc = yaml.safe_load(pod[0]["stdin"])
+    assert doc["metadata"]["name"] == "gpu-rocm-test"
+    assert doc["spec"]["containers"][0]["name"] == "gpu-sim"
+    assert doc["spec"]["containers"][0]["resources"]["limits"] == {"amd.com/gpu": 1}
+    assert world.state()["clusters"] == {}  # bench deletes unless --keep
+
+
+def test_shell_wrapper_is_executable():
+    p = os.path.join(os.path.dirname(os.path.dirname(__file__)), "kind-gpu-sim.sh")
+    assert os.access(p, os.X_OK)
