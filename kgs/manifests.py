@@ -29,9 +29,16 @@ class _Dumper(yaml.SafeDumper):
         return True
 
 
+_RESOLVER = yaml.resolver.Resolver()
+
+
 def _str_presenter(dumper, data):
     if "\n" in data:
         return dumper.represent_scalar("tag:yaml.org,2002:str", data, style="|")
+    # strings that would read back as bool/int/null ("true", "5000", "") get
+    # double quotes -- the repo's yamllint style (quote-type: double)
+    if data == "" or _RESOLVER.resolve(yaml.ScalarNode, data, (True, False)) != "tag:yaml.org,2002:str":
+        return dumper.represent_scalar("tag:yaml.org,2002:str", data, style='"')
     return dumper.represent_scalar("tag:yaml.org,2002:str", data)
 
 
