@@ -1,0 +1,101 @@
+"""Pod-manifest layout contract (pods/*.yaml) and renderer round-trips."""
+import glob
+import os
+
+import yaml
+
+from kgs import config as C
+from kgs import manifests
+
+PODS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "pods")
+
+
+def _load(name):
+    with open(os.path.join(PODS, name)) as f:
+        return yaml.safe_load(f)
+
+
+def test_every_pod_follows_reference_layout():
+    files = sorted(glob.glob(os.path.join(PODS, "*.yaml")))
+    assert len(files) >= 5
+    for f in files:
+        doc = yaml.safe_load(open(f))
+        assert doc["kind"] == "Pod" and doc["apiVersion"] == "v1", f
+        spec = doc["spec"]
+        assert spec["nodeSelector"] == {"hardware-type": "gpu"}, f
+        assert spec["tolerations"] == [{"key": "gpu", "operator": "Equal", "value": "true",
+                                        "effect": "NoSchedule"}], f  # value is a string (Q12)
+        ctr = spec["containers"][0]
+        assert "amd.com/gpu" in ctr["resources"]["limits"], f
+        assert "nvidia.com/gpu" not in str(doc)
+
+
+def test_gpu_test_pod_identity():
+    doc = _load("rocm-gpu-test-pod.yaml")
+    assert doc["metadata"]["name"] == "gpu-rocm-test"
+    assert doc["spec"]["containers"][0]["name"] == "gpu-sim"
+    assert doc["spec"]["containers"][0]["resources"]["limits"] == {"amd.com/gpu": 1}
+    assert doc == manifests.gpu_test_pod("localhost:5000/kgs-rocm-test:dev", gpus=1)
+
+
+def test_eight_gpu_pod():
+    doc = _load("rocm-gpu-test-8gpu-pod.yaml")
+    assert doc["spec"]["containers"][0]["resources"]["limits"] == {"amd.com/gpu": 8}
+    assert doc == manifests.gpu_test_pod("localhost:5000/kgs-rocm-test:dev", gpus=8, name="gpu-rocm-test-8")
+    vols = {v["name"]: v for v in doc["spec"]["volumes"]}
+    assert vols["dshm"]["emptyDir"]["medium"] == "Memory"
+
+
+def test_vllm_pod():
+    doc = _load("vllm-rocm-pod.yaml")
+    ctr = doc["spec"]["containers"][0]
+    args = " ".join(ctr["args"])
+    assert "Meta-Llama-3-8B" in args and "--dtype=bfloat16" in args and "--tensor-parallel-size=1" in args
+    assert ctr["resources"]["limits"] == {"amd.com/gpu": 1}
+    assert ctr["securityContext"]["privileged"] is True
+    assert doc["spec"]["restartPolicy"] == "Never"
+    assert {"containerPort": 8000} in ctr["ports"]
+
+
+def test_daemonset_render():
+    ds = manifests.plugin_daemonset("img:dev")
+    assert ds["metadata"]["name"] == C.PLUGIN_DS_NAME
+    ctr = ds["spec"]["template"]["spec"]["containers"][0]
+    assert ctr["readinessProbe"]["exec"]["command"] == ["test", "-f", "/tmp/kgs-dp-ready"]
+    env = {e["name"] for e in ctr["env"]}
+    assert "NODE_NAME" in env and "KGS_FAKE_GPUS" not in env
+    ds2 = manifests.plugin_daemonset("img:dev", fake_gpus=2)
+    env2 = {e["name"]: e.get("value") for e in ds2["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert env2["KGS_FAKE_GPUS"] == "2"
+
+
+def test_yaml_quoting_and_no_anchors():
+    text = manifests.dump(manifests.kind_config([{"kfd": True, "render_minors": [128]}] * 2, "/c", "/p"))
+    assert "&id" not in text and "*id" not in text
+    assert manifests.dump({"v": "true"}).strip() == 'v: "true"'
+    assert manifests.dump({"v": ""}).strip() == 'v: ""'
+    assert manifests.dump({"v": "gpu"}).strip() == "v: gpu"
+
+
+def test_kind_config_roundtrip():
+    cfg = manifests.kind_config([{"kfd": True, "render_minors": [128, 136]}, {"kfd": False}], "/certs", "/p.json",
+                                kind_node_image="kindest/node:v1.32.0")
+    back = yaml.safe_load(manifests.dump(cfg))
+    assert back == cfg
+    w1 = back["nodes"][1]
+    assert {"hostPath": "/dev/kfd", "containerPath": "/dev/kfd"} in w1["extraMounts"]
+    assert all(n["image"] == "kindest/node:v1.32.0" for n in back["nodes"])
+
+
+def test_partition_plan():
+    from kgs.cluster import plan_partitions
+
+    class G:
+        def __init__(self, i, numa):
+            self.render_minor, self.numa_node, self.index = 128 + 8 * i, numa, i
+
+    gpus = [G(i, i // 4) for i in range(8)]
+    assert plan_partitions(gpus, 2, "all-on-first") == [[128 + 8 * i for i in range(8)], []]
+    assert plan_partitions(gpus, 2, "split") == [[128, 136, 144, 152], [160, 168, 176, 184]]
+    assert plan_partitions(gpus, 3, "split") == [[128, 136, 144], [152, 160, 168], [176, 184]]
+    assert plan_partitions([], 2, "split") == [[], []]

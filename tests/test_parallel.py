@@ -1,0 +1,119 @@
+"""Distributed paths on CPU: gloo, world_size 2 (the RCCL code paths are the
+same torch.distributed calls; the GPU box only has one GPU)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, fn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        q.put((rank, fn(rank, world)))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def _spawn(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    return res
+
+
+def _init_and_reduce(rank, world):
+    from kgs.parallel import dist as kdist
+
+    ctx = kdist.init_from_env(expected_world=world, device_type="cpu")
+    assert ctx.backend == "gloo" and ctx.world_size == world and ctx.rank == rank
+    m = kdist.max_over_ranks(ctx, float(rank * 10))
+    g = kdist.all_gather_object(ctx, {"r": rank})
+    kdist.barrier(ctx)
+    return (m, [x["r"] for x in g])
+
+
+def test_init_from_env_gloo():
+    res = _spawn(_init_and_reduce)
+    assert res[0] == (10.0, [0, 1]) and res[1] == (10.0, [0, 1])
+
+
+def _sweep(rank, world):
+    from kgs.parallel import dist as kdist
+    from kgs.parallel.allreduce import allreduce_sweep
+
+    kdist.init_from_env(device_type="cpu")
+    pts = allreduce_sweep([1024, 1 << 16], iters=3, warmup=1, device=torch.device("cpu"))
+    return [(p.bytes, p.correct, p.busbw_gbs > 0, round(p.busbw_gbs / p.algbw_gbs, 3)) for p in pts]
+
+
+def test_allreduce_sweep_gloo():
+    res = _spawn(_sweep)
+    assert res[0] == res[1] or all(a[:3] == b[:3] for a, b in zip(res[0], res[1]))
+    for nbytes, ok, pos, ratio in res[0]:
+        assert ok and pos and ratio == 1.0  # 2(n-1)/n = 1 at n=2
+
+
+def _bucketer(rank, world):
+    from kgs.parallel import dist as kdist
+    from kgs.parallel.allreduce import GradBucketer
+
+    kdist.init_from_env(device_type="cpu")
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.ReLU(), torch.nn.Linear(32, 4))
+    b = GradBucketer(model.parameters(), bucket_mb=0.001)  # tiny buckets -> several buckets
+    nb = len(b.buckets)
+    x = torch.randn(8, 16) * (rank + 1)
+    model(x).pow(2).sum().backward()
+    b.wait()
+    grads = [p.grad.clone() for p in model.parameters()]
+    # reference: average of both ranks' local grads, computed here via all_gather
+    b.remove()
+    for p in model.parameters():
+        p.grad = None
+    model(x).pow(2).sum().backward()
+    local = [p.grad.clone() for p in model.parameters()]
+    ref = []
+    for t in local:
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        ref.append(sum(parts) / world)
+    return nb, all(torch.allclose(g, r, atol=1e-5) for g, r in zip(grads, ref))
+
+
+def test_grad_bucketer_matches_average():
+    res = _spawn(_bucketer)
+    for nb, ok in res.values():
+        assert nb >= 2 and ok
+
+
+def test_single_process_context():
+    from kgs.parallel import dist as kdist
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        os.environ.pop(k, None)
+    ctx = kdist.init_from_env(device_type="cpu")
+    assert not ctx.distributed and ctx.group is None
+    assert kdist.max_over_ranks(ctx, 3.5) == 3.5
+    with pytest.raises(SystemExit):
+        kdist.init_from_env(expected_world=2, device_type="cpu")
