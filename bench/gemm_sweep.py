@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/gemm_sweep.json")
+    ap.add_argument("--variants", default="auto", help="comma list of kgs variants: auto,fast,w4,generic")
     a = ap.parse_args()
     res = []
     for s in a.shapes.split(","):
@@ -42,26 +43,26 @@ def main():
         B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         C2 = torch.empty_like(C)
-        ours = lambda: gemm_nt(A, B, out=C)  # noqa: E731
-        ref = lambda: torch.matmul(A, B.T, out=C2)  # noqa: E731
-        for f in (ours, ref):
+        fns = {f"kgs_{v}": (lambda v=v: gemm_nt(A, B, out=C, variant=v)) for v in a.variants.split(",")}
+        fns["hipblaslt"] = lambda: torch.matmul(A, B.T, out=C2)
+        for f in fns.values():
             for _ in range(3):
                 f()
         torch.cuda.synchronize()
-        t_ours, t_ref = [], []
-        for _ in range(a.rounds):
-            t_ours.append(time_fn(ours, a.iters))
-            t_ref.append(time_fn(ref, a.iters))
-        err = ((C.float() - C2.float()).abs().max() / C2.float().abs().max()).item()
+        times = {k: [] for k in fns}
+        for _ in range(a.rounds):  # interleaved rounds in one process
+            for k, f in fns.items():
+                times[k].append(time_fn(f, a.iters))
+        errs = {}
+        for v in a.variants.split(","):
+            gemm_nt(A, B, out=C, variant=v)
+            errs[v] = ((C.float() - C2.float()).abs().max() / C2.float().abs().max()).item()
         fl = 2.0 * M * N * K
-        r = {
-            "shape": [M, N, K],
-            "kgs_tflops_median": round(fl / (sorted(t_ours)[len(t_ours) // 2] * 1e-3) / 1e12, 1),
-            "kgs_tflops_best": round(fl / (min(t_ours) * 1e-3) / 1e12, 1),
-            "hipblaslt_tflops_median": round(fl / (sorted(t_ref)[len(t_ref) // 2] * 1e-3) / 1e12, 1),
-            "hipblaslt_tflops_best": round(fl / (min(t_ref) * 1e-3) / 1e12, 1),
-            "rel_err_vs_hipblaslt": err,
-        }
+        r = {"shape": [M, N, K]}
+        for k, ts in times.items():
+            r[f"{k}_tflops_median"] = round(fl / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e12, 1)
+            r[f"{k}_tflops_best"] = round(fl / (min(ts) * 1e-3) / 1e12, 1)
+        r["rel_err_vs_hipblaslt"] = errs
         print(json.dumps(r), flush=True)
         res.append(r)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

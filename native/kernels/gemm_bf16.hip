@@ -131,41 +131,68 @@ __device__ __forceinline__ void mma_quadrant(Regs& R) {
             R.b[NH][n][s], R.a[i][s], R.acc[MH][i][NH][n], 0, 0, 0);
 }
 
-template <int QP>
+// Two schedules (template S):
+//  S=0  quadrants (0,0)(0,1)(1,1)(1,0); stream A0,B0,B1,A1; look-ahead 5;
+//       ds_reads per phase 12/4/8/0; vmcnt(6).
+//  S=1  quadrants (0,0)(0,1)(1,0)(1,1); stream B0,A0,B1,A1; look-ahead 7;
+//       B0 of the NEXT K-tile is read in phase 3 (its last use is now phase 2),
+//       so reads per phase are 8/4/8/4 and no partner MFMA block waits on a
+//       12-read burst; 5 half-tiles stay in flight (vmcnt(10)).
+//       Hazards (half-tile (t,pos) issued at phase 4t+pos-7, every read at
+//       distance 6 from its issue, every slot re-issued 2 phases after its last
+//       read): RAW needs distance >= 6 for vmcnt(10); WAR needs >= 2 with the
+//       one-barrier stagger -- both hold for all four slots.
+template <int QP, int S>
 __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   constexpr int q = QP & 3;
   constexpr int cbuf = QP >> 2;
   const char* buf = c.smem + cbuf * BUF_BYTES;
-  if constexpr (q == 0) {
-    read_a(c, R, buf + P_A0 * HALF_BYTES);
-    read_b<0>(c, R, buf + P_B0 * HALF_BYTES);
-  } else if constexpr (q == 1) {
-    read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
-  } else if constexpr (q == 2) {
-    read_a(c, R, buf + P_A1 * HALF_BYTES);
+  if constexpr ((S & 1) == 0) {
+    if constexpr (q == 0) {
+      read_a(c, R, buf + P_A0 * HALF_BYTES);
+      read_b<0>(c, R, buf + P_B0 * HALF_BYTES);
+    } else if constexpr (q == 1) {
+      read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
+    } else if constexpr (q == 2) {
+      read_a(c, R, buf + P_A1 * HALF_BYTES);
+    }
+  } else {
+    if constexpr (q == 0) read_a(c, R, buf + P_A0 * HALF_BYTES);
+    if constexpr (q == 1) read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
+    if constexpr (q == 2) read_a(c, R, buf + P_A1 * HALF_BYTES);
+    if constexpr (q == 3) read_b<0>(c, R, c.smem + (cbuf ^ 1) * BUF_BYTES + P_B0 * HALF_BYTES);
   }
-  // prefetch half-tile h = 8*it + QP + LOOKAHEAD; stream order A0,B0,B1,A1
-  constexpr int hoff = QP + LOOKAHEAD;
+  // prefetch half-tile h = 8*it + QP + look-ahead
+  constexpr int LA = (S & 1) == 0 ? LOOKAHEAD : 7;
+  constexpr int hoff = QP + LA;
   constexpr int toff = hoff >> 2;
   constexpr int jp = hoff & 3;
-  constexpr int part = jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1;
+  constexpr int part = (S & 1) == 0 ? (jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1)
+                                    : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
   int t = 2 * it + toff;
   t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
   issue<part>(c, toff & 1, t * BK);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  if constexpr ((S & 1) == 0)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
   bar();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_setprio(1);
+  if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
   if constexpr (q == 0) mma_quadrant<0, 0>(R);
   if constexpr (q == 1) mma_quadrant<0, 1>(R);
-  if constexpr (q == 2) mma_quadrant<1, 1>(R);
-  if constexpr (q == 3) mma_quadrant<1, 0>(R);
-  __builtin_amdgcn_s_setprio(0);
+  if constexpr (q == 2) {
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 1>(R); else mma_quadrant<1, 0>(R);
+  }
+  if constexpr (q == 3) {
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 0>(R); else mma_quadrant<1, 1>(R);
+  }
+  if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
   bar();
 }
 
-template <int EPI>
+template <int EPI, int S>
 __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restrict__ A,
                                                    const unsigned short* __restrict__ B,
                                                    unsigned short* __restrict__ C,
@@ -177,10 +204,12 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
   const int wg = xcd_remap(blockIdx.x, nwg);
-  const int per_group = GROUP_M * ntn;
+  // S bits 2-3 select the tile-group height (experiment knob): 8, 4, 16, 2
+  constexpr int GM = ((S >> 2) & 3) == 0 ? GROUP_M : ((S >> 2) & 3) == 1 ? 4 : ((S >> 2) & 3) == 2 ? 16 : 2;
+  const int per_group = GM * ntn;
   const int group = wg / per_group;
-  const int first_m = group * GROUP_M;
-  const int gsz = min(ntm - first_m, GROUP_M);
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
   const int tm = first_m + (wg % per_group) % gsz;
   const int tn = (wg % per_group) / gsz;
 
@@ -220,27 +249,41 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 #pragma unroll
         for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
-  issue<P_A0>(c, 0, 0);
-  issue<P_B0>(c, 0, 0);
-  issue<P_B1>(c, 0, 0);
-  issue<P_A1>(c, 0, 0);
-  issue<P_A0>(c, 1, k1);
-  asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
-  bar();
+  if constexpr ((S & 1) == 0) {
+    // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
+    issue<P_A0>(c, 0, 0);
+    issue<P_B0>(c, 0, 0);
+    issue<P_B1>(c, 0, 0);
+    issue<P_A1>(c, 0, 0);
+    issue<P_A0>(c, 1, k1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
+    bar();
+  } else {
+    // prologue: half-tiles 0..6 = B0 A0 B1 A1 of tile 0, B0 A0 B1 of tile 1
+    issue<P_B0>(c, 0, 0);
+    issue<P_A0>(c, 0, 0);
+    issue<P_B1>(c, 0, 0);
+    issue<P_A1>(c, 0, 0);
+    issue<P_B0>(c, 1, k1);
+    issue<P_A0>(c, 1, k1);
+    issue<P_B1>(c, 1, k1);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B0,A0 of tile 0 landed
+    bar();
+    read_b<0>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
+  }
   if (c.wr == 1) bar();  // stagger: waves 4-7 trail by one barrier
 
   const int iters = c.nt >> 1;
   for (int it = 0; it < iters; ++it) {
-    phase<0>(c, R, it);
-    phase<1>(c, R, it);
-    phase<2>(c, R, it);
-    phase<3>(c, R, it);
-    phase<4>(c, R, it);
-    phase<5>(c, R, it);
-    phase<6>(c, R, it);
-    phase<7>(c, R, it);
+    phase<0, S>(c, R, it);
+    phase<1, S>(c, R, it);
+    phase<2, S>(c, R, it);
+    phase<3, S>(c, R, it);
+    phase<4, S>(c, R, it);
+    phase<5, S>(c, R, it);
+    phase<6, S>(c, R, it);
+    phase<7, S>(c, R, it);
   }
   if (c.wr == 0) bar();  // balance the stagger barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
@@ -274,6 +317,205 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 }
 
 }  // namespace g256
+
+// ---------------------------------------------------------------------------
+// gemm_nt_256w4: 256x256 tile, 4 waves (one per SIMD), each wave 128x128 of C
+// (64 accumulators = 256 AGPRs), BK=32 stages in a 4-deep LDS-DMA ring.
+//
+// One barrier per 64-MFMA K-step. In step t a wave issues the glds for K-tile
+// t+4 (into the stage K-tile t vacated: its fragments are already in
+// registers), ds_reads K-tile t+1's fragments into the second register set and
+// runs the 64 MFMAs of K-tile t, interleaved by sched_group_barrier so the LDS
+// and DMA issue hides in the MFMA gaps. LDS traffic per K-tile is 2/3 of the
+// 8-wave kernel's (each wave reads 128 rows of A and of B instead of 128 + 64).
+// LDS image: 64-byte rows, 16-byte chunk c of row r at c ^ ((4 - (r>>2)) & 3):
+// every ds_read_b128 16-lane group hits 16 distinct bank slots.
+// ---------------------------------------------------------------------------
+namespace g4 {
+
+constexpr int BM = 256, BN = 256, BK = 32, STAGES = 4;
+constexpr int ROWB = BK * 2;                  // 64-byte rows
+constexpr int OPB = 256 * ROWB;               // one operand of one stage: 16 KiB
+constexpr int STAGE_BYTES = 2 * OPB;          // A + B
+constexpr int LDS_BYTES = STAGES * STAGE_BYTES;  // 128 KiB
+constexpr int GROUP_M = 8;
+
+__device__ __forceinline__ int swz(int r) { return (4 - ((r >> 2) & 3)) & 3; }
+
+struct Frags {
+  bf16x8 a[8];      // A fragments; a[i] is refilled with the next K-tile's row block i
+  bf16x8 b[2][8];   // B fragments, double-buffered across K-tiles (static set index)
+  f32x4 acc[8][8];  // 256 accumulator registers, pinned to AGPRs by the asm constraint
+};
+
+struct Ctx {
+  char* smem;
+  const unsigned short* Ag;
+  const unsigned short* Bg;
+  int ga[4], gb[4];  // per-lane glds source offsets (elements) for the 4 row blocks
+  int ro;            // per-lane ds_read byte offset inside a 16-row block
+  int wr, wc, w, nt;
+};
+
+__device__ __forceinline__ const char* a_base(const Ctx& c, int stage) {
+  return c.smem + stage * STAGE_BYTES + c.wr * 128 * ROWB + c.ro;
+}
+__device__ __forceinline__ const char* b_base(const Ctx& c, int stage) {
+  return c.smem + stage * STAGE_BYTES + OPB + c.wc * 128 * ROWB + c.ro;
+}
+
+// One MFMA whose accumulator lives in AGPRs. Issued as asm so the register
+// allocator keeps each of the 64 accumulators in place across the K-loop (the
+// builtin form makes hipcc rotate accumulators through v_accvgpr_{read,write}).
+// Operands come from ds_read (not VALU), so no wait states are needed in front;
+// the only hazard -- an MFMA result read by VALU -- is padded after the loop.
+__device__ __forceinline__ void mfma16(f32x4& acc, const bf16x8& b, const bf16x8& a) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(b), "v"(a));
+}
+
+__device__ __forceinline__ void issue_tile(const Ctx& c, int t, int stage) {
+  t = t < c.nt ? t : c.nt - 1;
+  const int k0 = t * BK;
+  char* dA = c.smem + stage * STAGE_BYTES + c.w * 1024;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) glds16(c.Ag + k0 + c.ga[j], dA + j * 4096);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) glds16(c.Bg + k0 + c.gb[j], dA + OPB + j * 4096);
+}
+
+__device__ __forceinline__ void sync_step() {
+  // s_waitcnt vmcnt(16) lgkmcnt(0): own glds of K-tile t+2 landed, own ds_reads
+  // of K-tile t+1 done. The builtin (not asm) lets hipcc's waitcnt pass see it,
+  // so it does not add a conservative lgkmcnt(0) in front of the next step's
+  // first MFMA (which would also wait for that step's freshly issued reads).
+  __builtin_amdgcn_s_waitcnt(0x4070);
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// K-step t: 8 groups, one per A row block i: {glds of K-tile t+4 (A blocks
+// 0-3, then B blocks 0-3) into the stage K-tile t vacated; ds_read next B[i];
+// 8 MFMAs of row i; ds_read next A[i] into the registers row i just released}.
+template <int SET>
+__device__ __forceinline__ void step(const Ctx& c, Frags& f, int t) {
+  const int nxt = (t + 1) & 3;
+  const char* sa = a_base(c, nxt);
+  const char* sb = b_base(c, nxt);
+  int tl = t + 4;
+  tl = tl < c.nt ? tl : c.nt - 1;  // past the end: re-load the last tile into a dead stage
+  const int k0 = tl * BK;
+  char* dA = c.smem + (t & 3) * STAGE_BYTES + c.w * 1024;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (i < 4)
+      glds16(c.Ag + k0 + c.ga[i], dA + i * 4096);
+    else
+      glds16(c.Bg + k0 + c.gb[i - 4], dA + OPB + (i - 4) * 4096);
+    f.b[SET ^ 1][i] = *(const bf16x8*)(sb + i * 16 * ROWB);
+#pragma unroll
+    for (int n = 0; n < 8; ++n) mfma16(f.acc[i][n], f.b[SET][n], f.a[i]);
+    f.a[i] = *(const bf16x8*)(sa + i * 16 * ROWB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  sync_step();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_256w4(
+    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
+    const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per_group = GROUP_M * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GROUP_M;
+  const int gsz = min(ntm - first_m, GROUP_M);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.w = w;
+  c.wr = w >> 1;
+  c.wc = w & 1;
+  c.nt = K / BK;
+  {
+    // glds j of wave w fills stage rows j*64 + w*16 + lane/4, physical chunk lane&3
+    const int rl = lane >> 2;
+    const int ch = (lane & 3) ^ swz(rl);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int row = j * 64 + w * 16 + rl;
+      c.ga[j] = row * lda + ch * 8;
+      c.gb[j] = row * ldb + ch * 8;
+    }
+    const int fr = lane & 15, fq = lane >> 4;
+    c.ro = fr * ROWB + ((fq ^ swz(fr)) * 16);
+  }
+  Frags f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) f.acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  issue_tile(c, 0, 0);
+  issue_tile(c, 1, 1);
+  issue_tile(c, 2, 2);
+  issue_tile(c, 3, 3);
+  asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // K-tile 0 landed
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  {
+    const char* sa = a_base(c, 0);
+    const char* sb = b_base(c, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f.a[i] = *(const bf16x8*)(sa + i * 16 * ROWB);
+      f.b[0][i] = *(const bf16x8*)(sb + i * 16 * ROWB);
+    }
+  }
+  sync_step();  // K-tile 1 visible, K-tile 0 fragments in registers
+
+  for (int t = 0; t < c.nt; t += 2) {
+    step<0>(c, f, t);
+    step<1>(c, f, t + 1);
+  }
+  // MFMA results -> VALU reads in the epilogue: pad the hazard (asm MFMAs are
+  // invisible to hipcc's hazard recognizer), drain the tail prefetches.
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+    unsigned short* crow = C + (long)row * ldc;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      const int col = tn * BN + c.wc * 128 + n * 16 + fq * 4;
+      f32x4 v = f.acc[i][n];
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EPI != EPI_NONE) {
+        bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+      }
+      uint2 o;
+      o.x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+      o.y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+      *(uint2*)(crow + col) = o;
+    }
+  }
+}
+
+}  // namespace g4
 
 namespace gen {
 
@@ -365,9 +607,37 @@ template <int EPI>
 static hipError_t launch(int variant, const unsigned short* A, const unsigned short* B, unsigned short* C,
                          const unsigned short* bias, int M, int N, int K, int lda, int ldb, int ldc,
                          hipStream_t s) {
+  // S: bit0 schedule (1 = balanced 8/4/8/4 reads, look-ahead 7), bit1 no
+  // s_setprio, bits2-3 GROUP_M (0:8 1:4 2:16 3:2). Production = 7 (measured
+  // best at 4096^3..16384^2x8192 in interleaved A/B, profiles/gemm_tuning.md).
+  const dim3 grid256((M / g256::BM) * (N / g256::BN));
   if (variant == 1) {
-    dim3 grid((M / g256::BM) * (N / g256::BN));
-    hipLaunchKernelGGL(g256::gemm_nt_256<EPI>, grid, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
+                       ldc);
+  } else if (variant >= 4 && variant <= 8) {
+    // tuning experiments (no-epilogue only)
+    if constexpr (EPI == EPI_NONE) {
+      if (variant == 4)  // with s_setprio around the MFMA blocks
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 5>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                           ldb, ldc);
+      if (variant == 5)  // GROUP_M 8
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                           ldb, ldc);
+      if (variant == 6)  // first schedule (12/4/8/0 reads, look-ahead 5), setprio, GROUP_M 8
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 0>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                           ldb, ldc);
+      if (variant == 7)  // GROUP_M 2
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                           ldb, ldc);
+      if (variant == 8)  // GROUP_M 16
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                           ldb, ldc);
+    } else {
+      return hipErrorInvalidValue;
+    }
+  } else if (variant == 3) {
+    dim3 grid((M / g4::BM) * (N / g4::BN));
+    hipLaunchKernelGGL(g4::gemm_nt_256w4<EPI>, grid, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
   } else {
     const int vec_ok = ((lda % 8) == 0 && (ldb % 8) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
     dim3 grid((N + gen::BN - 1) / gen::BN, (M + gen::BM - 1) / gen::BM);
@@ -391,7 +661,8 @@ KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void
   return 1;
 }
 
-// variant: 0 = auto, 1 = force 256x256 pipelined (must be eligible), 2 = force generic.
+// variant: 0 = auto, 1 = force 256x256 8-wave ping-pong, 2 = force generic,
+//          3 = force 256x256 4-wave (both pipelined variants need the same eligibility).
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                 int ldb, int ldc, int epi, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
@@ -402,8 +673,9 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   if (variant == 0) v = fast ? 1 : 2;
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
+  else if (variant >= 3 && variant <= 8) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
   else return KGS_ERR_ARG;
-  if (v == 1 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
+  if (v != 2 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;

