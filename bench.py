@@ -49,20 +49,25 @@ def parse(argv=None):
     ap.add_argument("--no-overlap", action="store_true", help="run the all-reduce after the GEMMs, same stream")
     ap.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt), untimed part")
     ap.add_argument("--verify", action="store_true", help="check one GEMM against fp32 torch before timing")
+    ap.add_argument("--backend", choices=("kgs", "torch"), default="kgs",
+                    help="kgs = hand-written gfx950 kernel (the benchmark); torch = reference / CPU test path")
+    ap.add_argument("--cpu", action="store_true", help="CPU + gloo (tests of the distributed plumbing only)")
     return ap.parse_args(argv)
 
 
 def main(argv=None) -> int:
     args = parse(argv)
     import torch
-    import torch.distributed as dist
-
     from kgs.models.gemm_workload import GemmWorkload
     from kgs.parallel import dist as kdist
 
-    ctx = kdist.init_from_env(expected_world=args.gpus)
+    ctx = kdist.init_from_env(expected_world=args.gpus, device_type="cpu" if args.cpu else None)
     rank, world = ctx.rank, ctx.world_size
     dev = ctx.device
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
 
     wl = GemmWorkload(
         m=args.m,
@@ -74,6 +79,7 @@ def main(argv=None) -> int:
         device=dev,
         group=ctx.group,
         seed=1234 + rank,
+        backend=args.backend,
     )
     if args.verify:
         err = wl.verify()
@@ -84,15 +90,15 @@ def main(argv=None) -> int:
 
     for _ in range(args.warmup):
         wl.step()
-    torch.cuda.synchronize(dev)
+    sync()
     kdist.barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
-    torch.cuda.synchronize(dev)
+    sync()
     kdist.barrier(ctx)
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
 
     elapsed_max = kdist.max_over_ranks(ctx, elapsed)
@@ -133,6 +139,7 @@ def main(argv=None) -> int:
             },
             "per_gpu_tflops": round(per_gpu_tflops, 2),
             "gemm_path": wl.path_name(),
+            "backend": args.backend,
             **extra,
         }
         print(json.dumps(out), flush=True)

@@ -31,9 +31,15 @@ class GemmWorkload:
         self.b = (torch.rand((n, k), generator=gen, device=self.device) * 2 - 1).to(torch.bfloat16)
         self.c = [torch.empty((m, n), dtype=torch.bfloat16, device=self.device) for _ in range(2)]
         self.bucket = None
+        self.cuda = self.device.type == "cuda"
+        if not self.cuda:
+            self.overlap = False  # CPU (gloo) path for tests: no streams
+            if backend == "kgs":
+                raise ValueError("the kgs HIP GEMM needs a GPU; use backend='torch' on CPU")
         if allreduce_bytes > 0:
             self.bucket = torch.rand(allreduce_bytes // 4, generator=gen, device=self.device)
-            self.comm_stream = torch.cuda.Stream(device=self.device)
+            if self.cuda:
+                self.comm_stream = torch.cuda.Stream(device=self.device)
         if backend == "kgs":
             from kgs.ops import gemm_nt
 
@@ -58,6 +64,12 @@ class GemmWorkload:
         dist.all_reduce(self.bucket, group=self.group)
 
     def step(self) -> None:
+        if not self.cuda:
+            for i in range(self.g):
+                self._gemm(i)
+            if self.bucket is not None:
+                self._allreduce()
+            return
         cur = torch.cuda.current_stream(self.device)
         if self.bucket is not None and self.overlap:
             self.comm_stream.wait_stream(cur)

@@ -117,3 +117,37 @@ def test_single_process_context():
     assert kdist.max_over_ranks(ctx, 3.5) == 3.5
     with pytest.raises(SystemExit):
         kdist.init_from_env(expected_world=2, device_type="cpu")
+
+
+def _bench_rank(rank, world):
+    import contextlib
+    import io
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--m", "64", "--n", "64", "--k", "64",
+                         "--allreduce-mb", "0.25", "--backend", "torch", "--cpu"])
+    out = buf.getvalue().strip()
+    return rc, (json.loads(out) if out else None)
+
+
+def test_bench_distributed_plumbing_gloo():
+    """bench.py's multi-rank path (barriers, max-over-ranks, bucket all-reduce,
+    rank-0-only JSON) on 2 CPU ranks; the GPU run uses the same code on RCCL."""
+    res = _spawn(_bench_rank)
+    rc0, j0 = res[0]
+    rc1, j1 = res[1]
+    assert rc0 == 0 and rc1 == 0
+    assert j1 is None  # only rank 0 prints
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in j0
+    assert j0["n_gpus"] == 2 and j0["steps"] == 2 and j0["scaling"] == "weak"
+    assert j0["config"]["parallelism"] == "dp2" and j0["config"]["global_batch"] == 8
+    assert j0["ms_per_step"] > 0 and j0["backend"] == "torch"
+    assert abs(j0["value"] - 2 * j0["per_gpu_tflops"]) <= 0.011  # aggregate = world x per-GPU (rounded)
