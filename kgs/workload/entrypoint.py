@@ -52,6 +52,29 @@ def allocated_gpus() -> list:
         return []
 
 
+def collect_counters(a, env) -> dict:
+    """Run the single-GPU worker (GEMM only) under rocprofv3, one pass per
+    counter set, and return the markdown summary plus the raw directory."""
+    from kgs.utils.profile import COUNTER_SETS, pmc_command, summarize
+
+    worker = [sys.executable, "-m", "kgs.workload.worker", "--gemm-size", str(a.gemm_size), "--gemm-iters", "5",
+              "--skip-allreduce"]
+    env1 = dict(env, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    ok = {}
+    for name, counters in COUNTER_SETS.items():
+        outdir = os.path.join(a.counters_dir, f"pmc_{name}")
+        cmd = pmc_command(worker, outdir, counters, name="gemm")
+        try:
+            r = subprocess.run(cmd, env=env1, capture_output=True, text=True, timeout=a.timeout)
+            ok[name] = r.returncode == 0
+        except (FileNotFoundError, subprocess.TimeoutExpired) as e:
+            ok[name] = f"failed: {e}"
+            break
+    summary = summarize(a.counters_dir, flops=2.0 * a.gemm_size ** 3)
+    print(summary, flush=True)
+    return {"dir": a.counters_dir, "passes": ok}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="kgs-workload")
     ap.add_argument("--pod", action="store_true", help="hold the container after the run (sleep)")
@@ -62,6 +85,9 @@ def main(argv=None) -> int:
     ap.add_argument("--nproc", type=int, default=0, help="override the GPU count")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--timeout", type=int, default=1200)
+    ap.add_argument("--counters", action="store_true",
+                    help="re-run one GPU's GEMM under rocprofv3 (MFMA busy, LDS conflicts, L2 hit) and summarise")
+    ap.add_argument("--counters-dir", default="/tmp/kgs-rocprof")
     a = ap.parse_args(argv)
 
     gpus = allocated_gpus()
@@ -91,6 +117,8 @@ def main(argv=None) -> int:
             else:
                 print(line, flush=True)
         result["worker_rc"] = p.returncode
+        if a.counters and p.returncode == 0:
+            result["counters"] = collect_counters(a, env)
     result["t_end"] = time.time()
     line = json.dumps(result)
     print(line, flush=True)
