@@ -5,9 +5,9 @@
 // Both operands are K-contiguous ("NT", the torch.nn.Linear weight layout), so
 // every MFMA fragment is one 16-byte LDS read.
 //
-// Two kernels:
+// Kernels (variant numbers are the C ABI's `variant` argument):
 //
-//  * gemm_nt_256 -- the hot path (M%256 == N%256 == 0, K%128 == 0).
+//  * gemm_nt_256 -- the hot path (M%256 == N%256 == 0, K%128 == 0), variant 1.
 //      256x256x64 block tile, 512 threads = 8 waves as 2(M) x 4(N), each wave
 //      owns 128x64 of C as 2x2 quadrants of 64x32 (4x2 MFMA 16x16x32 tiles).
 //      A and B K-tiles are split into 128-row halves (A0 A1 B0 B1, 16 KiB each)
@@ -17,26 +17,31 @@
 //      can be restaged independently of the other halves of its K-tile.
 //
 //      K-loop: 8 phases per iteration (2 K-tiles x 4 quadrants). Phase p:
-//         ds_read the quadrant's fragments (12 / 4 / 8 / 0 x ds_read_b128)
-//         issue half-tile h = p + 5 (2 x glds per wave)
-//         s_waitcnt vmcnt(6)            <- 3 half-tiles stay in flight
-//         s_barrier ; lgkmcnt(0) ; setprio(1) ; 16 x MFMA ; setprio(0) ; s_barrier
+//         ds_read the quadrant's fragments (8 / 4 / 8 / 4 x ds_read_b128)
+//         issue one half-tile (2 x glds per wave), 7 half-tiles ahead
+//         s_waitcnt vmcnt(10)           <- 5 half-tiles stay in flight
+//         s_barrier ; lgkmcnt(0) ; 16 x MFMA ; s_barrier
 //      Waves 4-7 run one barrier behind waves 0-3, so on every SIMD one wave's
-//      MFMA block overlaps its partner's LDS-read/DMA-issue block.
-//      Hazard accounting (phase p, half-tile h issued at p-5):
-//        RAW: h retired by the issuing waves' vmcnt(6) in phase h-2 and read at
-//             phase >= h-1 after >= 1 more barrier on every wave;
-//        WAR: a half-tile slot is re-issued >= 2 phases after its last ds_read
-//             (A0: read at 4t/4t+1, reissued at 4t+3), which with the one-barrier
-//             stagger still leaves a barrier between the last read and the DMA.
+//      MFMA block overlaps its partner's LDS-read/DMA-issue block. The RAW/WAR
+//      accounting of both schedules is next to phase<>() below.
 //      LDS image: 128-byte rows, 16-byte chunk c stored at c ^ ((row >> 1) & 7),
 //      which makes every ds_read_b128 16-lane group hit 16 distinct bank slots
-//      (conflict-free); the swizzle is applied to the glds SOURCE address.
-//      Grid: one block per 256x256 tile, XCD-bijective remap then GROUP_M=8
-//      grouped order so the ~32 co-resident tiles of an XCD share A/B panels.
+//      (conflict-free, SQ_LDS_BANK_CONFLICT = 0); the swizzle is applied to the
+//      glds SOURCE address. Grid: one block per 256x256 tile, XCD-bijective
+//      remap, then GROUP_M=4 grouped order so the 32 co-resident tiles of an
+//      XCD form a 4x8 patch sharing A/B panels (L2 hit 81 % = 1 - 12/64).
+//      Template S selects schedule knobs; variants 4-9 and 11 are the measured
+//      alternatives and timing probes (profiles/gemm_tuning.md).
 //
-//  * gemm_nt_generic -- any shape/stride (bounds-checked, register staged,
-//      128x128x32 tile). Used for ragged shapes and as the test oracle's twin.
+//  * gemm_nt_256p32 (variant 10) -- 32-MFMA phases (half the barriers) with a
+//      160 KiB 10-slot ring; correct but 10 % slower (kept as a measured
+//      negative result: its trailing waves issue 8 glds per phase).
+//
+//  * gemm_nt_256w4 (variant 3) -- 4 waves x 128x128 with AGPR-pinned asm MFMAs;
+//      correct, ~15 % slower (LDS-DMA issue inside the MFMA stream).
+//
+//  * gemm_nt_generic (variant 2) -- any shape/stride (bounds-checked, register
+//      staged, 128x128x32 tile). Used for ragged shapes and as the tests' twin.
 //
 // C ABI: kgs_gemm_bf16_nt(...) (bottom of file), loaded from Python via ctypes
 // (kgs/ops/_lib.py) and from the C++ benches.
@@ -98,7 +103,8 @@ __device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
 }
 
 // Read the 4 m-tiles x 2 k-subs of A for this wave from half-tile `part`.
-__device__ __forceinline__ void read_a(const Ctx& c, Regs& R, const char* half) {
+template <class CtxT>
+__device__ __forceinline__ void read_a(const CtxT& c, Regs& R, const char* half) {
   const char* p = half + c.wr * 64 * 128;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -107,8 +113,8 @@ __device__ __forceinline__ void read_a(const Ctx& c, Regs& R, const char* half) 
   }
 }
 
-template <int NH>
-__device__ __forceinline__ void read_b(const Ctx& c, Regs& R, const char* half) {
+template <int NH, class CtxT>
+__device__ __forceinline__ void read_b(const CtxT& c, Regs& R, const char* half) {
   const char* p = half + c.wc * 32 * 128;
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
@@ -180,6 +186,12 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
+  if constexpr (S & 16) {  // timing experiment only: twice the MFMAs per phase (wrong results)
+    if constexpr (q == 0) mma_quadrant<0, 0>(R);
+    if constexpr (q == 1) mma_quadrant<0, 1>(R);
+    if constexpr (q == 2) mma_quadrant<1, 0>(R);
+    if constexpr (q == 3) mma_quadrant<1, 1>(R);
+  }
   if constexpr (q == 0) mma_quadrant<0, 0>(R);
   if constexpr (q == 1) mma_quadrant<0, 1>(R);
   if constexpr (q == 2) {
@@ -215,8 +227,9 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 
   Ctx c;
   c.smem = smem;
-  c.Ag = A + (long)tm * BM * lda;
-  c.Bg = B + (long)tn * BN * ldb;
+  // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
+  c.Ag = A + (long)((S & 32) ? 0 : tm) * BM * lda;
+  c.Bg = B + (long)((S & 32) ? 0 : tn) * BN * ldb;
   c.a_half = 128L * lda;
   c.b_half = 128L * ldb;
   c.w = w;
@@ -317,6 +330,199 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 }
 
 }  // namespace g256
+
+// ---------------------------------------------------------------------------
+// gemm_nt_256p32: the ping-pong with 32-MFMA blocks (half the barriers of g256).
+//
+// Same block tile, wave layout, fragments and LDS image as g256, but a phase is
+// a whole m-half x both n-halves (32 MFMAs per wave) and a K-tile takes two
+// phases: X(t) = m-half 0 (reads A0, B0, B1), Y(t) = m-half 1 (reads A1).
+// Barrier overhead per MFMA halves; the price is LDS: a 32-MFMA phase consumes
+// 32 KiB, so the half-tile ring grows to 10 slots (160 KiB, the whole LDS) and
+// only the trailing wave group (waves 4-7) issues the LDS-DMA -- a slot may
+// then be refilled one phase after its last read instead of two.
+// Half-tile h = 4t + pos (pos: A0, B0, B1, A1) lives in slot h % 10; phase P
+// (X(t) = 2t, Y(t) = 2t+1) issues h = 2P+8 and 2P+9 (4 glds each per trailing
+// wave) and waits vmcnt(16) (two phases of DMA in flight).
+//   RAW: every half-tile is read >= 3 phases after its issue (vmcnt(16) in
+//        phase p retires everything issued up to p-2);
+//   WAR: h+10 is issued >= 1 phase after h's last read, by the trailing group,
+//        whose issue point (after its barrier 2p) follows every read of phase
+//        p-1 on both groups.
+// ---------------------------------------------------------------------------
+namespace g32 {
+
+using g256::BM;
+using g256::BN;
+using g256::BK;
+using g256::HALF_BYTES;
+constexpr int SLOTS = 10;
+constexpr int LDS_BYTES = SLOTS * HALF_BYTES;  // 160 KiB
+constexpr int GM = 4;
+
+struct Ctx {
+  char* smem;
+  const unsigned short* Ag;
+  const unsigned short* Bg;
+  long a_half, b_half;
+  int offA[4], offB[4];  // trailing-wave glds source offsets (elements), 4 x 8 rows
+  int ro0, ro1;
+  int wr, wc, w, nt;
+};
+
+__device__ __forceinline__ const char* slot_ptr(const Ctx& c, int h) {
+  return c.smem + (h % SLOTS) * HALF_BYTES;
+}
+
+// pos 0 A0, 1 B0, 2 B1, 3 A1 ; issued by waves 4-7 only (4 x glds of 8 rows each)
+template <int POS>
+__device__ __forceinline__ void issue_half(const Ctx& c, int h) {
+  int t = h >> 2;
+  t = t < c.nt ? t : c.nt - 1;  // past the end: reload the last tile into a dead slot
+  const unsigned short* src;
+  const int* off;
+  if constexpr (POS == 0 || POS == 3) {
+    src = c.Ag + (POS == 3 ? c.a_half : 0) + t * BK;
+    off = c.offA;
+  } else {
+    src = c.Bg + (POS == 2 ? c.b_half : 0) + t * BK;
+    off = c.offB;
+  }
+  char* dst = c.smem + (h % SLOTS) * HALF_BYTES + (c.w - 4) * 4096;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) glds16(src + off[j], dst + j * 1024);
+}
+
+template <int Y>
+__device__ __forceinline__ void phase(const Ctx& c, g256::Regs& R, int t) {
+  const int h0 = 4 * t;
+  if constexpr (Y == 0) {
+    g256::read_a(c, R, slot_ptr(c, h0 + 0));
+    g256::read_b<0>(c, R, slot_ptr(c, h0 + 1));
+    g256::read_b<1>(c, R, slot_ptr(c, h0 + 2));
+  } else {
+    g256::read_a(c, R, slot_ptr(c, h0 + 3));
+  }
+  if (c.wr == 1) {
+    if constexpr (Y == 0) {
+      issue_half<0>(c, h0 + 8);
+      issue_half<1>(c, h0 + 9);
+    } else {
+      issue_half<2>(c, h0 + 10);
+      issue_half<3>(c, h0 + 11);
+    }
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+  g256::bar();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  g256::mma_quadrant<Y, 0>(R);
+  g256::mma_quadrant<Y, 1>(R);
+  g256::bar();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_256p32(const unsigned short* __restrict__ A,
+                                                      const unsigned short* __restrict__ B,
+                                                      unsigned short* __restrict__ C,
+                                                      const unsigned short* __restrict__ bias,
+                                                      int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per_group = GM * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  {
+    // trailing wave b = w-4 fills half-tile rows b*32 + j*8 + lane/8 (j = 0..3)
+    const int b = (w & 3);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = b * 32 + j * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((r >> 1) & 7);
+      c.offA[j] = r * lda + ch * 8;
+      c.offB[j] = r * ldb + ch * 8;
+    }
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+  g256::Regs R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (c.wr == 1) {
+    // prologue: half-tiles 0..7 (K-tiles 0 and 1)
+    issue_half<0>(c, 0);
+    issue_half<1>(c, 1);
+    issue_half<2>(c, 2);
+    issue_half<3>(c, 3);
+    issue_half<0>(c, 4);
+    issue_half<1>(c, 5);
+    issue_half<2>(c, 6);
+    issue_half<3>(c, 7);
+    asm volatile("s_waitcnt vmcnt(20)" ::: "memory");  // A0 B0 B1 of K-tile 0 landed
+  }
+  g256::bar();
+  if (c.wr == 1) g256::bar();  // stagger: waves 4-7 trail by one barrier
+
+  for (int t = 0; t < c.nt; ++t) {
+    phase<0>(c, R, t);
+    phase<1>(c, R, t);
+  }
+  if (c.wr == 0) g256::bar();  // balance the stagger barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          f32x4 v = R.acc[mh][i][nh][n];
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI != EPI_NONE) {
+            bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+          }
+          uint2 o;
+          o.x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o.y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+          *(uint2*)(crow + col) = o;
+        }
+    }
+}
+
+}  // namespace g32
 
 // ---------------------------------------------------------------------------
 // gemm_nt_256w4: 256x256 tile, 4 waves (one per SIMD), each wave 128x128 of C
@@ -635,6 +841,21 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     } else {
       return hipErrorInvalidValue;
     }
+  } else if (variant == 11) {
+    // timing probe: production schedule, all blocks load the same (L2-resident) tiles (wrong C)
+    if constexpr (EPI == EPI_NONE)
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 32>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                         ldb, ldc);
+  } else if (variant == 10) {
+    hipLaunchKernelGGL(g32::gemm_nt_256p32<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else if (variant == 9) {
+    // timing probe: production schedule with every MFMA block doubled (wrong C)
+    if constexpr (EPI == EPI_NONE) {
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 16>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                         ldb, ldc);
+    } else {
+      return hipErrorInvalidValue;
+    }
   } else if (variant == 3) {
     dim3 grid((M / g4::BM) * (N / g4::BN));
     hipLaunchKernelGGL(g4::gemm_nt_256w4<EPI>, grid, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
@@ -673,7 +894,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   if (variant == 0) v = fast ? 1 : 2;
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if (variant >= 3 && variant <= 8) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
+  else if (variant >= 3 && variant <= 11) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
   else return KGS_ERR_ARG;
   if (v != 2 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;

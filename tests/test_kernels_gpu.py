@@ -67,7 +67,7 @@ def test_checksum():
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
 
 
-@pytest.mark.parametrize("variant", ["generic", "fast", "w4"])
+@pytest.mark.parametrize("variant", ["generic", "fast", "w4", "p32"])
 def test_gemm_identity_asymmetric(variant):
     from kgs.ops import gemm_nt
 
@@ -87,7 +87,7 @@ def test_gemm_identity_asymmetric(variant):
     "M,N,K",
     [(256, 256, 128), (512, 768, 256), (256, 512, 1024), (1024, 1024, 1024), (768, 256, 384), (2048, 1280, 640)],
 )
-@pytest.mark.parametrize("variant", ["fast", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
 def test_gemm_fast_random(M, N, K, variant):
     from kgs.ops import fast_path_ok, gemm_nt
 
@@ -112,7 +112,7 @@ def test_gemm_generic_ragged(M, N, K):
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
 
 
-@pytest.mark.parametrize("variant", ["fast", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
 def test_gemm_strided_operands(variant):
     from kgs.ops import gemm_nt
 
@@ -125,7 +125,7 @@ def test_gemm_strided_operands(variant):
 
 
 @pytest.mark.parametrize("act", ["bias", "gelu", "relu", "silu"])
-@pytest.mark.parametrize("variant", ["fast", "generic", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "generic", "w4", "p32"])
 def test_gemm_epilogues(act, variant):
     from kgs.ops import gemm_nt
 
@@ -138,7 +138,7 @@ def test_gemm_epilogues(act, variant):
     torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", ["fast", "w4"])
+@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
 def test_gemm_repeatable_large(variant):
     """Race screen: the pipelined kernels must be bitwise deterministic, and the
     two pipelined variants must agree bitwise (same K order per accumulator)."""
