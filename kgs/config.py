@@ -48,6 +48,7 @@ PLUGIN_NAMESPACE = "kube-system"
 PLUGIN_APP_LABEL = "amdgpu-device-plugin"
 PLUGIN_CONTAINER = "amdgpu-dp-ds"
 PLUGIN_READY_TIMEOUT_S = 60
+PLUGIN_METRICS_PORT = 9464  # Prometheus exporter of the plugin (kgs addition)
 KUBELET_DP_DIR = "/var/lib/kubelet/device-plugins"
 
 # --- workload images (in-tree Dockerfiles, images/) ---------------------------

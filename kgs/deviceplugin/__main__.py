@@ -34,6 +34,8 @@ def _args(argv=None):
     ap.add_argument("--health-interval", type=float, default=float(os.environ.get("KGS_HEALTH_INTERVAL", "5")))
     ap.add_argument("--no-amdsmi", action="store_true")
     ap.add_argument("--ready-file", default=os.environ.get("KGS_READY_FILE", "/tmp/kgs-dp-ready"))
+    ap.add_argument("--metrics-port", type=int, default=int(os.environ.get("KGS_METRICS_PORT", "0") or 0),
+                    help="serve Prometheus metrics on this port (0 = off)")
     ap.add_argument("--self-test", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     return ap.parse_args(argv)
@@ -99,6 +101,10 @@ def main(argv=None) -> int:
         return 0
     plug = AmdGpuDevicePlugin(src, a.resource, plugin_dir=a.plugin_dir, health_interval=a.health_interval,
                               ready_file=a.ready_file)
+    if a.metrics_port:
+        from .metrics import serve
+
+        serve(plug, a.metrics_port)
 
     def _term(signum, frame):
         plug.stop()

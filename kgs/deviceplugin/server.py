@@ -186,6 +186,7 @@ class AmdGpuDevicePlugin:
         self._stop = threading.Event()
         self.registrations = 0
         self.allocations = 0
+        self.health_flips = 0
 
     # ---- gRPC service ---------------------------------------------------------
     def GetDevicePluginOptions(self, request, context):
@@ -318,6 +319,7 @@ class AmdGpuDevicePlugin:
     def health_tick(self) -> bool:
         changed = self.source.refresh()
         if changed:
+            self.health_flips += 1
             self.notify()
         return changed
 

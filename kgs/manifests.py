@@ -116,6 +116,7 @@ def plugin_daemonset(image: str, fake_gpus: int = 0, health_interval: float = 5.
     env = [
         {"name": "NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}},
         {"name": "KGS_HEALTH_INTERVAL", "value": str(health_interval)},
+        {"name": "KGS_METRICS_PORT", "value": str(C.PLUGIN_METRICS_PORT)},
         {"name": "PYTHONUNBUFFERED", "value": "1"},
     ]
     if fake_gpus:
@@ -152,6 +153,7 @@ def plugin_daemonset(image: str, fake_gpus: int = 0, health_interval: float = 5.
                         "command": ["python3", "-m", "kgs.deviceplugin"],
                         "env": env,
                         "securityContext": {"privileged": True},
+                        "ports": [{"name": "metrics", "containerPort": C.PLUGIN_METRICS_PORT}],
                         "readinessProbe": {
                             "exec": {"command": ["test", "-f", "/tmp/kgs-dp-ready"]},
                             "periodSeconds": 1,

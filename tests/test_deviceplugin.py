@@ -243,3 +243,21 @@ def test_serve_forever_stops_promptly(short_tmp, host8):
     assert not t.is_alive() and time.monotonic() - t0 < 10
     assert not os.path.exists(plug.socket_path)
     kub.stop()
+
+
+def test_prometheus_metrics(cluster):
+    from prometheus_client import generate_latest
+
+    from kgs.deviceplugin.metrics import make_registry
+
+    kub, plug, src, host = cluster
+    kub.allocate([src.devices()[0].id])
+    remove_gpu_device(host, 136)
+    plug.health_tick()
+    text = generate_latest(make_registry(plug)).decode()
+    assert 'kgs_deviceplugin_devices{health="Healthy"} 7.0' in text
+    assert 'kgs_deviceplugin_devices{health="Unhealthy"} 1.0' in text
+    assert "kgs_deviceplugin_allocations_total 1.0" in text
+    assert "kgs_deviceplugin_registrations_total 1.0" in text
+    assert "kgs_deviceplugin_health_flips_total 1.0" in text
+    assert 'render_minor="136"' in text
