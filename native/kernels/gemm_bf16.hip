@@ -201,7 +201,10 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
     if constexpr ((S & 1) == 0) mma_quadrant<1, 0>(R); else mma_quadrant<1, 1>(R);
   }
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
-  bar();
+  // S bit 7 (with bit 6, lockstep): one barrier per phase. Still race-free: the
+  // slot a phase's DMA overwrites was last read >= 2 phases earlier, i.e. before
+  // the previous phase's barrier on every wave.
+  if constexpr (!(S & 128)) bar();
 }
 
 template <int EPI, int S>
@@ -285,7 +288,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     bar();
     read_b<0>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
   }
-  if (c.wr == 1) bar();  // stagger: waves 4-7 trail by one barrier
+  // stagger: waves 4-7 trail by one barrier (S bit 6: lockstep experiment, no stagger)
+  if (!(S & 64) && c.wr == 1) bar();
 
   const int iters = c.nt >> 1;
   for (int it = 0; it < iters; ++it) {
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     phase<6, S>(c, R, it);
     phase<7, S>(c, R, it);
   }
-  if (c.wr == 0) bar();  // balance the stagger barrier
+  if (!(S & 64) && c.wr == 0) bar();  // balance the stagger barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
 
   // epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n)
@@ -330,6 +334,211 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 }
 
 }  // namespace g256
+
+// ---------------------------------------------------------------------------
+// gemm_nt_256pl: lockstep 8 waves, in-wave software pipelining, ONE barrier per
+// 16-MFMA phase. Both waves of a SIMD run their MFMA blocks concurrently (32
+// MFMAs per SIMD per barrier), and each phase's ds_reads fetch the NEXT
+// quadrant's fragments, so LDS latency hides under the MFMAs instead of behind
+// a partner wave. Two A fragment sets (A0/A1 halves) and two B sets:
+//   phase q0 (A0,B0) reads B1(t)   q1 (A0,B1) reads A1(t)
+//   phase q2 (A1,B0) reads -       q3 (A1,B1) reads A0(t+1), B0(t+1)
+// Stream B0,A0,B1,A1, half-tile h issued at phase h-8, vmcnt(10):
+//   RAW: every half-tile is read >= 6 phases after its issue (5 in flight);
+//   WAR: a slot is refilled >= 1 phase after its last read, and reads of phase
+//        r are retired (lgkmcnt(0)) before the barrier that ends phase r.
+// ---------------------------------------------------------------------------
+namespace gpl {
+
+using g256::BM;
+using g256::BN;
+using g256::BK;
+using g256::HALF_BYTES;
+using g256::BUF_BYTES;
+using g256::LDS_BYTES;
+using g256::P_A0;
+using g256::P_A1;
+using g256::P_B0;
+using g256::P_B1;
+constexpr int GM = 4;
+
+struct Regs {
+  bf16x8 a[2][4][2];      // [A half][m-tile][k-sub]
+  bf16x8 b[2][2][2];      // [B half][n-tile][k-sub]
+  f32x4 acc[2][4][2][2];  // [m-half][m-tile][n-half][n-tile]
+};
+
+template <int AH>
+__device__ __forceinline__ void read_a(const g256::Ctx& c, Regs& R, const char* half) {
+  const char* p = half + c.wr * 64 * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    R.a[AH][i][0] = *(const bf16x8*)(p + i * 16 * 128 + c.ro0);
+    R.a[AH][i][1] = *(const bf16x8*)(p + i * 16 * 128 + c.ro1);
+  }
+}
+
+template <int BH>
+__device__ __forceinline__ void read_b(const g256::Ctx& c, Regs& R, const char* half) {
+  const char* p = half + c.wc * 32 * 128;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    R.b[BH][n][0] = *(const bf16x8*)(p + n * 16 * 128 + c.ro0);
+    R.b[BH][n][1] = *(const bf16x8*)(p + n * 16 * 128 + c.ro1);
+  }
+}
+
+template <int MH, int NH>
+__device__ __forceinline__ void mma(Regs& R) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        R.acc[MH][i][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(R.b[NH][n][s], R.a[MH][i][s],
+                                                                        R.acc[MH][i][NH][n], 0, 0, 0);
+}
+
+template <int QP>
+__device__ __forceinline__ void phase(const g256::Ctx& c, Regs& R, int it) {
+  constexpr int q = QP & 3;
+  constexpr int cbuf = QP >> 2;
+  const char* buf = c.smem + cbuf * BUF_BYTES;
+  const char* nbuf = c.smem + (cbuf ^ 1) * BUF_BYTES;
+  if constexpr (q == 0) read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
+  if constexpr (q == 1) read_a<1>(c, R, buf + P_A1 * HALF_BYTES);
+  if constexpr (q == 3) {
+    read_a<0>(c, R, nbuf + P_A0 * HALF_BYTES);
+    read_b<0>(c, R, nbuf + P_B0 * HALF_BYTES);
+  }
+  // half-tile h = 8*it + QP + 8; stream B0,A0,B1,A1
+  constexpr int hoff = QP + 8;
+  constexpr int toff = hoff >> 2;
+  constexpr int jp = hoff & 3;
+  constexpr int part = jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1;
+  int t = 2 * it + toff;
+  t = t < c.nt ? t : c.nt - 1;
+  g256::issue<part>(c, toff & 1, t * BK);
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (q == 0) mma<0, 0>(R);
+  if constexpr (q == 1) mma<0, 1>(R);
+  if constexpr (q == 2) mma<1, 0>(R);
+  if constexpr (q == 3) mma<1, 1>(R);
+  __builtin_amdgcn_sched_barrier(0);
+  // vmcnt(10) lgkmcnt(0) as one builtin so hipcc's waitcnt pass sees it
+  __builtin_amdgcn_s_waitcnt(0x0070 | (10 & 15) | ((10 >> 4) << 14));
+  g256::bar();
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_256pl(const unsigned short* __restrict__ A,
+                                                     const unsigned short* __restrict__ B,
+                                                     unsigned short* __restrict__ C,
+                                                     const unsigned short* __restrict__ bias,
+                                                     int M, int N, int K, int lda, int ldb, int ldc) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int per_group = GM * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  g256::Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  {
+    const int r0 = w * 16 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ ((r0 >> 1) & 7);
+    const int c1 = (lane & 7) ^ ((r1 >> 1) & 7);
+    c.offA0 = r0 * lda + c0 * 8;
+    c.offA1 = r1 * lda + c1 * 8;
+    c.offB0 = r0 * ldb + c0 * 8;
+    c.offB1 = r1 * ldb + c1 * 8;
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+  Regs R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: half-tiles 0..7 = K-tiles 0 and 1 (B0 A0 B1 A1 each)
+  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  g256::issue<P_B0>(c, 0, 0);
+  g256::issue<P_A0>(c, 0, 0);
+  g256::issue<P_B1>(c, 0, 0);
+  g256::issue<P_A1>(c, 0, 0);
+  g256::issue<P_B0>(c, 1, k1);
+  g256::issue<P_A0>(c, 1, k1);
+  g256::issue<P_B1>(c, 1, k1);
+  g256::issue<P_A1>(c, 1, k1);
+  asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // B0, A0 of K-tile 0
+  g256::bar();
+  read_a<0>(c, R, smem + P_A0 * HALF_BYTES);
+  read_b<0>(c, R, smem + P_B0 * HALF_BYTES);
+  __builtin_amdgcn_s_waitcnt(0x0070 | (10 & 15) | ((10 >> 4) << 14));  // B1 of K-tile 0; frags in
+  g256::bar();
+
+  const int iters = c.nt >> 1;
+  for (int it = 0; it < iters; ++it) {
+    phase<0>(c, R, it);
+    phase<1>(c, R, it);
+    phase<2>(c, R, it);
+    phase<3>(c, R, it);
+    phase<4>(c, R, it);
+    phase<5>(c, R, it);
+    phase<6>(c, R, it);
+    phase<7>(c, R, it);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          f32x4 v = R.acc[mh][i][nh][n];
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI != EPI_NONE) {
+            bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+          }
+          uint2 o;
+          o.x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o.y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+          *(uint2*)(crow + col) = o;
+        }
+    }
+}
+
+}  // namespace gpl
 
 // ---------------------------------------------------------------------------
 // gemm_nt_256p32: the ping-pong with 32-MFMA blocks (half the barriers of g256).
@@ -846,6 +1055,18 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     if constexpr (EPI == EPI_NONE)
       hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 32>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
                          ldb, ldc);
+  } else if (variant == 14) {
+    hipLaunchKernelGGL(gpl::gemm_nt_256pl<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else if (variant == 12 || variant == 13) {
+    // lockstep experiments: no ping-pong stagger (12), and with one barrier per phase (13)
+    if constexpr (EPI == EPI_NONE) {
+      if (variant == 12)
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K,
+                           lda, ldb, ldc);
+      else
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64 + 128>), grid256, dim3(512), 0, s, A, B, C, bias, M, N,
+                           K, lda, ldb, ldc);
+    }
   } else if (variant == 10) {
     hipLaunchKernelGGL(g32::gemm_nt_256p32<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
   } else if (variant == 9) {
@@ -894,7 +1115,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   if (variant == 0) v = fast ? 1 : 2;
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if (variant >= 3 && variant <= 11) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
+  else if (variant >= 3 && variant <= 14) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
   else return KGS_ERR_ARG;
   if (v != 2 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;
