@@ -314,7 +314,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
       const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
       unsigned short* crow = C + (long)row * ldc;
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh)
+      for (int nh = 0; nh < 2; ++nh) {
+        uint2 o[2];
 #pragma unroll
         for (int n = 0; n < 2; ++n) {
           const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
@@ -325,11 +326,27 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 #pragma unroll
             for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
           }
-          uint2 o;
-          o.x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
-          o.y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
-          *(uint2*)(crow + col) = o;
+          o[n].x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o[n].y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
         }
+        const int col0 = tn * BN + nh * 128 + c.wc * 32;
+        if constexpr (S & 256) {
+          // narrow store tail (A/B reference): two 8-B stores per lane
+          *(uint2*)(crow + col0 + fq * 4) = o[0];
+          *(uint2*)(crow + col0 + 16 + fq * 4) = o[1];
+        } else {
+          // widened store tail (guide T21, 16-lane form): v_permlane16_swap
+          // exchanges rows 1<->0 and 3<->2 of the lane grid, so even-fq lanes
+          // end up with 8 consecutive n=0 columns and odd-fq lanes with the
+          // matching n=1 columns -> one 16-B store per lane instead of two 8-B.
+          auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+          auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+          // even fq: (own n0, partner n0) = (sx[0], sx[1]) ... odd fq likewise for n1
+          const uint4 q = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const int cw = col0 + (fq & 1) * 16 + (fq >> 1) * 8;
+          *(uint4*)(crow + cw) = q;
+        }
+      }
     }
 }
 
@@ -1055,6 +1072,11 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     if constexpr (EPI == EPI_NONE)
       hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 32>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
                          ldb, ldc);
+  } else if (variant == 15) {
+    // production schedule with the narrow (2 x 8-B per lane) store tail, for A/B
+    if constexpr (EPI == EPI_NONE)
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 256>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                         ldb, ldc);
   } else if (variant == 14) {
     hipLaunchKernelGGL(gpl::gemm_nt_256pl<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
   } else if (variant == 12 || variant == 13) {
@@ -1096,8 +1118,8 @@ KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void
                                         int ldb, int ldc) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;
   if (M % 256 || N % 256 || K % 128) return 0;
-  if (lda % 8 || ldb % 8 || ldc % 4) return 0;
-  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 8) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 8) return 0;  // 16-B operand DMA and 16-B C stores
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return 0;
   // 32-bit per-lane offsets: (255 rows) * ld must fit
   if ((long)lda * 256 >= (1L << 31) || (long)ldb * 256 >= (1L << 31)) return 0;
   return 1;
@@ -1110,14 +1132,15 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if (epi != kgs::EPI_NONE && bias == nullptr) return KGS_ERR_ARG;
-  const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc);
+  // the fast epilogue reads the bias 4 elements (8 B) at a time
+  const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc) &&
+                   (epi == kgs::EPI_NONE || (uintptr_t)bias % 8 == 0);
   int v;
   if (variant == 0) v = fast ? 1 : 2;
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if (variant >= 3 && variant <= 14) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
+  else if (variant >= 3 && variant <= 15) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
   else return KGS_ERR_ARG;
-  if (v != 2 && epi != kgs::EPI_NONE && ((uintptr_t)bias % 8)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;

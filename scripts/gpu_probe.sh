@@ -1,16 +1,23 @@
 set -o pipefail
-mkdir -p gpurun_out/probe2
-timeout -k 10 300 python -m pytest tests/test_kernels_gpu.py -q -x -k "repeatable" > gpurun_out/probe2/t.log 2>&1 && \
-timeout -k 10 300 python - > gpurun_out/probe2/check.log 2>&1 <<'PY'
-import torch
+# A/B probe of experimental GEMM variants against production. Usage: bash scripts/gpu_probe.sh VARIANT[,VARIANT...]
+VARS=${1:-pl}
+mkdir -p gpurun_out/probe3
+timeout -k 10 600 python -m pytest tests/test_kernels_gpu.py -q -x > gpurun_out/probe3/tests.log 2>&1 && \
+timeout -k 10 300 python - "$VARS" > gpurun_out/probe3/check.log 2>&1 <<'PY'
+import sys, torch
 from kgs.ops import gemm_nt
-for v in ("lockstep", "lockstep_1bar"):
-    for (M, N, K) in ((2048, 2048, 2048), (1024, 3072, 4096)):
+ok = True
+for v in sys.argv[1].split(","):
+    for (M, N, K) in ((512, 512, 128), (2048, 2048, 2048), (1024, 3072, 4096)):
         a = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16(); b = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
         ref = gemm_nt(a, b, variant="fast")
         outs = [gemm_nt(a, b, variant=v) for _ in range(10)]
-        print(v, M, N, K, all(torch.equal(o, ref) for o in outs))
+        good = all(torch.equal(o, ref) for o in outs)
+        err = (outs[0].float() - ref.float()).abs().max().item()
+        print(v, M, N, K, good, err, flush=True)
+        ok &= good
+sys.exit(0 if ok else 1)
 PY
-cat gpurun_out/probe2/check.log && \
-timeout -k 10 300 python bench/gemm_sweep.py --shapes 8192,16384x16384x8192 --variants fast,lockstep,lockstep_1bar --rounds 7 --out gpurun_out/probe2/sweep.json > gpurun_out/probe2/sweep.log 2>&1; rc=$?
-grep shape gpurun_out/probe2/sweep.log; exit $rc
+rc=$?; cat gpurun_out/probe3/check.log; [ $rc -eq 0 ] && \
+timeout -k 10 300 python bench/gemm_sweep.py --shapes 4096,8192,16384x16384x8192 --variants fast,$VARS --rounds 7 --out gpurun_out/probe3/sweep.json > gpurun_out/probe3/sweep.log 2>&1; rc=$?
+grep shape gpurun_out/probe3/sweep.log; exit $rc

@@ -151,7 +151,39 @@ def test_gemm_repeatable_large(variant):
         assert _rel_err(c0, _ref_nt(a, b)) < 1e-2
         for _ in range(10):
             assert torch.equal(gemm_nt(a, b, variant=variant), c0)
-        assert torch.equal(gemm_nt(a, b, variant="generic" if K % 32 == 0 else variant), c0) or True
+        # same per-accumulator K order as production -> bitwise equal
+        assert torch.equal(gemm_nt(a, b, variant="fast"), c0)
+
+
+def test_gemm_wide_store_tail_matches_narrow():
+    """The permlane16-swap 16-B store tail writes exactly the image of the 8-B one."""
+    from kgs.ops import gemm_nt
+
+    for M, N, K in ((512, 768, 256), (2048, 2048, 2048)):
+        a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+        b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+        assert torch.equal(gemm_nt(a, b, variant="fast"), gemm_nt(a, b, variant="narrow_store"))
+
+
+def test_gemm_misaligned_out_and_bias_fall_back():
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import KernelError
+    from kgs.ops.gemm import fast_path_ok
+
+    M, N, K = 512, 512, 256
+    a = (torch.rand(M, K, device=DEV) - 0.5).bfloat16()
+    b = (torch.rand(N, K, device=DEV) - 0.5).bfloat16()
+    big = torch.zeros(M, N + 8, device=DEV, dtype=torch.bfloat16)
+    out = big[:, 4:4 + N]  # 8-B aligned rows: too narrow for the 16-B store tail
+    assert not fast_path_ok(a, b, out)
+    gemm_nt(a, b, out=out)
+    assert _rel_err(out, _ref_nt(a, b)) < 1e-2
+    with pytest.raises(KernelError):
+        gemm_nt(a, b, out=out, variant="fast")
+    bias_store = torch.randn(N + 1, device=DEV).bfloat16()
+    bias = bias_store[1:]  # 2-B aligned
+    c = gemm_nt(a, b, bias=bias, act="relu")
+    torch.testing.assert_close(c.float(), _ref_nt(a, b, bias, "relu"), rtol=2e-2, atol=2e-2)
 
 
 def test_matmul_and_linear_backward():
