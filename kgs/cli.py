@@ -49,6 +49,9 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
                     help="fake capacity via node-status patch (reference) or via the plugin's fake source")
     ap.add_argument("--registry-bind", default="127.0.0.1")
     ap.add_argument("--kind-node-image", default=None)
+    ap.add_argument("--base-mirror", default=C.BASE_MIRROR,
+                    help="registry prefix for library base images (python, registry); reference: patch_dockerfile")
+    ap.add_argument("--rocm-base-image", default=C.ROCM_BASE_IMAGE, help="PyTorch-ROCm base of the workload image")
     ap.add_argument("--plugin-image", default=None, help="use a prebuilt device-plugin image")
     ap.add_argument("--skip-build", action="store_true")
     ap.add_argument("--ready-timeout", type=int, default=C.PLUGIN_READY_TIMEOUT_S)
@@ -75,6 +78,7 @@ def settings_from(a) -> C.Settings:
         registry_bind=a.registry_bind, kind_node_image=a.kind_node_image, dry_run=a.dry_run,
         keep_on_fail=a.keep_on_fail, skip_build=a.skip_build, timings_json=a.timings_json,
         plugin_image=a.plugin_image, ready_timeout_s=a.ready_timeout, dev_root=a.dev_root,
+        base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image,
     )
 
 

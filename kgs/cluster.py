@@ -165,7 +165,7 @@ class Provisioner:
             return
         rt.cr("run", "-d", "--restart=always", "-p",
               f"{self.s.registry_bind}:{self.s.registry_port}:{C.REGISTRY_INTERNAL_PORT}",
-              "--name", name, self.s.registry_image)
+              "--name", name, self.s.registry_container_image)
 
     def write_node_files(self) -> tuple:
         """certs.d tree + partition file (bind-mounted into the nodes)."""
@@ -233,8 +233,8 @@ class Provisioner:
         tag = f"{self.s.registry_host}/{C.PLUGIN_IMAGE_REPO}:{C.PLUGIN_IMAGE_TAG}"
         self.out(" Building kgs ROCm device plugin image...")
         env = {"BUILDAH_FORMAT": "docker"} if rt.name == "podman" else None
-        rt.cr("build", "-t", tag, "-f", str(REPO_ROOT / "images" / "Dockerfile.deviceplugin"), str(REPO_ROOT),
-              env=env)
+        rt.cr("build", "-t", tag, *self.s.plugin_build_args(),
+              "-f", str(REPO_ROOT / "images" / "Dockerfile.deviceplugin"), str(REPO_ROOT), env=env)
         if rt.name == "docker":
             rt.cr("push", tag)
         else:

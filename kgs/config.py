@@ -10,7 +10,12 @@ from dataclasses import dataclass, field
 
 # --- flag defaults (kind-gpu-sim.sh:4-7) -------------------------------------
 DEFAULT_REGISTRY_PORT = 5000
-REGISTRY_IMAGE = "public.ecr.aws/docker/library/registry:2"
+# Docker-Hub library images are pulled through a public mirror to dodge Docker
+# Hub rate limits -- the reference's patch_dockerfile sed-rewrites FROM lines to
+# this mirror (kind-gpu-sim.sh:144-178, :5); here it is a build argument.
+BASE_MIRROR = "public.ecr.aws/docker/library"
+REGISTRY_IMAGE = f"{BASE_MIRROR}/registry:2"
+ROCM_BASE_IMAGE = "docker.io/rocm/pytorch:latest"
 DEFAULT_CLUSTER_NAME = "kind-gpu-sim"
 DEFAULT_IMAGE_NAME = "not-set"
 
@@ -79,7 +84,9 @@ class Settings:
     fake_gpus: int | None = None         # force the fake path with N per worker
     fake_mode: str = "patch"             # patch (reference) | plugin (kgs fake plugin)
     registry_bind: str = "127.0.0.1"     # Q4: do not publish the registry on all interfaces
-    registry_image: str = REGISTRY_IMAGE
+    registry_image: str | None = None    # None = <base_mirror>/registry:2
+    base_mirror: str = BASE_MIRROR       # C13: registry prefix for library base images
+    rocm_base_image: str = ROCM_BASE_IMAGE
     kind_node_image: str | None = None
     config_file: str = CONFIG_FILE
     dry_run: bool = False
@@ -90,6 +97,19 @@ class Settings:
     ready_timeout_s: int = PLUGIN_READY_TIMEOUT_S
     dev_root: str = "/"                  # host root for /dev and /sys discovery (tests use a fake tree)
     extra: dict = field(default_factory=dict)
+
+    def library_image(self, name: str) -> str:
+        """``name`` (e.g. ``python:3.12-slim``) from the configured library mirror."""
+        return f"{self.base_mirror.rstrip('/')}/{name}"
+
+    @property
+    def registry_container_image(self) -> str:
+        return self.registry_image or self.library_image("registry:2")
+
+    def plugin_build_args(self) -> list[str]:
+        """``--build-arg`` list for images/Dockerfile.deviceplugin."""
+        return ["--build-arg", f"PY_IMAGE={self.library_image('python:3.12-slim')}",
+                "--build-arg", f"BUILD_IMAGE={self.library_image('python:3.12')}"]
 
     @property
     def registry_host(self) -> str:

@@ -13,22 +13,20 @@ from __future__ import annotations
 from . import config as C
 from .cluster import REPO_ROOT
 
-ROCM_BASE = "docker.io/rocm/pytorch:latest"
-SLIM_BASE = "public.ecr.aws/docker/library/python:3.12-slim"
-
 
 def build_images(p, workload: bool = True, plugin: bool = True) -> int:
     rt = p.ensure_runtime()
     p.start_registry()
     if plugin:
         tag = f"{p.s.registry_host}/{C.PLUGIN_IMAGE_REPO}:{C.PLUGIN_IMAGE_TAG}"
-        rt.cr("build", "-t", tag, "-f", str(REPO_ROOT / "images" / "Dockerfile.deviceplugin"), str(REPO_ROOT))
+        rt.cr("build", "-t", tag, *p.s.plugin_build_args(),
+              "-f", str(REPO_ROOT / "images" / "Dockerfile.deviceplugin"), str(REPO_ROOT))
         if rt.name == "docker":
             rt.cr("push", tag)
     if workload:
         if p.topology is None and p.s.fake_gpus is None:
             p.discover()
-        base = SLIM_BASE if p.fake else ROCM_BASE
+        base = p.s.library_image("python:3.12-slim") if p.fake else p.s.rocm_base_image
         tag = f"{p.s.registry_host}/{C.WORKLOAD_IMAGE_REPO}:{C.WORKLOAD_IMAGE_TAG}"
         rt.cr("build", "-t", tag, "--build-arg", f"BASE_IMAGE={base}",
               "--build-arg", f"BUILD_NATIVE={'0' if p.fake else '1'}",

@@ -308,3 +308,20 @@ def test_bench_e2e(world, tmp_path, capsys):
 def test_shell_wrapper_is_executable():
     p = os.path.join(os.path.dirname(os.path.dirname(__file__)), "kind-gpu-sim.sh")
     assert os.access(p, os.X_OK)
+
+
+def test_base_mirror_rewrites_base_images(world):
+    """C13 analog: the reference sed-patches FROM lines to a public mirror
+    (kind-gpu-sim.sh:144-178); kgs passes the mirror as build arguments."""
+    assert run("create", "--dev-root", world.nogpu, "--base-mirror=mirror.example:5001/library") == 0
+    build = world.calls("docker", "build")[0]
+    assert "PY_IMAGE=mirror.example:5001/library/python:3.12-slim" in build
+    assert "BUILD_IMAGE=mirror.example:5001/library/python:3.12" in build
+    reg = world.state()["containers"][C.REGISTRY_NAME]
+    assert reg["image"] == "mirror.example:5001/library/registry:2"
+
+
+def test_default_base_images_use_public_mirror(world):
+    assert run("create", "--dev-root", world.nogpu) == 0
+    build = world.calls("docker", "build")[0]
+    assert f"PY_IMAGE={C.BASE_MIRROR}/python:3.12-slim" in build
