@@ -41,6 +41,19 @@ _SIGS = {
     "kgs_vector_add_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
     "kgs_transpose_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_checksum_bf16": ([_c_void_p, _c_long, _c_void_p, _c_void_p], _c_int),
+    # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)
+    "kgs_ar_signal_bytes": ([], _c_int),
+    "kgs_ar_max_blocks": ([], _c_int),
+    "kgs_ar_max_ranks": ([], _c_int),
+    "kgs_ar_ipc_handle_bytes": ([], _c_int),
+    "kgs_ar_alloc": ([ctypes.c_size_t, _c_int, ctypes.POINTER(_c_void_p)], _c_int),
+    "kgs_ar_free": ([_c_void_p], _c_int),
+    "kgs_ar_ipc_handle": ([_c_void_p, ctypes.c_char_p], _c_int),
+    "kgs_ar_ipc_open": ([ctypes.c_char_p, ctypes.POINTER(_c_void_p)], _c_int),
+    "kgs_ar_ipc_close": ([_c_void_p], _c_int),
+    "kgs_ar_run": ([ctypes.POINTER(_c_void_p), ctypes.POINTER(_c_void_p), _c_int, _c_int, _c_void_p, _c_void_p,
+                    _c_long, _c_long, _c_int, _c_int, ctypes.c_uint, _c_int, ctypes.c_double, _c_void_p, _c_void_p],
+                   _c_int),
 }
 
 

@@ -1,0 +1,119 @@
+"""Peer-to-peer xGMI all-reduce (native/kernels/allreduce_p2p.hip).
+
+GPU tests compare bitwise against the fp32 sum of the ranks' tensors in rank
+order (the kernel sums peers 0..N-1 in f32 on every rank). Two shapes of
+"multi-rank" fit a one-GPU box: N ranks played by one launch in one process (no IPC),
+and N processes sharing the GPU through IPC handles (the real code path).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+torch = pytest.importorskip("torch")
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bare(world, oneshot_max=None):
+    from kgs.parallel.p2p_allreduce import P2PAllReduce
+
+    ar = object.__new__(P2PAllReduce)
+    ar.world = world
+    ar.max_blocks = 128
+    ar.oneshot_max_bytes = oneshot_max if oneshot_max is not None else ((1 << 20) if world <= 4 else (256 << 10))
+    ar._epoch = 0
+    return ar
+
+
+def test_algo_and_grid_selection():
+    ar = _bare(8)
+    assert ar.pick_algo(4096) == "oneshot"
+    assert ar.pick_algo(256 << 10) == "oneshot"
+    assert ar.pick_algo((256 << 10) + 16) == "twoshot"
+    assert _bare(2).pick_algo(8 << 20) == "oneshot"  # two ranks: two-shot saves nothing
+    assert ar.blocks_for(16, "oneshot") == 1
+    assert ar.blocks_for(512 * 16 * 3, "oneshot") == 3
+    assert ar.blocks_for(1 << 30, "twoshot") == 128
+
+
+def test_epoch_never_zero():
+    ar = _bare(2)
+    ar._epoch = 0xFFFFFFFE
+    assert ar._next_epoch() == 0xFFFFFFFF
+    assert ar._next_epoch() == 1  # wraps past 0 (flags start zeroed)
+
+
+def _inputs(world, n, dtype, device):
+    return [((torch.arange(n, device=device, dtype=torch.float32) * (r + 3)) % 61 - 30).to(dtype) / 4
+            for r in range(world)]
+
+
+def _ref(xs):
+    acc = xs[0].float()
+    for x in xs[1:]:
+        acc = acc + x.float()
+    return acc.to(xs[0].dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("algo", ["oneshot", "twoshot"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_local_ranks_bitwise(world, algo, dtype):
+    from kgs.parallel.p2p_allreduce import P2PAllReduce
+
+    ar = P2PAllReduce.local_ranks(world, max_bytes=8 << 20, device="cuda", timeout_s=3.0)
+    try:
+        esz = torch.tensor([], dtype=dtype).element_size()
+        for nbytes in (16, 1008, 4096, (1 << 20) + 48, 8 << 20):
+            xs = _inputs(world, nbytes // esz, dtype, "cuda")
+            for _ in range(2):
+                outs = ar.all_reduce_local(xs, algo=algo)
+                ar.check()  # fail fast on a barrier timeout
+            ref = _ref(xs)
+            for o in outs:
+                assert torch.equal(o, ref), (algo, dtype, nbytes)
+        ar.check()
+    finally:
+        ar.close()
+
+
+@pytest.mark.gpu
+def test_missing_peer_times_out_instead_of_hanging():
+    from kgs.parallel.p2p_allreduce import P2PAllReduce
+
+    ar = P2PAllReduce.local_ranks(2, max_bytes=1 << 20, device="cuda", timeout_s=0.05)
+    try:
+        x = torch.ones(1024, device="cuda")
+        out = torch.empty_like(x)
+        # launch rank 0 only: its barrier can never complete
+        ar._launch(0, x, out, "oneshot", ar._next_epoch(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        with pytest.raises(RuntimeError, match="timed out"):
+            ar.check()
+    finally:
+        ar.close()
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
+def test_ipc_two_processes():
+    """Two processes, IPC-mapped staging buffers (same GPU on a one-GPU box)."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
+           os.path.join(ROOT, "tests", "workers", "p2p_worker.py")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["world"] == 2 and res["ok"], res
