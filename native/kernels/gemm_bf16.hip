@@ -40,8 +40,14 @@
 //  * gemm_nt_256w4 (variant 3) -- 4 waves x 128x128 with AGPR-pinned asm MFMAs;
 //      correct, ~15 % slower (LDS-DMA issue inside the MFMA stream).
 //
+//  * gemm_nt_256<.., S|512> (variant 16, "bounded") -- the same pipeline for any
+//      M, N and K % 8 == 0: operands are read by `buffer_load_dwordx4 ... lds`
+//      through buffer resources that end at the last valid row, so rows past M/N
+//      and K-chunks past K land as zeros; the store tail is predicated. `auto`
+//      uses it whenever the aligned path does not apply.
+//
 //  * gemm_nt_generic (variant 2) -- any shape/stride (bounds-checked, register
-//      staged, 128x128x32 tile). Used for ragged shapes and as the tests' twin.
+//      staged, 128x128x32 tile). Used for odd K / strides and as the tests' twin.
 //
 // C ABI: kgs_gemm_bf16_nt(...) (bottom of file), loaded from Python via ctypes
 // (kgs/ops/_lib.py) and from the C++ benches.
@@ -78,7 +84,15 @@ struct Ctx {
   int ro0, ro1;                    // per-lane ds_read byte offsets for k-sub 0/1
   int wr, wc, w;                   // wave coordinates (wave-uniform)
   int nt;                          // number of K-tiles
+  // bounded mode (S bit 9): operands read through buffer resources whose
+  // num_records ends at the last valid row, so rows >= M (N) load zeros; lanes
+  // whose 16-B chunk starts at k >= K get an out-of-range offset (zeros too).
+  __amdgpu_buffer_rsrc_t ra, rb;
+  int K, kc0, kc1;                 // K and the lane's logical chunk column (elements)
+  int a_half_i, b_half_i;          // 128*lda, 128*ldb as int
 };
+
+constexpr int OOB_OFFSET = 0x7FFFFFF0;  // > every num_records the bounded path builds
 
 __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
@@ -86,9 +100,20 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int PART>
+template <int PART, bool BND = false>
 __device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
   char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048;
+  if constexpr (BND) {
+    constexpr bool isA = PART == P_A0 || PART == P_A1;
+    const int half = PART == P_A1 ? c.a_half_i : PART == P_B1 ? c.b_half_i : 0;
+    const int o0 = (isA ? c.offA0 : c.offB0) + half + k0;
+    const int o1 = (isA ? c.offA1 : c.offB1) + half + k0;
+    const int v0 = k0 + c.kc0 < c.K ? o0 * 2 : OOB_OFFSET;
+    const int v1 = k0 + c.kc1 < c.K ? o1 * 2 : OOB_OFFSET;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? c.ra : c.rb, (KGS_LDS void*)dst, 16, v0, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? c.ra : c.rb, (KGS_LDS void*)(dst + 1024), 16, v1, 0, 0, 0);
+    return;
+  }
   const unsigned short* src;
   int o0, o1;
   if constexpr (PART == P_A0 || PART == P_A1) {
@@ -177,7 +202,7 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
                                     : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
   int t = 2 * it + toff;
   t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
-  issue<part>(c, toff & 1, t * BK);
+  issue<part, (S & 512) != 0>(c, toff & 1, t * BK);
   if constexpr ((S & 1) == 0)
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else
@@ -215,9 +240,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
                                                    int M, int N, int K, int lda, int ldb, int ldc) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
+  constexpr bool BND = (S & 512) != 0;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  const int ntm = BND ? (M + BM - 1) / BM : M / BM, ntn = BND ? (N + BN - 1) / BN : N / BN, nwg = ntm * ntn;
   const int wg = xcd_remap(blockIdx.x, nwg);
   // S bits 2-3 select the tile-group height (experiment knob): 8, 4, 16, 2
   constexpr int GM = ((S >> 2) & 3) == 0 ? GROUP_M : ((S >> 2) & 3) == 1 ? 4 : ((S >> 2) & 3) == 2 ? 16 : 2;
@@ -239,6 +265,15 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   c.wr = w >> 2;
   c.wc = w & 3;
   c.nt = K / BK;
+  if constexpr (BND) {
+    c.nt = (((K + BK - 1) / BK) + 1) & ~1;  // whole K-loop iterations; tail tiles load zeros
+    c.K = K;
+    c.a_half_i = 128 * lda;
+    c.b_half_i = 128 * ldb;
+    const int rows_a = min(M - tm * BM, BM), rows_b = min(N - tn * BN, BN);
+    c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)c.Ag, 0, rows_a * lda * 2, 0x00020000);
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)c.Bg, 0, rows_b * ldb * 2, 0x00020000);
+  }
   {
     // glds j (0/1) of wave w fills half-tile rows w*16 + j*8 + lane/8; lane's
     // physical 16-B chunk is lane&7 and holds logical chunk (lane&7)^f(row).
@@ -249,6 +284,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     c.offA1 = r1 * lda + c1 * 8;
     c.offB0 = r0 * ldb + c0 * 8;
     c.offB1 = r1 * ldb + c1 * 8;
+    c.kc0 = c0 * 8;
+    c.kc1 = c1 * 8;
     // fragment read: row lane&15, logical chunk 4*s + lane/16
     const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
     c.ro0 = fr * 128 + ((fq ^ f) * 16);
@@ -268,22 +305,22 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
   if constexpr ((S & 1) == 0) {
     // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
-    issue<P_A0>(c, 0, 0);
-    issue<P_B0>(c, 0, 0);
-    issue<P_B1>(c, 0, 0);
-    issue<P_A1>(c, 0, 0);
-    issue<P_A0>(c, 1, k1);
+    issue<P_A0, BND>(c, 0, 0);
+    issue<P_B0, BND>(c, 0, 0);
+    issue<P_B1, BND>(c, 0, 0);
+    issue<P_A1, BND>(c, 0, 0);
+    issue<P_A0, BND>(c, 1, k1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
     bar();
   } else {
     // prologue: half-tiles 0..6 = B0 A0 B1 A1 of tile 0, B0 A0 B1 of tile 1
-    issue<P_B0>(c, 0, 0);
-    issue<P_A0>(c, 0, 0);
-    issue<P_B1>(c, 0, 0);
-    issue<P_A1>(c, 0, 0);
-    issue<P_B0>(c, 1, k1);
-    issue<P_A0>(c, 1, k1);
-    issue<P_B1>(c, 1, k1);
+    issue<P_B0, BND>(c, 0, 0);
+    issue<P_A0, BND>(c, 0, 0);
+    issue<P_B1, BND>(c, 0, 0);
+    issue<P_A1, BND>(c, 0, 0);
+    issue<P_B0, BND>(c, 1, k1);
+    issue<P_A0, BND>(c, 1, k1);
+    issue<P_B1, BND>(c, 1, k1);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B0,A0 of tile 0 landed
     bar();
     read_b<0>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
@@ -313,6 +350,9 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     for (int i = 0; i < 4; ++i) {
       const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
       unsigned short* crow = C + (long)row * ldc;
+      // bounded mode: rows past M are dropped (the permlane swaps below stay
+      // wave-uniform, only the stores are predicated)
+      const bool row_ok = !BND || row < M;
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
         uint2 o[2];
@@ -322,9 +362,14 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
           f32x4 v = R.acc[mh][i][nh][n];
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (EPI != EPI_NONE) {
-            bf16x4 bb = *(const bf16x4*)(bias + col);
+            if (!BND || col + 4 <= N) {
+              bf16x4 bb = *(const bf16x4*)(bias + col);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+              for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
+            }
           }
           o[n].x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
           o[n].y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
@@ -344,7 +389,14 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
           // even fq: (own n0, partner n0) = (sx[0], sx[1]) ... odd fq likewise for n1
           const uint4 q = make_uint4(sx[0], sy[0], sx[1], sy[1]);
           const int cw = col0 + (fq & 1) * 16 + (fq >> 1) * 8;
-          *(uint4*)(crow + cw) = q;
+          if (!BND || (row_ok && cw + 8 <= N)) {
+            *(uint4*)(crow + cw) = q;
+          } else if (row_ok) {
+            const unsigned wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (cw + e < N) crow[cw + e] = (unsigned short)(wd[e >> 1] >> ((e & 1) * 16));
+          }
         }
       }
     }
@@ -1046,6 +1098,12 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
                        ldc);
+  } else if (variant == 16) {
+    // the same pipeline on any M, N and K % 8 == 0: buffer-resource loads zero
+    // the rows / K-chunks past the edges, stores are predicated
+    const dim3 gridb(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512>), gridb, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
+                       ldc);
   } else if (variant >= 4 && variant <= 8) {
     // tuning experiments (no-epilogue only)
     if constexpr (EPI == EPI_NONE) {
@@ -1125,6 +1183,18 @@ KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void
   return 1;
 }
 
+// Can the bounded 256x256 kernel (variant 16) take this problem? Any M, N;
+// K, the leading dimensions and the pointers in 16-B units.
+KGS_EXPORT int kgs_gemm_bf16_nt_bounded_ok(const void* A, const void* B, const void* C, int M, int N, int K,
+                                           int lda, int ldb, int ldc) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (K % 8 || lda % 8 || ldb % 8 || ldc % 8) return 0;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return 0;
+  // buffer offsets are 32-bit: 256 rows * ld * 2 B must stay below the OOB offset
+  if ((long)lda * 512 >= kgs::g256::OOB_OFFSET || (long)ldb * 512 >= kgs::g256::OOB_OFFSET) return 0;
+  return 1;
+}
+
 // variant: 0 = auto, 1 = force 256x256 8-wave ping-pong, 2 = force generic,
 //          3 = force 256x256 4-wave (both pipelined variants need the same eligibility).
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
@@ -1133,10 +1203,12 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if (epi != kgs::EPI_NONE && bias == nullptr) return KGS_ERR_ARG;
   // the fast epilogue reads the bias 4 elements (8 B) at a time
-  const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc) &&
-                   (epi == kgs::EPI_NONE || (uintptr_t)bias % 8 == 0);
+  const int bias_ok = epi == kgs::EPI_NONE || (uintptr_t)bias % 8 == 0;
+  const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
+  const int bounded = kgs_gemm_bf16_nt_bounded_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
   int v;
-  if (variant == 0) v = fast ? 1 : 2;
+  if (variant == 0) v = fast ? 1 : bounded ? 16 : 2;
+  else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
   else if (variant >= 3 && variant <= 15) { if (!fast) return KGS_ERR_ALIGN; v = variant; }

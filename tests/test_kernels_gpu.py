@@ -155,6 +155,46 @@ def test_gemm_repeatable_large(variant):
         assert torch.equal(gemm_nt(a, b, variant="fast"), c0)
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 1000, 1000), (300, 520, 72), (257, 264, 8), (4113, 1016, 4104),
+                                   (256, 256, 136), (2048, 768, 2048)])
+def test_gemm_bounded_ragged(M, N, K):
+    """Variant 16: the pipelined kernel on ragged M/N/K (buffer-resource zero fill)."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    c = gemm_nt(a, b, variant="bounded")
+    assert _rel_err(c, _ref_nt(a, b)) < 1e-2
+    assert torch.equal(gemm_nt(a, b), c)  # auto picks the bounded kernel here
+    for _ in range(3):
+        assert torch.equal(gemm_nt(a, b, variant="bounded"), c)
+
+
+def test_gemm_bounded_matches_fast_on_aligned():
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(1024, 2048, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(768, 2048, device=DEV) * 2 - 1).bfloat16()
+    assert torch.equal(gemm_nt(a, b, variant="bounded"), gemm_nt(a, b, variant="fast"))
+
+
+@pytest.mark.parametrize("act", ["bias", "gelu"])
+def test_gemm_bounded_partial_columns_and_epilogue(act):
+    """N % 8 != 0 inside a padded output (ldc % 8 == 0): the predicated store tail."""
+    from kgs.ops import gemm_nt
+
+    M, N, K = 300, 251, 96
+    a = (torch.rand(M, K, device=DEV) - 0.5).bfloat16()
+    b = (torch.rand(N, K, device=DEV) - 0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    big = torch.full((M, 256), 7.0, device=DEV, dtype=torch.bfloat16)
+    out = big[:, :N]
+    gemm_nt(a, b, bias=bias, act=act, out=out, variant="bounded")
+    torch.testing.assert_close(out.float(), _ref_nt(a, b, bias, None if act == "bias" else act), rtol=2e-2,
+                               atol=2e-2)
+    assert torch.all(big[:, N:] == 7.0)  # nothing written past N
+
+
 def test_gemm_wide_store_tail_matches_narrow():
     """The permlane16-swap 16-B store tail writes exactly the image of the 8-B one."""
     from kgs.ops import gemm_nt
