@@ -9,6 +9,8 @@ pods/rocm-gpu-test-pod.yaml runs ``python3 -m kgs.workload.entrypoint --pod``:
    device plugin passed in), then start one worker process per GPU with
    ``torch.distributed.run`` -- vector add, bf16 MFMA GEMM, RCCL all-reduce
    sweep (:mod:`kgs.workload.worker`) -- and print one JSON result line.
+   ``--smoke`` (BASELINE config 2) runs ``rocminfo`` and the HIP vector add
+   only: passthrough works and a kernel launches, nothing heavier.
 3. ``--pod`` keeps the container Running afterwards (``sleep 3600`` in the
    reference) so ``kubectl logs`` / ``kubectl wait`` behave the same.
 
@@ -52,6 +54,29 @@ def allocated_gpus() -> list:
         return []
 
 
+def rocminfo_agents(timeout: int = 60) -> dict:
+    """GPU agents reported by ``rocminfo`` (run as a child process: the parent
+    never initialises the GPU itself)."""
+    exe = None
+    for cand in ("rocminfo", "/opt/rocm/bin/rocminfo"):
+        for d in [""] + os.environ.get("PATH", "").split(os.pathsep):
+            path = os.path.join(d, cand) if d else cand
+            if os.path.isfile(path) and os.access(path, os.X_OK):
+                exe = path
+                break
+        if exe:
+            break
+    if exe is None:
+        return {"ok": False, "error": "rocminfo not found"}
+    try:
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"ok": False, "error": "rocminfo timed out"}
+    names = [ln.split(":", 1)[1].strip() for ln in r.stdout.splitlines()
+             if ln.strip().startswith("Name:") and "gfx" in ln]
+    return {"ok": r.returncode == 0 and bool(names), "gpu_agents": names}
+
+
 def collect_counters(a, env) -> dict:
     """Run the single-GPU worker (GEMM only) under rocprofv3, one pass per
     counter set, and return the markdown summary plus the raw directory."""
@@ -88,6 +113,7 @@ def main(argv=None) -> int:
     ap.add_argument("--counters", action="store_true",
                     help="re-run one GPU's GEMM under rocprofv3 (MFMA busy, LDS conflicts, L2 hit) and summarise")
     ap.add_argument("--counters-dir", default="/tmp/kgs-rocprof")
+    ap.add_argument("--smoke", action="store_true", help="config 2: rocminfo + HIP vector add only")
     a = ap.parse_args(argv)
 
     gpus = allocated_gpus()
@@ -100,6 +126,9 @@ def main(argv=None) -> int:
         for g in gpus:
             print(f"  renderD{g.render_minor} {g.bdf} {g.gfx_arch} {g.cu_count} CUs {g.num_xcc} XCDs "
                   f"{g.vram_bytes / 2**30:.0f} GiB numa{g.numa_node}", flush=True)
+        if a.smoke:
+            result["rocminfo"] = rocminfo_agents()
+            print(f"rocminfo GPU agents: {result['rocminfo'].get('gpu_agents')}", flush=True)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ)
         env["PYTHONPATH"] = root + (":" + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
@@ -109,6 +138,8 @@ def main(argv=None) -> int:
                "--gemm-size", str(a.gemm_size), "--gemm-iters", str(a.gemm_iters)]
         if a.allreduce_sizes:
             cmd += ["--allreduce-sizes", a.allreduce_sizes]
+        if a.smoke:
+            cmd += ["--skip-gemm", "--skip-allreduce"]
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
         sys.stderr.write(p.stderr[-4000:])
         for line in p.stdout.splitlines():
@@ -126,6 +157,8 @@ def main(argv=None) -> int:
         with open(a.json_out, "w") as f:
             f.write(line + "\n")
     rc = 0 if result.get("worker_rc", 0) == 0 and result.get("all_ok", True) else 1
+    if a.smoke and n and not result.get("rocminfo", {}).get("ok"):
+        rc = 1
     if a.pod:
         time.sleep(a.hold)
     return rc

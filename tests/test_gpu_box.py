@@ -78,3 +78,14 @@ def test_workload_entrypoint_pod_command():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = _last_json(r.stdout)
     assert res["mode"] == "gpu" and res["worker_rc"] == 0
+
+
+def test_workload_entrypoint_smoke_mode():
+    """BASELINE config 2: rocminfo + HIP vector add."""
+    r = subprocess.run([sys.executable, "-m", "kgs.workload.entrypoint", "--smoke", "--nproc", "1"],
+                       env=ENV, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _last_json(r.stdout)
+    assert "gfx950" in res["rocminfo"]["gpu_agents"]
+    assert res["ranks"][0]["vector_add"]["ok"]
+    assert all("gemm" not in r for r in res["ranks"])

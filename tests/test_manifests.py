@@ -99,3 +99,9 @@ def test_partition_plan():
     assert plan_partitions(gpus, 2, "split") == [[128, 136, 144, 152], [160, 168, 176, 184]]
     assert plan_partitions(gpus, 3, "split") == [[128, 136, 144], [152, 160, 168], [176, 184]]
     assert plan_partitions([], 2, "split") == [[], []]
+
+
+def test_smoke_pod():
+    doc = _load("rocm-gpu-smoke-pod.yaml")
+    assert doc == manifests.gpu_test_pod("localhost:5000/kgs-rocm-test:dev", gpus=1, name="gpu-rocm-smoke",
+                                         command=["python3", "-m", "kgs.workload.entrypoint", "--smoke", "--pod"])
