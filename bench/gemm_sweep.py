@@ -34,7 +34,11 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default="gpurun_out/gemm_sweep.json")
     ap.add_argument("--variants", default="auto", help="comma list of kgs variants: auto,fast,w4,generic")
+    ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8: kgs gemm_fp8_nt (e4m3, scaled MFMA) vs torch._scaled_mm (hipBLASLt fp8)")
     a = ap.parse_args()
+    if a.dtype == "fp8":
+        return sweep_fp8(a)
     res = []
     for s in a.shapes.split(","):
         dims = [int(x) for x in s.split("x")]
@@ -63,6 +67,55 @@ def main():
             r[f"{k}_tflops_median"] = round(fl / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e12, 1)
             r[f"{k}_tflops_best"] = round(fl / (min(ts) * 1e-3) / 1e12, 1)
         r["rel_err_vs_hipblaslt"] = errs
+        print(json.dumps(r), flush=True)
+        res.append(r)
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+def sweep_fp8(a):
+    from kgs.ops import gemm_fp8_nt, quantize_fp8
+
+    res = []
+    for s in a.shapes.split(","):
+        dims = [int(x) for x in s.split("x")]
+        M, N, K = (dims * 3)[:3] if len(dims) == 1 else dims
+        qa, sa = quantize_fp8(torch.rand(M, K, device="cuda") * 2 - 1)
+        qb, sb = quantize_fp8(torch.rand(N, K, device="cuda") * 2 - 1)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        C2 = torch.empty_like(C)
+        ta = torch.tensor(sa, device="cuda")
+        tb = torch.tensor(sb, device="cuda")
+        fns = {f"kgs_fp8_{v}": (lambda v=v: gemm_fp8_nt(qa, qb, sa, sb, out=C, variant=v))
+               for v in a.variants.split(",")}
+        try:
+            torch._scaled_mm(qa, qb.T, scale_a=ta, scale_b=tb, out_dtype=torch.bfloat16)
+            fns["hipblaslt_fp8"] = lambda: torch._scaled_mm(qa, qb.T, scale_a=ta, scale_b=tb,
+                                                           out_dtype=torch.bfloat16, out=C2)
+        except Exception as e:  # pragma: no cover - depends on the torch build
+            print(f"torch._scaled_mm unavailable: {e}", file=sys.stderr)
+        for f in fns.values():
+            for _ in range(3):
+                f()
+        torch.cuda.synchronize()
+        times = {k: [] for k in fns}
+        for _ in range(a.rounds):
+            for k, f in fns.items():
+                times[k].append(time_fn(f, a.iters))
+        ref = (qa.float() * sa) @ (qb.float() * sb).T
+        errs = {}
+        for v in a.variants.split(","):
+            gemm_fp8_nt(qa, qb, sa, sb, out=C, variant=v)
+            errs[v] = ((C.float() - ref).abs().max() / ref.abs().max()).item()
+        if "hipblaslt_fp8" in fns:
+            errs["hipblaslt_fp8"] = ((C2.float() - ref).abs().max() / ref.abs().max()).item()
+        fl = 2.0 * M * N * K
+        r = {"shape": [M, N, K], "dtype": "fp8_e4m3"}
+        for k, ts in times.items():
+            r[f"{k}_tflops_median"] = round(fl / (sorted(ts)[len(ts) // 2] * 1e-3) / 1e12, 1)
+            r[f"{k}_tflops_best"] = round(fl / (min(ts) * 1e-3) / 1e12, 1)
+        r["rel_err_vs_fp32_dequant"] = errs
         print(json.dumps(r), flush=True)
         res.append(r)
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)

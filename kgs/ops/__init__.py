@@ -12,7 +12,8 @@ from ._lib import KernelError, NativeUnavailable, available  # noqa: F401
 
 
 def __getattr__(name):  # lazy: keep `import kgs.ops` free of torch for CPU-only tools
-    if name in ("gemm_nt", "matmul", "linear", "Linear", "fast_path_ok", "transpose", "EPI"):
+    if name in ("gemm_nt", "matmul", "linear", "Linear", "fast_path_ok", "transpose", "EPI", "gemm_fp8_nt",
+                "quantize_fp8"):
         from . import gemm
 
         return getattr(gemm, name)

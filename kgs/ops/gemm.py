@@ -2,7 +2,8 @@
 
 ``gemm_nt(a, b)`` computes ``a @ b.T`` for ``a: [M, K]``, ``b: [N, K]`` (both
 K-contiguous bf16 on a gfx950 device), with optional fused bias + activation in
-the kernel epilogue. ``matmul`` and ``Linear`` are built on it; the backward pass
+the kernel epilogue. ``gemm_fp8_nt`` is the same pipeline on OCP e4m3 operands
+with the scaled fp8 MFMA and a per-tensor dequant scale. ``matmul`` and ``Linear`` are built on it; the backward pass
 re-uses the same NT kernel after a HIP transpose, so every FLOP of the in-pod
 workload runs on the hand-written MFMA kernel.
 """
@@ -82,6 +83,68 @@ def gemm_nt(
         _lib.stream_handle(a.device),
     )
     _lib.check(rc, f"gemm_nt[{M}x{N}x{K}]")
+    return out
+
+
+FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
+FP8_MAX = 448.0
+FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}
+
+
+def quantize_fp8(x: torch.Tensor, scale: float | None = None) -> tuple[torch.Tensor, float]:
+    """Per-tensor e4m3 quantisation: returns ``(x_fp8, scale)`` with
+    ``x ~= x_fp8.float() * scale`` (scale = amax / 448 unless given)."""
+    if scale is None:
+        amax = float(x.detach().abs().max().float().item()) if x.numel() else 0.0
+        scale = amax / FP8_MAX if amax > 0 else 1.0
+    q = (x.float() / scale).clamp(-FP8_MAX, FP8_MAX).to(FP8_DTYPE)
+    return q, float(scale)
+
+
+def gemm_fp8_nt(
+    a: torch.Tensor,
+    b: torch.Tensor,
+    scale_a: float = 1.0,
+    scale_b: float = 1.0,
+    bias: torch.Tensor | None = None,
+    act: str | None = None,
+    out: torch.Tensor | None = None,
+    variant: str = "auto",
+) -> torch.Tensor:
+    """``act(scale_a*scale_b * (a @ b.T) + bias)`` in bf16 from e4m3 operands.
+
+    a: [M, K], b: [N, K], both ``torch.float8_e4m3fn`` K-contiguous on a gfx950
+    device; K % 16 == 0 (K % 256 and M, N % 256 for the aligned path). f32
+    accumulation on the scaled 16x16x128 fp8 MFMA (2x the bf16 MFMA rate).
+    """
+    for t, name in ((a, "a"), (b, "b")):
+        if t.dtype != FP8_DTYPE:
+            raise TypeError(f"{name} must be {FP8_DTYPE}, got {t.dtype}")
+        if not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError(f"{name} must be a 2-D row-major GPU matrix")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    epi_name = act if act is not None else ("bias" if bias is not None else None)
+    if epi_name not in EPI:
+        raise ValueError(f"unknown activation {act!r}")
+    epi = EPI[epi_name]
+    if epi and bias is None:
+        bias = torch.zeros(N, dtype=torch.bfloat16, device=a.device)
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous bf16 vector of length N")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out")
+        if tuple(out.shape) != (M, N):
+            raise ValueError(f"out has shape {tuple(out.shape)}, expected {(M, N)}")
+    rc = _lib.lib().kgs_gemm_fp8_nt(
+        a.data_ptr(), b.data_ptr(), out.data_ptr(), bias.data_ptr() if bias is not None else None,
+        M, N, K, a.stride(0), b.stride(0), out.stride(0), float(scale_a) * float(scale_b), epi,
+        FP8_VARIANTS[variant], _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_fp8_nt[{M}x{N}x{K}]")
     return out
 
 

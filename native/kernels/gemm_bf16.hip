@@ -148,8 +148,33 @@ __device__ __forceinline__ void read_b(const CtxT& c, Regs& R, const char* half)
   }
 }
 
-template <int MH, int NH>
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// Two 16-B fragments (k-sub 0 and 1 of the same 128-byte LDS row slice) as one
+// 32-B operand of the fp8 MFMA.
+__device__ __forceinline__ i32x8 cat32(const bf16x8& lo, const bf16x8& hi) {
+  typedef short s16 __attribute__((ext_vector_type(16)));
+  s16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  return __builtin_bit_cast(i32x8, v);
+}
+
+template <int MH, int NH, bool FP8 = false>
 __device__ __forceinline__ void mma_quadrant(Regs& R) {
+  if constexpr (FP8) {
+    // fp8 (OCP e4m3) mode: the LDS rows hold 128 fp8 K-values; one scaled
+    // 16x16x128 MFMA (unit E8M0 scales = 2^0) consumes what the bf16 path does
+    // in two 16x16x32 ones -- twice the FLOPs for the same bytes moved. Lane
+    // group g holds K-bytes [16g,16g+16) and [64+16g,64+16g+16) of its row, for
+    // A and B alike, so the K pairing is consistent (the sum is order-free).
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        R.acc[MH][i][NH][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            cat32(R.b[NH][n][0], R.b[NH][n][1]), cat32(R.a[i][0], R.a[i][1]), R.acc[MH][i][NH][n], 0, 0, 0, 127,
+            0, 127);
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -212,18 +237,18 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
   if constexpr (S & 16) {  // timing experiment only: twice the MFMAs per phase (wrong results)
-    if constexpr (q == 0) mma_quadrant<0, 0>(R);
-    if constexpr (q == 1) mma_quadrant<0, 1>(R);
-    if constexpr (q == 2) mma_quadrant<1, 0>(R);
-    if constexpr (q == 3) mma_quadrant<1, 1>(R);
+    if constexpr (q == 0) mma_quadrant<0, 0, (S & 1024) != 0>(R);
+    if constexpr (q == 1) mma_quadrant<0, 1, (S & 1024) != 0>(R);
+    if constexpr (q == 2) mma_quadrant<1, 0, (S & 1024) != 0>(R);
+    if constexpr (q == 3) mma_quadrant<1, 1, (S & 1024) != 0>(R);
   }
-  if constexpr (q == 0) mma_quadrant<0, 0>(R);
-  if constexpr (q == 1) mma_quadrant<0, 1>(R);
+  if constexpr (q == 0) mma_quadrant<0, 0, (S & 1024) != 0>(R);
+  if constexpr (q == 1) mma_quadrant<0, 1, (S & 1024) != 0>(R);
   if constexpr (q == 2) {
-    if constexpr ((S & 1) == 0) mma_quadrant<1, 1>(R); else mma_quadrant<1, 0>(R);
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 1, (S & 1024) != 0>(R); else mma_quadrant<1, 0, (S & 1024) != 0>(R);
   }
   if constexpr (q == 3) {
-    if constexpr ((S & 1) == 0) mma_quadrant<1, 0>(R); else mma_quadrant<1, 1>(R);
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 0, (S & 1024) != 0>(R); else mma_quadrant<1, 1, (S & 1024) != 0>(R);
   }
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
   // S bit 7 (with bit 6, lockstep): one barrier per phase. Still race-free: the
@@ -237,7 +262,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
                                                    const unsigned short* __restrict__ B,
                                                    unsigned short* __restrict__ C,
                                                    const unsigned short* __restrict__ bias,
-                                                   int M, int N, int K, int lda, int ldb, int ldc) {
+                                                   int M, int N, int K, int lda, int ldb, int ldc,
+                                                   float alpha) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   constexpr bool BND = (S & 512) != 0;
@@ -360,6 +386,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
         for (int n = 0; n < 2; ++n) {
           const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
           f32x4 v = R.acc[mh][i][nh][n];
+          if constexpr (S & 1024) v *= alpha;  // fp8: per-tensor dequant scale sa*sb
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (EPI != EPI_NONE) {
             if (!BND || col + 4 <= N) {
@@ -1097,31 +1124,31 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
   if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                       ldc);
+                       ldc, 1.0f);
   } else if (variant == 16) {
     // the same pipeline on any M, N and K % 8 == 0: buffer-resource loads zero
     // the rows / K-chunks past the edges, stores are predicated
     const dim3 gridb(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512>), gridb, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                       ldc);
+                       ldc, 1.0f);
   } else if (variant >= 4 && variant <= 8) {
     // tuning experiments (no-epilogue only)
     if constexpr (EPI == EPI_NONE) {
       if (variant == 4)  // with s_setprio around the MFMA blocks
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 5>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc);
+                           ldb, ldc, 1.0f);
       if (variant == 5)  // GROUP_M 8
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc);
+                           ldb, ldc, 1.0f);
       if (variant == 6)  // first schedule (12/4/8/0 reads, look-ahead 5), setprio, GROUP_M 8
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 0>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc);
+                           ldb, ldc, 1.0f);
       if (variant == 7)  // GROUP_M 2
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc);
+                           ldb, ldc, 1.0f);
       if (variant == 8)  // GROUP_M 16
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc);
+                           ldb, ldc, 1.0f);
     } else {
       return hipErrorInvalidValue;
     }
@@ -1129,12 +1156,12 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     // timing probe: production schedule, all blocks load the same (L2-resident) tiles (wrong C)
     if constexpr (EPI == EPI_NONE)
       hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 32>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                         ldb, ldc);
+                         ldb, ldc, 1.0f);
   } else if (variant == 15) {
     // production schedule with the narrow (2 x 8-B per lane) store tail, for A/B
     if constexpr (EPI == EPI_NONE)
       hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 256>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                         ldb, ldc);
+                         ldb, ldc, 1.0f);
   } else if (variant == 14) {
     hipLaunchKernelGGL(gpl::gemm_nt_256pl<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
   } else if (variant == 12 || variant == 13) {
@@ -1142,10 +1169,10 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     if constexpr (EPI == EPI_NONE) {
       if (variant == 12)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K,
-                           lda, ldb, ldc);
+                           lda, ldb, ldc, 1.0f);
       else
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64 + 128>), grid256, dim3(512), 0, s, A, B, C, bias, M, N,
-                           K, lda, ldb, ldc);
+                           K, lda, ldb, ldc, 1.0f);
     }
   } else if (variant == 10) {
     hipLaunchKernelGGL(g32::gemm_nt_256p32<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
@@ -1153,7 +1180,7 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     // timing probe: production schedule with every MFMA block doubled (wrong C)
     if constexpr (EPI == EPI_NONE) {
       hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 16>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                         ldb, ldc);
+                         ldb, ldc, 1.0f);
     } else {
       return hipErrorInvalidValue;
     }
@@ -1224,6 +1251,80 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
     case kgs::EPI_BIAS_GELU: e = kgs::launch<kgs::EPI_BIAS_GELU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
     case kgs::EPI_BIAS_RELU: e = kgs::launch<kgs::EPI_BIAS_RELU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
     case kgs::EPI_BIAS_SILU: e = kgs::launch<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    default: return KGS_ERR_ARG;
+  }
+  return (int)e;
+}
+
+// ---------------------------------------------------------------------------
+// fp8 (OCP e4m3fn) GEMM: C = epilogue(alpha * A . B^T), A [M,K] and B [N,K]
+// fp8 K-contiguous, C bf16. The same 256x256 pipeline with the scaled
+// 16x16x128 f8f6f4 MFMA: the kernel sees each fp8 row as K/2 16-bit words, so
+// the LDS-DMA, swizzle and schedule are byte-for-byte those of the bf16 path.
+// variant 0 = auto, 1 = aligned (M, N % 256, K % 256), 16 = bounded (any M, N;
+// K % 16). Lengths and leading dimensions are in fp8 elements (= bytes).
+// ---------------------------------------------------------------------------
+namespace {
+
+template <int EPI>
+hipError_t launch_fp8(int v, const unsigned short* A, const unsigned short* B, unsigned short* C,
+                      const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
+                      hipStream_t s) {
+  using namespace kgs;
+  if (v == 1) {
+    const dim3 grid((M / g256::BM) * (N / g256::BN));
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
+                       ldbw, ldc, alpha);
+  } else {
+    const dim3 grid(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
+                       ldaw, ldbw, ldc, alpha);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+KGS_EXPORT int kgs_gemm_fp8_nt_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda, int ldb,
+                                  int ldc, int bounded) {
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return 0;
+  if (K % 16 || lda % 16 || ldb % 16 || ldc % 8) return 0;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return 0;
+  if ((long)(lda / 2) * 512 >= kgs::g256::OOB_OFFSET || (long)(ldb / 2) * 512 >= kgs::g256::OOB_OFFSET) return 0;
+  if (!bounded && (M % 256 || N % 256 || K % 256)) return 0;
+  return 1;
+}
+
+KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                               int ldb, int ldc, float alpha, int epi, int variant, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
+  if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (epi != kgs::EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
+  const int fast = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 0);
+  const int bounded = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 1);
+  int v;
+  if (variant == 0) v = fast ? 1 : 16;
+  else if (variant == 1 || variant == 16) v = variant;
+  else return KGS_ERR_ARG;
+  if (!(v == 1 ? fast : bounded)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto bb = (const unsigned short*)bias;
+  const int Kw = K / 2, ldaw = lda / 2, ldbw = ldb / 2;  // fp8 rows as 16-bit words
+  hipError_t e;
+  switch (epi) {
+    case kgs::EPI_NONE: e = launch_fp8<kgs::EPI_NONE>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream); break;
+    case kgs::EPI_BIAS: e = launch_fp8<kgs::EPI_BIAS>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream); break;
+    case kgs::EPI_BIAS_GELU:
+      e = launch_fp8<kgs::EPI_BIAS_GELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      break;
+    case kgs::EPI_BIAS_RELU:
+      e = launch_fp8<kgs::EPI_BIAS_RELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      break;
+    case kgs::EPI_BIAS_SILU:
+      e = launch_fp8<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      break;
     default: return KGS_ERR_ARG;
   }
   return (int)e;

@@ -249,3 +249,60 @@ def test_matmul_and_linear_backward():
     assert _rel_err(x.grad, xr.grad) < 3e-2
     assert _rel_err(lin.weight.grad, wr.grad) < 3e-2
     assert _rel_err(lin.bias.grad, br.grad) < 3e-2
+
+
+# ----------------------------------------------------------------- fp8 GEMM --
+def _fp8_pair(M, N, K, seed=0):
+    from kgs.ops import quantize_fp8
+
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    a = torch.randn(M, K, device=DEV, generator=g)
+    b = torch.randn(N, K, device=DEV, generator=g)
+    qa, sa = quantize_fp8(a)
+    qb, sb = quantize_fp8(b)
+    return qa, sa, qb, sb
+
+
+def _fp8_ref(qa, sa, qb, sb, bias=None, act=None):
+    y = (qa.float() * sa) @ (qb.float() * sb).T
+    if bias is not None:
+        y = y + bias.float()
+    if act == "gelu":
+        y = torch.nn.functional.gelu(y, approximate="tanh")
+    return y
+
+
+def test_gemm_fp8_identity_asymmetric():
+    """A = I, B with distinct small integers (exact in e4m3): C must equal B
+    exactly, so a transposed or mis-paired K layout cannot pass."""
+    from kgs.ops import gemm_fp8_nt
+
+    K = 256
+    a = torch.eye(K, device=DEV).to(torch.float8_e4m3fn)
+    bf = ((torch.arange(256 * K, device=DEV) * 7 % 31) - 15).float().reshape(256, K)
+    b = bf.to(torch.float8_e4m3fn)
+    c = gemm_fp8_nt(a, b)
+    assert torch.equal(c.float(), bf.T)
+
+
+@pytest.mark.parametrize("M,N,K,variant", [(512, 512, 512, "fast"), (1024, 768, 2048, "fast"),
+                                           (300, 520, 144, "bounded"), (257, 264, 16, "bounded"),
+                                           (2048, 1024, 4096, "auto")])
+def test_gemm_fp8_random(M, N, K, variant):
+    from kgs.ops import gemm_fp8_nt
+
+    qa, sa, qb, sb = _fp8_pair(M, N, K)
+    c = gemm_fp8_nt(qa, qb, sa, sb, variant=variant)
+    assert _rel_err(c, _fp8_ref(qa, sa, qb, sb)) < 1e-2
+    for _ in range(3):
+        assert torch.equal(gemm_fp8_nt(qa, qb, sa, sb, variant=variant), c)
+
+
+def test_gemm_fp8_epilogue_and_bounded_equals_fast():
+    from kgs.ops import gemm_fp8_nt
+
+    qa, sa, qb, sb = _fp8_pair(512, 768, 1024, seed=3)
+    bias = torch.randn(768, device=DEV).bfloat16()
+    c = gemm_fp8_nt(qa, qb, sa, sb, bias=bias, act="gelu")
+    torch.testing.assert_close(c.float(), _fp8_ref(qa, sa, qb, sb, bias, "gelu"), rtol=2e-2, atol=2e-2)
+    assert torch.equal(gemm_fp8_nt(qa, qb, sa, sb, variant="bounded"), gemm_fp8_nt(qa, qb, sa, sb, variant="fast"))
