@@ -114,6 +114,7 @@ def main(argv=None) -> int:
                     help="re-run one GPU's GEMM under rocprofv3 (MFMA busy, LDS conflicts, L2 hit) and summarise")
     ap.add_argument("--counters-dir", default="/tmp/kgs-rocprof")
     ap.add_argument("--smoke", action="store_true", help="config 2: rocminfo + HIP vector add only")
+    ap.add_argument("--fp8", action="store_true", help="also report the e4m3 GEMM TFLOPS")
     a = ap.parse_args(argv)
 
     gpus = allocated_gpus()
@@ -140,6 +141,8 @@ def main(argv=None) -> int:
             cmd += ["--allreduce-sizes", a.allreduce_sizes]
         if a.smoke:
             cmd += ["--skip-gemm", "--skip-allreduce"]
+        if a.fp8:
+            cmd += ["--fp8"]
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
         sys.stderr.write(p.stderr[-4000:])
         for line in p.stdout.splitlines():

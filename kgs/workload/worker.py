@@ -26,6 +26,7 @@ def _args(argv=None):
     ap.add_argument("--allreduce-iters", type=int, default=20)
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-allreduce", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="also run the e4m3 GEMM (scaled fp8 MFMA)")
     return ap.parse_args(argv)
 
 
@@ -79,6 +80,35 @@ def gemm_check(dev, size: int, iters: int) -> dict:
             "kernel": "gemm_nt_256" if fast_path_ok(A, B, C) else "gemm_nt_generic"}
 
 
+def gemm_fp8_check(dev, size: int, iters: int) -> dict:
+    """The same GEMM on OCP e4m3 operands (scaled fp8 MFMA), per-tensor scales."""
+    import torch
+
+    from kgs.ops import gemm_fp8_nt, quantize_fp8
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    qa, sa = quantize_fp8(torch.rand(size, size, generator=g, device=dev) * 2 - 1)
+    qb, sb = quantize_fp8(torch.rand(size, size, generator=g, device=dev) * 2 - 1)
+    C = torch.empty(size, size, device=dev, dtype=torch.bfloat16)
+    gemm_fp8_nt(qa, qb, sa, sb, out=C)
+    rows = min(size, 512)
+    ref = (qa[:rows].float() * sa) @ (qb.float() * sb).T
+    err = ((C[:rows].float() - ref).abs().max() / ref.abs().max()).item()
+    for _ in range(3):
+        gemm_fp8_nt(qa, qb, sa, sb, out=C)
+    torch.cuda.synchronize(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        gemm_fp8_nt(qa, qb, sa, sb, out=C)
+    e.record()
+    torch.cuda.synchronize(dev)
+    ms = s.elapsed_time(e) / iters
+    return {"size": size, "rel_err": err, "ok": err < 2e-2, "ms": round(ms, 4),
+            "tflops": round(2.0 * size ** 3 / (ms * 1e-3) / 1e12, 1), "dtype": "fp8_e4m3"}
+
+
 def main(argv=None) -> int:
     a = _args(argv)
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -97,6 +127,8 @@ def main(argv=None) -> int:
         res["vector_add"] = vector_add_check(dev, a.vadd_elems)
         if not a.skip_gemm:
             res["gemm"] = gemm_check(dev, a.gemm_size, a.gemm_iters)
+            if a.fp8:
+                res["gemm_fp8"] = gemm_fp8_check(dev, a.gemm_size, a.gemm_iters)
         res["compute_s"] = round(time.perf_counter() - t0, 3)
     results = kdist.all_gather_object(ctx, res)
     sweep = None
@@ -110,7 +142,9 @@ def main(argv=None) -> int:
         out = {"world_size": ctx.world_size, "ranks": results,
                "gemm_tflops_total": round(sum(gemm_tf), 1),
                "all_ok": all(r.get("vector_add", {}).get("ok", True) and r.get("gemm", {}).get("ok", True)
-                             for r in results)}
+                             and r.get("gemm_fp8", {}).get("ok", True) for r in results)}
+        if any("gemm_fp8" in r for r in results):
+            out["gemm_fp8_tflops_total"] = round(sum(r.get("gemm_fp8", {}).get("tflops", 0.0) for r in results), 1)
         if sweep:
             out["allreduce"] = sweep
             out["allreduce_peak_busbw_gbs"] = round(max(p["busbw_gbs"] for p in sweep), 1)

@@ -74,10 +74,11 @@ def test_rccl_bench_binary():
 def test_workload_entrypoint_pod_command():
     """The gpu-rocm-test container command, one GPU, small GEMM."""
     r = subprocess.run([sys.executable, "-m", "kgs.workload.entrypoint", "--nproc", "1", "--gemm-size", "2048",
-                        "--gemm-iters", "3"], env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
+                        "--gemm-iters", "3", "--fp8"], env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = _last_json(r.stdout)
     assert res["mode"] == "gpu" and res["worker_rc"] == 0
+    assert res["ranks"][0]["gemm"]["ok"] and res["ranks"][0]["gemm_fp8"]["ok"]
 
 
 def test_workload_entrypoint_smoke_mode():
