@@ -88,7 +88,7 @@ def gemm_nt(
 
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
-FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}
+FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16, "gm8": 17, "gm16": 18, "gm2": 19}  # gm*: experiments
 
 
 def quantize_fp8(x: torch.Tensor, scale: float | None = None) -> tuple[torch.Tensor, float]:

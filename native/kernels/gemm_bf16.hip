@@ -1271,10 +1271,23 @@ hipError_t launch_fp8(int v, const unsigned short* A, const unsigned short* B, u
                       const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
                       hipStream_t s) {
   using namespace kgs;
+  const dim3 grid_al((M / g256::BM) * (N / g256::BN));
   if (v == 1) {
-    const dim3 grid((M / g256::BM) * (N / g256::BN));
-    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
                        ldbw, ldc, alpha);
+  } else if (v >= 17 && v <= 19) {
+    // tile-group height experiments for fp8 (aligned shapes): GROUP_M 8 / 16 / 2
+    if constexpr (EPI == EPI_NONE) {
+      if (v == 17)
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
+                           ldaw, ldbw, ldc, alpha);
+      if (v == 18)
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
+                           ldaw, ldbw, ldc, alpha);
+      if (v == 19)
+        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
+                           ldaw, ldbw, ldc, alpha);
+    }
   } else {
     const dim3 grid(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
@@ -1304,9 +1317,9 @@ KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void
   const int bounded = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 1);
   int v;
   if (variant == 0) v = fast ? 1 : 16;
-  else if (variant == 1 || variant == 16) v = variant;
+  else if (variant == 1 || variant == 16 || (variant >= 17 && variant <= 19)) v = variant;
   else return KGS_ERR_ARG;
-  if (!(v == 1 ? fast : bounded)) return KGS_ERR_ALIGN;
+  if (!(v == 16 ? bounded : fast)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
