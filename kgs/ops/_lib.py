@@ -44,6 +44,9 @@ _SIGS = {
     "kgs_vector_add_f32": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
     "kgs_vector_add_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
     "kgs_transpose_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
+    "kgs_transpose_bf16_v": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
+    "kgs_vector_add_f32_v": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p], _c_int),
+    "kgs_vector_add_bf16_v": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p], _c_int),
     "kgs_checksum_bf16": ([_c_void_p, _c_long, _c_void_p, _c_void_p], _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)
     "kgs_ar_signal_bytes": ([], _c_int),

@@ -14,8 +14,11 @@ def _dev_check(*ts: torch.Tensor) -> None:
             raise ValueError("tensor must be contiguous")
 
 
-def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-    """``a + b`` elementwise (f32 or bf16) on the HIP vector-add kernel."""
+def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, variant: int = 0) -> torch.Tensor:
+    """``a + b`` elementwise (f32 or bf16) on the HIP vector-add kernel.
+
+    variant selects a streaming configuration (0 = default; 1-6 are the measured
+    alternatives in native/kernels/elementwise.hip)."""
     _dev_check(a, b)
     if a.shape != b.shape or a.dtype != b.dtype:
         raise ValueError("a and b must match in shape and dtype")
@@ -23,24 +26,27 @@ def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None
     _dev_check(out)
     n = a.numel()
     if a.dtype == torch.float32:
-        fn = _lib.lib().kgs_vector_add_f32
+        fn = _lib.lib().kgs_vector_add_f32_v
     elif a.dtype == torch.bfloat16:
-        fn = _lib.lib().kgs_vector_add_bf16
+        fn = _lib.lib().kgs_vector_add_bf16_v
     else:
         raise TypeError(f"unsupported dtype {a.dtype}")
-    _lib.check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), n, _lib.stream_handle(a.device)), "vector_add")
+    _lib.check(fn(a.data_ptr(), b.data_ptr(), out.data_ptr(), n, variant, _lib.stream_handle(a.device)),
+               "vector_add")
     return out
 
 
-def transpose_bf16(x: torch.Tensor) -> torch.Tensor:
+def transpose_bf16(x: torch.Tensor, variant: int = 0) -> torch.Tensor:
+    """Materialised ``x.T`` (variant 0 = auto: 16-B path when shapes allow,
+    1 = element-wise tile, 2 = force the 16-B path)."""
     if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1:
         raise ValueError("transpose_bf16 needs a row-major bf16 matrix")
     if not x.is_cuda:
         raise ValueError("tensor must be on a GPU")
     rows, cols = x.shape
     out = torch.empty((cols, rows), dtype=torch.bfloat16, device=x.device)
-    rc = _lib.lib().kgs_transpose_bf16(x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0), rows,
-                                       _lib.stream_handle(x.device))
+    rc = _lib.lib().kgs_transpose_bf16_v(x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0), rows, variant,
+                                         _lib.stream_handle(x.device))
     _lib.check(rc, "transpose_bf16")
     return out
 

@@ -13,13 +13,28 @@ namespace kgs {
 constexpr int EW_THREADS = 256;
 constexpr int EW_MAX_BLOCKS = 256 * 8;
 
-__global__ __launch_bounds__(EW_THREADS) void vadd_f32(const float4* __restrict__ a, const float4* __restrict__ b,
-                                                       float4* __restrict__ c, long n4) {
+// U vectors per thread per trip, all loads issued before the first add, so a
+// wave keeps 2*U 16-B loads in flight (HBM streaming wants bytes in flight,
+// not more waves). NT: non-temporal loads/stores (streamed once, keep them out
+// of the way of L2/MALL residents).
+template <int U, bool NT>
+__global__ __launch_bounds__(EW_THREADS) void vadd_f32(const f32x4* __restrict__ a, const f32x4* __restrict__ b,
+                                                       f32x4* __restrict__ c, long n4) {
   const long stride = (long)gridDim.x * EW_THREADS;
-  for (long i = (long)blockIdx.x * EW_THREADS + threadIdx.x; i < n4; i += stride) {
-    float4 x = a[i], y = b[i];
-    c[i] = make_float4(x.x + y.x, x.y + y.y, x.z + y.z, x.w + y.w);
+  long i = (long)blockIdx.x * EW_THREADS + threadIdx.x;
+  for (; i + (U - 1) * stride < n4; i += U * stride) {
+    f32x4 x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      x[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+      y[u] = NT ? __builtin_nontemporal_load(b + i + u * stride) : b[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) __builtin_nontemporal_store(x[u] + y[u], c + i + u * stride); else c[i + u * stride] = x[u] + y[u];
+    }
   }
+  for (; i < n4; i += stride) c[i] = a[i] + b[i];
 }
 
 __global__ void vadd_f32_tail(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ c,
@@ -28,22 +43,77 @@ __global__ void vadd_f32_tail(const float* __restrict__ a, const float* __restri
   if (i < n) c[i] = a[i] + b[i];
 }
 
+__device__ __forceinline__ bf16x8 add_bf16x8(const bf16x8& x, const bf16x8& y) {
+  bf16x8 z;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) z[e] = (short)f2bf(bf2f((unsigned short)x[e]) + bf2f((unsigned short)y[e]));
+  return z;
+}
+
+template <int U, bool NT>
 __global__ __launch_bounds__(EW_THREADS) void vadd_bf16(const bf16x8* __restrict__ a, const bf16x8* __restrict__ b,
                                                         bf16x8* __restrict__ c, long n8) {
   const long stride = (long)gridDim.x * EW_THREADS;
-  for (long i = (long)blockIdx.x * EW_THREADS + threadIdx.x; i < n8; i += stride) {
-    bf16x8 x = a[i], y = b[i], z;
+  long i = (long)blockIdx.x * EW_THREADS + threadIdx.x;
+  for (; i + (U - 1) * stride < n8; i += U * stride) {
+    bf16x8 x[U], y[U];
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-      z[e] = (short)f2bf(bf2f((unsigned short)x[e]) + bf2f((unsigned short)y[e]));
-    c[i] = z;
+    for (int u = 0; u < U; ++u) {
+      x[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+      y[u] = NT ? __builtin_nontemporal_load(b + i + u * stride) : b[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bf16x8 z = add_bf16x8(x[u], y[u]);
+      if (NT) __builtin_nontemporal_store(z, c + i + u * stride); else c[i + u * stride] = z;
+    }
   }
+  for (; i < n8; i += stride) c[i] = add_bf16x8(a[i], b[i]);
 }
 
 __global__ void vadd_bf16_tail(const unsigned short* __restrict__ a, const unsigned short* __restrict__ b,
                                unsigned short* __restrict__ c, long start, long n) {
   long i = start + (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) c[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+// out[c][r] = in[r][c] with 16-B global accesses on both sides: a 64x64 tile
+// is loaded as 8-element row chunks into LDS (row pitch 72 elements = 144 B
+// keeps 16-B alignment and staggers banks), then each thread gathers 8
+// consecutive INPUT rows of one column from LDS and writes them as one 16-B
+// output chunk; 8 lanes cover one 128-B output row segment. Needs cols, rows, ld_in, ld_out % 8 == 0 and 16-B aligned
+// pointers; transpose_bf16 below handles everything else.
+constexpr int TP = 72;
+__global__ __launch_bounds__(256) void transpose_bf16_v8(const bf16x8* __restrict__ in, bf16x8* __restrict__ out,
+                                                         int rows, int cols, int ld_in8, int ld_out8) {
+  __shared__ __attribute__((aligned(16))) unsigned short tile[64 * TP];
+  // diagonal block order: blocks that run together write output rows spread
+  // over the column tiles instead of 64-row strides of one power-of-two pitch
+  // (HBM channel camping on square power-of-two shapes)
+  const int bx = (blockIdx.x + blockIdx.y) % gridDim.x;
+  const int r0 = blockIdx.y * 64, c0 = bx * 64;
+  const int t = threadIdx.x;
+  // load: 64 rows x 8 chunks = 512 chunks, 2 per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = t + k * 256, r = idx >> 3, ch = idx & 7;
+    const int gr = r0 + r, gc = c0 + ch * 8;
+    bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (gr < rows && gc < cols) v = in[(long)gr * ld_in8 + (gc >> 3)];
+    *(bf16x8*)&tile[r * TP + ch * 8] = v;
+  }
+  __syncthreads();
+  // store: a wave writes 8 output rows x 128 contiguous bytes per instruction
+  // (lane>>3 = output row, lane&7 = 16-B chunk = 8 input rows)
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int col = (t >> 3) + k * 32, rb = (t & 7) * 8;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (short)tile[(rb + j) * TP + col];
+    const int oc = c0 + col, orr = r0 + rb;
+    if (oc < cols && orr < rows) out[(long)oc * ld_out8 + (orr >> 3)] = v;
+  }
 }
 
 // out[c][r] = in[r][c]; 64x64 tile through LDS (+1 pad column: conflict-free
@@ -109,13 +179,53 @@ static int blocks_for(long n) {
 
 }  // namespace kgs
 
-KGS_EXPORT int kgs_vector_add_f32(const void* a, const void* b, void* c, long n, hipStream_t s) {
+namespace {
+
+// Streaming configurations (variant): unroll, non-temporal, block cap.
+struct EwCfg {
+  int unroll;
+  bool nt;
+  long max_blocks;
+};
+constexpr EwCfg EW_CFGS[] = {
+    {1, false, 1L << 30},            // 0: default = one-shot grid (measured best, profiles/elementwise.json)
+    {1, false, kgs::EW_MAX_BLOCKS},  // 1: one vector per trip
+    {2, false, kgs::EW_MAX_BLOCKS},  // 2
+    {4, false, kgs::EW_MAX_BLOCKS},  // 3
+    {4, true, kgs::EW_MAX_BLOCKS},   // 4: non-temporal
+    {1, false, 1L << 30},            // 5: one-shot grid, no loop
+    {4, false, 1024},                // 6: fewer blocks
+};
+constexpr int EW_NCFG = sizeof(EW_CFGS) / sizeof(EW_CFGS[0]);
+
+int ew_blocks(long nvec, const EwCfg& c) {
+  long b = (nvec + (long)kgs::EW_THREADS * c.unroll - 1) / ((long)kgs::EW_THREADS * c.unroll);
+  if (b < 1) b = 1;
+  return (int)(b < c.max_blocks ? b : c.max_blocks);
+}
+
+}  // namespace
+
+#define KGS_EW_LAUNCH(KERNEL, VT, a, b, c, nvec, cfg, s)                                                     \
+  do {                                                                                                        \
+    const dim3 g(ew_blocks(nvec, cfg)), blk(kgs::EW_THREADS);                                                 \
+    if (cfg.unroll == 4 && cfg.nt)                                                                            \
+      hipLaunchKernelGGL((KERNEL<4, true>), g, blk, 0, s, (const VT*)a, (const VT*)b, (VT*)c, nvec);          \
+    else if (cfg.unroll == 4)                                                                                 \
+      hipLaunchKernelGGL((KERNEL<4, false>), g, blk, 0, s, (const VT*)a, (const VT*)b, (VT*)c, nvec);         \
+    else if (cfg.unroll == 2)                                                                                 \
+      hipLaunchKernelGGL((KERNEL<2, false>), g, blk, 0, s, (const VT*)a, (const VT*)b, (VT*)c, nvec);         \
+    else                                                                                                      \
+      hipLaunchKernelGGL((KERNEL<1, false>), g, blk, 0, s, (const VT*)a, (const VT*)b, (VT*)c, nvec);         \
+  } while (0)
+
+KGS_EXPORT int kgs_vector_add_f32_v(const void* a, const void* b, void* c, long n, int variant, hipStream_t s) {
   if (n < 0) return KGS_ERR_SHAPE;
+  if (variant < 0 || variant >= EW_NCFG) return KGS_ERR_ARG;
   if (n == 0) return 0;
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && ((uintptr_t)c % 16 == 0);
   long n4 = aligned ? n / 4 : 0;
-  if (n4) hipLaunchKernelGGL(kgs::vadd_f32, dim3(kgs::blocks_for(n4)), dim3(kgs::EW_THREADS), 0, s,
-                             (const float4*)a, (const float4*)b, (float4*)c, n4);
+  if (n4) KGS_EW_LAUNCH(kgs::vadd_f32, f32x4, a, b, c, n4, EW_CFGS[variant], s);
   long rest = n - n4 * 4;
   if (rest)
     hipLaunchKernelGGL(kgs::vadd_f32_tail, dim3((rest + 255) / 256), dim3(256), 0, s, (const float*)a,
@@ -123,13 +233,13 @@ KGS_EXPORT int kgs_vector_add_f32(const void* a, const void* b, void* c, long n,
   return (int)hipGetLastError();
 }
 
-KGS_EXPORT int kgs_vector_add_bf16(const void* a, const void* b, void* c, long n, hipStream_t s) {
+KGS_EXPORT int kgs_vector_add_bf16_v(const void* a, const void* b, void* c, long n, int variant, hipStream_t s) {
   if (n < 0) return KGS_ERR_SHAPE;
+  if (variant < 0 || variant >= EW_NCFG) return KGS_ERR_ARG;
   if (n == 0) return 0;
   const bool aligned = ((uintptr_t)a % 16 == 0) && ((uintptr_t)b % 16 == 0) && ((uintptr_t)c % 16 == 0);
   long n8 = aligned ? n / 8 : 0;
-  if (n8) hipLaunchKernelGGL(kgs::vadd_bf16, dim3(kgs::blocks_for(n8)), dim3(kgs::EW_THREADS), 0, s,
-                             (const bf16x8*)a, (const bf16x8*)b, (bf16x8*)c, n8);
+  if (n8) KGS_EW_LAUNCH(kgs::vadd_bf16, bf16x8, a, b, c, n8, EW_CFGS[variant], s);
   long rest = n - n8 * 8;
   if (rest)
     hipLaunchKernelGGL(kgs::vadd_bf16_tail, dim3((rest + 255) / 256), dim3(256), 0, s,
@@ -137,13 +247,36 @@ KGS_EXPORT int kgs_vector_add_bf16(const void* a, const void* b, void* c, long n
   return (int)hipGetLastError();
 }
 
+KGS_EXPORT int kgs_vector_add_f32(const void* a, const void* b, void* c, long n, hipStream_t s) {
+  return kgs_vector_add_f32_v(a, b, c, n, 0, s);
+}
+
+KGS_EXPORT int kgs_vector_add_bf16(const void* a, const void* b, void* c, long n, hipStream_t s) {
+  return kgs_vector_add_bf16_v(a, b, c, n, 0, s);
+}
+
+// variant 0 = auto (16-B path when rows, cols, both ld % 8 == 0 and pointers
+// are 16-B aligned), 1 = element-wise tile, 2 = force the 16-B path.
+KGS_EXPORT int kgs_transpose_bf16_v(const void* in, void* out, int rows, int cols, int ld_in, int ld_out, int variant,
+                                    hipStream_t s) {
+  if (rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return KGS_ERR_SHAPE;
+  const bool v8ok = rows % 8 == 0 && cols % 8 == 0 && ld_in % 8 == 0 && ld_out % 8 == 0 &&
+                    ((uintptr_t)in | (uintptr_t)out) % 16 == 0;
+  if (variant == 2 && !v8ok) return KGS_ERR_ALIGN;
+  if (variant < 0 || variant > 2) return KGS_ERR_ARG;
+  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
+  if (variant != 1 && v8ok)
+    hipLaunchKernelGGL(kgs::transpose_bf16_v8, grid, dim3(256), 0, s, (const bf16x8*)in, (bf16x8*)out, rows, cols,
+                       ld_in / 8, ld_out / 8);
+  else
+    hipLaunchKernelGGL(kgs::transpose_bf16, grid, dim3(256), 0, s, (const unsigned short*)in, (unsigned short*)out,
+                       rows, cols, ld_in, ld_out);
+  return (int)hipGetLastError();
+}
+
 KGS_EXPORT int kgs_transpose_bf16(const void* in, void* out, int rows, int cols, int ld_in, int ld_out,
                                   hipStream_t s) {
-  if (rows <= 0 || cols <= 0 || ld_in < cols || ld_out < rows) return KGS_ERR_SHAPE;
-  dim3 grid((cols + 63) / 64, (rows + 63) / 64);
-  hipLaunchKernelGGL(kgs::transpose_bf16, grid, dim3(256), 0, s, (const unsigned short*)in, (unsigned short*)out,
-                     rows, cols, ld_in, ld_out);
-  return (int)hipGetLastError();
+  return kgs_transpose_bf16_v(in, out, rows, cols, ld_in, ld_out, 0, s);
 }
 
 // out2 must hold 2 floats, zeroed by the caller (sum, sum|x|). n % 8 == 0, 16-B aligned.
