@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
 import socket
 import subprocess
 import sys
@@ -57,15 +58,7 @@ def allocated_gpus() -> list:
 def rocminfo_agents(timeout: int = 60) -> dict:
     """GPU agents reported by ``rocminfo`` (run as a child process: the parent
     never initialises the GPU itself)."""
-    exe = None
-    for cand in ("rocminfo", "/opt/rocm/bin/rocminfo"):
-        for d in [""] + os.environ.get("PATH", "").split(os.pathsep):
-            path = os.path.join(d, cand) if d else cand
-            if os.path.isfile(path) and os.access(path, os.X_OK):
-                exe = path
-                break
-        if exe:
-            break
+    exe = shutil.which("rocminfo") or shutil.which("rocminfo", path="/opt/rocm/bin")
     if exe is None:
         return {"ok": False, "error": "rocminfo not found"}
     try:

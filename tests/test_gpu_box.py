@@ -90,3 +90,16 @@ def test_workload_entrypoint_smoke_mode():
     assert "gfx950" in res["rocminfo"]["gpu_agents"]
     assert res["ranks"][0]["vector_add"]["ok"]
     assert all("gemm" not in r for r in res["ranks"])
+
+
+def test_workload_entrypoint_counters(tmp_path):
+    """BASELINE config 3: the pod's GEMM re-run under rocprofv3 (--pmc passes only,
+    never combined with tracing), summarised to MFMA busy / LDS conflicts / L2 hit."""
+    env = dict(ENV, TMPDIR="/tmp")
+    r = subprocess.run([sys.executable, "-m", "kgs.workload.entrypoint", "--nproc", "1", "--gemm-size", "4096",
+                        "--gemm-iters", "3", "--counters", "--counters-dir", str(tmp_path / "prof")],
+                       env=env, capture_output=True, text=True, timeout=900, cwd="/tmp")
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = _last_json(r.stdout)
+    assert all(v is True for v in res["counters"]["passes"].values()), res["counters"]
+    assert "MFMA busy" in r.stdout and "L2 hit" in r.stdout
