@@ -151,3 +151,33 @@ def test_bench_distributed_plumbing_gloo():
     assert j0["config"]["parallelism"] == "dp2" and j0["config"]["global_batch"] == 8
     assert j0["ms_per_step"] > 0 and j0["backend"] == "torch"
     assert abs(j0["value"] - 2 * j0["per_gpu_tflops"]) <= 0.011  # aggregate = world x per-GPU (rounded)
+
+
+MLP_DIMS = [64, 96, 48, 32]
+
+
+def _mlp_dp(rank, world):
+    from kgs.models.mlp import train_dp
+    from kgs.parallel import dist as kdist
+
+    ctx = kdist.init_from_env(device_type="cpu")
+    r = train_dp(MLP_DIMS, steps=4, global_batch=64, lr=0.1, backend="torch", device="cpu", group=ctx.group,
+                 bucket_mb=0.01, dtype=torch.float32)  # tiny buckets: several all-reduces per step
+    return [p.detach().clone() for p in r["model"].parameters()], r["losses"]
+
+
+def test_mlp_dp_matches_single_process_full_batch():
+    """DP over 2 gloo ranks (bucketed, backward-overlapped all-reduce) must train
+    the same weights as one process on the whole batch."""
+    from kgs.models.mlp import train_dp
+
+    res = _spawn(_mlp_dp)
+    ref = train_dp(MLP_DIMS, steps=4, global_batch=64, lr=0.1, backend="torch", device="cpu",
+                   dtype=torch.float32)
+    ref_params = [p.detach() for p in ref["model"].parameters()]
+    for rank in (0, 1):
+        params, losses = res[rank]
+        for p, q in zip(params, ref_params):
+            torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
+        assert abs(losses[-1] - ref["losses"][-1]) < 1e-5
+    assert ref["losses"][-1] < ref["losses"][0]
