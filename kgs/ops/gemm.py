@@ -2,10 +2,12 @@
 
 ``gemm_nt(a, b)`` computes ``a @ b.T`` for ``a: [M, K]``, ``b: [N, K]`` (both
 K-contiguous bf16 on a gfx950 device), with optional fused bias + activation in
-the kernel epilogue. ``gemm_fp8_nt`` is the same pipeline on OCP e4m3 operands
-with the scaled fp8 MFMA and a per-tensor dequant scale. ``matmul`` and ``Linear`` are built on it; the backward pass
-re-uses the same NT kernel after a HIP transpose, so every FLOP of the in-pod
-workload runs on the hand-written MFMA kernel.
+the kernel epilogue. :func:`gemm_bf16` covers the other layouts: operands stored
+K-major are read with ``ds_read_b64_tr_b16``, so no transpose copy is made.
+``gemm_fp8_nt`` is the same pipeline on OCP e4m3 operands with the scaled fp8
+MFMA and a per-tensor dequant scale. ``matmul`` and ``Linear`` are built on
+these; the backward pass uses the transposed-read layouts, so every FLOP of the
+in-pod workload runs on the hand-written MFMA kernel.
 """
 from __future__ import annotations
 
@@ -165,9 +167,65 @@ def transpose(x: torch.Tensor) -> torch.Tensor:
     return transpose_bf16(x)
 
 
+TR_READ_A = False        # route K-major A through ds_read_b64_tr_b16 (else transpose + NT)
+TR_READ_B_MAX_M = 4096   # K-major B: tr reads up to this M, transpose + NT above
+
+
+def gemm_bf16(a: torch.Tensor, b: torch.Tensor, trans_a: bool = False, trans_b: bool = False,
+         bias: torch.Tensor | None = None, act: str | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``op(a) @ op(b)`` for row-major bf16 matrices, any of the four layouts:
+
+    * ``trans_a=False``: ``a`` is [M, K];  ``trans_a=True``: ``a`` is [K, M] (use ``a.T``)
+    * ``trans_b=False``: ``b`` is [K, N];  ``trans_b=True``: ``b`` is [N, K] (the NT layout)
+
+    (so ``gemm_bf16(a, b) == a @ b`` and ``gemm_bf16(a, b, trans_b=True) == a @ b.T``).
+    A K-major operand is either read in place through the pipeline's
+    transposed-read path (``ds_read_b64_tr_b16``, aligned shapes) or
+    materialised by the 6.3 TB/s HIP transpose and fed to the NT kernel,
+    whichever measured faster for the shape (module constants below).
+    """
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = (a.shape[1], a.shape[0]) if trans_a else (a.shape[0], a.shape[1])
+    N, K2 = (b.shape[0], b.shape[1]) if trans_b else (b.shape[1], b.shape[0])
+    if K != K2:
+        raise ValueError(f"inner dims differ: op(a) {M}x{K}, op(b) {K2}x{N}")
+    ta, tb = int(trans_a), int(not trans_b)  # kernel flags: 1 = operand stored [K][rows]
+    if ta and not TR_READ_A:
+        # measured: the tr-read A path runs ~20 % behind a 6.3 TB/s transpose + NT
+        # at 8192^3 and ties at 4096^3 (profiles/gemm_layouts.json)
+        a, ta = transpose(a), 0
+    if tb and M > TR_READ_B_MAX_M:
+        # the B transpose costs ~ 476/M of the GEMM time; above M = 4096 it is
+        # cheaper than the tr-read path's LDS cost (profiles/gemm_layouts.json)
+        b, tb = transpose(b), 0
+    if not ta and not tb:
+        return gemm_nt(a, b, bias=bias, act=act, out=out)
+    epi_name = act if act is not None else ("bias" if bias is not None else None)
+    if epi_name not in EPI:
+        raise ValueError(f"unknown activation {act!r}")
+    epi = EPI[epi_name]
+    if epi and bias is None:
+        bias = torch.zeros(N, dtype=torch.bfloat16, device=a.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    so = _lib.lib()
+    ok = so.kgs_gemm_bf16_layout_ok(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                    out.stride(0), ta, tb)
+    if not ok or (bias is not None and bias.data_ptr() % 8):
+        aa = transpose(a) if ta else a
+        bb = transpose(b) if tb else b
+        return gemm_nt(aa, bb, bias=bias, act=act, out=out)
+    rc = so.kgs_gemm_bf16(a.data_ptr(), b.data_ptr(), out.data_ptr(), bias.data_ptr() if bias is not None else None,
+                          M, N, K, a.stride(0), b.stride(0), out.stride(0), ta, tb, epi,
+                          _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm[{M}x{N}x{K}, ta={ta}, tb={tb}]")
+    return out
+
+
 def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """``a @ b`` with ``b: [K, N]`` row-major: one HIP transpose + the NT kernel."""
-    return gemm_nt(a, transpose(b))
+    """``a @ b`` with ``b: [K, N]`` row-major (transposed-read path, no transpose copy)."""
+    return gemm_bf16(a, b)
 
 
 class _LinearFn(torch.autograd.Function):
@@ -195,10 +253,10 @@ class _LinearFn(torch.autograd.Function):
                 y = _act(z, ctx.act)
             (gz,) = torch.autograd.grad(y, z, gy.float())
             gy = gz.to(torch.bfloat16).contiguous()
-        # dX[M,K] = dY[M,N] . W[N,K]      -> NT with B = W^T [K,N]
-        gx = gemm_nt(gy, transpose(w))
-        # dW[N,K] = dY^T[N,M] . X[M,K]    -> NT with A = dY^T [N,M], B = X^T [K,M]
-        gw = gemm_nt(transpose(gy), transpose(x))
+        # dX[M,K] = dY[M,N] . W[N,K]      (W read K-major: transposed-read path)
+        gx = gemm_bf16(gy, w)
+        # dW[N,K] = dY^T[N,M] . X[M,K]    (both operands M-major)
+        gw = gemm_bf16(gy, x, trans_a=True)
         gb = gy.float().sum(0).to(torch.bfloat16) if bias is not None else None
         return gx, gw, gb, None
 

@@ -90,6 +90,12 @@ struct Ctx {
   __amdgpu_buffer_rsrc_t ra, rb;
   int K, kc0, kc1;                 // K and the lane's logical chunk column (elements)
   int a_half_i, b_half_i;          // 128*lda, 128*ldb as int
+  // transposed operands (S bits 11/12: A stored [K][M] / B stored [K][N]):
+  // half-tiles are [64 k][128 cols] with 256-B rows, read with
+  // ds_read_b64_tr_b16; see read_a_tr / read_b_tr
+  long a_kstride, b_kstride;       // elements between consecutive k (lda / ldb)
+  int tr_base;                     // per-lane byte offset of the tr-read block
+  int tr_x;                        // per-lane chunk XOR (2 * gsw)
 };
 
 constexpr int OOB_OFFSET = 0x7FFFFFF0;  // > every num_records the bounded path builds
@@ -100,9 +106,19 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int PART, bool BND = false>
+template <int PART, bool BND = false, bool TR = false>
 __device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
   char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048;
+  if constexpr (TR) {
+    // operand stored [K][cols]: the half-tile is 64 k-rows x 128 columns; the
+    // per-lane offsets already hold row*ld + swizzled column
+    constexpr bool isA = PART == P_A0 || PART == P_A1;
+    const unsigned short* src = (isA ? c.Ag : c.Bg) + ((PART == P_A1 || PART == P_B1) ? 128 : 0) +
+                                (long)k0 * (isA ? c.a_kstride : c.b_kstride);
+    glds16(src + (isA ? c.offA0 : c.offB0), dst);
+    glds16(src + (isA ? c.offA1 : c.offB1), dst + 1024);
+    return;
+  }
   if constexpr (BND) {
     constexpr bool isA = PART == P_A0 || PART == P_A1;
     const int half = PART == P_A1 ? c.a_half_i : PART == P_B1 ? c.b_half_i : 0;
@@ -146,6 +162,62 @@ __device__ __forceinline__ void read_b(const CtxT& c, Regs& R, const char* half)
     R.b[NH][n][0] = *(const bf16x8*)(p + n * 16 * 128 + c.ro0);
     R.b[NH][n][1] = *(const bf16x8*)(p + n * 16 * 128 + c.ro1);
   }
+}
+
+// Transposed operands. Half-tile image: [64 k][128 cols] bf16, 256-B rows,
+// 16-B chunk c of row r stored at c ^ (2 * gsw(r)), gsw(r) = (r & 3) | ((r >> 3) & 1) << 2.
+// An MFMA fragment (8 consecutive k of one column per lane) is two
+// ds_read_b64_tr_b16: in each 16-lane group, lane 4q+p addresses row k0+q,
+// columns 4p..4p+3 and receives its own column over the 4 rows. Per 32-lane
+// half the 8 rows {0-3, 8-11} (+4 for the second read) hit 8 distinct gsw
+// values, so the 16 chunks read land on 16 distinct bank groups: no conflicts.
+typedef short bf16x4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* p) {
+  const bf16x4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)p);
+  const bf16x4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(p + 4 * 256));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// column chunk base `ch` (even) -> byte offset of this lane's tr-read address
+__device__ __forceinline__ int tr_col(const Ctx& c, int ch) { return ((ch ^ c.tr_x) << 4) + c.tr_base; }
+
+__device__ __forceinline__ void read_a_tr(const Ctx& c, Regs& R, const char* half) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const char* p = half + tr_col(c, c.wr * 8 + 2 * i);
+    R.a[i][0] = tr_frag(p);
+    R.a[i][1] = tr_frag(p + 32 * 256);
+  }
+}
+
+template <int NH>
+__device__ __forceinline__ void read_b_tr(const Ctx& c, Regs& R, const char* half) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const char* p = half + tr_col(c, c.wc * 4 + 2 * n);
+    R.b[NH][n][0] = tr_frag(p);
+    R.b[NH][n][1] = tr_frag(p + 32 * 256);
+  }
+}
+
+// S bit 13 / 14 (timing probes, wrong results): keep the transposed DMA but read
+// with ds_read_b128 (13), or keep the tr reads but DMA in the NT pattern (14)
+template <int S>
+__device__ __forceinline__ void rd_a(const Ctx& c, Regs& R, const char* half) {
+  if constexpr ((S & 2048) && !(S & 8192)) read_a_tr(c, R, half); else read_a(c, R, half);
+}
+
+template <int NH, int S>
+__device__ __forceinline__ void rd_b(const Ctx& c, Regs& R, const char* half) {
+  if constexpr (S & 4096) read_b_tr<NH>(c, R, half); else read_b<NH>(c, R, half);
+}
+
+template <int PART, int S>
+__device__ __forceinline__ void issue_s(const Ctx& c, int buf, int k0) {
+  constexpr bool isA = PART == P_A0 || PART == P_A1;
+  constexpr bool tr = (S & 16384) ? false : isA ? (S & 2048) != 0 : (S & 4096) != 0;
+  issue<PART, (S & 512) != 0, tr>(c, buf, k0);
 }
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -205,18 +277,18 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   const char* buf = c.smem + cbuf * BUF_BYTES;
   if constexpr ((S & 1) == 0) {
     if constexpr (q == 0) {
-      read_a(c, R, buf + P_A0 * HALF_BYTES);
-      read_b<0>(c, R, buf + P_B0 * HALF_BYTES);
+      rd_a<S>(c, R, buf + P_A0 * HALF_BYTES);
+      rd_b<0, S>(c, R, buf + P_B0 * HALF_BYTES);
     } else if constexpr (q == 1) {
-      read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
+      rd_b<1, S>(c, R, buf + P_B1 * HALF_BYTES);
     } else if constexpr (q == 2) {
-      read_a(c, R, buf + P_A1 * HALF_BYTES);
+      rd_a<S>(c, R, buf + P_A1 * HALF_BYTES);
     }
   } else {
-    if constexpr (q == 0) read_a(c, R, buf + P_A0 * HALF_BYTES);
-    if constexpr (q == 1) read_b<1>(c, R, buf + P_B1 * HALF_BYTES);
-    if constexpr (q == 2) read_a(c, R, buf + P_A1 * HALF_BYTES);
-    if constexpr (q == 3) read_b<0>(c, R, c.smem + (cbuf ^ 1) * BUF_BYTES + P_B0 * HALF_BYTES);
+    if constexpr (q == 0) rd_a<S>(c, R, buf + P_A0 * HALF_BYTES);
+    if constexpr (q == 1) rd_b<1, S>(c, R, buf + P_B1 * HALF_BYTES);
+    if constexpr (q == 2) rd_a<S>(c, R, buf + P_A1 * HALF_BYTES);
+    if constexpr (q == 3) rd_b<0, S>(c, R, c.smem + (cbuf ^ 1) * BUF_BYTES + P_B0 * HALF_BYTES);
   }
   // prefetch half-tile h = 8*it + QP + look-ahead
   constexpr int LA = (S & 1) == 0 ? LOOKAHEAD : 7;
@@ -227,7 +299,7 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
                                     : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
   int t = 2 * it + toff;
   t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
-  issue<part, (S & 512) != 0>(c, toff & 1, t * BK);
+  issue_s<part, S>(c, toff & 1, t * BK);
   if constexpr ((S & 1) == 0)
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else
@@ -283,8 +355,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   Ctx c;
   c.smem = smem;
   // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
-  c.Ag = A + (long)((S & 32) ? 0 : tm) * BM * lda;
-  c.Bg = B + (long)((S & 32) ? 0 : tn) * BN * ldb;
+  c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;
+  c.Bg = (S & 4096) ? B + (long)tn * BN : B + (long)((S & 32) ? 0 : tn) * BN * ldb;
+  c.a_kstride = lda;
+  c.b_kstride = ldb;
   c.a_half = 128L * lda;
   c.b_half = 128L * ldb;
   c.w = w;
@@ -312,6 +386,26 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     c.offB1 = r1 * ldb + c1 * 8;
     c.kc0 = c0 * 8;
     c.kc1 = c1 * 8;
+    if constexpr ((S & 2048) || (S & 4096)) {
+      // [64 k][128 col] half-tiles: glds j of wave w fills rows 4*(2w+j) + lane/16;
+      // lane's physical chunk lane&15 holds logical chunk (lane&15) ^ (2 gsw(row))
+      const int tr0 = 4 * (2 * w) + (lane >> 4), tr1 = tr0 + 4;
+      const int g0 = (tr0 & 3) | (((tr0 >> 3) & 1) << 2), g1 = (tr1 & 3) | (((tr1 >> 3) & 1) << 2);
+      const int lc0 = (lane & 15) ^ (2 * g0), lc1 = (lane & 15) ^ (2 * g1);
+      if constexpr ((S & 2048) && !(S & 16384)) {
+        c.offA0 = tr0 * lda + lc0 * 8;
+        c.offA1 = tr1 * lda + lc1 * 8;
+      }
+      if constexpr (S & 4096) {
+        c.offB0 = tr0 * ldb + lc0 * 8;
+        c.offB1 = tr1 * ldb + lc1 * 8;
+      }
+      // tr reads: 16-lane group g (= lane>>4) takes rows 8g + q (q = (lane&15)>>2)
+      // and columns 4p..4p+3 (p = lane&3) of the fragment's 16-column block
+      const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+      c.tr_x = 2 * (q | ((g & 1) << 2));
+      c.tr_base = (8 * g + q) * 256 + (pp >> 1) * 16 + (pp & 1) * 8;
+    }
     // fragment read: row lane&15, logical chunk 4*s + lane/16
     const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
     c.ro0 = fr * 128 + ((fq ^ f) * 16);
@@ -331,25 +425,25 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
   if constexpr ((S & 1) == 0) {
     // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
-    issue<P_A0, BND>(c, 0, 0);
-    issue<P_B0, BND>(c, 0, 0);
-    issue<P_B1, BND>(c, 0, 0);
-    issue<P_A1, BND>(c, 0, 0);
-    issue<P_A0, BND>(c, 1, k1);
+    issue_s<P_A0, S>(c, 0, 0);
+    issue_s<P_B0, S>(c, 0, 0);
+    issue_s<P_B1, S>(c, 0, 0);
+    issue_s<P_A1, S>(c, 0, 0);
+    issue_s<P_A0, S>(c, 1, k1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
     bar();
   } else {
     // prologue: half-tiles 0..6 = B0 A0 B1 A1 of tile 0, B0 A0 B1 of tile 1
-    issue<P_B0, BND>(c, 0, 0);
-    issue<P_A0, BND>(c, 0, 0);
-    issue<P_B1, BND>(c, 0, 0);
-    issue<P_A1, BND>(c, 0, 0);
-    issue<P_B0, BND>(c, 1, k1);
-    issue<P_A0, BND>(c, 1, k1);
-    issue<P_B1, BND>(c, 1, k1);
+    issue_s<P_B0, S>(c, 0, 0);
+    issue_s<P_A0, S>(c, 0, 0);
+    issue_s<P_B1, S>(c, 0, 0);
+    issue_s<P_A1, S>(c, 0, 0);
+    issue_s<P_B0, S>(c, 1, k1);
+    issue_s<P_A0, S>(c, 1, k1);
+    issue_s<P_B1, S>(c, 1, k1);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B0,A0 of tile 0 landed
     bar();
-    read_b<0>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
+    rd_b<0, S>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
   }
   // stagger: waves 4-7 trail by one barrier (S bit 6: lockstep experiment, no stagger)
   if (!(S & 64) && c.wr == 1) bar();
@@ -1337,6 +1431,80 @@ KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void
       break;
     case kgs::EPI_BIAS_SILU:
       e = launch_fp8<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      break;
+    default: return KGS_ERR_ARG;
+  }
+  return (int)e;
+}
+
+// ---------------------------------------------------------------------------
+// General layouts: C[M,N] = epilogue(op(A) . op(B)) with
+//   ta = 0: A stored [M][K] (K contiguous)     ta = 1: A stored [K][M]
+//   tb = 0: B stored [N][K] (the NT layout)    tb = 1: B stored [K][N]
+// The transposed operands go through the same pipeline: their half-tiles are
+// staged as [64 k][128 cols] and read with ds_read_b64_tr_b16, so no
+// materialised transpose is needed (Linear backward: dX = dY.W is tb=1,
+// dW = dY^T.X is ta=1, tb=1). Aligned shapes only (M, N % 256, K % 128).
+// ---------------------------------------------------------------------------
+namespace {
+
+template <int EPI, int T>
+hipError_t launch_t(const unsigned short* A, const unsigned short* B, unsigned short* C, const unsigned short* bias,
+                    int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s) {
+  using namespace kgs;
+  const dim3 grid((M / g256::BM) * (N / g256::BN));
+  hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + T>), grid, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
+                     1.0f);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_layout(int ta, int tb, const unsigned short* A, const unsigned short* B, unsigned short* C,
+                         const unsigned short* bias, int M, int N, int K, int lda, int ldb, int ldc, hipStream_t s) {
+  if constexpr (EPI == kgs::EPI_NONE) {
+    if (ta == 2) return launch_t<EPI, 2048 + 8192>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);   // probe
+    if (ta == 3) return launch_t<EPI, 2048 + 16384>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);  // probe
+  }
+  if (ta && tb) return launch_t<EPI, 2048 + 4096>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+  if (ta) return launch_t<EPI, 2048>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+  return launch_t<EPI, 4096>(A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+}
+
+}  // namespace
+
+KGS_EXPORT int kgs_gemm_bf16_layout_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
+                                       int ldb, int ldc, int ta, int tb) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  if (M % 256 || N % 256 || K % 128) return 0;
+  if (lda % 8 || ldb % 8 || ldc % 8) return 0;
+  if (lda < (ta ? M : K) || ldb < (tb ? N : K) || ldc < N) return 0;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return 0;
+  // per-tile 32-bit lane offsets: 256 rows (NT) or 64 k-rows (transposed) times ld
+  if ((long)lda * 256 >= (1L << 31) || (long)ldb * 256 >= (1L << 31)) return 0;
+  return 1;
+}
+
+KGS_EXPORT int kgs_gemm_bf16(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                             int ldb, int ldc, int ta, int tb, int epi, hipStream_t stream) {
+  if (!ta && !tb) return kgs_gemm_bf16_nt(A, B, C, bias, M, N, K, lda, ldb, ldc, epi, 0, stream);
+  if (epi != kgs::EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
+  if (!kgs_gemm_bf16_layout_ok(A, B, C, M, N, K, lda, ldb, ldc, ta, tb)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto bb = (const unsigned short*)bias;
+  hipError_t e;
+  switch (epi) {
+    case kgs::EPI_NONE: e = launch_layout<kgs::EPI_NONE>(ta, tb, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS: e = launch_layout<kgs::EPI_BIAS>(ta, tb, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
+    case kgs::EPI_BIAS_GELU:
+      e = launch_layout<kgs::EPI_BIAS_GELU>(ta, tb, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
+      break;
+    case kgs::EPI_BIAS_RELU:
+      e = launch_layout<kgs::EPI_BIAS_RELU>(ta, tb, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
+      break;
+    case kgs::EPI_BIAS_SILU:
+      e = launch_layout<kgs::EPI_BIAS_SILU>(ta, tb, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
       break;
     default: return KGS_ERR_ARG;
   }

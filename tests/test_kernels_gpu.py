@@ -306,3 +306,60 @@ def test_gemm_fp8_epilogue_and_bounded_equals_fast():
     c = gemm_fp8_nt(qa, qb, sa, sb, bias=bias, act="gelu")
     torch.testing.assert_close(c.float(), _fp8_ref(qa, sa, qb, sb, bias, "gelu"), rtol=2e-2, atol=2e-2)
     assert torch.equal(gemm_fp8_nt(qa, qb, sa, sb, variant="bounded"), gemm_fp8_nt(qa, qb, sa, sb, variant="fast"))
+
+
+# ------------------------------------------------- transposed-read layouts --
+@pytest.mark.parametrize("force_tr", [True, False])
+@pytest.mark.parametrize("trans_a,trans_b", [(False, False), (True, False), (True, True), (False, True)])
+@pytest.mark.parametrize("M,N,K", [(256, 512, 128), (1024, 768, 2048), (512, 512, 384)])
+def test_gemm_layouts_bitwise_vs_nt(trans_a, trans_b, M, N, K, force_tr, monkeypatch):
+    """Every layout, through the tr-read path (forced) and through the measured
+    default routing, must equal the NT kernel on the explicitly transposed
+    operands bit for bit (same K order per accumulator)."""
+    import kgs.ops.gemm as gm
+    from kgs.ops import gemm_bf16 as gemm
+    from kgs.ops import gemm_nt
+
+    if force_tr:
+        monkeypatch.setattr(gm, "TR_READ_A", True)
+        monkeypatch.setattr(gm, "TR_READ_B_MAX_M", 1 << 30)
+
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a_mk = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b_nk = (torch.rand(N, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    a = a_mk.t().contiguous() if trans_a else a_mk
+    b = b_nk if trans_b else b_nk.t().contiguous()
+    c = gemm(a, b, trans_a=trans_a, trans_b=trans_b)
+    ref = gemm_nt(a_mk, b_nk)
+    assert torch.equal(c, ref)
+    assert _rel_err(c, _ref_nt(a_mk, b_nk)) < 1e-2
+
+
+def test_gemm_layout_asymmetric_identity(monkeypatch):
+    """A = I stored K-major, B asymmetric stored K-major: C must be B exactly
+    (tr-read path forced for both operands)."""
+    import kgs.ops.gemm as gm
+    from kgs.ops import gemm_bf16 as gemm
+
+    monkeypatch.setattr(gm, "TR_READ_A", True)
+    monkeypatch.setattr(gm, "TR_READ_B_MAX_M", 1 << 30)
+
+    M = K = 256
+    N = 512
+    eye = torch.eye(K, device=DEV).bfloat16()
+    b_kn = ((torch.arange(K * N, device=DEV) % 97) - 48).float().reshape(K, N).bfloat16()
+    c = gemm(eye, b_kn, trans_a=True)  # A stored [K][M]; B stored [K][N]
+    assert torch.equal(c, b_kn)
+
+
+def test_gemm_layout_epilogue_and_fallback():
+    from kgs.ops import gemm_bf16 as gemm
+
+    a = (torch.rand(300, 96, device=DEV) - 0.5).bfloat16()   # ragged: falls back to transpose + NT
+    b = (torch.rand(96, 200, device=DEV) - 0.5).bfloat16()
+    torch.testing.assert_close(gemm(a, b).float(), a.float() @ b.float(), rtol=2e-2, atol=2e-2)
+    a = (torch.rand(512, 256, device=DEV) - 0.5).bfloat16()
+    b = (torch.rand(256, 768, device=DEV) - 0.5).bfloat16()
+    bias = torch.randn(768, device=DEV).bfloat16()
+    ref = torch.nn.functional.gelu(a.float() @ b.float() + bias.float(), approximate="tanh")
+    torch.testing.assert_close(gemm(a, b, bias=bias, act="gelu").float(), ref, rtol=2e-2, atol=2e-2)
