@@ -41,9 +41,11 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--m", type=int, default=8192)
-    ap.add_argument("--n", type=int, default=8192)
-    ap.add_argument("--k", type=int, default=8192)
+    # --gemm-m/n/k (not --m/--n/--k: torchrun's parser would take those as
+    # abbreviations of its own options)
+    ap.add_argument("--gemm-m", "--m", dest="m", type=int, default=8192)
+    ap.add_argument("--gemm-n", "--n", dest="n", type=int, default=8192)
+    ap.add_argument("--gemm-k", "--k", dest="k", type=int, default=8192)
     ap.add_argument("--gemms-per-step", type=int, default=4)
     ap.add_argument("--allreduce-mb", type=float, default=64.0, help="gradient bucket all-reduced per step (MiB)")
     ap.add_argument("--no-overlap", action="store_true", help="run the all-reduce after the GEMMs, same stream")

@@ -130,7 +130,7 @@ def _bench_rank(rank, world):
 
     buf = io.StringIO()
     with contextlib.redirect_stdout(buf):
-        rc = bench.main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--m", "64", "--n", "64", "--k", "64",
+        rc = bench.main(["--gpus", str(world), "--steps", "2", "--warmup", "1", "--gemm-m", "64", "--gemm-n", "64", "--gemm-k", "64",
                          "--allreduce-mb", "0.25", "--backend", "torch", "--cpu"])
     out = buf.getvalue().strip()
     return rc, (json.loads(out) if out else None)
