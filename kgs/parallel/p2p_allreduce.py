@@ -17,6 +17,11 @@ Algorithms (native/kernels/allreduce_p2p.hip):
 * ``twoshot`` -- reduce-scatter into the staging buffers, then all-gather:
   2(N-1)/N of the message per rank. Wins once the message is bandwidth-bound.
 
+Every call is one kernel whose barrier epoch lives on the device (a per-block
+counter in the rank's signal block), so calls can be captured in a hipGraph
+(``torch.cuda.CUDAGraph``) and replayed: a TP layer's GEMM + all-reduce chain
+becomes one graph launch.
+
 ``algo="auto"`` picks one-shot up to :attr:`oneshot_max_bytes` (256 KiB at
 8 ranks, 1 MiB at <= 4), two-shot above, and RCCL (``dist.all_reduce``) beyond
 ``max_bytes`` or for unsupported dtypes/shapes -- results are then identical in
@@ -143,7 +148,9 @@ class P2PAllReduce:
         return max(1, min(cap, math.ceil(nvec / per_block)))
 
     def _next_epoch(self) -> int:
-        # flags start at 0, so epoch 0 is never used; uint32 wrap skips it too
+        """Host-side call numbers (diagnostics only; the API uses the device
+        counters -- never mix the two on one instance). Flags start at 0, so
+        epoch 0 is never used; the uint32 wrap skips it too."""
         self._epoch = self._epoch % 0xFFFFFFFF + 1
         return self._epoch
 
@@ -176,12 +183,14 @@ class P2PAllReduce:
         nbytes = t.numel() * t.element_size()
         algo = self.pick_algo(nbytes) if algo == "auto" else algo
         out = torch.empty_like(t) if out is None else out
-        self._launch(self.rank, t, out, algo, self._next_epoch(), _lib.stream_handle(self.device))
+        # epoch 0: the kernel keeps the call count on the device, so the call
+        # can be captured in a hipGraph (torch.cuda.CUDAGraph) and replayed
+        self._launch(self.rank, t, out, algo, 0, _lib.stream_handle(self.device))
         return out
 
-    def all_reduce_local(self, inputs: list, algo: str = "auto") -> list:
+    def all_reduce_local(self, inputs: list, algo: str = "auto", outs: list | None = None) -> list:
         """local_ranks instances: reduce ``inputs[r]`` (rank r's tensor) with one
-        launch on the current stream; returns the N outputs."""
+        launch on the current stream; returns the N outputs (``outs`` if given)."""
         if not self.local:
             raise RuntimeError("not a local_ranks instance")
         if len(inputs) != self.world:
@@ -191,10 +200,10 @@ class P2PAllReduce:
             raise ValueError("inputs must be equal-shape contiguous f32/bf16 tensors on this device, 16-B sized")
         nbytes = t0.numel() * t0.element_size()
         algo = self.pick_algo(nbytes) if algo == "auto" else algo
-        outs = [torch.empty_like(x) for x in inputs]
+        outs = [torch.empty_like(x) for x in inputs] if outs is None else outs
         ins = (ctypes.c_void_p * self.world)(*[x.data_ptr() for x in inputs])
         outp = (ctypes.c_void_p * self.world)(*[o.data_ptr() for o in outs])
-        self._run(-1, ins, outp, nbytes, t0.dtype, algo, self._next_epoch(), _lib.stream_handle(self.device))
+        self._run(-1, ins, outp, nbytes, t0.dtype, algo, 0, _lib.stream_handle(self.device))
         return outs
 
     def check(self) -> None:

@@ -21,7 +21,10 @@
 // exactly the data they share. A flag store is a system-scope release (L2
 // write-back of the copied data before the flag), a flag poll a system-scope
 // acquire (L2/L1 invalidate before the peer data is read). Flags carry an epoch
-// that the host bumps on every call, so they never need resetting. Every poll
+// (the host's, or -- epoch argument 0 -- a per-block counter kept in the rank's
+// own signal block, so a captured hipGraph replays correctly: every replay
+// reads and bumps the counter on the device) that changes on every call, so
+// flags never need resetting. Every poll
 // is bounded by a wall-clock timeout (s_memrealtime, 100 MHz): a missing peer
 // sets a bit in *err and the kernel drains instead of hanging the GPU.
 #include <cstring>
@@ -38,6 +41,7 @@ constexpr int PHASES = 4;
 
 struct Signal {
   unsigned flag[PHASES][MAX_BLOCKS][MAX_RANKS];
+  unsigned epoch[MAX_BLOCKS];  // device-side call counter of this rank's block b
 };
 
 struct Ptrs {
@@ -63,6 +67,18 @@ __device__ __forceinline__ Who who(int rank_arg, int nb) {
   if (rank_arg >= 0) return {rank_arg, (int)blockIdx.x, 0};
   const int r = blockIdx.x / nb;
   return {r, (int)blockIdx.x - r * nb, r};
+}
+
+// host epoch, or (host_epoch == 0) this block's device counter + 1, skipping 0
+__device__ __forceinline__ unsigned call_epoch(const Ptrs& P, const Who& me, unsigned host_epoch) {
+  if (host_epoch) return host_epoch;
+  const unsigned e = P.sig[me.rank]->epoch[me.b] + 1;
+  return e ? e : 1;
+}
+
+// after the end barrier: the next launch (stream-ordered) sees the new counter
+__device__ __forceinline__ void commit_epoch(const Ptrs& P, const Who& me, unsigned host_epoch, unsigned e) {
+  if (!host_epoch && threadIdx.x == 0) P.sig[me.rank]->epoch[me.b] = e;
 }
 
 __device__ __forceinline__ unsigned long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -146,6 +162,8 @@ template <bool BF16, int NR>
 __global__ __launch_bounds__(THREADS) void allreduce_oneshot(Ptrs P, IO io, int rank_arg, int nb, long nvec,
                                                              unsigned epoch, unsigned long timeout, int* err) {
   const Who me = who(rank_arg, nb);
+  const unsigned host_epoch = epoch;
+  epoch = call_epoch(P, me, host_epoch);
   const long stride = (long)nb * THREADS;
   const long i0 = (long)me.b * THREADS + threadIdx.x;
   const uint4* __restrict__ in = io.in[me.slot];
@@ -155,12 +173,15 @@ __global__ __launch_bounds__(THREADS) void allreduce_oneshot(Ptrs P, IO io, int 
   block_barrier<NR>(P, me.rank, me.b, 0, epoch, timeout, err);
   for (long i = i0; i < nvec; i += stride) out[i] = reduce_at<BF16, NR>(P, i);
   block_barrier<NR>(P, me.rank, me.b, 3, epoch, timeout, err);
+  commit_epoch(P, me, host_epoch, epoch);
 }
 
 template <bool BF16, int NR>
 __global__ __launch_bounds__(THREADS) void allreduce_twoshot(Ptrs P, IO io, int rank_arg, int nb, long nvec,
                                                              unsigned epoch, unsigned long timeout, int* err) {
   const Who me = who(rank_arg, nb);
+  const unsigned host_epoch = epoch;
+  epoch = call_epoch(P, me, host_epoch);
   const long stride = (long)nb * THREADS;
   const long i0 = (long)me.b * THREADS + threadIdx.x;
   const uint4* __restrict__ in = io.in[me.slot];
@@ -181,6 +202,7 @@ __global__ __launch_bounds__(THREADS) void allreduce_twoshot(Ptrs P, IO io, int 
     for (long i = first_at_or_after(i0, stride, slo); i < shi; i += stride) out[i] = src[i];
   }
   block_barrier<NR>(P, me.rank, me.b, 3, epoch, timeout, err);
+  commit_epoch(P, me, host_epoch, epoch);
 }
 
 template <bool BF16, int NR>
@@ -268,7 +290,6 @@ KGS_EXPORT int kgs_ar_run(void* const* data, void* const* sigs, int nranks, int 
   if (dtype != 0 && dtype != 1) return KGS_ERR_ARG;
   if (algo != 0 && algo != 1) return KGS_ERR_ARG;
   if (nbytes <= 0 || nbytes % 16 || nbytes > cap_bytes) return KGS_ERR_SHAPE;
-  if (epoch == 0) return KGS_ERR_ARG;  // signal blocks start zeroed
   if (blocks < 1 || blocks > MAX_BLOCKS) return KGS_ERR_ARG;
   if (!(timeout_s > 0.0) || timeout_s > 600.0) return KGS_ERR_ARG;
   Ptrs P = {};

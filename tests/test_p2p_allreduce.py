@@ -83,6 +83,39 @@ def test_local_ranks_bitwise(world, algo, dtype):
 
 
 @pytest.mark.gpu
+def test_graph_capture_replays_with_device_epochs():
+    """Captured once, replayed with new inputs: each replay must synchronise
+    afresh (device-side epochs), not pass on the flags of the capture-time call."""
+    from kgs.parallel.p2p_allreduce import P2PAllReduce
+
+    world, n = 4, 1 << 16
+    ar = P2PAllReduce.local_ranks(world, max_bytes=1 << 20, device="cuda", timeout_s=3.0)
+    try:
+        xs = [torch.zeros(n, device="cuda") for _ in range(world)]
+        outs = [torch.empty(n, device="cuda") for _ in range(world)]
+        ar.all_reduce_local(xs, outs=outs)  # warm up outside the capture
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                ar.all_reduce_local(xs, outs=outs)
+        torch.cuda.current_stream().wait_stream(s)
+        for it in range(5):
+            for r in range(world):
+                xs[r].fill_(float(r + 1 + it))
+            g.replay()
+            torch.cuda.synchronize()
+            ar.check()
+            want = float(sum(r + 1 + it for r in range(world)))
+            for o in outs:
+                assert torch.all(o == want), (it, o[:4])
+    finally:
+        ar.close()
+
+
+@pytest.mark.gpu
 def test_missing_peer_times_out_instead_of_hanging():
     from kgs.parallel.p2p_allreduce import P2PAllReduce
 
