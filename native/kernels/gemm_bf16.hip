@@ -96,6 +96,10 @@ struct Ctx {
   long a_kstride, b_kstride;       // elements between consecutive k (lda / ldb)
   int tr_base;                     // per-lane byte offset of the tr-read block
   int tr_x;                        // per-lane chunk XOR (2 * gsw)
+  // persistent mode (S bit 15): operand panels of the tile this block does next
+  const unsigned short* Ag2;
+  const unsigned short* Bg2;
+  int has_next;
 };
 
 constexpr int OOB_OFFSET = 0x7FFFFFF0;  // > every num_records the bounded path builds
@@ -107,7 +111,7 @@ __device__ __forceinline__ void bar() {
 }
 
 template <int PART, bool BND = false, bool TR = false>
-__device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
+__device__ __forceinline__ void issue(const Ctx& c, int buf, int k0, bool nxt = false) {
   char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048;
   if constexpr (TR) {
     // operand stored [K][cols]: the half-tile is 64 k-rows x 128 columns; the
@@ -133,10 +137,10 @@ __device__ __forceinline__ void issue(const Ctx& c, int buf, int k0) {
   const unsigned short* src;
   int o0, o1;
   if constexpr (PART == P_A0 || PART == P_A1) {
-    src = c.Ag + (PART == P_A1 ? c.a_half : 0) + k0;
+    src = (nxt ? c.Ag2 : c.Ag) + (PART == P_A1 ? c.a_half : 0) + k0;
     o0 = c.offA0; o1 = c.offA1;
   } else {
-    src = c.Bg + (PART == P_B1 ? c.b_half : 0) + k0;
+    src = (nxt ? c.Bg2 : c.Bg) + (PART == P_B1 ? c.b_half : 0) + k0;
     o0 = c.offB0; o1 = c.offB1;
   }
   glds16(src + o0, dst);
@@ -214,10 +218,10 @@ __device__ __forceinline__ void rd_b(const Ctx& c, Regs& R, const char* half) {
 }
 
 template <int PART, int S>
-__device__ __forceinline__ void issue_s(const Ctx& c, int buf, int k0) {
+__device__ __forceinline__ void issue_s(const Ctx& c, int buf, int k0, bool nxt = false) {
   constexpr bool isA = PART == P_A0 || PART == P_A1;
   constexpr bool tr = (S & 16384) ? false : isA ? (S & 2048) != 0 : (S & 4096) != 0;
-  issue<PART, (S & 512) != 0, tr>(c, buf, k0);
+  issue<PART, (S & 512) != 0, tr>(c, buf, k0, nxt);
 }
 
 typedef int i32x8 __attribute__((ext_vector_type(8)));
@@ -298,8 +302,19 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   constexpr int part = (S & 1) == 0 ? (jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1)
                                     : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
   int t = 2 * it + toff;
-  t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
-  issue_s<part, S>(c, toff & 1, t * BK);
+  if constexpr (S & 32768) {
+    // persistent: past the end the stream continues into the next tile's first
+    // K-tiles (same slots, same parity: nt is even), so the pipeline never drains
+    if (t >= c.nt && c.has_next) {
+      issue_s<part, S>(c, toff & 1, (t - c.nt) * BK, true);
+    } else {
+      t = t < c.nt ? t : c.nt - 1;
+      issue_s<part, S>(c, toff & 1, t * BK);
+    }
+  } else {
+    t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
+    issue_s<part, S>(c, toff & 1, t * BK);
+  }
   if constexpr ((S & 1) == 0)
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else
@@ -327,6 +342,73 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   // slot a phase's DMA overwrites was last read >= 2 phases earlier, i.e. before
   // the previous phase's barrier on every wave.
   if constexpr (!(S & 128)) bar();
+}
+
+// Epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n); bias and
+// activation fused, bf16 out through the widened (16-B) store tail.
+template <int EPI, int S>
+__device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned short* __restrict__ C,
+                                           const unsigned short* __restrict__ bias, int M, int N, int ldc,
+                                           float alpha, int tm, int tn, int lane) {
+  constexpr bool BND = (S & 512) != 0;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+      // bounded mode: rows past M are dropped (the permlane swaps below stay
+      // wave-uniform, only the stores are predicated)
+      const bool row_ok = !BND || row < M;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        uint2 o[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          f32x4 v = R.acc[mh][i][nh][n];
+          if constexpr (S & 1024) v *= alpha;  // fp8: per-tensor dequant scale sa*sb
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI != EPI_NONE) {
+            if (!BND || col + 4 <= N) {
+              bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
+            }
+          }
+          o[n].x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o[n].y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+        }
+        const int col0 = tn * BN + nh * 128 + c.wc * 32;
+        if constexpr (S & 256) {
+          // narrow store tail (A/B reference): two 8-B stores per lane
+          *(uint2*)(crow + col0 + fq * 4) = o[0];
+          *(uint2*)(crow + col0 + 16 + fq * 4) = o[1];
+        } else {
+          // widened store tail (guide T21, 16-lane form): v_permlane16_swap
+          // exchanges rows 1<->0 and 3<->2 of the lane grid, so even-fq lanes
+          // end up with 8 consecutive n=0 columns and odd-fq lanes with the
+          // matching n=1 columns -> one 16-B store per lane instead of two 8-B.
+          auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+          auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+          // even fq: (own n0, partner n0) = (sx[0], sx[1]) ... odd fq likewise for n1
+          const uint4 q = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const int cw = col0 + (fq & 1) * 16 + (fq >> 1) * 8;
+          if (!BND || (row_ok && cw + 8 <= N)) {
+            *(uint4*)(crow + cw) = q;
+          } else if (row_ok) {
+            const unsigned wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (cw + e < N) crow[cw + e] = (unsigned short)(wd[e >> 1] >> ((e & 1) * 16));
+          }
+        }
+      }
+    }
 }
 
 template <int EPI, int S>
@@ -462,65 +544,132 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   if (!(S & 64) && c.wr == 0) bar();  // balance the stagger barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
 
-  // epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n)
-  const int fr = lane & 15, fq = lane >> 4;
+  store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+}
+
+// Persistent variant (S bit 15, balanced schedule, aligned shapes): one block
+// per CU walks tiles vb = blockIdx.x, +gridDim.x, ... in the same XCD-remapped,
+// grouped order the one-shot grid would run them. The look-ahead DMA of a
+// tile's last phases already fetches the next tile's first 7 half-tiles and
+// B0(0) fragments, so the next tile's loads are in flight while this tile's
+// epilogue stores drain; the wave groups keep their one-barrier stagger across
+// tiles. RAW/WAR accounting is unchanged: the half-tile stream is simply
+// continuous across tile boundaries.
+__device__ __forceinline__ void tile_coords(int vb, int nwg, int ntm, int ntn, int& tm, int& tn) {
+  const int wg = xcd_remap(vb, nwg);
+  constexpr int GM = 4;
+  const int per_group = GM * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  tm = first_m + (wg % per_group) % gsz;
+  tn = (wg % per_group) / gsz;
+}
+
+template <int EPI, int S>
+__global__ __launch_bounds__(512) void gemm_nt_256_persist(const unsigned short* __restrict__ A,
+                                                           const unsigned short* __restrict__ B,
+                                                           unsigned short* __restrict__ C,
+                                                           const unsigned short* __restrict__ bias,
+                                                           int M, int N, int K, int lda, int ldb, int ldc,
+                                                           float alpha) {
+  static_assert((S & 1) && (S & 32768) && !(S & 512) && !(S & (2048 | 4096)), "persistent: aligned NT only");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  int vb = blockIdx.x;
+  int tm, tn;
+  tile_coords(vb, nwg, ntm, ntn, tm, tn);
+
+  Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  {
+    const int r0 = w * 16 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ ((r0 >> 1) & 7);
+    const int c1 = (lane & 7) ^ ((r1 >> 1) & 7);
+    c.offA0 = r0 * lda + c0 * 8;
+    c.offA1 = r1 * lda + c1 * 8;
+    c.offB0 = r0 * ldb + c0 * 8;
+    c.offB1 = r1 * ldb + c1 * 8;
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+  int vb2 = vb + gridDim.x;
+  c.has_next = vb2 < nwg;
+  int tm2 = 0, tn2 = 0;
+  if (c.has_next) tile_coords(vb2, nwg, ntm, ntn, tm2, tn2);
+  c.Ag2 = A + (long)tm2 * BM * lda;
+  c.Bg2 = B + (long)tn2 * BN * ldb;
+
+  Regs R;
 #pragma unroll
-  for (int mh = 0; mh < 2; ++mh)
+  for (int a = 0; a < 2; ++a)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
-      unsigned short* crow = C + (long)row * ldc;
-      // bounded mode: rows past M are dropped (the permlane swaps below stay
-      // wave-uniform, only the stores are predicated)
-      const bool row_ok = !BND || row < M;
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int nh = 0; nh < 2; ++nh) {
-        uint2 o[2];
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
-          f32x4 v = R.acc[mh][i][nh][n];
-          if constexpr (S & 1024) v *= alpha;  // fp8: per-tensor dequant scale sa*sb
-          float bv[4] = {0.f, 0.f, 0.f, 0.f};
-          if constexpr (EPI != EPI_NONE) {
-            if (!BND || col + 4 <= N) {
-              bf16x4 bb = *(const bf16x4*)(bias + col);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
-            } else {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
-            }
-          }
-          o[n].x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
-          o[n].y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
-        }
-        const int col0 = tn * BN + nh * 128 + c.wc * 32;
-        if constexpr (S & 256) {
-          // narrow store tail (A/B reference): two 8-B stores per lane
-          *(uint2*)(crow + col0 + fq * 4) = o[0];
-          *(uint2*)(crow + col0 + 16 + fq * 4) = o[1];
-        } else {
-          // widened store tail (guide T21, 16-lane form): v_permlane16_swap
-          // exchanges rows 1<->0 and 3<->2 of the lane grid, so even-fq lanes
-          // end up with 8 consecutive n=0 columns and odd-fq lanes with the
-          // matching n=1 columns -> one 16-B store per lane instead of two 8-B.
-          auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
-          auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
-          // even fq: (own n0, partner n0) = (sx[0], sx[1]) ... odd fq likewise for n1
-          const uint4 q = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-          const int cw = col0 + (fq & 1) * 16 + (fq >> 1) * 8;
-          if (!BND || (row_ok && cw + 8 <= N)) {
-            *(uint4*)(crow + cw) = q;
-          } else if (row_ok) {
-            const unsigned wd[4] = {q.x, q.y, q.z, q.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-              if (cw + e < N) crow[cw + e] = (unsigned short)(wd[e >> 1] >> ((e & 1) * 16));
-          }
-        }
-      }
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  issue<P_B0>(c, 0, 0);
+  issue<P_A0>(c, 0, 0);
+  issue<P_B1>(c, 0, 0);
+  issue<P_A1>(c, 0, 0);
+  issue<P_B0>(c, 1, k1);
+  issue<P_A0>(c, 1, k1);
+  issue<P_B1>(c, 1, k1);
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  bar();
+  read_b<0>(c, R, smem + P_B0 * HALF_BYTES);
+  if (c.wr == 1) bar();
+
+  const int iters = c.nt >> 1;
+  for (;;) {
+    for (int it = 0; it < iters; ++it) {
+      phase<0, S>(c, R, it);
+      phase<1, S>(c, R, it);
+      phase<2, S>(c, R, it);
+      phase<3, S>(c, R, it);
+      phase<4, S>(c, R, it);
+      phase<5, S>(c, R, it);
+      phase<6, S>(c, R, it);
+      phase<7, S>(c, R, it);
     }
+    store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+    if (!c.has_next) break;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    tm = tm2;
+    tn = tn2;
+    c.Ag = c.Ag2;
+    c.Bg = c.Bg2;
+    vb2 += gridDim.x;
+    c.has_next = vb2 < nwg;
+    if (c.has_next) {
+      tile_coords(vb2, nwg, ntm, ntn, tm2, tn2);
+      c.Ag2 = A + (long)tm2 * BM * lda;
+      c.Bg2 = B + (long)tn2 * BN * ldb;
+    }
+  }
+  if (c.wr == 0) bar();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 }  // namespace g256
@@ -1219,6 +1368,18 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
                        ldc, 1.0f);
+  } else if (variant == 20) {
+    // persistent: one block per CU walking the tiles (aligned shapes)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    const int nwg = (M / g256::BM) * (N / g256::BN);
+    const dim3 gridp(nwg < cus ? nwg : cus);
+    hipLaunchKernelGGL((g256::gemm_nt_256_persist<EPI, 7 + 32768>), gridp, dim3(512), 0, s, A, B, C, bias, M, N, K,
+                       lda, ldb, ldc, 1.0f);
   } else if (variant == 16) {
     // the same pipeline on any M, N and K % 8 == 0: buffer-resource loads zero
     // the rows / K-chunks past the edges, stores are predicated
@@ -1332,7 +1493,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if (variant >= 3 && variant <= 15) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
+  else if ((variant >= 3 && variant <= 15) || variant == 20) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
   else return KGS_ERR_ARG;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
