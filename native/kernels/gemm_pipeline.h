@@ -1,0 +1,636 @@
+// The 256x256 bf16/fp8 MFMA pipeline for gfx950 (MI355X / CDNA4), shared by the
+// production kernels (gemm_bf16.hip) and the measured alternatives
+// (gemm_experiments.hip). See gemm_bf16.hip for the design summary and
+// profiles/gemm_tuning.md for every schedule variant's numbers.
+//
+// Template knob S (bit: meaning):
+//   0 balanced schedule (reads 8/4/8/4, look-ahead 7)   1 no s_setprio
+//   2-3 GROUP_M (0:8 1:4 2:16 3:2)                       4 probe: 2x MFMA per block
+//   5 probe: all blocks load tile (0,0)                  6 lockstep (no stagger)
+//   7 one barrier per phase (with 6)                     8 narrow store tail
+//   9 bounded (buffer-resource zero fill, any M/N)       10 fp8 e4m3 (scaled MFMA)
+//   11 A stored [K][M]   12 B stored [K][N]  (ds_read_b64_tr_b16 fragments)
+//   13/14 probes for 11   15 persistent tile walk
+// Production bf16 = 7 (balanced, no setprio, GROUP_M 4).
+#pragma once
+
+#include "kgs_common.h"
+
+namespace kgs {
+namespace g256 {
+
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HALF_BYTES = 128 * BK * 2;   // 16 KiB: 128 rows x 128 B
+constexpr int BUF_BYTES = 4 * HALF_BYTES;  // A0 A1 B0 B1
+constexpr int LDS_BYTES = 2 * BUF_BYTES;   // 2-deep ring = 128 KiB
+constexpr int P_A0 = 0, P_A1 = 1, P_B0 = 2, P_B1 = 3;
+constexpr int LOOKAHEAD = 5;               // half-tiles issued ahead of use
+constexpr int GROUP_M = 8;
+
+struct Regs {
+  bf16x8 a[4][2];        // A fragments of the current m-half: [m-tile][k-sub]
+  bf16x8 b[2][2][2];     // B fragments of both n-halves: [n-half][n-tile][k-sub]
+  f32x4 acc[2][4][2][2]; // [m-half][m-tile][n-half][n-tile]
+};
+
+struct Ctx {
+  char* smem;
+  const unsigned short* Ag;  // A + tile_m*256*lda
+  const unsigned short* Bg;  // B + tile_n*256*ldb
+  long a_half;               // 128*lda (elements)
+  long b_half;
+  int offA0, offA1, offB0, offB1;  // per-lane glds source offsets (elements)
+  int ro0, ro1;                    // per-lane ds_read byte offsets for k-sub 0/1
+  int wr, wc, w;                   // wave coordinates (wave-uniform)
+  int nt;                          // number of K-tiles
+  // bounded mode (S bit 9): operands read through buffer resources whose
+  // num_records ends at the last valid row, so rows >= M (N) load zeros; lanes
+  // whose 16-B chunk starts at k >= K get an out-of-range offset (zeros too).
+  __amdgpu_buffer_rsrc_t ra, rb;
+  int K, kc0, kc1;                 // K and the lane's logical chunk column (elements)
+  int a_half_i, b_half_i;          // 128*lda, 128*ldb as int
+  // transposed operands (S bits 11/12: A stored [K][M] / B stored [K][N]):
+  // half-tiles are [64 k][128 cols] with 256-B rows, read with
+  // ds_read_b64_tr_b16; see read_a_tr / read_b_tr
+  long a_kstride, b_kstride;       // elements between consecutive k (lda / ldb)
+  int tr_base;                     // per-lane byte offset of the tr-read block
+  int tr_x;                        // per-lane chunk XOR (2 * gsw)
+  // persistent mode (S bit 15): operand panels of the tile this block does next
+  const unsigned short* Ag2;
+  const unsigned short* Bg2;
+  int has_next;
+};
+
+constexpr int OOB_OFFSET = 0x7FFFFFF0;  // > every num_records the bounded path builds
+
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int PART, bool BND = false, bool TR = false>
+__device__ __forceinline__ void issue(const Ctx& c, int buf, int k0, bool nxt = false) {
+  char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048;
+  if constexpr (TR) {
+    // operand stored [K][cols]: the half-tile is 64 k-rows x 128 columns; the
+    // per-lane offsets already hold row*ld + swizzled column
+    constexpr bool isA = PART == P_A0 || PART == P_A1;
+    const unsigned short* src = (isA ? c.Ag : c.Bg) + ((PART == P_A1 || PART == P_B1) ? 128 : 0) +
+                                (long)k0 * (isA ? c.a_kstride : c.b_kstride);
+    glds16(src + (isA ? c.offA0 : c.offB0), dst);
+    glds16(src + (isA ? c.offA1 : c.offB1), dst + 1024);
+    return;
+  }
+  if constexpr (BND) {
+    constexpr bool isA = PART == P_A0 || PART == P_A1;
+    const int half = PART == P_A1 ? c.a_half_i : PART == P_B1 ? c.b_half_i : 0;
+    const int o0 = (isA ? c.offA0 : c.offB0) + half + k0;
+    const int o1 = (isA ? c.offA1 : c.offB1) + half + k0;
+    const int v0 = k0 + c.kc0 < c.K ? o0 * 2 : OOB_OFFSET;
+    const int v1 = k0 + c.kc1 < c.K ? o1 * 2 : OOB_OFFSET;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? c.ra : c.rb, (KGS_LDS void*)dst, 16, v0, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(isA ? c.ra : c.rb, (KGS_LDS void*)(dst + 1024), 16, v1, 0, 0, 0);
+    return;
+  }
+  const unsigned short* src;
+  int o0, o1;
+  if constexpr (PART == P_A0 || PART == P_A1) {
+    src = (nxt ? c.Ag2 : c.Ag) + (PART == P_A1 ? c.a_half : 0) + k0;
+    o0 = c.offA0; o1 = c.offA1;
+  } else {
+    src = (nxt ? c.Bg2 : c.Bg) + (PART == P_B1 ? c.b_half : 0) + k0;
+    o0 = c.offB0; o1 = c.offB1;
+  }
+  glds16(src + o0, dst);
+  glds16(src + o1, dst + 1024);
+}
+
+// Read the 4 m-tiles x 2 k-subs of A for this wave from half-tile `part`.
+template <class CtxT>
+__device__ __forceinline__ void read_a(const CtxT& c, Regs& R, const char* half) {
+  const char* p = half + c.wr * 64 * 128;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    R.a[i][0] = *(const bf16x8*)(p + i * 16 * 128 + c.ro0);
+    R.a[i][1] = *(const bf16x8*)(p + i * 16 * 128 + c.ro1);
+  }
+}
+
+template <int NH, class CtxT>
+__device__ __forceinline__ void read_b(const CtxT& c, Regs& R, const char* half) {
+  const char* p = half + c.wc * 32 * 128;
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    R.b[NH][n][0] = *(const bf16x8*)(p + n * 16 * 128 + c.ro0);
+    R.b[NH][n][1] = *(const bf16x8*)(p + n * 16 * 128 + c.ro1);
+  }
+}
+
+// Transposed operands. Half-tile image: [64 k][128 cols] bf16, 256-B rows,
+// 16-B chunk c of row r stored at c ^ (2 * gsw(r)), gsw(r) = (r & 3) | ((r >> 3) & 1) << 2.
+// An MFMA fragment (8 consecutive k of one column per lane) is two
+// ds_read_b64_tr_b16: in each 16-lane group, lane 4q+p addresses row k0+q,
+// columns 4p..4p+3 and receives its own column over the 4 rows. Per 32-lane
+// half the 8 rows {0-3, 8-11} (+4 for the second read) hit 8 distinct gsw
+// values, so the 16 chunks read land on 16 distinct bank groups: no conflicts.
+typedef short bf16x4s __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8 tr_frag(const char* p) {
+  const bf16x4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)p);
+  const bf16x4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(p + 4 * 256));
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// column chunk base `ch` (even) -> byte offset of this lane's tr-read address
+__device__ __forceinline__ int tr_col(const Ctx& c, int ch) { return ((ch ^ c.tr_x) << 4) + c.tr_base; }
+
+__device__ __forceinline__ void read_a_tr(const Ctx& c, Regs& R, const char* half) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const char* p = half + tr_col(c, c.wr * 8 + 2 * i);
+    R.a[i][0] = tr_frag(p);
+    R.a[i][1] = tr_frag(p + 32 * 256);
+  }
+}
+
+template <int NH>
+__device__ __forceinline__ void read_b_tr(const Ctx& c, Regs& R, const char* half) {
+#pragma unroll
+  for (int n = 0; n < 2; ++n) {
+    const char* p = half + tr_col(c, c.wc * 4 + 2 * n);
+    R.b[NH][n][0] = tr_frag(p);
+    R.b[NH][n][1] = tr_frag(p + 32 * 256);
+  }
+}
+
+// S bit 13 / 14 (timing probes, wrong results): keep the transposed DMA but read
+// with ds_read_b128 (13), or keep the tr reads but DMA in the NT pattern (14)
+template <int S>
+__device__ __forceinline__ void rd_a(const Ctx& c, Regs& R, const char* half) {
+  if constexpr ((S & 2048) && !(S & 8192)) read_a_tr(c, R, half); else read_a(c, R, half);
+}
+
+template <int NH, int S>
+__device__ __forceinline__ void rd_b(const Ctx& c, Regs& R, const char* half) {
+  if constexpr (S & 4096) read_b_tr<NH>(c, R, half); else read_b<NH>(c, R, half);
+}
+
+template <int PART, int S>
+__device__ __forceinline__ void issue_s(const Ctx& c, int buf, int k0, bool nxt = false) {
+  constexpr bool isA = PART == P_A0 || PART == P_A1;
+  constexpr bool tr = (S & 16384) ? false : isA ? (S & 2048) != 0 : (S & 4096) != 0;
+  issue<PART, (S & 512) != 0, tr>(c, buf, k0, nxt);
+}
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// Two 16-B fragments (k-sub 0 and 1 of the same 128-byte LDS row slice) as one
+// 32-B operand of the fp8 MFMA.
+__device__ __forceinline__ i32x8 cat32(const bf16x8& lo, const bf16x8& hi) {
+  typedef short s16 __attribute__((ext_vector_type(16)));
+  s16 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  return __builtin_bit_cast(i32x8, v);
+}
+
+template <int MH, int NH, bool FP8 = false>
+__device__ __forceinline__ void mma_quadrant(Regs& R) {
+  if constexpr (FP8) {
+    // fp8 (OCP e4m3) mode: the LDS rows hold 128 fp8 K-values; one scaled
+    // 16x16x128 MFMA (unit E8M0 scales = 2^0) consumes what the bf16 path does
+    // in two 16x16x32 ones -- twice the FLOPs for the same bytes moved. Lane
+    // group g holds K-bytes [16g,16g+16) and [64+16g,64+16g+16) of its row, for
+    // A and B alike, so the K pairing is consistent (the sum is order-free).
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        R.acc[MH][i][NH][n] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+            cat32(R.b[NH][n][0], R.b[NH][n][1]), cat32(R.a[i][0], R.a[i][1]), R.acc[MH][i][NH][n], 0, 0, 0, 127,
+            0, 127);
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+        // operands swapped (B first) so each lane ends up holding 4
+        // consecutive output COLUMNS of one row: C[m = lane&15][n = 4*(lane>>4)+e]
+        R.acc[MH][i][NH][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            R.b[NH][n][s], R.a[i][s], R.acc[MH][i][NH][n], 0, 0, 0);
+}
+
+// Two schedules (template S):
+//  S=0  quadrants (0,0)(0,1)(1,1)(1,0); stream A0,B0,B1,A1; look-ahead 5;
+//       ds_reads per phase 12/4/8/0; vmcnt(6).
+//  S=1  quadrants (0,0)(0,1)(1,0)(1,1); stream B0,A0,B1,A1; look-ahead 7;
+//       B0 of the NEXT K-tile is read in phase 3 (its last use is now phase 2),
+//       so reads per phase are 8/4/8/4 and no partner MFMA block waits on a
+//       12-read burst; 5 half-tiles stay in flight (vmcnt(10)).
+//       Hazards (half-tile (t,pos) issued at phase 4t+pos-7, every read at
+//       distance 6 from its issue, every slot re-issued 2 phases after its last
+//       read): RAW needs distance >= 6 for vmcnt(10); WAR needs >= 2 with the
+//       one-barrier stagger -- both hold for all four slots.
+template <int QP, int S>
+__device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
+  constexpr int q = QP & 3;
+  constexpr int cbuf = QP >> 2;
+  const char* buf = c.smem + cbuf * BUF_BYTES;
+  if constexpr ((S & 1) == 0) {
+    if constexpr (q == 0) {
+      rd_a<S>(c, R, buf + P_A0 * HALF_BYTES);
+      rd_b<0, S>(c, R, buf + P_B0 * HALF_BYTES);
+    } else if constexpr (q == 1) {
+      rd_b<1, S>(c, R, buf + P_B1 * HALF_BYTES);
+    } else if constexpr (q == 2) {
+      rd_a<S>(c, R, buf + P_A1 * HALF_BYTES);
+    }
+  } else {
+    if constexpr (q == 0) rd_a<S>(c, R, buf + P_A0 * HALF_BYTES);
+    if constexpr (q == 1) rd_b<1, S>(c, R, buf + P_B1 * HALF_BYTES);
+    if constexpr (q == 2) rd_a<S>(c, R, buf + P_A1 * HALF_BYTES);
+    if constexpr (q == 3) rd_b<0, S>(c, R, c.smem + (cbuf ^ 1) * BUF_BYTES + P_B0 * HALF_BYTES);
+  }
+  // prefetch half-tile h = 8*it + QP + look-ahead
+  constexpr int LA = (S & 1) == 0 ? LOOKAHEAD : 7;
+  constexpr int hoff = QP + LA;
+  constexpr int toff = hoff >> 2;
+  constexpr int jp = hoff & 3;
+  constexpr int part = (S & 1) == 0 ? (jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1)
+                                    : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
+  int t = 2 * it + toff;
+  if constexpr (S & 32768) {
+    // persistent: past the end the stream continues into the next tile's first
+    // K-tiles (same slots, same parity: nt is even), so the pipeline never drains
+    if (t >= c.nt && c.has_next) {
+      issue_s<part, S>(c, toff & 1, (t - c.nt) * BK, true);
+    } else {
+      t = t < c.nt ? t : c.nt - 1;
+      issue_s<part, S>(c, toff & 1, t * BK);
+    }
+  } else {
+    t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
+    issue_s<part, S>(c, toff & 1, t * BK);
+  }
+  if constexpr ((S & 1) == 0)
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  bar();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
+  if constexpr (S & 16) {  // timing experiment only: twice the MFMAs per phase (wrong results)
+    if constexpr (q == 0) mma_quadrant<0, 0, (S & 1024) != 0>(R);
+    if constexpr (q == 1) mma_quadrant<0, 1, (S & 1024) != 0>(R);
+    if constexpr (q == 2) mma_quadrant<1, 0, (S & 1024) != 0>(R);
+    if constexpr (q == 3) mma_quadrant<1, 1, (S & 1024) != 0>(R);
+  }
+  if constexpr (q == 0) mma_quadrant<0, 0, (S & 1024) != 0>(R);
+  if constexpr (q == 1) mma_quadrant<0, 1, (S & 1024) != 0>(R);
+  if constexpr (q == 2) {
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 1, (S & 1024) != 0>(R); else mma_quadrant<1, 0, (S & 1024) != 0>(R);
+  }
+  if constexpr (q == 3) {
+    if constexpr ((S & 1) == 0) mma_quadrant<1, 0, (S & 1024) != 0>(R); else mma_quadrant<1, 1, (S & 1024) != 0>(R);
+  }
+  if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
+  // S bit 7 (with bit 6, lockstep): one barrier per phase. Still race-free: the
+  // slot a phase's DMA overwrites was last read >= 2 phases earlier, i.e. before
+  // the previous phase's barrier on every wave.
+  if constexpr (!(S & 128)) bar();
+}
+
+// Epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n); bias and
+// activation fused, bf16 out through the widened (16-B) store tail.
+template <int EPI, int S>
+__device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned short* __restrict__ C,
+                                           const unsigned short* __restrict__ bias, int M, int N, int ldc,
+                                           float alpha, int tm, int tn, int lane) {
+  constexpr bool BND = (S & 512) != 0;
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+      // bounded mode: rows past M are dropped (the permlane swaps below stay
+      // wave-uniform, only the stores are predicated)
+      const bool row_ok = !BND || row < M;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh) {
+        uint2 o[2];
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          f32x4 v = R.acc[mh][i][nh][n];
+          if constexpr (S & 1024) v *= alpha;  // fp8: per-tensor dequant scale sa*sb
+          float bv[4] = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (EPI != EPI_NONE) {
+            if (!BND || col + 4 <= N) {
+              bf16x4 bb = *(const bf16x4*)(bias + col);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bv[e] = bf2f((unsigned short)bb[e]);
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e) bv[e] = col + e < N ? bf2f(bias[col + e]) : 0.f;
+            }
+          }
+          o[n].x = pack_bf16x2(epilogue<EPI>(v[0], bv[0]), epilogue<EPI>(v[1], bv[1]));
+          o[n].y = pack_bf16x2(epilogue<EPI>(v[2], bv[2]), epilogue<EPI>(v[3], bv[3]));
+        }
+        const int col0 = tn * BN + nh * 128 + c.wc * 32;
+        if constexpr (S & 256) {
+          // narrow store tail (A/B reference): two 8-B stores per lane
+          *(uint2*)(crow + col0 + fq * 4) = o[0];
+          *(uint2*)(crow + col0 + 16 + fq * 4) = o[1];
+        } else {
+          // widened store tail (guide T21, 16-lane form): v_permlane16_swap
+          // exchanges rows 1<->0 and 3<->2 of the lane grid, so even-fq lanes
+          // end up with 8 consecutive n=0 columns and odd-fq lanes with the
+          // matching n=1 columns -> one 16-B store per lane instead of two 8-B.
+          auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+          auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+          // even fq: (own n0, partner n0) = (sx[0], sx[1]) ... odd fq likewise for n1
+          const uint4 q = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+          const int cw = col0 + (fq & 1) * 16 + (fq >> 1) * 8;
+          if (!BND || (row_ok && cw + 8 <= N)) {
+            *(uint4*)(crow + cw) = q;
+          } else if (row_ok) {
+            const unsigned wd[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              if (cw + e < N) crow[cw + e] = (unsigned short)(wd[e >> 1] >> ((e & 1) * 16));
+          }
+        }
+      }
+    }
+}
+
+template <int EPI, int S>
+__global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restrict__ A,
+                                                   const unsigned short* __restrict__ B,
+                                                   unsigned short* __restrict__ C,
+                                                   const unsigned short* __restrict__ bias,
+                                                   int M, int N, int K, int lda, int ldb, int ldc,
+                                                   float alpha) {
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  constexpr bool BND = (S & 512) != 0;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = BND ? (M + BM - 1) / BM : M / BM, ntn = BND ? (N + BN - 1) / BN : N / BN, nwg = ntm * ntn;
+  const int wg = xcd_remap(blockIdx.x, nwg);
+  // S bits 2-3 select the tile-group height (experiment knob): 8, 4, 16, 2
+  constexpr int GM = ((S >> 2) & 3) == 0 ? GROUP_M : ((S >> 2) & 3) == 1 ? 4 : ((S >> 2) & 3) == 2 ? 16 : 2;
+  const int per_group = GM * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  const int tm = first_m + (wg % per_group) % gsz;
+  const int tn = (wg % per_group) / gsz;
+
+  Ctx c;
+  c.smem = smem;
+  // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
+  c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;
+  c.Bg = (S & 4096) ? B + (long)tn * BN : B + (long)((S & 32) ? 0 : tn) * BN * ldb;
+  c.a_kstride = lda;
+  c.b_kstride = ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  if constexpr (BND) {
+    c.nt = (((K + BK - 1) / BK) + 1) & ~1;  // whole K-loop iterations; tail tiles load zeros
+    c.K = K;
+    c.a_half_i = 128 * lda;
+    c.b_half_i = 128 * ldb;
+    const int rows_a = min(M - tm * BM, BM), rows_b = min(N - tn * BN, BN);
+    c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)c.Ag, 0, rows_a * lda * 2, 0x00020000);
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)c.Bg, 0, rows_b * ldb * 2, 0x00020000);
+  }
+  {
+    // glds j (0/1) of wave w fills half-tile rows w*16 + j*8 + lane/8; lane's
+    // physical 16-B chunk is lane&7 and holds logical chunk (lane&7)^f(row).
+    const int r0 = w * 16 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ ((r0 >> 1) & 7);
+    const int c1 = (lane & 7) ^ ((r1 >> 1) & 7);
+    c.offA0 = r0 * lda + c0 * 8;
+    c.offA1 = r1 * lda + c1 * 8;
+    c.offB0 = r0 * ldb + c0 * 8;
+    c.offB1 = r1 * ldb + c1 * 8;
+    c.kc0 = c0 * 8;
+    c.kc1 = c1 * 8;
+    if constexpr ((S & 2048) || (S & 4096)) {
+      // [64 k][128 col] half-tiles: glds j of wave w fills rows 4*(2w+j) + lane/16;
+      // lane's physical chunk lane&15 holds logical chunk (lane&15) ^ (2 gsw(row))
+      const int tr0 = 4 * (2 * w) + (lane >> 4), tr1 = tr0 + 4;
+      const int g0 = (tr0 & 3) | (((tr0 >> 3) & 1) << 2), g1 = (tr1 & 3) | (((tr1 >> 3) & 1) << 2);
+      const int lc0 = (lane & 15) ^ (2 * g0), lc1 = (lane & 15) ^ (2 * g1);
+      if constexpr ((S & 2048) && !(S & 16384)) {
+        c.offA0 = tr0 * lda + lc0 * 8;
+        c.offA1 = tr1 * lda + lc1 * 8;
+      }
+      if constexpr (S & 4096) {
+        c.offB0 = tr0 * ldb + lc0 * 8;
+        c.offB1 = tr1 * ldb + lc1 * 8;
+      }
+      // tr reads: 16-lane group g (= lane>>4) takes rows 8g + q (q = (lane&15)>>2)
+      // and columns 4p..4p+3 (p = lane&3) of the fragment's 16-column block
+      const int g = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+      c.tr_x = 2 * (q | ((g & 1) << 2));
+      c.tr_base = (8 * g + q) * 256 + (pp >> 1) * 16 + (pp & 1) * 8;
+    }
+    // fragment read: row lane&15, logical chunk 4*s + lane/16
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+
+  Regs R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  if constexpr ((S & 1) == 0) {
+    // prologue: half-tiles 0..4 = A0 B0 B1 A1 of tile 0, A0 of tile 1
+    issue_s<P_A0, S>(c, 0, 0);
+    issue_s<P_B0, S>(c, 0, 0);
+    issue_s<P_B1, S>(c, 0, 0);
+    issue_s<P_A1, S>(c, 0, 0);
+    issue_s<P_A0, S>(c, 1, k1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
+    bar();
+  } else {
+    // prologue: half-tiles 0..6 = B0 A0 B1 A1 of tile 0, B0 A0 B1 of tile 1
+    issue_s<P_B0, S>(c, 0, 0);
+    issue_s<P_A0, S>(c, 0, 0);
+    issue_s<P_B1, S>(c, 0, 0);
+    issue_s<P_A1, S>(c, 0, 0);
+    issue_s<P_B0, S>(c, 1, k1);
+    issue_s<P_A0, S>(c, 1, k1);
+    issue_s<P_B1, S>(c, 1, k1);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");  // B0,A0 of tile 0 landed
+    bar();
+    rd_b<0, S>(c, R, smem + P_B0 * HALF_BYTES);  // phase 0 reads A0 itself
+  }
+  // stagger: waves 4-7 trail by one barrier (S bit 6: lockstep experiment, no stagger)
+  if (!(S & 64) && c.wr == 1) bar();
+
+  const int iters = c.nt >> 1;
+  for (int it = 0; it < iters; ++it) {
+    phase<0, S>(c, R, it);
+    phase<1, S>(c, R, it);
+    phase<2, S>(c, R, it);
+    phase<3, S>(c, R, it);
+    phase<4, S>(c, R, it);
+    phase<5, S>(c, R, it);
+    phase<6, S>(c, R, it);
+    phase<7, S>(c, R, it);
+  }
+  if (!(S & 64) && c.wr == 0) bar();  // balance the stagger barrier
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
+
+  store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+}
+
+// Persistent variant (S bit 15, balanced schedule, aligned shapes): one block
+// per CU walks tiles vb = blockIdx.x, +gridDim.x, ... in the same XCD-remapped,
+// grouped order the one-shot grid would run them. The look-ahead DMA of a
+// tile's last phases already fetches the next tile's first 7 half-tiles and
+// B0(0) fragments, so the next tile's loads are in flight while this tile's
+// epilogue stores drain; the wave groups keep their one-barrier stagger across
+// tiles. RAW/WAR accounting is unchanged: the half-tile stream is simply
+// continuous across tile boundaries.
+__device__ __forceinline__ void tile_coords(int vb, int nwg, int ntm, int ntn, int& tm, int& tn) {
+  const int wg = xcd_remap(vb, nwg);
+  constexpr int GM = 4;
+  const int per_group = GM * ntn;
+  const int group = wg / per_group;
+  const int first_m = group * GM;
+  const int gsz = min(ntm - first_m, GM);
+  tm = first_m + (wg % per_group) % gsz;
+  tn = (wg % per_group) / gsz;
+}
+
+template <int EPI, int S>
+__global__ __launch_bounds__(512) void gemm_nt_256_persist(const unsigned short* __restrict__ A,
+                                                           const unsigned short* __restrict__ B,
+                                                           unsigned short* __restrict__ C,
+                                                           const unsigned short* __restrict__ bias,
+                                                           int M, int N, int K, int lda, int ldb, int ldc,
+                                                           float alpha) {
+  static_assert((S & 1) && (S & 32768) && !(S & 512) && !(S & (2048 | 4096)), "persistent: aligned NT only");
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
+  int vb = blockIdx.x;
+  int tm, tn;
+  tile_coords(vb, nwg, ntm, ntn, tm, tn);
+
+  Ctx c;
+  c.smem = smem;
+  c.Ag = A + (long)tm * BM * lda;
+  c.Bg = B + (long)tn * BN * ldb;
+  c.a_half = 128L * lda;
+  c.b_half = 128L * ldb;
+  c.w = w;
+  c.wr = w >> 2;
+  c.wc = w & 3;
+  c.nt = K / BK;
+  {
+    const int r0 = w * 16 + (lane >> 3), r1 = r0 + 8;
+    const int c0 = (lane & 7) ^ ((r0 >> 1) & 7);
+    const int c1 = (lane & 7) ^ ((r1 >> 1) & 7);
+    c.offA0 = r0 * lda + c0 * 8;
+    c.offA1 = r1 * lda + c1 * 8;
+    c.offB0 = r0 * ldb + c0 * 8;
+    c.offB1 = r1 * ldb + c1 * 8;
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+  int vb2 = vb + gridDim.x;
+  c.has_next = vb2 < nwg;
+  int tm2 = 0, tn2 = 0;
+  if (c.has_next) tile_coords(vb2, nwg, ntm, ntn, tm2, tn2);
+  c.Ag2 = A + (long)tm2 * BM * lda;
+  c.Bg2 = B + (long)tn2 * BN * ldb;
+
+  Regs R;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  issue<P_B0>(c, 0, 0);
+  issue<P_A0>(c, 0, 0);
+  issue<P_B1>(c, 0, 0);
+  issue<P_A1>(c, 0, 0);
+  issue<P_B0>(c, 1, k1);
+  issue<P_A0>(c, 1, k1);
+  issue<P_B1>(c, 1, k1);
+  asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  bar();
+  read_b<0>(c, R, smem + P_B0 * HALF_BYTES);
+  if (c.wr == 1) bar();
+
+  const int iters = c.nt >> 1;
+  for (;;) {
+    for (int it = 0; it < iters; ++it) {
+      phase<0, S>(c, R, it);
+      phase<1, S>(c, R, it);
+      phase<2, S>(c, R, it);
+      phase<3, S>(c, R, it);
+      phase<4, S>(c, R, it);
+      phase<5, S>(c, R, it);
+      phase<6, S>(c, R, it);
+      phase<7, S>(c, R, it);
+    }
+    store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+    if (!c.has_next) break;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int n = 0; n < 2; ++n) R.acc[a][i][b][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    tm = tm2;
+    tn = tn2;
+    c.Ag = c.Ag2;
+    c.Bg = c.Bg2;
+    vb2 += gridDim.x;
+    c.has_next = vb2 < nwg;
+    if (c.has_next) {
+      tile_coords(vb2, nwg, ntm, ntn, tm2, tn2);
+      c.Ag2 = A + (long)tm2 * BM * lda;
+      c.Bg2 = B + (long)tn2 * BN * ldb;
+    }
+  }
+  if (c.wr == 0) bar();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace g256
+
+}  // namespace kgs
