@@ -22,7 +22,7 @@ import sys
 
 from . import config as C
 
-VERBS = ("create", "delete", "load", "status", "bench", "images")
+VERBS = ("create", "delete", "load", "status", "bench", "images", "doctor")
 
 
 class _Parser(argparse.ArgumentParser):
@@ -110,6 +110,10 @@ def main(argv=None, prog: str = "kgs") -> int:
 
             return run_e2e(p, gpus=a.gpus, pod_timeout=a.pod_timeout, keep=a.keep,
                            workload_image=a.workload_image)
+        if a.verb == "doctor":
+            from .doctor import run_doctor
+
+            return run_doctor(s, as_json=a.json)
         if a.verb == "images":
             from .images import build_images
 

@@ -67,7 +67,7 @@ TEST_POD_READY_TIMEOUT_S = 60
 
 SUCCESS_FMT_FAKE = " Simulated GPU Kind cluster is ready for '{gpu_type}'!"  # kind-gpu-sim.sh:388
 SUCCESS_FMT_REAL = " MI355X Kind cluster is ready for '{gpu_type}' ({n} amd.com/gpu advertised)!"
-USAGE = "Usage: {prog} {{create [rocm]|delete|load|status|bench}} [--registry-port=N] [--cluster-name=S] " \
+USAGE = "Usage: {prog} {{create [rocm]|delete|load|status|bench|doctor}} [--registry-port=N] [--cluster-name=S] " \
         "[--image-name=S] [--runtime=docker|podman] [--dry-run] ..."
 
 

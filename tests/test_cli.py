@@ -325,3 +325,29 @@ def test_default_base_images_use_public_mirror(world):
     assert run("create", "--dev-root", world.nogpu) == 0
     build = world.calls("docker", "build")[0]
     assert f"PY_IMAGE={C.BASE_MIRROR}/python:3.12-slim" in build
+
+
+def test_doctor_cpu_only_host(world, capsys):
+    """No /dev/kfd: runtime/kind/kubectl OK (fakes on PATH), devices WARN, exit 0."""
+    assert run("doctor", "--dev-root", world.nogpu, "--json", "--registry-port", "0") == 0
+    rep = json.loads(capsys.readouterr().out)
+    st = {c["name"]: c["status"] for c in rep["checks"]}
+    assert st["container runtime"] == "OK" and st["kind"] == "OK" and st["kubectl"] == "OK"
+    assert st["/dev/kfd"] == "WARN" and rep["ok"] is True
+
+
+def test_doctor_fake_mi355x_box(world, tmp_path, capsys):
+    root = str(make_fake_mi355x(str(tmp_path / "host8")))
+    assert run("doctor", "--dev-root", root, "--json", "--registry-port", "0") == 0
+    rep = json.loads(capsys.readouterr().out)
+    st = {c["name"]: (c["status"], c["detail"]) for c in rep["checks"]}
+    assert st["GPUs"][0] == "OK" and "8 x gfx950" in st["GPUs"][1]
+    assert st["xGMI mesh"] == ("OK", "all 28 pairs directly linked")
+    assert st["health"][0] == "OK"
+
+
+def test_doctor_missing_tools_fails(world, monkeypatch, capsys):
+    monkeypatch.setenv("PATH", "/nonexistent")
+    assert run("doctor", "--dev-root", world.nogpu, "--registry-port", "0") == 1
+    out = capsys.readouterr().out
+    assert "FAIL" in out and "kind not on PATH" in out

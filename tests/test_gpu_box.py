@@ -103,3 +103,13 @@ def test_workload_entrypoint_counters(tmp_path):
     res = _last_json(r.stdout)
     assert all(v is True for v in res["counters"]["passes"].values()), res["counters"]
     assert "MFMA busy" in r.stdout and "L2 hit" in r.stdout
+
+
+def test_doctor_device_checks_on_the_box():
+    """`kgs doctor` on the MI355X box: the device checks pass (docker/kind are
+    not installed on the box, so the tool checks FAIL and the exit status is 1)."""
+    r = subprocess.run([sys.executable, "-m", "kgs", "doctor", "--json", "--registry-port", "0"],
+                       env=ENV, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    rep = json.loads(r.stdout)
+    st = {c["name"]: c["status"] for c in rep["checks"]}
+    assert st["/dev/kfd"] == "OK" and st["GPUs"] == "OK" and st["render nodes"] == "OK" and st["health"] == "OK"
