@@ -13,7 +13,7 @@ from ._lib import KernelError, NativeUnavailable, available  # noqa: F401
 
 def __getattr__(name):  # lazy: keep `import kgs.ops` free of torch for CPU-only tools
     if name in ("gemm_nt", "matmul", "linear", "Linear", "fast_path_ok", "transpose", "EPI", "gemm_fp8_nt",
-                "quantize_fp8", "gemm_bf16"):
+                "quantize_fp8", "gemm_bf16", "quantize_fp8_dev", "Fp8Linear"):
         from . import gemm
 
         return getattr(gemm, name)

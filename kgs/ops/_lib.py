@@ -41,6 +41,9 @@ _SIGS = {
     "kgs_gemm_fp8_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [ctypes.c_float, _c_int, _c_int,
                                                                                      _c_void_p], _c_int),
     "kgs_gemm_fp8_nt_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 7, _c_int),
+    "kgs_gemm_fp8_nt_dev": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 +
+                            [ctypes.c_float, _c_void_p, _c_int, _c_int, _c_void_p], _c_int),
+    "kgs_quantize_fp8": ([_c_void_p, _c_long, _c_int, _c_void_p, _c_void_p, _c_void_p], _c_int),
     "kgs_gemm_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 9 + [_c_void_p], _c_int),
     "kgs_gemm_bf16_layout_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8, _c_int),
     "kgs_vector_add_f32": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),

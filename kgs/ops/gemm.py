@@ -103,10 +103,28 @@ def quantize_fp8(x: torch.Tensor, scale: float | None = None) -> tuple[torch.Ten
     return q, float(scale)
 
 
+def quantize_fp8_dev(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-tensor e4m3 quantisation on the GPU (native/kernels/quant_fp8.hip).
+
+    Returns ``(q, scale)`` where ``scale`` is a 1-element f32 DEVICE tensor
+    (``x ~= q.float() * scale``); nothing is copied to the host, so the call is
+    graph-capturable. ``x``: contiguous f32/bf16, numel % 8 == 0."""
+    if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_cuda or not x.is_contiguous():
+        raise ValueError("quantize_fp8_dev needs a contiguous f32/bf16 GPU tensor")
+    if x.numel() % 8:
+        raise ValueError("numel must be a multiple of 8")
+    q = torch.empty(x.shape, dtype=FP8_DTYPE, device=x.device)
+    out2 = torch.empty(2, dtype=torch.float32, device=x.device)
+    rc = _lib.lib().kgs_quantize_fp8(x.data_ptr(), x.numel(), 1 if x.dtype == torch.bfloat16 else 0, q.data_ptr(),
+                                     out2.data_ptr(), _lib.stream_handle(x.device))
+    _lib.check(rc, "quantize_fp8")
+    return q, out2[1:2]
+
+
 def gemm_fp8_nt(
     a: torch.Tensor,
     b: torch.Tensor,
-    scale_a: float = 1.0,
+    scale_a: float | torch.Tensor = 1.0,
     scale_b: float = 1.0,
     bias: torch.Tensor | None = None,
     act: str | None = None,
@@ -142,9 +160,16 @@ def gemm_fp8_nt(
         _check_operand(out, "out")
         if tuple(out.shape) != (M, N):
             raise ValueError(f"out has shape {tuple(out.shape)}, expected {(M, N)}")
-    rc = _lib.lib().kgs_gemm_fp8_nt(
+    if isinstance(scale_a, torch.Tensor):
+        # device-resident (dynamic) activation scale: read in the kernel epilogue
+        if scale_a.dtype != torch.float32 or scale_a.numel() != 1 or scale_a.device != a.device:
+            raise ValueError("a device scale_a must be a 1-element f32 tensor on a's device")
+        alpha, alpha_ptr = float(scale_b), scale_a.data_ptr()
+    else:
+        alpha, alpha_ptr = float(scale_a) * float(scale_b), None
+    rc = _lib.lib().kgs_gemm_fp8_nt_dev(
         a.data_ptr(), b.data_ptr(), out.data_ptr(), bias.data_ptr() if bias is not None else None,
-        M, N, K, a.stride(0), b.stride(0), out.stride(0), float(scale_a) * float(scale_b), epi,
+        M, N, K, a.stride(0), b.stride(0), out.stride(0), alpha, alpha_ptr, epi,
         FP8_VARIANTS[variant], _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_fp8_nt[{M}x{N}x{K}]")
     return out
@@ -293,4 +318,32 @@ class Linear(torch.nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape
         y = linear(x.reshape(-1, shp[-1]).contiguous(), self.weight, self.bias, self.act)
+        return y.reshape(*shp[:-1], y.shape[-1])
+
+
+class Fp8Linear(torch.nn.Module):
+    """W8A8 inference Linear on the fp8 MFMA GEMM.
+
+    The weight is quantised once to e4m3 with a per-tensor host scale. Each
+    forward quantises the activation on the GPU (dynamic per-tensor scale,
+    device-resident) and runs ``gemm_fp8_nt`` with the bias/activation epilogue
+    fused: two small kernels and one GEMM, no host synchronisation
+    (hipGraph-capturable)."""
+
+    def __init__(self, weight: torch.Tensor, bias: torch.Tensor | None = None, act: str | None = None):
+        super().__init__()
+        qw, sw = quantize_fp8(weight.detach())
+        self.register_buffer("qweight", qw.contiguous())
+        self.w_scale = sw
+        self.register_buffer("bias", None if bias is None else bias.detach().to(torch.bfloat16).contiguous())
+        self.act = act
+
+    @classmethod
+    def from_linear(cls, lin: torch.nn.Module) -> "Fp8Linear":
+        return cls(lin.weight, getattr(lin, "bias", None), getattr(lin, "act", None))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        qx, sx = quantize_fp8_dev(x.reshape(-1, shp[-1]).contiguous())
+        y = gemm_fp8_nt(qx, self.qweight, sx, self.w_scale, bias=self.bias, act=self.act)
         return y.reshape(*shp[:-1], y.shape[-1])

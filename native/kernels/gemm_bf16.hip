@@ -160,18 +160,18 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
   if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                       ldc, 1.0f);
+                       ldc, 1.0f, nullptr);
   } else if (variant == 16) {
     // the same pipeline on any M, N and K % 8 == 0: buffer-resource loads zero
     // the rows / K-chunks past the edges, stores are predicated
     const dim3 gridb(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512>), gridb, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                       ldc, 1.0f);
+                       ldc, 1.0f, nullptr);
   } else if (variant == 15) {
     // production schedule with the narrow (2 x 8-B per lane) store tail, for A/B
     if constexpr (EPI != EPI_NONE) return hipErrorInvalidValue;
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 256>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                       ldb, ldc, 1.0f);
+                       ldb, ldc, 1.0f, nullptr);
   } else if (variant == 20) {
     // persistent: one block per CU walking the tiles (aligned shapes; measured
     // slightly slower than the one-shot grid, kept for A/B)
@@ -184,7 +184,7 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     const int nwg = (M / g256::BM) * (N / g256::BN);
     const dim3 gridp(nwg < cus ? nwg : cus);
     hipLaunchKernelGGL((g256::gemm_nt_256_persist<EPI, 7 + 32768>), gridp, dim3(512), 0, s, A, B, C, bias, M, N, K,
-                       lda, ldb, ldc, 1.0f);
+                       lda, ldb, ldc, 1.0f, nullptr);
   } else {
     const int vec_ok = ((lda % 8) == 0 && (ldb % 8) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
     dim3 grid((N + gen::BN - 1) / gen::BN, (M + gen::BM - 1) / gen::BM);
@@ -268,29 +268,29 @@ namespace {
 template <int EPI>
 hipError_t launch_fp8(int v, const unsigned short* A, const unsigned short* B, unsigned short* C,
                       const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
-                      hipStream_t s) {
+                      const float* alpha_ptr, hipStream_t s) {
   using namespace kgs;
   const dim3 grid_al((M / g256::BM) * (N / g256::BN));
   if (v == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
-                       ldbw, ldc, alpha);
+                       ldbw, ldc, alpha, alpha_ptr);
   } else if (v >= 17 && v <= 19) {
     // tile-group height experiments for fp8 (aligned shapes): GROUP_M 8 / 16 / 2
     if constexpr (EPI == EPI_NONE) {
       if (v == 17)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha);
+                           ldaw, ldbw, ldc, alpha, alpha_ptr);
       if (v == 18)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha);
+                           ldaw, ldbw, ldc, alpha, alpha_ptr);
       if (v == 19)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha);
+                           ldaw, ldbw, ldc, alpha, alpha_ptr);
     }
   } else {
     const dim3 grid(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                       ldaw, ldbw, ldc, alpha);
+                       ldaw, ldbw, ldc, alpha, alpha_ptr);
   }
   return hipGetLastError();
 }
@@ -307,8 +307,11 @@ KGS_EXPORT int kgs_gemm_fp8_nt_ok(const void* A, const void* B, const void* C, i
   return 1;
 }
 
-KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
-                               int ldb, int ldc, float alpha, int epi, int variant, hipStream_t stream) {
+// alpha_ptr: optional device float multiplied into alpha in the epilogue (the
+// dynamic activation scale written by kgs_quantize_fp8), so no host sync.
+KGS_EXPORT int kgs_gemm_fp8_nt_dev(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                                   int lda, int ldb, int ldc, float alpha, const float* alpha_ptr, int epi,
+                                   int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if (epi != kgs::EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
@@ -326,20 +329,29 @@ KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void
   const int Kw = K / 2, ldaw = lda / 2, ldbw = ldb / 2;  // fp8 rows as 16-bit words
   hipError_t e;
   switch (epi) {
-    case kgs::EPI_NONE: e = launch_fp8<kgs::EPI_NONE>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream); break;
-    case kgs::EPI_BIAS: e = launch_fp8<kgs::EPI_BIAS>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream); break;
+    case kgs::EPI_NONE:
+      e = launch_fp8<kgs::EPI_NONE>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, stream);
+      break;
+    case kgs::EPI_BIAS:
+      e = launch_fp8<kgs::EPI_BIAS>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, stream);
+      break;
     case kgs::EPI_BIAS_GELU:
-      e = launch_fp8<kgs::EPI_BIAS_GELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      e = launch_fp8<kgs::EPI_BIAS_GELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, stream);
       break;
     case kgs::EPI_BIAS_RELU:
-      e = launch_fp8<kgs::EPI_BIAS_RELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      e = launch_fp8<kgs::EPI_BIAS_RELU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, stream);
       break;
     case kgs::EPI_BIAS_SILU:
-      e = launch_fp8<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, stream);
+      e = launch_fp8<kgs::EPI_BIAS_SILU>(v, a, b, c, bb, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, stream);
       break;
     default: return KGS_ERR_ARG;
   }
   return (int)e;
+}
+
+KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
+                               int ldb, int ldc, float alpha, int epi, int variant, hipStream_t stream) {
+  return kgs_gemm_fp8_nt_dev(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, nullptr, epi, variant, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -359,7 +371,7 @@ hipError_t launch_t(const unsigned short* A, const unsigned short* B, unsigned s
   using namespace kgs;
   const dim3 grid((M / g256::BM) * (N / g256::BN));
   hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + T>), grid, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
-                     1.0f);
+                     1.0f, nullptr);
   return hipGetLastError();
 }
 

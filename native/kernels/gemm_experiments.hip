@@ -622,19 +622,19 @@ static hipError_t launch_experiment(int variant, const unsigned short* A, const 
     if constexpr (EPI == EPI_NONE) {
       if (variant == 4)  // with s_setprio around the MFMA blocks
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 5>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 5)  // GROUP_M 8
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 6)  // first schedule (12/4/8/0 reads, look-ahead 5), setprio, GROUP_M 8
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 0>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 7)  // GROUP_M 2
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 8)  // GROUP_M 16
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;
@@ -643,16 +643,16 @@ static hipError_t launch_experiment(int variant, const unsigned short* A, const 
     if constexpr (EPI == EPI_NONE) {
       if (variant == 9)  // timing probe: every MFMA block doubled (wrong C)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 16>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 11)  // timing probe: all blocks load the same (L2-resident) tiles (wrong C)
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 32>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                           ldb, ldc, 1.0f);
+                           ldb, ldc, 1.0f, nullptr);
       if (variant == 12)  // lockstep: no ping-pong stagger
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K,
-                           lda, ldb, ldc, 1.0f);
+                           lda, ldb, ldc, 1.0f, nullptr);
       if (variant == 13)  // lockstep, one barrier per phase
         hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 64 + 128>), grid256, dim3(512), 0, s, A, B, C, bias, M, N,
-                           K, lda, ldb, ldc, 1.0f);
+                           K, lda, ldb, ldc, 1.0f, nullptr);
       return hipGetLastError();
     }
     return hipErrorInvalidValue;

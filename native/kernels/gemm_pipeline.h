@@ -376,7 +376,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
                                                    unsigned short* __restrict__ C,
                                                    const unsigned short* __restrict__ bias,
                                                    int M, int N, int K, int lda, int ldb, int ldc,
-                                                   float alpha) {
+                                                   float alpha, const float* __restrict__ alpha_ptr) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   constexpr bool BND = (S & 512) != 0;
@@ -503,6 +503,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   if (!(S & 64) && c.wr == 0) bar();  // balance the stagger barrier
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
 
+  // fp8: the dequant scale, times a device-resident factor (dynamic activation scale)
+  if constexpr (S & 1024) {
+    if (alpha_ptr) alpha *= *alpha_ptr;
+  }
   store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
 }
 
@@ -531,7 +535,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_persist(const unsigned short*
                                                            unsigned short* __restrict__ C,
                                                            const unsigned short* __restrict__ bias,
                                                            int M, int N, int K, int lda, int ldb, int ldc,
-                                                           float alpha) {
+                                                           float alpha, const float* __restrict__ alpha_ptr) {
   static_assert((S & 1) && (S & 32768) && !(S & 512) && !(S & (2048 | 4096)), "persistent: aligned NT only");
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
   const int lane = threadIdx.x & 63;
@@ -593,6 +597,9 @@ __global__ __launch_bounds__(512) void gemm_nt_256_persist(const unsigned short*
   read_b<0>(c, R, smem + P_B0 * HALF_BYTES);
   if (c.wr == 1) bar();
 
+  if constexpr (S & 1024) {
+    if (alpha_ptr) alpha *= *alpha_ptr;
+  }
   const int iters = c.nt >> 1;
   for (;;) {
     for (int it = 0; it < iters; ++it) {

@@ -363,3 +363,55 @@ def test_gemm_layout_epilogue_and_fallback():
     bias = torch.randn(768, device=DEV).bfloat16()
     ref = torch.nn.functional.gelu(a.float() @ b.float() + bias.float(), approximate="tanh")
     torch.testing.assert_close(gemm(a, b, bias=bias, act="gelu").float(), ref, rtol=2e-2, atol=2e-2)
+
+
+# ------------------------------------------------------ fp8 quant + W8A8 --
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_quantize_fp8_dev_matches_reference(dtype):
+    from kgs.ops import quantize_fp8_dev
+
+    x = (torch.randn(4096, 1024, device=DEV) * 3).to(dtype)
+    q, s = quantize_fp8_dev(x)
+    amax = x.float().abs().max()
+    torch.testing.assert_close(s, (amax / 448).reshape(1), rtol=1e-6, atol=0)
+    ref = (x.float() * (1.0 / s)).clamp(-448, 448).to(torch.float8_e4m3fn)
+    same = (q.view(torch.uint8) == ref.view(torch.uint8)).float().mean().item()
+    assert same > 0.999, same  # rounding of x * (1/scale) may differ in the last bit
+    deq = q.float() * s
+    assert torch.all((deq - x.float()).abs() <= 0.0625 * x.float().abs() + 2 * s * 2 ** -9)
+
+
+def test_gemm_fp8_device_scale_and_fp8_linear():
+    from kgs.ops import Fp8Linear, Linear, gemm_fp8_nt, quantize_fp8, quantize_fp8_dev
+
+    torch.manual_seed(0)
+    x = torch.randn(1024, 2048, device=DEV).bfloat16()
+    w = torch.randn(768, 2048, device=DEV).bfloat16() * 0.02
+    qx, sx = quantize_fp8_dev(x)
+    qw, sw = quantize_fp8(w)
+    dev = gemm_fp8_nt(qx, qw, sx, sw)
+    host = gemm_fp8_nt(qx, qw, float(sx.item()), sw)
+    torch.testing.assert_close(dev.float(), host.float(), rtol=1e-2, atol=1e-3)
+
+    lin = Linear(2048, 768, bias=True, act="gelu", device=DEV)
+    with torch.no_grad():
+        lin.weight.copy_(w)
+        lin.bias.copy_(torch.randn(768, device=DEV).bfloat16() * 0.1)
+    f8 = Fp8Linear.from_linear(lin)
+    with torch.no_grad():
+        ref = lin(x).float()
+        got = f8(x).float()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 0.05, rel
+
+    # the W8A8 forward has no host sync: capture it and replay on new data
+    xs = torch.zeros_like(x)
+    f8(xs)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ys = f8(xs)
+    xs.copy_(x)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(ys, f8(x))
