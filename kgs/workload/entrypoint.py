@@ -127,9 +127,14 @@ def main(argv=None) -> int:
         env = dict(os.environ)
         env["PYTHONPATH"] = root + (":" + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-               "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "kgs.workload.worker",
-               "--gemm-size", str(a.gemm_size), "--gemm-iters", str(a.gemm_iters)]
+        worker = ["-m", "kgs.workload.worker", "--gemm-size", str(a.gemm_size), "--gemm-iters", str(a.gemm_iters)]
+        if n == 1:
+            # one GPU: no process group to set up, skip torchrun's agent (~1 s)
+            env.update(WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+            cmd = [sys.executable, *worker]
+        else:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                   "--master-addr=127.0.0.1", f"--master-port={_free_port()}", *worker]
         if a.allreduce_sizes:
             cmd += ["--allreduce-sizes", a.allreduce_sizes]
         if a.smoke:
