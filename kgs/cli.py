@@ -59,6 +59,8 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
     ap.add_argument("--dev-root", default="/", help="host root for GPU discovery (tests)")
     ap.add_argument("--dry-run", action="store_true", help="print the command plan, change nothing")
     ap.add_argument("--keep-on-fail", action="store_true")
+    ap.add_argument("--serial", action="store_true",
+                    help="build the plugin image after the cluster (default: concurrently with kind create)")
     ap.add_argument("--json", action="store_true")
     # bench/images options
     ap.add_argument("--gpus", type=int, default=1, help="bench: amd.com/gpu requested by the test pod")
@@ -78,7 +80,7 @@ def settings_from(a) -> C.Settings:
         registry_bind=a.registry_bind, kind_node_image=a.kind_node_image, dry_run=a.dry_run,
         keep_on_fail=a.keep_on_fail, skip_build=a.skip_build, timings_json=a.timings_json,
         plugin_image=a.plugin_image, ready_timeout_s=a.ready_timeout, dev_root=a.dev_root,
-        base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image,
+        base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image, extra={"serial": a.serial},
     )
 
 

@@ -223,13 +223,19 @@ class Provisioner:
         return f"localhost/{repo}" if rt.name == "podman" else f"{self.s.registry_host}/{repo}"
 
     def build_plugin_image(self) -> str:
+        """Build (or pick) the plugin image and make it pullable by the nodes."""
+        self.plugin_image_stage1()
+        return self.plugin_image_stage2()
+
+    def plugin_image_stage1(self) -> None:
+        """Everything that does not need the cluster: docker build + push to the
+        local registry (podman: build + tag). Runs concurrently with
+        ``kind create cluster`` in ``create`` -- a cold image build is the
+        longest phase after cluster creation, and the reference runs it after."""
         rt = self.ensure_runtime()
         image = self.plugin_image()
         if self.s.plugin_image or self.s.skip_build:
-            self.out(f"Using prebuilt device-plugin image {image}")
-            if rt.name == "podman" or self.s.plugin_image:
-                rt.load_into_kind(image, self.s.cluster_name)
-            return image
+            return
         tag = f"{self.s.registry_host}/{C.PLUGIN_IMAGE_REPO}:{C.PLUGIN_IMAGE_TAG}"
         self.out(" Building kgs ROCm device plugin image...")
         env = {"BUILDAH_FORMAT": "docker"} if rt.name == "podman" else None
@@ -239,6 +245,17 @@ class Provisioner:
             rt.cr("push", tag)
         else:
             rt.cr("tag", tag, image)
+
+    def plugin_image_stage2(self) -> str:
+        """The cluster-dependent part: side-load into the kind nodes where the
+        nodes cannot pull it (podman, or a prebuilt image not in the registry)."""
+        rt = self.ensure_runtime()
+        image = self.plugin_image()
+        if self.s.plugin_image or self.s.skip_build:
+            self.out(f"Using prebuilt device-plugin image {image}")
+            if rt.name == "podman" or self.s.plugin_image:
+                rt.load_into_kind(image, self.s.cluster_name)
+        elif rt.name == "podman":
             rt.save_and_kind_load(image, self.s.cluster_name)
         return image
 
@@ -315,6 +332,11 @@ class Provisioner:
             self.start_registry()
         with t.phase("kind-config"):
             cfg = self.write_kind_config()
+        # the plugin image builds while kind creates the cluster (dry-run and
+        # --serial keep the reference's sequential order)
+        build = None
+        if not self.runner.dry_run and not self.s.extra.get("serial"):
+            build = _Background(self.plugin_image_stage1)
         try:
             with t.phase("kind-create") as rec:
                 if not self.runner.dry_run and self.cluster_exists():
@@ -330,8 +352,12 @@ class Provisioner:
                 rec["workers"] = self.configure_nodes()
             with t.phase("registry-configmap"):
                 self.apply_registry_configmap()
-            with t.phase("plugin-image"):
-                image = self.build_plugin_image()
+            with t.phase("plugin-image") as rec:
+                if build is not None:
+                    rec["overlapped_build_s"] = build.join()
+                    image = self.plugin_image_stage2()
+                else:
+                    image = self.build_plugin_image()
             with t.phase("plugin-deploy"):
                 self.deploy_plugin(image)
             with t.phase("plugin-ready"):
@@ -339,6 +365,8 @@ class Provisioner:
             with t.phase("capacity") as rec:
                 rec["amd.com/gpu"] = self.wait_capacity()
         except (ProvisionError, CommandError):
+            if build is not None:
+                build.join(reraise=False)
             if self.created_cluster and not self.s.keep_on_fail and not self.runner.dry_run:
                 self.out(f"create failed; deleting cluster '{self.s.cluster_name}' (use --keep-on-fail to keep it)")
                 self.kind("delete", "cluster", "--name", self.s.cluster_name, check=False)
@@ -398,3 +426,31 @@ class Provisioner:
             for line in info.get("plugin_pods", []):
                 self.out(f"  {line}")
         return 0
+
+
+class _Background:
+    """Run ``fn`` on a thread; ``join`` re-raises its exception in the caller."""
+
+    def __init__(self, fn):
+        import threading
+
+        self._exc = None
+        self._t0 = time.monotonic()
+        self._dt = None
+
+        def run():
+            try:
+                fn()
+            except BaseException as e:  # surfaced by join()
+                self._exc = e
+            finally:
+                self._dt = time.monotonic() - self._t0
+
+        self._thread = threading.Thread(target=run, name="kgs-image-build", daemon=True)
+        self._thread.start()
+
+    def join(self, reraise: bool = True) -> float:
+        self._thread.join()
+        if reraise and self._exc is not None:
+            raise self._exc
+        return round(self._dt or 0.0, 4)

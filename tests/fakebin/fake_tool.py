@@ -11,6 +11,7 @@ device-plugin DaemonSet is applied (from the bind-mounted partition file), etc.
 Fault injection: $KGS_FAKE_FAIL = comma list of {plugin-ready, kind-create,
 push, pod-running}.
 """
+import fcntl
 import json
 import os
 import sys
@@ -44,6 +45,12 @@ def err(msg, rc=1):
     sys.stderr.write(msg + "\n")
     sys.exit(rc)
 
+
+# The orchestrator runs some tools concurrently (the plugin image builds while
+# kind creates the cluster); serialise whole invocations on a lock next to the
+# state file, so the read-modify-write of the simulated world stays atomic.
+_lock = open(STATE + ".lock", "a")
+fcntl.flock(_lock, fcntl.LOCK_EX)
 
 stdin = None
 if not sys.stdin.isatty():

@@ -351,3 +351,24 @@ def test_doctor_missing_tools_fails(world, monkeypatch, capsys):
     assert run("doctor", "--dev-root", world.nogpu, "--registry-port", "0") == 1
     out = capsys.readouterr().out
     assert "FAIL" in out and "kind not on PATH" in out
+
+
+def test_plugin_image_builds_concurrently_with_kind_create(world, tmp_path):
+    tj = tmp_path / "t.json"
+    assert run("create", "--dev-root", world.nogpu, "--timings-json", str(tj)) == 0
+    phases = {p["phase"]: p for p in json.loads(tj.read_text())["phases"]}
+    assert "overlapped_build_s" in phases["plugin-image"]
+    # the pushed image is in the registry before the DaemonSet is applied
+    log = world.log()
+    push = next(i for i, e in enumerate(log) if e["tool"] == "docker" and e["argv"][:1] == ["push"])
+    apply_ds = next(i for i, e in enumerate(log) if e["tool"] == "kubectl" and "apply" in e["argv"]
+                    and e["stdin"] and "DaemonSet" in e["stdin"])
+    assert push < apply_ds
+
+
+def test_serial_flag_keeps_reference_order(world):
+    assert run("create", "--dev-root", world.nogpu, "--serial") == 0
+    log = world.log()
+    kind_create = next(i for i, e in enumerate(log) if e["tool"] == "kind" and e["argv"][:2] == ["create", "cluster"])
+    build = next(i for i, e in enumerate(log) if e["tool"] == "docker" and e["argv"][:1] == ["build"])
+    assert kind_create < build

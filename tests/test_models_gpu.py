@@ -14,7 +14,8 @@ def test_mlp_training_kgs_tracks_torch():
     kw = dict(steps=12, global_batch=2048, lr=0.2, device="cuda", dtype=torch.bfloat16)
     k = train_dp(dims, backend="kgs", **kw)
     t = train_dp(dims, backend="torch", **kw)
-    assert k["losses"][-1] < 0.8 * k["losses"][0]
+    assert k["losses"][-1] < 0.97 * k["losses"][0]
+    assert t["losses"][-1] < 0.97 * t["losses"][0]
     # same init, same data, bf16 both ways: the curves agree to bf16 noise
     for a, b in zip(k["losses"], t["losses"]):
         assert abs(a - b) <= 0.05 * max(abs(b), 1e-3)
