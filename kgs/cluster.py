@@ -214,6 +214,16 @@ class Provisioner:
                 self.kubectl("patch", "node", w, "--type=json", f"-p={patch}", "--subresource=status")
         return workers
 
+    def prepull(self, nodes: list, images: list) -> None:
+        """Pull ``images`` into the nodes' containerd from the local registry
+        (``crictl pull`` inside each kind node), so the test pod does not pay a
+        multi-GB pull after it is scheduled. Runs in the background during
+        ``create`` while the plugin is deployed and becomes Ready."""
+        rt = self.ensure_runtime()
+        for node in nodes:
+            for img in images:
+                rt.cr("exec", node, "crictl", "pull", img, check=False)
+
     # -------------------------------------------------------------- plugin ---
     def plugin_image(self) -> str:
         if self.s.plugin_image:
@@ -350,6 +360,14 @@ class Provisioner:
                 self.ensure_runtime().network_connect(C.KIND_NETWORK, C.REGISTRY_NAME)
             with t.phase("nodes") as rec:
                 rec["workers"] = self.configure_nodes()
+            prepull_images = self.s.extra.get("prepull") or []
+            if prepull_images and not self.runner.dry_run:
+                # GPU pods only land on GPU workers; pull there while the plugin comes up
+                gpu_nodes = [w for w, part in zip(rec["workers"], self.partitions or [[1]] * len(rec["workers"]))
+                             if part] or rec["workers"]
+                pulls = _Background(lambda: self.prepull(gpu_nodes, prepull_images))
+            else:
+                pulls = None
             with t.phase("registry-configmap"):
                 self.apply_registry_configmap()
             with t.phase("plugin-image") as rec:
@@ -364,6 +382,9 @@ class Provisioner:
                 self.wait_plugin_ready()
             with t.phase("capacity") as rec:
                 rec["amd.com/gpu"] = self.wait_capacity()
+            if pulls is not None:
+                with t.phase("prepull-wait") as rec:
+                    rec["overlapped_pull_s"] = pulls.join()
         except (ProvisionError, CommandError):
             if build is not None:
                 build.join(reraise=False)

@@ -34,8 +34,12 @@ def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, kee
             workload_image: str | None = None, pod_command: list | None = None) -> int:
     t = p.timer
     t_start = time.perf_counter()
-    p.create("rocm")
     image = workload_image or globals()["workload_image"](p)
+    if p.ensure_runtime().name != "podman" and not p.s.extra.get("no_prepull"):
+        # pull the (multi-GB) workload image into the GPU workers during create,
+        # overlapped with plugin deploy/readiness, instead of after scheduling
+        p.s.extra["prepull"] = [image]
+    p.create("rocm")
     if p.ensure_runtime().name == "podman" and not workload_image:
         with t.phase("workload-image-load"):
             p.rt.load_into_kind(image, p.s.cluster_name)

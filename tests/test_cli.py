@@ -303,6 +303,11 @@ def test_bench_e2e(world, tmp_path, capsys):
     assert doc["spec"]["containers"][0]["name"] == "gpu-sim"
     assert doc["spec"]["containers"][0]["resources"]["limits"] == {"amd.com/gpu": 1}
     assert world.state()["clusters"] == {}  # bench deletes unless --keep
+    # the workload image was pre-pulled into the workers during create
+    pulls = [e["argv"] for e in world.log() if e["tool"] == "docker" and e["argv"][:1] == ["exec"]
+             and "crictl" in e["argv"]]
+    assert pulls and all(a[-1] == "localhost:5000/kgs-rocm-test:dev" for a in pulls)
+    assert any(p["phase"] == "prepull-wait" for p in t["phases"])
 
 
 def test_shell_wrapper_is_executable():
