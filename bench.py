@@ -54,6 +54,8 @@ def parse(argv=None):
     ap.add_argument("--backend", choices=("kgs", "torch"), default="kgs",
                     help="kgs = hand-written gfx950 kernel (the benchmark); torch = reference / CPU test path")
     ap.add_argument("--cpu", action="store_true", help="CPU + gloo (tests of the distributed plumbing only)")
+    ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="bf16 = the headline (BASELINE.json); fp8 = e4m3 operands on the scaled MFMA (extra)")
     return ap.parse_args(argv)
 
 
@@ -82,6 +84,7 @@ def main(argv=None) -> int:
         group=ctx.group,
         seed=1234 + rank,
         backend=args.backend,
+        dtype=args.dtype,
     )
     if args.verify:
         err = wl.verify()
@@ -115,7 +118,9 @@ def main(argv=None) -> int:
 
     if rank == 0:
         out = {
-            "metric": "in-pod bf16 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 MFMA GEMM + RCCL grad all-reduce)",
+            "metric": "in-pod bf16 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 MFMA GEMM + RCCL grad all-reduce)"
+                      if args.dtype == "bf16" else
+                      "in-pod fp8 e4m3 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 scaled-MFMA GEMM + RCCL all-reduce)",
             "value": round(total_tflops, 2),
             "unit": "TFLOP/s",
             "n_gpus": world,
@@ -125,10 +130,10 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(total_tflops / BASELINE_VALUE, 4) if BASELINE_VALUE else None),
-            "dtype": "bf16",
+            "dtype": args.dtype if args.dtype == "bf16" else "fp8_e4m3",
             "data": "synthetic U[-1,1) operands, random-init",
             "config": {
-                "model": "rocm-gpu-test in-pod workload: bf16 GEMM C=A.B^T (kgs gfx950 MFMA kernel)",
+                "model": f"rocm-gpu-test in-pod workload: {args.dtype} GEMM C=A.B^T (kgs gfx950 MFMA kernel)",
                 "global_batch": args.gemms_per_step * world,
                 "seq_len": args.m,
                 "parallelism": f"dp{world}",

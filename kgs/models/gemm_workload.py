@@ -17,7 +17,7 @@ import torch
 
 class GemmWorkload:
     def __init__(self, m=8192, n=8192, k=8192, gemms_per_step=4, allreduce_bytes=0, overlap=True,
-                 device=None, group=None, seed=0, backend="kgs"):
+                 device=None, group=None, seed=0, backend="kgs", dtype="bf16"):
         self.m, self.n, self.k = m, n, k
         self.g = gemms_per_step
         self.device = torch.device(device) if device is not None else torch.device("cuda")
@@ -40,7 +40,23 @@ class GemmWorkload:
             self.bucket = torch.rand(allreduce_bytes // 4, generator=gen, device=self.device)
             if self.cuda:
                 self.comm_stream = torch.cuda.Stream(device=self.device)
-        if backend == "kgs":
+        self.dtype = dtype
+        if dtype == "fp8":
+            # e4m3 operands (per-tensor scales), bf16 out: the scaled fp8 MFMA path
+            from kgs.ops import quantize_fp8
+
+            self.qa, self.sa = quantize_fp8(self.a)
+            self.qb, self.sb = quantize_fp8(self.b)
+            if backend == "kgs":
+                from kgs.ops import gemm_fp8_nt
+
+                self._gemm = lambda i: gemm_fp8_nt(self.qa, self.qb, self.sa, self.sb, out=self.c[i & 1])
+            else:
+                ta = torch.tensor(self.sa, device=self.device)
+                tb = torch.tensor(self.sb, device=self.device)
+                self._gemm = lambda i: torch._scaled_mm(self.qa, self.qb.T, scale_a=ta, scale_b=tb,
+                                                        out_dtype=torch.bfloat16, out=self.c[i & 1])
+        elif backend == "kgs":
             from kgs.ops import gemm_nt
 
             self._gemm = lambda i: gemm_nt(self.a, self.b, out=self.c[i & 1])
@@ -51,6 +67,8 @@ class GemmWorkload:
         return 2.0 * self.m * self.n * self.k * self.g
 
     def path_name(self) -> str:
+        if self.dtype == "fp8":
+            return "kgs gemm_fp8_nt (scaled e4m3 MFMA)" if self.backend == "kgs" else "torch._scaled_mm"
         if self.backend != "kgs":
             return "torch.matmul"
         from kgs.ops import fast_path_ok
@@ -87,7 +105,10 @@ class GemmWorkload:
     def verify(self, rows: int = 256) -> float:
         """Relative max error of one GEMM's first ``rows`` rows vs fp32 torch."""
         self._gemm(0)
-        ref = self.a[:rows].float() @ self.b.float().T
+        if self.dtype == "fp8":
+            ref = (self.qa[:rows].float() * self.sa) @ (self.qb.float() * self.sb).T
+        else:
+            ref = self.a[:rows].float() @ self.b.float().T
         got = self.c[0][:rows].float()
         return ((got - ref).abs().max() / ref.abs().max()).item()
 
