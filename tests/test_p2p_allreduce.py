@@ -150,3 +150,32 @@ def test_ipc_two_processes():
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     res = json.loads(line)
     assert res["world"] == 2 and res["ok"], res
+
+
+@pytest.mark.gpu
+def test_tensor_parallel_mlp_on_p2p_allreduce():
+    """4-way TP MLP on the HIP GEMM, row-parallel partials summed by the P2P
+    kernel (one launch plays the 4 ranks): every rank gets the same output, and
+    it matches the unsplit MLP to bf16 accuracy."""
+    from kgs.parallel.p2p_allreduce import P2PAllReduce
+    from kgs.parallel.tensor_parallel import reference_mlp, tp_mlp_local
+
+    g = torch.Generator(device="cuda").manual_seed(3)
+    din, dff, dout, world = 1024, 4096, 1024, 4
+    x = (torch.randn(512, din, device="cuda", generator=g)).bfloat16()
+    w1 = (torch.randn(dff, din, device="cuda", generator=g) * din ** -0.5).bfloat16()
+    b1 = (torch.randn(dff, device="cuda", generator=g) * 0.1).bfloat16()
+    w2 = (torch.randn(dout, dff, device="cuda", generator=g) * dff ** -0.5).bfloat16()
+    b2 = (torch.randn(dout, device="cuda", generator=g) * 0.1).bfloat16()
+    ar = P2PAllReduce.local_ranks(world, max_bytes=8 << 20, device="cuda", timeout_s=3.0)
+    try:
+        outs = tp_mlp_local(x, w1, b1, w2, b2, world, p2p_local=ar)
+        torch.cuda.synchronize()
+        ar.check()
+    finally:
+        ar.close()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    ref = reference_mlp(x, w1, b1, w2, b2)
+    rel = ((outs[0].float() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel

@@ -181,3 +181,34 @@ def test_mlp_dp_matches_single_process_full_batch():
             torch.testing.assert_close(p, q, rtol=1e-5, atol=1e-6)
         assert abs(losses[-1] - ref["losses"][-1]) < 1e-5
     assert ref["losses"][-1] < ref["losses"][0]
+
+
+def _tp_weights(din=64, dff=128, dout=48, dtype=torch.float32, device="cpu"):
+    g = torch.Generator().manual_seed(7)
+    w1 = (torch.randn(dff, din, generator=g) * din ** -0.5).to(dtype).to(device)
+    b1 = (torch.randn(dff, generator=g) * 0.1).to(dtype).to(device)
+    w2 = (torch.randn(dout, dff, generator=g) * dff ** -0.5).to(dtype).to(device)
+    b2 = (torch.randn(dout, generator=g) * 0.1).to(dtype).to(device)
+    x = torch.randn(32, din, generator=g).to(dtype).to(device)
+    return x, w1, b1, w2, b2
+
+
+def _tp_rank(rank, world):
+    from kgs.parallel import dist as kdist
+    from kgs.parallel.tensor_parallel import TPMLP, make_reducer
+
+    ctx = kdist.init_from_env(device_type="cpu")
+    x, w1, b1, w2, b2 = _tp_weights()
+    mlp = TPMLP(w1, b1, w2, b2, world, rank, make_reducer(ctx.group), backend="torch")
+    return mlp(x)
+
+
+def test_tensor_parallel_mlp_gloo():
+    """Column(gelu) -> row split over 2 ranks + one all-reduce == the full MLP."""
+    from kgs.parallel.tensor_parallel import reference_mlp
+
+    res = _spawn(_tp_rank)
+    x, w1, b1, w2, b2 = _tp_weights()
+    ref = reference_mlp(x, w1, b1, w2, b2)
+    for r in (0, 1):
+        torch.testing.assert_close(res[r], ref, rtol=1e-5, atol=1e-5)
