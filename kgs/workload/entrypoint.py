@@ -108,6 +108,7 @@ def main(argv=None) -> int:
     ap.add_argument("--counters-dir", default="/tmp/kgs-rocprof")
     ap.add_argument("--smoke", action="store_true", help="config 2: rocminfo + HIP vector add only")
     ap.add_argument("--fp8", action="store_true", help="also report the e4m3 GEMM TFLOPS")
+    ap.add_argument("--p2p", action="store_true", help="multi-GPU pods: P2P all-reduce latency vs RCCL")
     a = ap.parse_args(argv)
 
     gpus = allocated_gpus()
@@ -141,6 +142,8 @@ def main(argv=None) -> int:
             cmd += ["--skip-gemm", "--skip-allreduce"]
         if a.fp8:
             cmd += ["--fp8"]
+        if a.p2p:
+            cmd += ["--p2p"]
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
         sys.stderr.write(p.stderr[-4000:])
         for line in p.stdout.splitlines():

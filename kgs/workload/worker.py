@@ -27,6 +27,8 @@ def _args(argv=None):
     ap.add_argument("--skip-gemm", action="store_true")
     ap.add_argument("--skip-allreduce", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="also run the e4m3 GEMM (scaled fp8 MFMA)")
+    ap.add_argument("--p2p", action="store_true",
+                    help="with >1 GPU: P2P (IPC/xGMI) all-reduce latency vs RCCL, 1 KiB..8 MiB")
     return ap.parse_args(argv)
 
 
@@ -137,6 +139,13 @@ def main(argv=None) -> int:
 
         sizes = [int(x) for x in a.allreduce_sizes.split(",") if x] or None
         sweep = [p.as_dict() for p in allreduce_sweep(sizes, iters=a.allreduce_iters, device=dev)]
+    p2p_rows = None
+    if ctx.distributed and a.p2p and dev.type == "cuda":
+        from kgs.parallel.p2p_allreduce import P2PAllReduce, latency_sweep
+
+        ar = P2PAllReduce(group=ctx.group, max_bytes=8 << 20, device=dev)
+        p2p_rows = latency_sweep(ar, iters=20)
+        ar.close()
     if ctx.rank == 0:
         gemm_tf = [r.get("gemm", {}).get("tflops", 0.0) for r in results]
         out = {"world_size": ctx.world_size, "ranks": results,
@@ -145,6 +154,8 @@ def main(argv=None) -> int:
                              and r.get("gemm_fp8", {}).get("ok", True) for r in results)}
         if any("gemm_fp8" in r for r in results):
             out["gemm_fp8_tflops_total"] = round(sum(r.get("gemm_fp8", {}).get("tflops", 0.0) for r in results), 1)
+        if p2p_rows:
+            out["p2p_allreduce"] = p2p_rows
         if sweep:
             out["allreduce"] = sweep
             out["allreduce_peak_busbw_gbs"] = round(max(p["busbw_gbs"] for p in sweep), 1)
