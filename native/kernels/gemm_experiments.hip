@@ -690,3 +690,17 @@ extern "C" hipError_t kgs_gemm_bf16_nt_experiment(int variant, int epi, const un
     default: return hipErrorInvalidValue;
   }
 }
+
+// Diagnostic build: the production schedule with s_memtime stamps (S bit 16).
+// stamps: 4 * STAMP_N u64 (blocks 0..3); layout in gemm_pipeline.h (stamp()).
+extern "C" int kgs_gemm_bf16_nt_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                       int ldc, void* stamps, hipStream_t s) {
+  if (M % 256 || N % 256 || K % 128 || (K / 128) < kgs::g256::STAMP_IT0 + kgs::g256::STAMP_ITS) return KGS_ERR_SHAPE;
+  const dim3 grid((M / 256) * (N / 256));
+  hipLaunchKernelGGL((kgs::g256::gemm_nt_256<kgs::EPI_NONE, 7 + 65536>), grid, dim3(512), 0, s,
+                     (const unsigned short*)A, (const unsigned short*)B, (unsigned short*)C, nullptr, M, N, K, lda,
+                     ldb, ldc, 1.0f, (const float*)stamps);
+  return (int)hipGetLastError();
+}
+
+extern "C" int kgs_gemm_stamp_n() { return kgs::g256::STAMP_N; }

@@ -59,7 +59,34 @@ struct Ctx {
   const unsigned short* Ag2;
   const unsigned short* Bg2;
   int has_next;
+  // timing diagnostics (S bit 16): s_memtime stamps in LDS, copied out at the end
+  KGS_LDS unsigned long* st;
 };
+
+// S bit 16 (diagnostic build, gemm_experiments.hip): per wave, 5 s_memtime
+// stamps per phase for iterations STAMP_IT0 .. +STAMP_ITS-1, kept in LDS (not
+// global memory: stores there would count in vmcnt and perturb the schedule).
+constexpr int STAMP_IT0 = 8, STAMP_ITS = 4, STAMP_PTS = 5;
+constexpr int STAMP_N = STAMP_ITS * 8 * 8 * STAMP_PTS;  // iterations x phases x waves x points
+
+// s_memtime returns through the scalar memory path: the stamps are taken into
+// SGPRs and written to LDS only at the end of the phase, so no wait for a stamp
+// lands inside the section being timed.
+template <int S>
+__device__ __forceinline__ void stamp(unsigned long* ts, int pt) {
+  if constexpr (S & 65536) ts[pt] = __builtin_amdgcn_s_memtime();
+}
+
+template <int S>
+__device__ __forceinline__ void stamp_flush(const Ctx& c, int it, int qp, const unsigned long* ts) {
+  if constexpr (S & 65536) {
+    if (it >= STAMP_IT0 && it < STAMP_IT0 + STAMP_ITS && (threadIdx.x & 63) == 0) {
+#pragma unroll
+      for (int pt = 0; pt < STAMP_PTS; ++pt)
+        c.st[(((it - STAMP_IT0) * 8 + qp) * 8 + c.w) * STAMP_PTS + pt] = ts[pt];
+    }
+  }
+}
 
 constexpr int OOB_OFFSET = 0x7FFFFFF0;  // > every num_records the bounded path builds
 
@@ -238,6 +265,8 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   constexpr int q = QP & 3;
   constexpr int cbuf = QP >> 2;
   const char* buf = c.smem + cbuf * BUF_BYTES;
+  unsigned long ts[STAMP_PTS];
+  stamp<S>(ts, 0);
   if constexpr ((S & 1) == 0) {
     if constexpr (q == 0) {
       rd_a<S>(c, R, buf + P_A0 * HALF_BYTES);
@@ -278,8 +307,11 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  stamp<S>(ts, 1);
   bar();
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  stamp<S>(ts, 2);
   __builtin_amdgcn_sched_barrier(0);
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
   if constexpr (S & 16) {  // timing experiment only: twice the MFMAs per phase (wrong results)
@@ -297,10 +329,14 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
     if constexpr ((S & 1) == 0) mma_quadrant<1, 0, (S & 1024) != 0>(R); else mma_quadrant<1, 1, (S & 1024) != 0>(R);
   }
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+  stamp<S>(ts, 3);
   // S bit 7 (with bit 6, lockstep): one barrier per phase. Still race-free: the
   // slot a phase's DMA overwrites was last read >= 2 phases earlier, i.e. before
   // the previous phase's barrier on every wave.
   if constexpr (!(S & 128)) bar();
+  stamp<S>(ts, 4);
+  stamp_flush<S>(c, it, QP, ts);
 }
 
 // Epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n); bias and
@@ -378,6 +414,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
                                                    int M, int N, int K, int lda, int ldb, int ldc,
                                                    float alpha, const float* __restrict__ alpha_ptr) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  __shared__ unsigned long stamps_lds[(S & 65536) ? STAMP_N : 1];
 
   constexpr bool BND = (S & 512) != 0;
   const int lane = threadIdx.x & 63;
@@ -395,6 +432,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 
   Ctx c;
   c.smem = smem;
+  c.st = (KGS_LDS unsigned long*)stamps_lds;
   // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
   c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;
   c.Bg = (S & 4096) ? B + (long)tn * BN : B + (long)((S & 32) ? 0 : tn) * BN * ldb;
@@ -508,6 +546,14 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     if (alpha_ptr) alpha *= *alpha_ptr;
   }
   store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+  if constexpr (S & 65536) {
+    // diagnostic: blocks 0..3 copy their stamps to alpha_ptr (a u64 buffer)
+    __syncthreads();
+    if (blockIdx.x < 4) {
+      unsigned long* out = (unsigned long*)alpha_ptr + blockIdx.x * STAMP_N;
+      for (int i = threadIdx.x; i < STAMP_N; i += blockDim.x) out[i] = c.st[i];
+    }
+  }
 }
 
 // Persistent variant (S bit 15, balanced schedule, aligned shapes): one block
