@@ -16,7 +16,7 @@ import torch
 from . import _lib
 
 EPI = {None: 0, "none": 0, "bias": 1, "gelu": 2, "relu": 3, "silu": 4}
-VARIANTS = {"auto": 0, "fast": 1, "pingpong": 1, "generic": 2, "w4": 3, "bounded": 16, "persistent": 20,
+VARIANTS = {"auto": 0, "fast": 1, "pingpong": 1, "generic": 2, "w4": 3, "bounded": 16, "persistent": 20, "vgpr_stage": 21, "vgpr_stage2": 22,
             # tuning experiments (no epilogue), see native/kernels/gemm_bf16.hip launch():
             "pp_prio": 4, "pp_gm8": 5, "pp_v0": 6, "pp_gm2": 7, "pp_gm16": 8, "probe_2xmfma": 9,
             "p32": 10, "probe_l2": 11, "lockstep": 12, "lockstep_1bar": 13, "pl": 14,

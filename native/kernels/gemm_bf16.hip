@@ -236,13 +236,16 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if ((variant >= 3 && variant <= 15) || variant == 20) { if (!fast) return KGS_ERR_ALIGN; v = variant; }
+  else if ((variant >= 3 && variant <= 15) || variant == 20 || variant == 21 || variant == 22) {
+    if (!fast) return KGS_ERR_ALIGN;
+    v = variant;
+  }
   else return KGS_ERR_ARG;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
   auto bb = (const unsigned short*)bias;
-  if (v >= 3 && v <= 14) return (int)kgs_gemm_bf16_nt_experiment(v, epi, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
+  if ((v >= 3 && v <= 14) || v == 21 || v == 22) return (int)kgs_gemm_bf16_nt_experiment(v, epi, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
   hipError_t e;
   switch (epi) {
     case kgs::EPI_NONE: e = kgs::launch<kgs::EPI_NONE>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;

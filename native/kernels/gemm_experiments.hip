@@ -657,7 +657,15 @@ static hipError_t launch_experiment(int variant, const unsigned short* A, const 
     }
     return hipErrorInvalidValue;
   }
-  if (variant == 14) {
+  if (variant == 21) {
+    // VGPR staging (global_load + ds_write) instead of LDS-DMA, 4 phases in flight
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 131072>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                       ldb, ldc, 1.0f, nullptr);
+  } else if (variant == 22) {
+    // VGPR staging, 2 phases in flight
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 131072 + 262144>), grid256, dim3(512), 0, s, A, B, C, bias, M, N,
+                       K, lda, ldb, ldc, 1.0f, nullptr);
+  } else if (variant == 14) {
     hipLaunchKernelGGL(gpl::gemm_nt_256pl<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
   } else if (variant == 10) {
     hipLaunchKernelGGL(g32::gemm_nt_256p32<EPI>, grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);

@@ -31,6 +31,7 @@ struct Regs {
   bf16x8 a[4][2];        // A fragments of the current m-half: [m-tile][k-sub]
   bf16x8 b[2][2][2];     // B fragments of both n-halves: [n-half][n-tile][k-sub]
   f32x4 acc[2][4][2][2]; // [m-half][m-tile][n-half][n-tile]
+  uint4 stg[4][2];       // S bit 17: VGPR staging ring (4 phases x 2 pieces)
 };
 
 struct Ctx {
@@ -61,7 +62,37 @@ struct Ctx {
   int has_next;
   // timing diagnostics (S bit 16): s_memtime stamps in LDS, copied out at the end
   KGS_LDS unsigned long* st;
+  int lane16;  // lane * 16 (VGPR-staged LDS writes)
 };
+
+// S bit 17: stage operands through VGPRs (global_load_dwordx4 + ds_write_b128)
+// instead of LDS-DMA -- same source addresses (swizzle on the source) and the
+// same lane-linear LDS image. A half-tile is loaded 7 phases ahead of its read,
+// written to LDS 4 phases after its load and read 2 phases after the write
+// (the stagger's extra barrier); 8 loads in flight per wave = 32 VGPRs.
+template <int PART>
+__device__ __forceinline__ void vload(const Ctx& c, int k0, uint4& r0, uint4& r1) {
+  const unsigned short* src;
+  int o0, o1;
+  if constexpr (PART == P_A0 || PART == P_A1) {
+    src = c.Ag + (PART == P_A1 ? c.a_half : 0) + k0;
+    o0 = c.offA0; o1 = c.offA1;
+  } else {
+    src = c.Bg + (PART == P_B1 ? c.b_half : 0) + k0;
+    o0 = c.offB0; o1 = c.offB1;
+  }
+  r0 = *(const uint4*)(src + o0);
+  r1 = *(const uint4*)(src + o1);
+}
+
+template <int PART>
+__device__ __forceinline__ void vstore(const Ctx& c, int buf, const uint4& r0, const uint4& r1) {
+  char* dst = c.smem + buf * BUF_BYTES + PART * HALF_BYTES + c.w * 2048 + c.lane16;
+  *(uint4*)dst = r0;
+  *(uint4*)(dst + 1024) = r1;
+}
+
+constexpr int stream_part(int jp) { return jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1; }
 
 // S bit 16 (diagnostic build, gemm_experiments.hip): per wave, 5 s_memtime
 // stamps per phase for iterations STAMP_IT0 .. +STAMP_ITS-1, kept in LDS (not
@@ -290,7 +321,19 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   constexpr int part = (S & 1) == 0 ? (jp == 0 ? P_A0 : jp == 1 ? P_B0 : jp == 2 ? P_B1 : P_A1)
                                     : (jp == 0 ? P_B0 : jp == 1 ? P_A0 : jp == 2 ? P_B1 : P_A1);
   int t = 2 * it + toff;
-  if constexpr (S & 32768) {
+  if constexpr (S & 131072) {
+    static_assert((S & 1) && !(S & (512 | 2048 | 4096 | 32768)), "VGPR staging: balanced NT schedule only");
+    // write half-tile QP+7-D (loaded D phases ago) from its ring slot, then load
+    // half-tile QP+7 into the same slot (S bit 18: D = 2, else D = 4)
+    constexpr int D = (S & 262144) ? 2 : 4;
+    constexpr int hw = QP + 7 - D, slot = hw & (D - 1);
+    vstore<stream_part(hw & 3)>(c, (hw >> 2) & 1, R.stg[slot][0], R.stg[slot][1]);
+    t = t < c.nt ? t : c.nt - 1;
+    vload<part>(c, t * BK, R.stg[slot][0], R.stg[slot][1]);
+    stamp<S>(ts, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's LDS writes (and reads) done
+    bar();
+  } else if constexpr (S & 32768) {
     // persistent: past the end the stream continues into the next tile's first
     // K-tiles (same slots, same parity: nt is even), so the pipeline never drains
     if (t >= c.nt && c.has_next) {
@@ -303,12 +346,14 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
     t = t < c.nt ? t : c.nt - 1;  // past the end: harmless re-load of the last tile
     issue_s<part, S>(c, toff & 1, t * BK);
   }
-  if constexpr ((S & 1) == 0)
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  stamp<S>(ts, 1);
-  bar();
+  if constexpr (!(S & 131072)) {
+    if constexpr ((S & 1) == 0)
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    stamp<S>(ts, 1);
+    bar();
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   stamp<S>(ts, 2);
@@ -433,6 +478,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   Ctx c;
   c.smem = smem;
   c.st = (KGS_LDS unsigned long*)stamps_lds;
+  c.lane16 = lane * 16;
   // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
   c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;
   c.Bg = (S & 4096) ? B + (long)tn * BN : B + (long)((S & 32) ? 0 : tn) * BN * ldb;
@@ -511,6 +557,39 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
     issue_s<P_A0, S>(c, 1, k1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0,B0 of tile 0 landed
     bar();
+  } else if constexpr ((S & 131072) && !(S & 262144)) {
+    // VGPR staging prologue (D = 4): half-tiles 0..2 straight to LDS, 3..6
+    // into ring slots h & 3 (written by phases 0..3)
+    vload<P_B0>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vload<P_A0>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vload<P_B1>(c, 0, R.stg[2][0], R.stg[2][1]);
+    vstore<P_B0>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vstore<P_A0>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vstore<P_B1>(c, 0, R.stg[2][0], R.stg[2][1]);
+    vload<P_A1>(c, 0, R.stg[3][0], R.stg[3][1]);
+    vload<P_B0>(c, k1, R.stg[0][0], R.stg[0][1]);
+    vload<P_A0>(c, k1, R.stg[1][0], R.stg[1][1]);
+    vload<P_B1>(c, k1, R.stg[2][0], R.stg[2][1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    rd_b<0, S>(c, R, smem + P_B0 * HALF_BYTES);
+  } else if constexpr (S & 131072) {
+    // D = 2: half-tiles 0..4 straight to LDS, 5 and 6 into ring slots 1 and 0
+    vload<P_B0>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vload<P_A0>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vstore<P_B0>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vstore<P_A0>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vload<P_B1>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vload<P_A1>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vstore<P_B1>(c, 0, R.stg[0][0], R.stg[0][1]);
+    vstore<P_A1>(c, 0, R.stg[1][0], R.stg[1][1]);
+    vload<P_B0>(c, k1, R.stg[0][0], R.stg[0][1]);
+    vstore<P_B0>(c, 1, R.stg[0][0], R.stg[0][1]);
+    vload<P_A0>(c, k1, R.stg[1][0], R.stg[1][1]);
+    vload<P_B1>(c, k1, R.stg[0][0], R.stg[0][1]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    rd_b<0, S>(c, R, smem + P_B0 * HALF_BYTES);
   } else {
     // prologue: half-tiles 0..6 = B0 A0 B1 A1 of tile 0, B0 A0 B1 of tile 1
     issue_s<P_B0, S>(c, 0, 0);
