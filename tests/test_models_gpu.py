@@ -20,3 +20,19 @@ def test_mlp_training_kgs_tracks_torch():
     for a, b in zip(k["losses"], t["losses"]):
         assert abs(a - b) <= 0.05 * max(abs(b), 1e-3)
     assert k["tflops_per_rank"] > 0
+
+
+def test_llama_block_kgs_matches_torch_and_fp8_close():
+    """Llama-3-architecture prefill (tiny config): kgs GEMMs vs torch.matmul on
+    the same random weights, and the W8A8 fp8 path within fp8 tolerance."""
+    from kgs.models.llama import LlamaConfig, LlamaModel
+
+    cfg = LlamaConfig(hidden=512, intermediate=1024, heads=8, kv_heads=2, layers=2, vocab=1024)
+    tokens = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
+    ref = LlamaModel(cfg, backend="torch").forward(tokens).float()
+    got = LlamaModel(cfg, backend="kgs").forward(tokens).float()
+    rel = ((got - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel
+    f8 = LlamaModel(cfg, backend="fp8").forward(tokens).float()
+    rel8 = ((f8 - ref).norm() / ref.norm()).item()
+    assert rel8 < 0.15, rel8
