@@ -4,6 +4,9 @@
   (``native/kernels/gemm_bf16.hip``)
 * :func:`vector_add`, :func:`transpose_bf16`, :func:`checksum` -- memory-bound
   helpers (``native/kernels/elementwise.hip``)
+* :func:`add_rmsnorm`, :func:`rope_qkv_`, :func:`silu_mul`, :func:`attention_qkv` --
+  fused decoder-block ops and flash attention (``native/kernels/transformer.hip``,
+  ``native/kernels/attention.hip``)
 
 Importing this package does not touch the GPU; the native library is loaded on
 first use and raises :class:`NativeUnavailable` if it is missing.
@@ -17,6 +20,10 @@ def __getattr__(name):  # lazy: keep `import kgs.ops` free of torch for CPU-only
         from . import gemm
 
         return getattr(gemm, name)
+    if name in ("add_rmsnorm", "rms_norm", "rope_qkv_", "rope_tables", "silu_mul", "attention_qkv"):
+        from . import transformer
+
+        return getattr(transformer, name)
     if name in ("vector_add", "transpose_bf16", "checksum"):
         from . import elementwise
 

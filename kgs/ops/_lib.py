@@ -53,6 +53,12 @@ _SIGS = {
     "kgs_vector_add_f32_v": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p], _c_int),
     "kgs_vector_add_bf16_v": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_int, _c_void_p], _c_int),
     "kgs_checksum_bf16": ([_c_void_p, _c_long, _c_void_p, _c_void_p], _c_int),
+    # fused decoder-block ops (native/kernels/transformer.hip, attention.hip)
+    "kgs_add_rmsnorm_bf16": ([_c_void_p] * 5 + [_c_int, _c_int, _c_long, _c_long, ctypes.c_float, _c_void_p], _c_int),
+    "kgs_rope_qkv_bf16": ([_c_void_p] * 4 + [_c_long, _c_int, _c_int, _c_long, _c_int, _c_void_p], _c_int),
+    "kgs_silu_mul_bf16": ([_c_void_p, _c_void_p, _c_long, _c_int, _c_long, _c_long, _c_void_p], _c_int),
+    "kgs_attn_fwd_bf16": ([_c_void_p] * 4 + [_c_int] * 5 + [_c_long] * 4 + [ctypes.c_float, _c_int, _c_void_p],
+                          _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)
     "kgs_ar_signal_bytes": ([], _c_int),
     "kgs_ar_max_blocks": ([], _c_int),
