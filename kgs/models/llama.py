@@ -7,12 +7,14 @@ architecture's prefill on the kgs kernels, with no network and no checkpoint.
 * projections: fused QKV [q + 2 kv heads], O, fused gate|up, down, lm-head on
   :func:`kgs.ops.gemm_nt` (bf16) or :class:`kgs.ops.Fp8Linear` (W8A8 e4m3,
   dynamic per-tensor activation scales, no host sync);
-* attention: ``torch.nn.functional.scaled_dot_product_attention`` (causal, GQA)
-  -- the GEMMs are the kgs part, attention is PyTorch-ROCm's;
-* RMSNorm, RoPE and SwiGLU's ``silu(g) * u`` in PyTorch.
+* attention: :func:`kgs.ops.attention_qkv` -- the hand-written flash-attention
+  forward (causal, GQA) reading q/k/v in place from the QKV output;
+* residual add + RMSNorm, rotate-half RoPE and SwiGLU's ``silu(g) * u`` as one
+  fused kernel each (``native/kernels/transformer.hip``).
 
-``backend="torch"`` runs the same weights through ``torch.matmul`` (hipBLASLt),
-so the two backends can be compared numerically and for speed.
+``backend="torch"`` runs the same weights and the same math through PyTorch-ROCm
+(``torch.matmul`` = hipBLASLt, ``scaled_dot_product_attention``, elementwise
+ops), so the backends can be compared numerically and for speed.
 """
 from __future__ import annotations
 
@@ -52,18 +54,12 @@ def _rms_norm(x, w, eps):
     return (xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()).to(x.dtype)
 
 
-def _rope(q, k, theta):
-    # q, k: [B, H, S, D]
-    d = q.shape[-1]
-    s = q.shape[-2]
-    inv = 1.0 / (theta ** (torch.arange(0, d, 2, device=q.device, dtype=torch.float32) / d))
-    ang = torch.arange(s, device=q.device, dtype=torch.float32)[:, None] * inv[None, :]
-    cos, sin = ang.cos(), ang.sin()
-
+def _rope_torch(q, k, cos, sin):
+    # q, k: [B, H, S, D]; rotate-half (neox) pairs (i, i + D/2)
     def rot(x):
-        x1, x2 = x.float()[..., 0::2], x.float()[..., 1::2]
-        out = torch.stack((x1 * cos - x2 * sin, x1 * sin + x2 * cos), dim=-1).flatten(-2)
-        return out.to(x.dtype)
+        xf = x.float()
+        x1, x2 = xf[..., : xf.shape[-1] // 2], xf[..., xf.shape[-1] // 2:]
+        return torch.cat((x1 * cos - x2 * sin, x2 * cos + x1 * sin), dim=-1).to(x.dtype)
 
     return rot(q), rot(k)
 
@@ -119,9 +115,43 @@ class LlamaModel:
 
     @torch.no_grad()
     def forward(self, tokens: torch.Tensor) -> torch.Tensor:
+        if self.backend == "torch":
+            return self._forward_torch(tokens)
+        from kgs.ops.transformer import add_rmsnorm, attention_qkv, rope_qkv_, rope_tables, silu_mul
+
         cfg = self.cfg
         b, s = tokens.shape
         h, hd, nh, nkv = cfg.hidden, cfg.head_dim, cfg.heads, cfg.kv_heads
+        cos, sin = self._tables(s, lambda: rope_tables(s, hd, cfg.rope_theta, tokens.device))
+        x = self.embed[tokens].reshape(b * s, h)
+        y = add_rmsnorm(x, None, self.layers[0]["ln1"], cfg.eps)
+        for i, L in enumerate(self.layers):
+            qkv = L["qkv"](y)
+            rope_qkv_(qkv, cos, sin, nh + nkv, hd, s)
+            a = attention_qkv(qkv, b, s, nh, nkv, head_dim=hd, causal=True)
+            y = add_rmsnorm(x, L["o"](a), L["ln2"], cfg.eps)  # x += o-proj
+            act = silu_mul(L["gate_up"](y))
+            nxt = self.layers[i + 1]["ln1"] if i + 1 < len(self.layers) else self.norm
+            y = add_rmsnorm(x, L["down"](act), nxt, cfg.eps)  # x += down-proj
+        return self.lm_head(y).reshape(b, s, cfg.vocab)
+
+    def _tables(self, s, make):
+        if getattr(self, "_rope_key", None) != s:
+            self._rope_key, self._rope = s, make()
+        return self._rope
+
+    def _forward_torch(self, tokens: torch.Tensor) -> torch.Tensor:
+        cfg = self.cfg
+        b, s = tokens.shape
+        h, hd, nh, nkv = cfg.hidden, cfg.head_dim, cfg.heads, cfg.kv_heads
+        dev = tokens.device
+
+        def make():
+            inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, hd, 2, device=dev, dtype=torch.float32) / hd))
+            ang = torch.arange(s, device=dev, dtype=torch.float32)[:, None] * inv[None, :]
+            return ang.cos(), ang.sin()
+
+        cos, sin = self._tables(s, make)
         x = self.embed[tokens].reshape(b * s, h)
         for L in self.layers:
             y = _rms_norm(x, L["ln1"], cfg.eps)
@@ -129,7 +159,7 @@ class LlamaModel:
             q = qkv[:, :h].reshape(b, s, nh, hd).transpose(1, 2)
             k = qkv[:, h:h + nkv * hd].reshape(b, s, nkv, hd).transpose(1, 2)
             v = qkv[:, h + nkv * hd:].reshape(b, s, nkv, hd).transpose(1, 2)
-            q, k = _rope(q, k, cfg.rope_theta)
+            q, k = _rope_torch(q, k, cos, sin)
             a = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True, enable_gqa=True)
             x = x + L["o"](a.transpose(1, 2).reshape(b * s, h).contiguous())
             y = _rms_norm(x, L["ln2"], cfg.eps)

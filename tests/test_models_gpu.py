@@ -27,7 +27,7 @@ def test_llama_block_kgs_matches_torch_and_fp8_close():
     the same random weights, and the W8A8 fp8 path within fp8 tolerance."""
     from kgs.models.llama import LlamaConfig, LlamaModel
 
-    cfg = LlamaConfig(hidden=512, intermediate=1024, heads=8, kv_heads=2, layers=2, vocab=1024)
+    cfg = LlamaConfig(hidden=1024, intermediate=2048, heads=8, kv_heads=2, layers=2, vocab=1024)
     tokens = torch.randint(0, cfg.vocab, (2, 128), device="cuda")
     ref = LlamaModel(cfg, backend="torch").forward(tokens).float()
     got = LlamaModel(cfg, backend="kgs").forward(tokens).float()
