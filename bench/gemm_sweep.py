@@ -17,6 +17,9 @@ import torch  # noqa: E402
 from kgs.ops import gemm_nt  # noqa: E402
 
 
+_rand = None
+
+
 def time_fn(fn, iters):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -36,15 +39,20 @@ def main():
     ap.add_argument("--variants", default="auto", help="comma list of kgs variants: auto,fast,w4,generic")
     ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
                     help="fp8: kgs gemm_fp8_nt (e4m3, scaled MFMA) vs torch._scaled_mm (hipBLASLt fp8)")
+    ap.add_argument("--data", choices=("uniform", "normal"), default="uniform",
+                    help="operand distribution: U[-1,1) or N(0,1) (activation/weight-like)")
     a = ap.parse_args()
+    global _rand
+    _rand = (lambda *sh: torch.rand(*sh, device="cuda") * 2 - 1) if a.data == "uniform" else \
+        (lambda *sh: torch.randn(*sh, device="cuda"))
     if a.dtype == "fp8":
         return sweep_fp8(a)
     res = []
     for s in a.shapes.split(","):
         dims = [int(x) for x in s.split("x")]
         M, N, K = (dims * 3)[:3] if len(dims) == 1 else dims
-        A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
-        B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
+        A = _rand(M, K).bfloat16()
+        B = _rand(N, K).bfloat16()
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         C2 = torch.empty_like(C)
         fns = {f"kgs_{v}": (lambda v=v: gemm_nt(A, B, out=C, variant=v)) for v in a.variants.split(",")}
@@ -81,8 +89,8 @@ def sweep_fp8(a):
     for s in a.shapes.split(","):
         dims = [int(x) for x in s.split("x")]
         M, N, K = (dims * 3)[:3] if len(dims) == 1 else dims
-        qa, sa = quantize_fp8(torch.rand(M, K, device="cuda") * 2 - 1)
-        qb, sb = quantize_fp8(torch.rand(N, K, device="cuda") * 2 - 1)
+        qa, sa = quantize_fp8(_rand(M, K))
+        qb, sb = quantize_fp8(_rand(N, K))
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         C2 = torch.empty_like(C)
         ta = torch.tensor(sa, device="cuda")

@@ -356,8 +356,10 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
-  stamp<S>(ts, 2);
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (S & 65536) {  // stamp fences only in the diagnostic build: they
+    stamp<S>(ts, 2);          // change the schedule (fp8 spilled 6 VGPRs with them)
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(1);
   if constexpr (S & 16) {  // timing experiment only: twice the MFMAs per phase (wrong results)
     if constexpr (q == 0) mma_quadrant<0, 0, (S & 1024) != 0>(R);
@@ -374,8 +376,10 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
     if constexpr ((S & 1) == 0) mma_quadrant<1, 0, (S & 1024) != 0>(R); else mma_quadrant<1, 1, (S & 1024) != 0>(R);
   }
   if constexpr (!(S & 2)) __builtin_amdgcn_s_setprio(0);
-  __builtin_amdgcn_sched_barrier(0);
-  stamp<S>(ts, 3);
+  if constexpr (S & 65536) {
+    __builtin_amdgcn_sched_barrier(0);
+    stamp<S>(ts, 3);
+  }
   // S bit 7 (with bit 6, lockstep): one barrier per phase. Still race-free: the
   // slot a phase's DMA overwrites was last read >= 2 phases earlier, i.e. before
   // the previous phase's barrier on every wave.
@@ -459,7 +463,6 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
                                                    int M, int N, int K, int lda, int ldb, int ldc,
                                                    float alpha, const float* __restrict__ alpha_ptr) {
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
-  __shared__ unsigned long stamps_lds[(S & 65536) ? STAMP_N : 1];
 
   constexpr bool BND = (S & 512) != 0;
   const int lane = threadIdx.x & 63;
@@ -477,7 +480,12 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
 
   Ctx c;
   c.smem = smem;
-  c.st = (KGS_LDS unsigned long*)stamps_lds;
+  if constexpr (S & 65536) {
+    // diagnostic builds only: a second LDS array shifts smem and costs the
+    // production kernels VGPRs (measured: fp8 spilled 6 with it declared)
+    __shared__ unsigned long stamps_lds[STAMP_N];
+    c.st = (KGS_LDS unsigned long*)stamps_lds;
+  }
   c.lane16 = lane * 16;
   // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
   c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;

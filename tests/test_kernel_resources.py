@@ -1,0 +1,52 @@
+"""Compile-time resource guard for the production kernels (CPU: hipcc
+cross-compiles gfx950 here). A VGPR spill in a hot kernel is a silent
+performance regression -- the fp8 GEMM once lost 25 % to six spilled VGPRs
+introduced by an unrelated scheduling fence -- so spills fail the suite."""
+import re
+import shutil
+import subprocess
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+HIPCC = "/opt/rocm/bin/hipcc"
+
+pytestmark = pytest.mark.skipif(not Path(HIPCC).exists() and shutil.which("hipcc") is None,
+                                reason="hipcc not available")
+
+
+def _resources(src: str, tmp_path) -> dict:
+    cmd = [HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c",
+           str(ROOT / "native" / "kernels" / src), "-o", str(tmp_path / (src + ".o")),
+           "-Rpass-analysis=kernel-resource-usage"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res, name = {}, None
+    for line in out.stderr.splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            name = m.group(1)
+            res[name] = {}
+            continue
+        m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[bytes/\w+\])?: (\d+)", line)
+        if m and name:
+            res[name][m.group(1).strip()] = int(m.group(2))
+    return res
+
+
+def test_gemm_production_kernels_do_not_spill(tmp_path):
+    res = _resources("gemm_bf16.hip", tmp_path)
+    prod = [n for n in res if re.search(r"gemm_nt_256ILi[0-4]ELi(7|519|263)E", n)]
+    prod += [n for n in res if re.search(r"gemm_nt_256ILi[0-2]ELi(1031|1543)E", n)]
+    assert len(prod) >= 15, list(res)[:20]
+    bad = {n: r.get("VGPRs Spill") for n, r in res.items() if n in prod and r.get("VGPRs Spill", 0)}
+    assert not bad, bad
+
+
+def test_attention_fits_two_workgroups_per_cu(tmp_path):
+    res = _resources("attention.hip", tmp_path)
+    (name, r), = [(n, r) for n, r in res.items() if "attn3fwd" in n]
+    assert r.get("VGPRs Spill", 0) == 0
+    assert r["VGPRs"] + r.get("AGPRs", 0) <= 256  # 2 waves / SIMD
+    assert r["LDS Size"] <= 80 * 1024            # 2 workgroups / CU (160 KiB)
