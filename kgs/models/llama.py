@@ -5,8 +5,9 @@ itself ships in its own image (docs/vllm.md); this model shows the same
 architecture's prefill on the kgs kernels, with no network and no checkpoint.
 
 * projections: fused QKV [q + 2 kv heads], O, fused gate|up, down, lm-head on
-  :func:`kgs.ops.gemm_nt` (bf16) or :class:`kgs.ops.Fp8Linear` (W8A8 e4m3,
-  dynamic per-tensor activation scales, no host sync);
+  :func:`kgs.ops.gemm_nt` (bf16) or :class:`kgs.ops.Fp8Linear` (W8A8 e4m3:
+  per-tensor weight scales, per-token dynamic activation scales produced by
+  the fused norm / SwiGLU / row-quantise kernels, no host sync);
 * attention: :func:`kgs.ops.attention_qkv` -- the hand-written flash-attention
   forward (causal, GQA) reading q/k/v in place from the QKV output;
 * residual add + RMSNorm, rotate-half RoPE and SwiGLU's ``silu(g) * u`` as one
@@ -124,6 +125,8 @@ class LlamaModel:
         h, hd, nh, nkv = cfg.hidden, cfg.head_dim, cfg.heads, cfg.kv_heads
         cos, sin = self._tables(s, lambda: rope_tables(s, hd, cfg.rope_theta, tokens.device))
         x = self.embed[tokens].reshape(b * s, h)
+        if self.backend == "fp8":
+            return self._forward_fp8(x, b, s, cos, sin)
         y = add_rmsnorm(x, None, self.layers[0]["ln1"], cfg.eps)
         for i, L in enumerate(self.layers):
             qkv = L["qkv"](y)
@@ -134,6 +137,26 @@ class LlamaModel:
             nxt = self.layers[i + 1]["ln1"] if i + 1 < len(self.layers) else self.norm
             y = add_rmsnorm(x, L["down"](act), nxt, cfg.eps)  # x += down-proj
         return self.lm_head(y).reshape(b, s, cfg.vocab)
+
+    def _forward_fp8(self, x, b, s, cos, sin):
+        """W8A8: every producer (norm, SwiGLU, attention-output quantiser) emits
+        e4m3 rows with per-token scales; the GEMMs dequantise per row in their
+        epilogue (kgs_gemm_fp8_nt_rows). Attention and the residual stay bf16."""
+        from kgs.ops.transformer import (add_rmsnorm_fp8, attention_qkv, quantize_rows_fp8, rope_qkv_,
+                                         silu_mul_fp8)
+
+        cfg = self.cfg
+        hd, nh, nkv = cfg.head_dim, cfg.heads, cfg.kv_heads
+        y8, ys = add_rmsnorm_fp8(x, None, self.layers[0]["ln1"], cfg.eps)
+        for i, L in enumerate(self.layers):
+            qkv = L["qkv"].f8.forward_q(y8, ys)
+            rope_qkv_(qkv, cos, sin, nh + nkv, hd, s)
+            a8, as_ = quantize_rows_fp8(attention_qkv(qkv, b, s, nh, nkv, head_dim=hd, causal=True))
+            y8, ys = add_rmsnorm_fp8(x, L["o"].f8.forward_q(a8, as_), L["ln2"], cfg.eps)
+            m8, ms = silu_mul_fp8(L["gate_up"].f8.forward_q(y8, ys))
+            nxt = self.layers[i + 1]["ln1"] if i + 1 < len(self.layers) else self.norm
+            y8, ys = add_rmsnorm_fp8(x, L["down"].f8.forward_q(m8, ms), nxt, cfg.eps)
+        return self.lm_head.f8.forward_q(y8, ys).reshape(b, s, cfg.vocab)
 
     def _tables(self, s, make):
         if getattr(self, "_rope_key", None) != s:

@@ -16,11 +16,12 @@ from ._lib import KernelError, NativeUnavailable, available  # noqa: F401
 
 def __getattr__(name):  # lazy: keep `import kgs.ops` free of torch for CPU-only tools
     if name in ("gemm_nt", "matmul", "linear", "Linear", "fast_path_ok", "transpose", "EPI", "gemm_fp8_nt",
-                "quantize_fp8", "gemm_bf16", "quantize_fp8_dev", "Fp8Linear"):
+                "quantize_fp8", "gemm_bf16", "quantize_fp8_dev", "Fp8Linear", "gemm_fp8_rows"):
         from . import gemm
 
         return getattr(gemm, name)
-    if name in ("add_rmsnorm", "rms_norm", "rope_qkv_", "rope_tables", "silu_mul", "attention_qkv"):
+    if name in ("add_rmsnorm", "rms_norm", "rope_qkv_", "rope_tables", "silu_mul", "attention_qkv",
+                "add_rmsnorm_fp8", "silu_mul_fp8", "quantize_rows_fp8"):
         from . import transformer
 
         return getattr(transformer, name)

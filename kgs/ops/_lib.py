@@ -57,6 +57,11 @@ _SIGS = {
     "kgs_add_rmsnorm_bf16": ([_c_void_p] * 5 + [_c_int, _c_int, _c_long, _c_long, ctypes.c_float, _c_void_p], _c_int),
     "kgs_rope_qkv_bf16": ([_c_void_p] * 4 + [_c_long, _c_int, _c_int, _c_long, _c_int, _c_void_p], _c_int),
     "kgs_silu_mul_bf16": ([_c_void_p, _c_void_p, _c_long, _c_int, _c_long, _c_long, _c_void_p], _c_int),
+    "kgs_add_rmsnorm_fp8": ([_c_void_p] * 6 + [_c_int, _c_int, _c_long, _c_long, ctypes.c_float, _c_void_p], _c_int),
+    "kgs_quant_rows_fp8": ([_c_void_p] * 3 + [_c_int, _c_int, _c_long, _c_long, _c_void_p], _c_int),
+    "kgs_silu_mul_fp8": ([_c_void_p] * 3 + [_c_long, _c_int, _c_long, _c_long, _c_void_p], _c_int),
+    "kgs_gemm_fp8_nt_rows": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 +
+                             [ctypes.c_float, _c_void_p, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_attn_fwd_bf16": ([_c_void_p] * 4 + [_c_int] * 5 + [_c_long] * 4 + [ctypes.c_float, _c_int, _c_void_p],
                           _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)

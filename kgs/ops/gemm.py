@@ -175,6 +175,44 @@ def gemm_fp8_nt(
     return out
 
 
+def gemm_fp8_rows(
+    a: torch.Tensor,
+    a_scales: torch.Tensor,
+    b: torch.Tensor,
+    scale_b: float = 1.0,
+    bias: torch.Tensor | None = None,
+    out: torch.Tensor | None = None,
+    variant: str = "auto",
+) -> torch.Tensor:
+    """``a_scales[m] * scale_b * (a @ b.T) (+ bias)`` in bf16 from e4m3 operands with
+    per-row (per-token) activation scales -- the output of the fused quantising
+    producers in :mod:`kgs.ops.transformer` (``add_rmsnorm_fp8``, ``silu_mul_fp8``,
+    ``quantize_rows_fp8``)."""
+    for t, name in ((a, "a"), (b, "b")):
+        if t.dtype != FP8_DTYPE:
+            raise TypeError(f"{name} must be {FP8_DTYPE}, got {t.dtype}")
+        if not t.is_cuda or t.dim() != 2 or t.stride(1) != 1:
+            raise ValueError(f"{name} must be a 2-D row-major GPU matrix")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if a_scales.dtype != torch.float32 or a_scales.numel() != M or not a_scales.is_contiguous():
+        raise ValueError("a_scales must be a contiguous f32 vector of length M")
+    if bias is not None and (bias.dtype != torch.bfloat16 or bias.numel() != N or not bias.is_contiguous()):
+        raise ValueError("bias must be a contiguous bf16 vector of length N")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    else:
+        _check_operand(out, "out")
+    rc = _lib.lib().kgs_gemm_fp8_nt_rows(
+        a.data_ptr(), b.data_ptr(), out.data_ptr(), bias.data_ptr() if bias is not None else None,
+        M, N, K, a.stride(0), b.stride(0), out.stride(0), float(scale_b), a_scales.data_ptr(),
+        EPI["bias"] if bias is not None else 0, FP8_VARIANTS[variant], _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_fp8_rows[{M}x{N}x{K}]")
+    return out
+
+
 def fast_path_ok(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None) -> bool:
     M, K = a.shape
     N = b.shape[0]
@@ -341,6 +379,13 @@ class Fp8Linear(torch.nn.Module):
     @classmethod
     def from_linear(cls, lin: torch.nn.Module) -> "Fp8Linear":
         return cls(lin.weight, getattr(lin, "bias", None), getattr(lin, "act", None))
+
+    def forward_q(self, x8: torch.Tensor, x_scales: torch.Tensor) -> torch.Tensor:
+        """Pre-quantised activation (e4m3 rows + per-row f32 scales, e.g. from
+        ``kgs.ops.add_rmsnorm_fp8``); bias only (no activation epilogue)."""
+        if self.act is not None:
+            raise ValueError("forward_q supports no fused activation")
+        return gemm_fp8_rows(x8, x_scales, self.qweight, self.w_scale, bias=self.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape

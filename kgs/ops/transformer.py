@@ -7,6 +7,9 @@ tests compare them with.
 * :func:`rope_qkv_` -- rotate-half RoPE on the q and k heads of a fused QKV
   projection output, in place
 * :func:`silu_mul` -- SwiGLU ``silu(gate) * up`` from a fused gate|up output
+* :func:`add_rmsnorm_fp8`, :func:`silu_mul_fp8`, :func:`quantize_rows_fp8` -- the
+  same producers emitting e4m3 rows + per-row scales for
+  :func:`kgs.ops.gemm.gemm_fp8_rows` (W8A8, per-token dynamic activation scales)
 * :func:`attention_qkv` -- causal/full GQA flash attention (head_dim 128) reading
   q, k, v straight out of the fused QKV buffer and writing ``[tokens, H*128]``
 
@@ -55,6 +58,56 @@ def add_rmsnorm(x: torch.Tensor, d: torch.Tensor | None, w: torch.Tensor, eps: f
 
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     return add_rmsnorm(x, None, w, eps)
+
+
+def _fp8_out(rows, cols, device):
+    from .gemm import FP8_DTYPE
+
+    return (torch.empty((rows, cols), dtype=FP8_DTYPE, device=device),
+            torch.empty(rows, dtype=torch.float32, device=device))
+
+
+def add_rmsnorm_fp8(x: torch.Tensor, d: torch.Tensor | None, w: torch.Tensor, eps: float = 1e-5):
+    """As :func:`add_rmsnorm`, but the normalised rows come back as e4m3 with a
+    per-row scale: returns ``(y8, scales)``, ``y ~= y8.float() * scales[:, None]``."""
+    _need(x, "x")
+    rows, cols = x.shape
+    if d is not None:
+        _need(d, "d")
+        if d.shape != x.shape or d.stride(0) != x.stride(0):
+            raise ValueError("d must match x in shape and row stride")
+    if w.shape != (cols,) or w.dtype != torch.bfloat16 or not w.is_contiguous():
+        raise ValueError("w must be a contiguous bf16 vector of length cols")
+    y8, ys = _fp8_out(rows, cols, x.device)
+    rc = _lib.lib().kgs_add_rmsnorm_fp8(x.data_ptr(), 0 if d is None else d.data_ptr(),
+                                        0 if d is None else x.data_ptr(), w.data_ptr(), y8.data_ptr(), ys.data_ptr(),
+                                        rows, cols, x.stride(0), y8.stride(0), float(eps),
+                                        _lib.stream_handle(x.device))
+    _lib.check(rc, "add_rmsnorm_fp8")
+    return y8, ys
+
+
+def quantize_rows_fp8(x: torch.Tensor):
+    """bf16 rows -> ``(e4m3 rows, per-row f32 scales)`` in one pass (cols % 512 == 0)."""
+    _need(x, "x")
+    rows, cols = x.shape
+    y8, ys = _fp8_out(rows, cols, x.device)
+    rc = _lib.lib().kgs_quant_rows_fp8(x.data_ptr(), y8.data_ptr(), ys.data_ptr(), rows, cols, x.stride(0),
+                                       y8.stride(0), _lib.stream_handle(x.device))
+    _lib.check(rc, "quantize_rows_fp8")
+    return y8, ys
+
+
+def silu_mul_fp8(gu: torch.Tensor):
+    """SwiGLU into e4m3 rows with per-row scales: ``(a8, scales)``."""
+    _need(gu, "gu")
+    rows, w2 = gu.shape
+    inter = w2 // 2
+    y8, ys = _fp8_out(rows, inter, gu.device)
+    rc = _lib.lib().kgs_silu_mul_fp8(gu.data_ptr(), y8.data_ptr(), ys.data_ptr(), rows, inter, gu.stride(0),
+                                     y8.stride(0), _lib.stream_handle(gu.device))
+    _lib.check(rc, "silu_mul_fp8")
+    return y8, ys
 
 
 def rope_tables(seq: int, head_dim: int, theta: float, device) -> tuple[torch.Tensor, torch.Tensor]:

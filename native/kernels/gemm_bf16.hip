@@ -352,6 +352,50 @@ KGS_EXPORT int kgs_gemm_fp8_nt_dev(const void* A, const void* B, void* C, const 
   return (int)e;
 }
 
+// Per-row activation scales (W8A8 with per-token dynamic activation scales):
+// C = epilogue(alpha * row_scale[m] * A . B^T). EPI_NONE / EPI_BIAS only.
+KGS_EXPORT int kgs_gemm_fp8_nt_rows(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                                    int lda, int ldb, int ldc, float alpha, const float* row_scale, int epi,
+                                    int variant, hipStream_t stream) {
+  using namespace kgs;
+  if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
+  if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (row_scale == nullptr || (uintptr_t)row_scale % 4) return KGS_ERR_ARG;
+  if (epi != EPI_NONE && epi != EPI_BIAS) return KGS_ERR_ARG;
+  if (epi != EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
+  const int fast = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 0);
+  const int bounded = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 1);
+  int v;
+  if (variant == 0) v = fast ? 1 : 16;
+  else if (variant == 1 || variant == 16) v = variant;
+  else return KGS_ERR_ARG;
+  if (!(v == 16 ? bounded : fast)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto bb = (const unsigned short*)bias;
+  const int Kw = K / 2, ldaw = lda / 2, ldbw = ldb / 2;
+  constexpr int RS = 524288 + 1024 + 7;
+  if (v == 1) {
+    const dim3 grid((M / g256::BM) * (N / g256::BN));
+    if (epi == EPI_NONE)
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, RS>), grid, dim3(512), 0, stream, a, b, c, bb, M, N, Kw, ldaw,
+                         ldbw, ldc, alpha, row_scale);
+    else
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI_BIAS, RS>), grid, dim3(512), 0, stream, a, b, c, bb, M, N, Kw, ldaw,
+                         ldbw, ldc, alpha, row_scale);
+  } else {
+    const dim3 grid(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
+    if (epi == EPI_NONE)
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, RS + 512>), grid, dim3(512), 0, stream, a, b, c, bb, M, N, Kw,
+                         ldaw, ldbw, ldc, alpha, row_scale);
+    else
+      hipLaunchKernelGGL((g256::gemm_nt_256<EPI_BIAS, RS + 512>), grid, dim3(512), 0, stream, a, b, c, bb, M, N, Kw,
+                         ldaw, ldbw, ldc, alpha, row_scale);
+  }
+  return (int)hipGetLastError();
+}
+
 KGS_EXPORT int kgs_gemm_fp8_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                int ldb, int ldc, float alpha, int epi, int variant, hipStream_t stream) {
   return kgs_gemm_fp8_nt_dev(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, nullptr, epi, variant, stream);

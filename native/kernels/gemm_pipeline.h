@@ -390,10 +390,14 @@ __device__ __forceinline__ void phase(const Ctx& c, Regs& R, int it) {
 
 // Epilogue: lane holds C[row][col..col+3] for every (mh, i, nh, n); bias and
 // activation fused, bf16 out through the widened (16-B) store tail.
+// S bit 19 (fp8 only): alpha_ptr is a per-row [M] scale vector (per-token
+// dynamic activation scales from the fused quantising producers), multiplied
+// with alpha per output row.
 template <int EPI, int S>
 __device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned short* __restrict__ C,
                                            const unsigned short* __restrict__ bias, int M, int N, int ldc,
-                                           float alpha, int tm, int tn, int lane) {
+                                           float alpha, int tm, int tn, int lane,
+                                           const float* __restrict__ row_scale = nullptr) {
   constexpr bool BND = (S & 512) != 0;
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
@@ -405,6 +409,8 @@ __device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned
       // bounded mode: rows past M are dropped (the permlane swaps below stay
       // wave-uniform, only the stores are predicated)
       const bool row_ok = !BND || row < M;
+      float ralpha = alpha;
+      if constexpr (S & 524288) ralpha = alpha * (row_ok ? row_scale[row] : 0.f);
 #pragma unroll
       for (int nh = 0; nh < 2; ++nh) {
         uint2 o[2];
@@ -412,7 +418,7 @@ __device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned
         for (int n = 0; n < 2; ++n) {
           const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
           f32x4 v = R.acc[mh][i][nh][n];
-          if constexpr (S & 1024) v *= alpha;  // fp8: per-tensor dequant scale sa*sb
+          if constexpr (S & 1024) v *= ralpha;  // fp8: dequant scale sa*sb (sa per row with S bit 19)
           float bv[4] = {0.f, 0.f, 0.f, 0.f};
           if constexpr (EPI != EPI_NONE) {
             if (!BND || col + 4 <= N) {
@@ -629,10 +635,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain tail prefetches
 
   // fp8: the dequant scale, times a device-resident factor (dynamic activation scale)
-  if constexpr (S & 1024) {
+  if constexpr ((S & 1024) && !(S & 524288)) {
     if (alpha_ptr) alpha *= *alpha_ptr;
   }
-  store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane);
+  store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane, alpha_ptr);
   if constexpr (S & 65536) {
     // diagnostic: blocks 0..3 copy their stamps to alpha_ptr (a u64 buffer)
     __syncthreads();

@@ -6,6 +6,9 @@
 //   * rope_qkv    : rotate-half (neox) RoPE on the q and k heads of the fused
 //                   QKV projection output, in place, from an fp32 cos/sin table
 //   * silu_mul    : SwiGLU's silu(g) * u from the fused gate|up output
+//   * *_fp8 forms of add_rmsnorm / silu_mul and quant_rows: e4m3 output with a
+//     per-row (per-token) dynamic scale, so the W8A8 GEMM that consumes the
+//     activation needs no separate amax + quantise passes
 //
 // All math is fp32 with one bf16 rounding per output. The PyTorch version of
 // the same block (kgs/models/llama.py, backend "torch") runs ~10 kernels per op
@@ -22,14 +25,36 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+constexpr float E4M3_MAX = 448.f;
+
+// 8 floats (already divided by the scale) -> 8 e4m3 bytes (OCP e4m3fn, RNE)
+__device__ __forceinline__ uint2 to_e4m3x8(const float* v) {
+  float c[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) c[e] = fminf(fmaxf(v[e], -E4M3_MAX), E4M3_MAX);
+  unsigned lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+  unsigned hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+  return make_uint2(lo, hi);
+}
+
 // One wave per row; lane owns 16-B chunks lane + 64*j (j < NC) -- a wave reads
 // 1 KB contiguous per j. cols == 512 * NC.
-template <int NC>
+// Q8: y is written as e4m3 bytes with a per-row scale ys[row] = amax/448
+// (per-token dynamic quantisation for the fp8 GEMM that consumes y).
+template <int NC, bool Q8 = false>
 __global__ __launch_bounds__(256) void add_rmsnorm(unsigned short* __restrict__ x, const unsigned short* __restrict__ d,
                                                    unsigned short* __restrict__ xo,
                                                    const unsigned short* __restrict__ w,
                                                    unsigned short* __restrict__ y, int rows, long ldx, long ldy,
-                                                   float eps) {
+                                                   float eps, float* __restrict__ ys = nullptr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -67,15 +92,114 @@ __global__ __launch_bounds__(256) void add_rmsnorm(unsigned short* __restrict__ 
   ss = wave_sum(ss);
   const float r = rsqrtf(ss / (float)(NC * 512) + eps);
   const bf16x8* wr = (const bf16x8*)w;
-  bf16x8* yr = (bf16x8*)(y + row * ldy);
+  if constexpr (Q8) {
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const bf16x8 wv = wr[lane + 64 * j];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[j][e] = v[j][e] * r * bf2f((unsigned short)wv[e]);
+        am = fmaxf(am, fabsf(v[j][e]));
+      }
+    }
+    am = wave_max(am);
+    const float sc = fmaxf(am, 1e-12f) / E4M3_MAX, inv = 1.f / sc;
+    uint2* yq = (uint2*)((unsigned char*)y + row * ldy);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[j][e] *= inv;
+      yq[lane + 64 * j] = to_e4m3x8(v[j]);
+    }
+    if (lane == 0) ys[row] = sc;
+  } else {
+    bf16x8* yr = (bf16x8*)(y + row * ldy);
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const bf16x8 wv = wr[lane + 64 * j];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[j][e] * r * bf2f((unsigned short)wv[e]));
+      yr[lane + 64 * j] = o;
+    }
+  }
+}
+
+// bf16 rows -> e4m3 rows + per-row scales; one wave per row, cols == 512 * NC
+template <int NC>
+__global__ __launch_bounds__(256) void quant_rows(const unsigned short* __restrict__ x, unsigned char* __restrict__ y,
+                                                  float* __restrict__ ys, int rows, long ldx, long ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const bf16x8* xr = (const bf16x8*)(x + row * ldx);
+  float v[NC][8];
+  float am = 0.f;
 #pragma unroll
   for (int j = 0; j < NC; ++j) {
-    const bf16x8 wv = wr[lane + 64 * j];
-    bf16x8 o;
+    const bf16x8 h = xr[lane + 64 * j];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (short)f2bf(v[j][e] * r * bf2f((unsigned short)wv[e]));
-    yr[lane + 64 * j] = o;
+    for (int e = 0; e < 8; ++e) {
+      v[j][e] = bf2f((unsigned short)h[e]);
+      am = fmaxf(am, fabsf(v[j][e]));
+    }
   }
+  am = wave_max(am);
+  const float sc = fmaxf(am, 1e-12f) / E4M3_MAX, inv = 1.f / sc;
+  uint2* yq = (uint2*)(y + row * ldy);
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[j][e] *= inv;
+    yq[lane + 64 * j] = to_e4m3x8(v[j]);
+  }
+  if (lane == 0) ys[row] = sc;
+}
+
+// SwiGLU with per-row e4m3 output: one 256-thread block per row, CPT 8-wide
+// chunks per thread held in registers across the block's amax reduction.
+template <int CPT>
+__global__ __launch_bounds__(256) void silu_mul_q8(const unsigned short* __restrict__ gu, unsigned char* __restrict__ out,
+                                                   float* __restrict__ ys, int inter, long ld_in, long ld_out) {
+  __shared__ float red[4];
+  const long r = blockIdx.x;
+  const int tid = threadIdx.x, nch = inter / 8;
+  const bf16x8* gp = (const bf16x8*)(gu + r * ld_in);
+  const bf16x8* up = (const bf16x8*)(gu + r * ld_in + inter);
+  float v[CPT][8];
+  float am = 0.f;
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = tid + 256 * k;
+    if (c < nch) {
+      const bf16x8 g = __builtin_nontemporal_load(gp + c);
+      const bf16x8 u = __builtin_nontemporal_load(up + c);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float gf = bf2f((unsigned short)g[e]);
+        // round through bf16 like the bf16 path, so both paths quantise the same values
+        v[k][e] = bf2f(f2bf(gf / (1.0f + __expf(-gf)) * bf2f((unsigned short)u[e])));
+        am = fmaxf(am, fabsf(v[k][e]));
+      }
+    }
+  }
+  am = wave_max(am);
+  if ((tid & 63) == 0) red[tid >> 6] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const float sc = fmaxf(am, 1e-12f) / E4M3_MAX, inv = 1.f / sc;
+  uint2* oq = (uint2*)(out + r * ld_out);
+#pragma unroll
+  for (int k = 0; k < CPT; ++k) {
+    const int c = tid + 256 * k;
+    if (c < nch) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[k][e] *= inv;
+      oq[c] = to_e4m3x8(v[k]);
+    }
+  }
+  if (tid == 0) ys[r] = sc;
 }
 
 // Thread = one 8-wide chunk of the first half of one (token, head); it also
@@ -186,5 +310,75 @@ KGS_EXPORT int kgs_silu_mul_bf16(const void* gu, void* out, long rows, int inter
   if (n == 0) return 0;
   hipLaunchKernelGGL(kgs::tfm::silu_mul, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
                      (const unsigned short*)gu, (unsigned short*)out, rows, inter, ld_in, ld_out);
+  return (int)hipGetLastError();
+}
+
+// fp8 (e4m3) output with per-row scales ys[rows]: y is [rows, ldy] bytes.
+KGS_EXPORT int kgs_add_rmsnorm_fp8(void* x, const void* d, void* xo, const void* w, void* y, float* ys, int rows,
+                                  int cols, long ldx, long ldy, float eps, hipStream_t s) {
+  if (rows < 0 || cols <= 0) return KGS_ERR_SHAPE;
+  if (cols % 512 || cols > 8192 || ldx < cols || ldy < cols) return KGS_ERR_SHAPE;
+  if (!al16(x) || !al16(w) || !al16(y) || ((uintptr_t)ys & 3) || (d && (!al16(d) || !al16(xo))) || ldx % 8 ||
+      ldy % 16)
+    return KGS_ERR_ALIGN;
+  if (rows == 0) return 0;
+  if (d != nullptr && xo == nullptr) xo = x;
+  using namespace kgs::tfm;
+  const dim3 g((rows + 3) / 4), b(256);
+  auto X = (unsigned short*)x;
+  auto D = (const unsigned short*)d;
+  auto XO = (unsigned short*)xo;
+  auto W = (const unsigned short*)w;
+  auto Y = (unsigned short*)y;
+  switch (cols / 512) {
+#define KGS_NC(n) \
+  case n: hipLaunchKernelGGL((add_rmsnorm<n, true>), g, b, 0, s, X, D, XO, W, Y, rows, ldx, ldy, eps, ys); break;
+    KGS_NC(1) KGS_NC(2) KGS_NC(4) KGS_NC(6) KGS_NC(8) KGS_NC(10) KGS_NC(12) KGS_NC(16)
+#undef KGS_NC
+    default: return KGS_ERR_SHAPE;
+  }
+  return (int)hipGetLastError();
+}
+
+KGS_EXPORT int kgs_quant_rows_fp8(const void* x, void* y, float* ys, int rows, int cols, long ldx, long ldy,
+                                 hipStream_t s) {
+  if (rows < 0 || cols <= 0 || cols % 512 || cols > 8192 || ldx < cols || ldy < cols) return KGS_ERR_SHAPE;
+  if (!al16(x) || !al16(y) || ((uintptr_t)ys & 3) || ldx % 8 || ldy % 16) return KGS_ERR_ALIGN;
+  if (rows == 0) return 0;
+  using namespace kgs::tfm;
+  const dim3 g((rows + 3) / 4), b(256);
+  auto X = (const unsigned short*)x;
+  auto Y = (unsigned char*)y;
+  switch (cols / 512) {
+#define KGS_NC(n) \
+  case n: hipLaunchKernelGGL(quant_rows<n>, g, b, 0, s, X, Y, ys, rows, ldx, ldy); break;
+    KGS_NC(1) KGS_NC(2) KGS_NC(4) KGS_NC(6) KGS_NC(8) KGS_NC(10) KGS_NC(12) KGS_NC(16)
+#undef KGS_NC
+    default: return KGS_ERR_SHAPE;
+  }
+  return (int)hipGetLastError();
+}
+
+// silu(gate) * up -> e4m3 [rows, ld_out] bytes + per-row scales; inter <= 32768.
+KGS_EXPORT int kgs_silu_mul_fp8(const void* gu, void* out, float* ys, long rows, int inter, long ld_in, long ld_out,
+                               hipStream_t s) {
+  if (rows < 0 || inter <= 0 || inter % 8 || inter > 32768 || ld_in < 2L * inter || ld_out < inter)
+    return KGS_ERR_SHAPE;
+  if (!al16(gu) || !al16(out) || ((uintptr_t)ys & 3) || ld_in % 8 || ld_out % 16) return KGS_ERR_ALIGN;
+  if (rows == 0) return 0;
+  if (rows > 0x7fffffff) return KGS_ERR_SHAPE;
+  using namespace kgs::tfm;
+  const int cpt = (inter / 8 + 255) / 256;
+  auto G = (const unsigned short*)gu;
+  auto O = (unsigned char*)out;
+  const dim3 g((unsigned)rows), b(256);
+  switch (cpt) {
+#define KGS_CPT(n) \
+  case n: hipLaunchKernelGGL(silu_mul_q8<n>, g, b, 0, s, G, O, ys, inter, ld_in, ld_out); break;
+    KGS_CPT(1) KGS_CPT(2) KGS_CPT(3) KGS_CPT(4) KGS_CPT(5) KGS_CPT(6) KGS_CPT(7) KGS_CPT(8)
+    KGS_CPT(9) KGS_CPT(10) KGS_CPT(11) KGS_CPT(12) KGS_CPT(13) KGS_CPT(14) KGS_CPT(15) KGS_CPT(16)
+#undef KGS_CPT
+    default: return KGS_ERR_SHAPE;
+  }
   return (int)hipGetLastError();
 }

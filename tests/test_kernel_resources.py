@@ -39,7 +39,8 @@ def test_gemm_production_kernels_do_not_spill(tmp_path):
     res = _resources("gemm_bf16.hip", tmp_path)
     prod = [n for n in res if re.search(r"gemm_nt_256ILi[0-4]ELi(7|519|263)E", n)]
     prod += [n for n in res if re.search(r"gemm_nt_256ILi[0-2]ELi(1031|1543)E", n)]
-    assert len(prod) >= 15, list(res)[:20]
+    prod += [n for n in res if re.search(r"gemm_nt_256ILi[01]ELi(525319|525831)E", n)]
+    assert len(prod) >= 19, list(res)[:20]
     bad = {n: r.get("VGPRs Spill") for n, r in res.items() if n in prod and r.get("VGPRs Spill", 0)}
     assert not bad, bad
 

@@ -154,3 +154,72 @@ def test_attention_rejects_bad_shapes():
     qkv = _bf(100, 3 * 128)
     with pytest.raises(KernelError):
         attention_qkv(qkv, 1, 100, 1, 1)  # seq % 128 != 0
+
+
+def _deq(y8, ys):
+    return y8.float() * ys[:, None]
+
+
+def _close_fp8(deq, ref):
+    # e4m3: 3 mantissa bits -> <= 2^-4 relative per element, plus the subnormal
+    # floor relative to the row amax
+    tol = 0.0625 * ref.abs() + 2e-3 * ref.abs().amax(dim=1, keepdim=True)
+    return bool(((deq - ref).abs() <= tol + 1e-6).all())
+
+
+@pytest.mark.parametrize("with_delta", [False, True])
+def test_add_rmsnorm_fp8(with_delta):
+    from kgs.ops.transformer import add_rmsnorm_fp8, ref_add_rmsnorm
+
+    x = _bf(64, 4096)
+    d = _bf(64, 4096) if with_delta else None
+    w = _bf(4096, scale=0.5) + 1
+    xr, _ = ref_add_rmsnorm(x, d, w)
+    xf = xr.float()
+    yref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    x2 = x.clone()
+    y8, ys = add_rmsnorm_fp8(x2, d, w)
+    torch.cuda.synchronize()
+    assert torch.equal(x2, xr)
+    assert _close_fp8(_deq(y8, ys), yref)
+    # per-row scale = row amax / 448 (the largest element maps to e4m3's max)
+    assert torch.allclose(ys, yref.abs().amax(dim=1) / 448, rtol=1e-5)
+
+
+def test_quantize_rows_fp8():
+    from kgs.ops.transformer import quantize_rows_fp8
+
+    x = _bf(33, 1024, scale=3.0)
+    x[5] = 0  # an all-zero row must not produce NaN
+    y8, ys = quantize_rows_fp8(x)
+    deq = _deq(y8, ys)
+    assert torch.isfinite(deq).all() and deq[5].abs().max().item() == 0
+    assert _close_fp8(deq, x.float())
+
+
+def test_silu_mul_fp8():
+    from kgs.ops.transformer import ref_silu_mul, silu_mul_fp8
+
+    gu = _bf(48, 2 * 14336, scale=2.0)
+    a8, s = silu_mul_fp8(gu)
+    assert _close_fp8(_deq(a8, s), ref_silu_mul(gu).float())
+
+
+@pytest.mark.parametrize("m,n,k", [(512, 768, 1024), (300, 520, 272)])
+def test_gemm_fp8_rows(m, n, k):
+    from kgs.ops.gemm import gemm_fp8_rows, quantize_fp8
+    from kgs.ops.transformer import quantize_rows_fp8
+
+    a = _bf(m, k) if k % 512 == 0 else None
+    if a is not None:
+        a8, sa = quantize_rows_fp8(a)
+    else:  # odd K: build the per-row-scaled operand on the host side
+        af = torch.randn(m, k, device=DEV)
+        sa = af.abs().amax(dim=1) / 448
+        a8 = (af / sa[:, None]).to(torch.float8_e4m3fn)
+    b8, sb = quantize_fp8(torch.randn(n, k, device=DEV))
+    bias = _bf(n)
+    got = gemm_fp8_rows(a8, sa.contiguous(), b8, sb, bias=bias)
+    ref = (a8.float() * sa[:, None]) @ (b8.float() * sb).T + bias.float()
+    rel = ((got.float() - ref).abs().max() / ref.abs().max()).item()
+    assert rel < 1e-2, rel
