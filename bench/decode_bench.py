@@ -1,0 +1,126 @@
+#!/usr/bin/env python3
+"""Decode-kernel microbenchmarks on one MI355X: the skinny GEMM on the Llama-3-8B
+projection shapes (vs torch.matmul = hipBLASLt on the unpacked weight) and the
+paged decode attention (vs KV bytes). Prints one JSON line per measurement.
+
+  python bench/decode_bench.py [--gemm] [--attn] [--iters 50]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+SWEEP = False
+SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
+          "lm_head": (128256, 4096)}
+
+
+def _time(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def bench_gemm(iters, ms, ring_bytes=3 << 30):
+    """Each call reads a different copy of the weight (a ring of copies larger
+    than the 256 MB MALL), as a real decode step streams 32 layers' weights."""
+    from kgs.ops.decode import PackedWeight, choose_ksplit, skinny_gemm
+
+    for name, (n, k) in SHAPES.items():
+        copies = max(2, min(64, ring_bytes // (n * k * 2)))
+        ws = [(torch.randn(n, k, device="cuda") * k ** -0.5).to(torch.bfloat16) for _ in range(copies)]
+        pws = [PackedWeight(w) for w in ws]
+        for m in ms:
+            x = (torch.rand(m, k, device="cuda") * 2 - 1).to(torch.bfloat16)
+            out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            it = {"i": 0}
+
+            def kgs_call():
+                it["i"] = (it["i"] + 1) % copies
+                skinny_gemm(x, pws[it["i"]], out=out)
+
+            def torch_call():
+                it["i"] = (it["i"] + 1) % copies
+                torch.matmul(x, ws[it["i"]].T, out=out)
+
+            t_k = _time(kgs_call, iters)
+            t_t = _time(torch_call, iters)
+            sweep = {}
+            if SWEEP:
+                from kgs.ops.decode import skinny_geometry
+
+                nch = k // skinny_geometry(m)[1]
+                for ks in [d for d in range(1, nch + 1) if nch % d == 0 and d <= 64]:
+                    def ks_call(ks=ks):
+                        it["i"] = (it["i"] + 1) % copies
+                        skinny_gemm(x, pws[it["i"]], out=out, ksplit=ks)
+                    sweep[ks] = round(_time(ks_call, iters), 2)
+            ref = x.float() @ ws[0].float().T
+            err = ((skinny_gemm(x, pws[0]).float() - ref).abs().max() / ref.abs().max()).item()
+            byts = n * k * 2 + m * k * 2 + m * n * 2
+            print(json.dumps({"op": "skinny_gemm", "shape": name, "m": m, "n": n, "k": k, "copies": copies,
+                              "ksplit": choose_ksplit(m, n, k), "us": round(t_k, 2), "tbps": round(byts / t_k / 1e6, 2),
+                              "torch_us": round(t_t, 2), "torch_tbps": round(byts / t_t / 1e6, 2),
+                              "speedup": round(t_t / t_k, 3), "rel_err": round(err, 5), "ksplit_us": sweep}),
+                  flush=True)
+        del ws, pws
+        torch.cuda.empty_cache()
+
+
+def bench_attn(iters):
+    from kgs.ops.decode import PagedKVCache, decode_splits, paged_decode_attention
+
+    heads, hkv = 32, 8
+    for b, ctx in ((1, 4096), (16, 1024), (64, 1024), (64, 4096), (256, 1024), (256, 2048)):
+        pages_per_seq = (ctx + 31) // 32
+        total = b * pages_per_seq
+        cache = PagedKVCache(1, total, hkv, "cuda")
+        cache.data.uniform_(-1, 1)
+        bt = torch.randperm(total, device="cuda").int().reshape(b, pages_per_seq).contiguous()
+        ctx_t = torch.full((b,), ctx, dtype=torch.int32, device="cuda")
+        q = (torch.randn(b, heads * 128, device="cuda")).to(torch.bfloat16)
+        out = torch.empty(b, heads * 128, dtype=torch.bfloat16, device="cuda")
+        t = _time(lambda: paged_decode_attention(q, cache.layer(0), bt, ctx_t, heads, hkv, out=out), iters)
+        byts = b * ctx * hkv * 128 * 2 * 2
+        pps, ns = decode_splits(b, hkv, pages_per_seq)
+        print(json.dumps({"op": "paged_decode", "batch": b, "ctx": ctx, "heads": heads, "kv_heads": hkv,
+                          "nsplit": ns, "us": round(t, 2), "tbps": round(byts / t / 1e6, 2)}), flush=True)
+        del cache
+        torch.cuda.empty_cache()
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gemm", action="store_true")
+    ap.add_argument("--attn", action="store_true")
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--ms", default="1,16,32,64,128,256")
+    ap.add_argument("--sweep", action="store_true", help="time every valid split-K factor")
+    a = ap.parse_args(argv)
+    global SWEEP
+    SWEEP = a.sweep
+    both = not (a.gemm or a.attn)
+    if a.gemm or both:
+        bench_gemm(a.iters, [int(v) for v in a.ms.split(",")])
+    if a.attn or both:
+        bench_attn(a.iters)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

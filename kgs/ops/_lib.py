@@ -64,6 +64,11 @@ _SIGS = {
                              [ctypes.c_float, _c_void_p, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_attn_fwd_bf16": ([_c_void_p] * 4 + [_c_int] * 5 + [_c_long] * 4 + [ctypes.c_float, _c_int, _c_void_p],
                           _c_int),
+    # decode path (native/kernels/decode.hip)
+    "kgs_skinny_geometry": ([_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)], _c_int),
+    "kgs_skinny_gemm_bf16": ([_c_void_p] * 5 + [_c_int] * 3 + [_c_long, _c_long, _c_int, _c_void_p], _c_int),
+    "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_void_p], _c_int),
+    "kgs_paged_decode_bf16": ([_c_void_p] * 7 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_void_p], _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)
     "kgs_ar_signal_bytes": ([], _c_int),
     "kgs_ar_max_blocks": ([], _c_int),

@@ -1,0 +1,292 @@
+"""Decode-path ops on ``native/kernels/decode.hip`` -- the one-token-per-sequence
+half of LLM serving, which is HBM-bound on the weights and the KV cache.
+
+* :func:`pack_weight` / :class:`PackedWeight` -- a ``[N, K]`` bf16 weight
+  rearranged ONCE into MFMA A-fragment order (``[N/16][K/32][64][8]``), so the
+  skinny GEMM streams it as contiguous 1 KB wave loads straight into registers.
+* :func:`skinny_gemm` -- ``x[M, K] @ W^T`` for a decode batch ``M <= 256``
+  (split-K with an in-kernel last-arriver reduction when ``N`` is small).
+* :class:`PagedKVCache` -- ``[layers, pages, kv_heads, K|V, 32 x 128]`` bf16
+  pages whose element order IS the MFMA operand order of the decode attention
+  (:func:`kv_index_tables`); a 32-token page of one KV head is 16 KB.
+* :func:`rope_cache_` -- RoPE on the q/k heads of fused QKV rows + scatter of k/v
+  into their cache slots, one launch.
+* :func:`paged_decode_attention` -- GQA decode attention over the paged cache
+  (context split across waves, log-sum-exp merge).
+
+Every op raises :class:`kgs.ops.NativeUnavailable` when the native library is
+missing; the ``ref_*`` functions are the plain-PyTorch fp32 references (they run
+on CPU too and define the cache layout for tests).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import _lib
+
+PAGE = 32
+HEAD_DIM = 128
+CUS = 256  # MI355X compute units (grid sizing)
+
+
+# ----------------------------------------------------------------------------
+# weights
+
+def pack_weight(w: torch.Tensor) -> torch.Tensor:
+    """``[N, K]`` -> ``[N/16, K/32, 64, 8]``: lane ``g*16 + r`` of fragment
+    ``(nt, kk)`` holds ``W[16 nt + r, 32 kk + 8 g : +8]`` (16x16x32 bf16 A map)."""
+    n, k = w.shape
+    if n % 16 or k % 32:
+        raise ValueError(f"pack_weight needs N % 16 == 0 and K % 32 == 0, got {tuple(w.shape)}")
+    return w.reshape(n // 16, 16, k // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def unpack_weight(p: torch.Tensor) -> torch.Tensor:
+    nt, kk = p.shape[:2]
+    return p.reshape(nt, kk, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, kk * 32)
+
+
+class PackedWeight:
+    """A projection weight in skinny-GEMM fragment order (plus its shape)."""
+
+    __slots__ = ("data", "n", "k")
+
+    def __init__(self, w: torch.Tensor):
+        self.n, self.k = w.shape
+        self.data = pack_weight(w.to(torch.bfloat16))
+
+    def unpacked(self) -> torch.Tensor:
+        return unpack_weight(self.data)
+
+
+def skinny_geometry(m: int) -> tuple[int, int, int]:
+    """(rows of W per workgroup strip, k per x chunk, padded batch) -- mirrors
+    ``kgs_skinny_geometry`` in decode.hip."""
+    if not 0 < m <= 256:
+        raise ValueError(f"skinny GEMM batch must be 1..256, got {m}")
+    mt = 1 if m <= 16 else 2 if m <= 32 else 4 if m <= 64 else 8 if m <= 128 else 16
+    return 64 * (2 if mt >= 8 else 1), 32 * (2 if mt >= 8 else 16), 16 * mt
+
+
+def choose_ksplit(m: int, n: int, k: int, cus: int = CUS) -> int:
+    """Largest divisor of the k-chunk count that keeps the grid within one
+    workgroup per CU (measured best: long-running streaming workgroups,
+    profiles/decode_kernels.md) and the fp32 slabs within 64 MB (1 = no split)."""
+    rps, kpc, mpad = skinny_geometry(m)
+    nstrip, nchunks = n // rps, k // kpc
+    best = 1
+    for d in range(2, nchunks + 1):
+        if nchunks % d:
+            continue
+        if nstrip * d > max(cus, nstrip) or d * mpad * n * 4 > (64 << 20):
+            break
+        best = d
+    return best
+
+
+_WS: dict = {}
+
+
+def _workspace(device: torch.device, floats: int, ints: int):
+    """Per-device split-K slab buffer and zeroed ticket counters (the kernel
+    re-arms the counters it uses). GEMMs of one device are stream-ordered."""
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    ws, cnt = _WS.get(key, (None, None))
+    if ws is None or ws.numel() < floats:
+        ws = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device)
+    if cnt is None or cnt.numel() < ints:
+        cnt = torch.zeros(max(ints, 4096), dtype=torch.int32, device=device)
+    _WS[key] = (ws, cnt)
+    return ws, cnt
+
+
+def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = None,
+                ksplit: int | None = None) -> torch.Tensor:
+    """``x @ W^T`` (bf16, fp32 accumulate) for ``x: [M <= 256, K]`` row-major."""
+    if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1:
+        raise ValueError("x must be a row-major bf16 GPU matrix")
+    m, k = x.shape
+    if k != w.k:
+        raise ValueError(f"inner dims differ: x {tuple(x.shape)} vs W [{w.n}, {w.k}]")
+    rps, kpc, mpad = skinny_geometry(m)
+    if w.n % rps or k % kpc:
+        raise ValueError(f"skinny GEMM needs N % {rps} == 0 and K % {kpc} == 0 (N={w.n}, K={k})")
+    if out is None:
+        out = torch.empty((m, w.n), dtype=torch.bfloat16, device=x.device)
+    ks = choose_ksplit(m, w.n, k) if ksplit is None else ksplit
+    ws, cnt = _workspace(x.device, ks * mpad * w.n if ks > 1 else 0, w.n // rps)
+    rc = _lib.lib().kgs_skinny_gemm_bf16(w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(),
+                                         cnt.data_ptr(), m, w.n, k, x.stride(0), out.stride(0), ks,
+                                         _lib.stream_handle(x.device))
+    _lib.check(rc, f"skinny_gemm[{m}x{w.n}x{k}, ksplit={ks}]")
+    return out
+
+
+def reserve_workspace(device) -> None:
+    """Allocate the largest split-K slab buffer :func:`choose_ksplit` can ask
+    for (64 MB) up front, e.g. before hipGraph capture."""
+    _workspace(torch.device(device), 16 << 20, 1 << 16)
+
+
+# ----------------------------------------------------------------------------
+# paged KV cache
+
+def kv_index_tables(device="cpu") -> tuple[torch.Tensor, torch.Tensor]:
+    """``(K_IDX, V_IDX)``, each ``[32, 128]`` int64: the position of token ``tau``,
+    dim ``d`` inside a page's K / V region (``kv_k_index`` / ``kv_v_index`` in
+    decode.hip). K is in S^T = K.Q^T A-fragment order, V in O^T = V^T.P^T
+    A-fragment order with the token order S^T's accumulator produces."""
+    tau = torch.arange(PAGE, device=device)[:, None]
+    d = torch.arange(HEAD_DIM, device=device)[None, :]
+    k_idx = (((tau >> 4) * 4 + (d >> 5)) * 64 + ((d >> 3) & 3) * 16 + (tau & 15)) * 8 + (d & 7)
+    v_idx = ((d >> 4) * 64 + ((tau >> 2) & 3) * 16 + (d & 15)) * 8 + (tau & 3) + 4 * (tau >> 4)
+    return k_idx, v_idx
+
+
+class PagedKVCache:
+    """All layers' KV pages in one allocation: ``[layers, pages, kv_heads, 2, 4096]``
+    bf16 (2 = K then V region of a 32-token page). Page 0.. are handed out by the
+    scheduler's block allocator (kgs.serve)."""
+
+    def __init__(self, layers: int, pages: int, kv_heads: int, device, dtype=torch.bfloat16):
+        self.layers, self.pages, self.kv_heads = layers, pages, kv_heads
+        self.data = torch.zeros(layers, pages, kv_heads, 2, PAGE * HEAD_DIM, dtype=dtype, device=device)
+
+    def layer(self, i: int) -> torch.Tensor:
+        return self.data[i]
+
+    @staticmethod
+    def bytes_per_page(layers: int, kv_heads: int) -> int:
+        return layers * kv_heads * 2 * PAGE * HEAD_DIM * 2
+
+
+def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positions: torch.Tensor,
+                slots: torch.Tensor, cache_layer: torch.Tensor, heads: int, kv_heads: int) -> torch.Tensor:
+    """In place: rotate the q and k heads of every row of the fused ``qkv``
+    ``[T, (H + 2 HKV) * 128]`` at ``positions[t]``, and write k, v into cache slot
+    ``slots[t]`` (``page * 32 + offset``; < 0 skips the write)."""
+    t = qkv.shape[0]
+    if qkv.dtype != torch.bfloat16 or not qkv.is_cuda or qkv.stride(1) != 1:
+        raise ValueError("qkv must be a row-major bf16 GPU matrix")
+    for v, name in ((positions, "positions"), (slots, "slots")):
+        if v.dtype != torch.int32 or not v.is_contiguous() or v.numel() != t:
+            raise ValueError(f"{name} must be a contiguous int32 vector of length {t}")
+    for v in (cos, sin):
+        if v.dtype != torch.float32 or not v.is_contiguous() or v.shape[-1] != HEAD_DIM // 2:
+            raise ValueError("cos/sin must be contiguous fp32 [max_pos, 64]")
+    if cache_layer.dtype != torch.bfloat16 or not cache_layer.is_contiguous():
+        raise ValueError("cache_layer must be a contiguous bf16 page array")
+    rc = _lib.lib().kgs_rope_cache_bf16(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), positions.data_ptr(),
+                                        slots.data_ptr(), cache_layer.data_ptr(), t, heads, kv_heads, HEAD_DIM,
+                                        qkv.stride(0), _lib.stream_handle(qkv.device))
+    _lib.check(rc, "rope_cache")
+    return qkv
+
+
+def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS) -> tuple[int, int]:
+    """(pages_per_split, nsplit): split each sequence's context so the grid has
+    about 8 waves per CU."""
+    want = max(1, math.ceil(8 * cus / max(1, batch * kv_heads)))
+    nsplit = max(1, min(max_pages, want))
+    pps = math.ceil(max_pages / nsplit)
+    return pps, math.ceil(max_pages / pps)
+
+
+_AWS: dict = {}
+
+
+def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tables: torch.Tensor,
+                           ctx_lens: torch.Tensor, heads: int, kv_heads: int, out: torch.Tensor | None = None,
+                           scale: float | None = None, pages_per_split: int | None = None) -> torch.Tensor:
+    """One query token per sequence: ``q`` rows ``[B, >= H*128]`` (e.g. the rotated
+    q heads at the front of the fused QKV rows), ``block_tables`` int32
+    ``[B, max_pages]``, ``ctx_lens`` int32 ``[B]`` (cached tokens incl. the new
+    one). Returns ``[B, H*128]`` bf16."""
+    b = q.shape[0]
+    if q.dtype != torch.bfloat16 or not q.is_cuda or q.stride(1) != 1:
+        raise ValueError("q must be a row-major bf16 GPU matrix")
+    if block_tables.dtype != torch.int32 or not block_tables.is_contiguous() or block_tables.shape[0] != b:
+        raise ValueError("block_tables must be contiguous int32 [B, max_pages]")
+    if ctx_lens.dtype != torch.int32 or not ctx_lens.is_contiguous() or ctx_lens.numel() != b:
+        raise ValueError("ctx_lens must be contiguous int32 [B]")
+    max_pages = block_tables.shape[1]
+    if pages_per_split is None:
+        pps, nsplit = decode_splits(b, kv_heads, max_pages)
+    else:
+        pps, nsplit = pages_per_split, math.ceil(max_pages / pages_per_split)
+    if out is None:
+        out = torch.empty((b, heads * HEAD_DIM), dtype=torch.bfloat16, device=q.device)
+    po = pml = None
+    if nsplit > 1:
+        need = b * heads * nsplit
+        key = q.device.index
+        po, pml = _AWS.get(key, (None, None))
+        if po is None or po.numel() < need * HEAD_DIM:
+            po = torch.empty(need * HEAD_DIM, dtype=torch.float32, device=q.device)
+            pml = torch.empty(need * 2, dtype=torch.float32, device=q.device)
+            _AWS[key] = (po, pml)
+    scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
+    rc = _lib.lib().kgs_paged_decode_bf16(q.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(),
+                                          ctx_lens.data_ptr(), out.data_ptr(), po.data_ptr() if po is not None else None,
+                                          pml.data_ptr() if pml is not None else None, b, heads, kv_heads, HEAD_DIM,
+                                          max_pages, pps, nsplit, q.stride(0), out.stride(0), float(scale),
+                                          _lib.stream_handle(q.device))
+    _lib.check(rc, "paged_decode_attention")
+    return out
+
+
+# ----------------------------------------------------------------------------
+# plain-PyTorch references (fp32 math; CPU or GPU)
+
+def ref_cache_write(cache_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor) -> None:
+    """Scatter ``k, v: [T, HKV, 128]`` into ``cache_layer [pages, HKV, 2, 4096]``."""
+    k_idx, v_idx = kv_index_tables(cache_layer.device)
+    keep = slots >= 0
+    slots = slots[keep].long()
+    k, v = k[keep], v[keep]
+    page, tau = slots // PAGE, slots % PAGE
+    hkv = cache_layer.shape[1]
+    for h in range(hkv):
+        cache_layer[page[:, None], h, 0, k_idx[tau]] = k[:, h].to(cache_layer.dtype)
+        cache_layer[page[:, None], h, 1, v_idx[tau]] = v[:, h].to(cache_layer.dtype)
+
+
+def ref_gather_kv(cache_layer: torch.Tensor, pages: torch.Tensor, ctx: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """The first ``ctx`` tokens of one sequence: ``(k, v)``, each ``[ctx, HKV, 128]`` fp32."""
+    k_idx, v_idx = kv_index_tables(cache_layer.device)
+    pos = torch.arange(ctx, device=cache_layer.device)
+    page = pages.long()[pos // PAGE]
+    tau = pos % PAGE
+    hkv = cache_layer.shape[1]
+    k = torch.stack([cache_layer[page[:, None], h, 0, k_idx[tau]] for h in range(hkv)], dim=1)
+    v = torch.stack([cache_layer[page[:, None], h, 1, v_idx[tau]] for h in range(hkv)], dim=1)
+    return k.float(), v.float()
+
+
+def ref_paged_decode(q: torch.Tensor, cache_layer: torch.Tensor, block_tables: torch.Tensor, ctx_lens: torch.Tensor,
+                     heads: int, kv_heads: int, scale: float | None = None) -> torch.Tensor:
+    scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
+    rep = heads // kv_heads
+    outs = []
+    for i in range(q.shape[0]):
+        ctx = int(ctx_lens[i])
+        k, v = ref_gather_kv(cache_layer, block_tables[i], ctx)
+        qi = q[i, :heads * HEAD_DIM].float().reshape(heads, HEAD_DIM)
+        kk = k.repeat_interleave(rep, dim=1)  # [ctx, H, D]
+        vv = v.repeat_interleave(rep, dim=1)
+        s = torch.einsum("hd,thd->ht", qi, kk) * scale
+        p = torch.softmax(s, dim=-1)
+        outs.append(torch.einsum("ht,thd->hd", p, vv).reshape(-1))
+    return torch.stack(outs)
+
+
+def ref_rope_rows(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positions: torch.Tensor,
+                  heads: int) -> torch.Tensor:
+    """Rotate-half RoPE of the first ``heads`` 128-wide heads of each row (fp32 result)."""
+    t = x.shape[0]
+    xf = x[:, :heads * HEAD_DIM].float().reshape(t, heads, HEAD_DIM)
+    c, s = cos[positions.long()][:, None, :], sin[positions.long()][:, None, :]
+    x1, x2 = xf[..., :HEAD_DIM // 2], xf[..., HEAD_DIM // 2:]
+    return torch.cat((x1 * c - x2 * s, x2 * c + x1 * s), dim=-1).reshape(t, heads * HEAD_DIM)

@@ -1,0 +1,127 @@
+"""Offline serving throughput of :class:`kgs.serve.LLMEngine` (BASELINE config 5
+stand-in): N requests of synthetic random-token prompts, fixed output length
+(EOS ignored), continuous batching, Llama-3-8B architecture with random-init
+bf16 weights on one MI355X. Prints one JSON line.
+
+Optional baseline (``--hf``): the same architecture in HF ``transformers``
+(``LlamaForCausalLM``, SDPA attention, eager ``generate`` with static batches)
+on the same GPU -- what a PyTorch user gets without a serving engine.
+
+  python -m kgs.serve bench [--requests 256] [--input-len 512] [--output-len 256]
+                            [--max-batch 256] [--layers 32] [--hf]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import time
+
+import numpy as np
+import torch
+
+
+def _prompts(n, length, vocab, seed=0):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(3, vocab, size=length).tolist() for _ in range(n)]
+
+
+def run_engine(a) -> dict:
+    from kgs.models.llama import LlamaConfig
+
+    from .engine import EngineConfig, LLMEngine, SamplingParams
+
+    mc = LlamaConfig.llama3_8b(layers=a.layers)
+    ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
+                      max_prefill_tokens=a.max_prefill_tokens)
+    t0 = time.perf_counter()
+    eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
+    t_load = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    if not a.no_graphs:
+        widths = sorted({w for w in (8, 16, 32, 64, 128, 256)
+                         if w >= (a.input_len + 32) // 32 and w <= 2 * ((a.input_len + a.output_len) // 32 + 1)})
+        eng.warmup(widths=widths or None)
+    # one short request end to end (prefill + decode paths compiled/allocated)
+    eng.generate(_prompts(1, 16, mc.vocab, seed=9), SamplingParams(max_tokens=4, ignore_eos=True))
+    torch.cuda.synchronize()
+    t_warm = time.perf_counter() - t0
+    prompts = _prompts(a.requests, a.input_len, mc.vocab)
+    params = SamplingParams(max_tokens=a.output_len, ignore_eos=True)
+    for k in eng.stats:
+        eng.stats[k] = 0
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    outs = eng.generate(prompts, params)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    n_out = sum(len(r.output) for r in outs)
+    n_in = a.requests * a.input_len
+    ttft = sorted(r.t_first - r.t_arrival for r in outs)
+    tpot = sorted((r.t_done - r.t_first) / max(1, len(r.output) - 1) for r in outs)
+    return {
+        "metric": "offline serving throughput (kgs.serve, Llama-3-8B arch, random init)",
+        "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
+        "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
+        "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
+        "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
+        "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
+        "load_s": round(t_load, 1), "warmup_s": round(t_warm, 1), "stats": dict(eng.stats),
+    }
+
+
+def run_hf(a) -> dict:
+    """HF transformers eager generate, static batches of max_batch, same shapes."""
+    import transformers
+
+    cfg = transformers.LlamaConfig(vocab_size=128256, hidden_size=4096, intermediate_size=14336,
+                                   num_hidden_layers=a.layers, num_attention_heads=32, num_key_value_heads=8,
+                                   max_position_embeddings=8192, rope_theta=500000.0, rms_norm_eps=1e-5,
+                                   torch_dtype="bfloat16", attn_implementation="sdpa")
+    torch.set_default_dtype(torch.bfloat16)
+    with torch.device("cuda"):
+        model = transformers.LlamaForCausalLM(cfg)
+    torch.set_default_dtype(torch.float32)
+    model.eval()
+    prompts = torch.tensor(_prompts(a.requests, a.input_len, 128256), device="cuda")
+    bs = min(a.max_batch, a.requests)
+    gen = dict(max_new_tokens=a.output_len, min_new_tokens=a.output_len, do_sample=False, pad_token_id=0)
+    with torch.no_grad():
+        model.generate(prompts[:1, :16], max_new_tokens=2, do_sample=False, pad_token_id=0)  # warm up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        n_out = 0
+        for i in range(0, a.requests, bs):
+            out = model.generate(prompts[i:i + bs], attention_mask=torch.ones_like(prompts[i:i + bs]), **gen)
+            n_out += (out.shape[1] - a.input_len) * out.shape[0]
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+    return {"metric": "offline generation throughput (HF transformers eager generate, same arch)",
+            "backend": f"hf-transformers-{transformers.__version__}", "requests": a.requests,
+            "input_len": a.input_len, "output_len": a.output_len, "batch": bs, "layers": a.layers,
+            "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
+            "total_tok_per_s": round((n_out + a.requests * a.input_len) / dt, 1)}
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(prog="python -m kgs.serve bench", description=__doc__.splitlines()[0])
+    ap.add_argument("--requests", type=int, default=256)
+    ap.add_argument("--input-len", type=int, default=512)
+    ap.add_argument("--output-len", type=int, default=256)
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--max-prefill-tokens", type=int, default=16384)
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")
+    ap.add_argument("--hf-only", action="store_true")
+    a = ap.parse_args(argv)
+    if not a.hf_only:
+        print(json.dumps(run_engine(a)), flush=True)
+        torch.cuda.empty_cache()
+    if a.hf or a.hf_only:
+        print(json.dumps(run_hf(a)), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,265 @@
+"""LLM serving engine: native continuous-batching scheduler + paged-KV model
+runner + sampler, with hipGraph-captured decode steps.
+
+One engine step = one scheduler plan (``kgs._native._serve``): a prefill of newly
+admitted prompts, or a decode of every running sequence. Decode steps are
+padded to a batch bucket (1, 2, 4, ..., max_batch) and a page-table width
+bucket and replayed from a captured hipGraph per (batch, width) pair, so the
+~260 kernel launches of a Llama-3-8B step cost one graph launch. Padded rows
+point at the scheduler's null page 0 and write nothing (slot -1).
+
+:meth:`LLMEngine.generate` is the offline API; :mod:`kgs.serve.api` drives
+:meth:`LLMEngine.step` from a background thread for the HTTP server.
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from kgs.models.llama import LlamaConfig
+from kgs.ops.decode import PAGE, PagedKVCache
+
+from .model import ServingModel
+
+
+@dataclass
+class SamplingParams:
+    max_tokens: int = 16
+    temperature: float = 0.0   # 0 = greedy
+    top_k: int = 0             # 0 = full vocabulary
+    ignore_eos: bool = False
+    stop_token_ids: tuple = ()
+
+
+@dataclass
+class Request:
+    id: int
+    prompt: list
+    params: SamplingParams
+    output: list = field(default_factory=list)
+    finished: bool = False
+    finish_reason: str | None = None
+    t_arrival: float = 0.0
+    t_first: float | None = None
+    t_done: float | None = None
+
+
+@dataclass
+class EngineConfig:
+    num_pages: int | None = None      # None: size from free HBM (kv_fraction)
+    kv_fraction: float = 0.85         # of the memory left after weights
+    max_batch: int = 256
+    max_prefill_tokens: int = 16384
+    max_model_len: int = 8192
+    eos_token_id: int = 2
+    cuda_graphs: bool = True
+    seed: int = 0
+
+
+def _bucket(n: int, cap: int) -> int:
+    b = 1
+    while b < n:
+        b *= 2
+    return min(b, cap)
+
+
+class LLMEngine:
+    def __init__(self, model_cfg: LlamaConfig, cfg: EngineConfig | None = None, device="cuda", backend: str = "kgs"):
+        from kgs._native import _serve
+
+        self.cfg = cfg = cfg or EngineConfig()
+        self.device = torch.device(device)
+        self.backend = backend
+        num_pages = cfg.num_pages or self._pages_from_memory(model_cfg)
+        self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
+                                  max_model_len=cfg.max_model_len)
+        sc = _serve.SchedulerConfig()
+        sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
+        sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
+        self.sched = _serve.Scheduler(sc)
+        self.num_pages = num_pages
+        self.requests: dict[int, Request] = {}
+        self._ids = itertools.count()
+        self._graphs: dict = {}
+        self._gen = torch.Generator(device=self.device).manual_seed(cfg.seed)
+        self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
+                      "preemptions": 0, "graph_replays": 0, "graph_captures": 0}
+        self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs"
+
+    def _pages_from_memory(self, mc: LlamaConfig) -> int:
+        if self.device.type != "cuda":
+            return 256
+        free, _ = torch.cuda.mem_get_info(self.device)
+        h, i, kvd = mc.hidden, mc.intermediate, mc.kv_heads * mc.head_dim
+        per_layer = h * (h + 2 * kvd) + h * h + 2 * h * i + i * h
+        weights = 2 * (mc.layers * per_layer + 2 * mc.vocab * h)
+        # the kgs backend keeps prefill-order and prepacked decode copies of every projection
+        resident = weights * (2 if self.backend == "kgs" else 1)
+        avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
+        return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads)))
+
+    # ----------------------------------------------------------------- API
+    def add_request(self, prompt: list[int], params: SamplingParams | None = None) -> int:
+        params = params or SamplingParams()
+        rid = next(self._ids)
+        if not self.sched.add(rid, np.asarray(prompt, dtype=np.int32), int(params.max_tokens)):
+            raise ValueError(f"request does not fit: prompt {len(prompt)} + max_tokens {params.max_tokens} "
+                             f"(max_model_len {self.cfg.max_model_len}, {self.num_pages} pages)")
+        self.requests[rid] = Request(rid, list(prompt), params, t_arrival=time.perf_counter())
+        return rid
+
+    def abort(self, rid: int) -> None:
+        if self.sched.abort(rid):
+            r = self.requests[rid]
+            r.finished, r.finish_reason, r.t_done = True, "abort", time.perf_counter()
+            self.sched.release(rid)
+
+    def has_work(self) -> bool:
+        return self.sched.num_waiting + self.sched.num_running > 0
+
+    def step(self) -> list[tuple[int, int, bool]]:
+        """Run one scheduler step; returns [(request id, new token, finished)]."""
+        plan = self.sched.schedule()
+        if plan.kind == 0:
+            return []
+        self.stats["preemptions"] += len(plan.preempted)
+        ids = plan.seq_ids
+        if plan.kind == 1:
+            logits = self._run_prefill(plan)
+            self.stats["prefill_steps"] += 1
+            self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
+        else:
+            logits = self._run_decode(plan)
+            self.stats["decode_steps"] += 1
+            self.stats["decode_tokens"] += len(ids)
+        toks = self._sample(ids, logits).cpu().numpy().astype(np.int32)
+        eos = np.zeros(len(ids), dtype=np.uint8)
+        now = time.perf_counter()
+        for j, rid in enumerate(ids):
+            r = self.requests[int(rid)]
+            t = int(toks[j])
+            if not r.params.ignore_eos and (t == self.cfg.eos_token_id or t in r.params.stop_token_ids):
+                eos[j] = 1
+        done = set(int(d) for d in self.sched.update(ids, toks, eos))
+        out = []
+        for j, rid in enumerate(ids):
+            rid = int(rid)
+            r = self.requests[rid]
+            r.output.append(int(toks[j]))
+            if r.t_first is None:
+                r.t_first = now
+            fin = rid in done
+            if fin:
+                r.finished, r.t_done = True, now
+                r.finish_reason = "stop" if eos[j] else "length"
+                self.sched.release(rid)
+            out.append((rid, int(toks[j]), fin))
+        return out
+
+    def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None
+                 ) -> list[Request]:
+        ps = params if isinstance(params, list) else [params or SamplingParams()] * len(prompts)
+        rids = [self.add_request(p, q) for p, q in zip(prompts, ps)]
+        while self.has_work():
+            self.step()
+        return [self.requests.pop(r) for r in rids]
+
+    # -------------------------------------------------------------- runners
+    def _dev(self, a, dtype=torch.int32):
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if self.device.type == "cuda":
+            t = t.pin_memory().to(self.device, non_blocking=True)
+        return t.to(dtype)
+
+    def _run_prefill(self, plan) -> torch.Tensor:
+        return self.model.prefill(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots),
+                                  plan.seq_starts.tolist(), plan.seq_lens.tolist(), plan.padded_lens.tolist())
+
+    def _run_decode(self, plan) -> torch.Tensor:
+        b = len(plan.seq_ids)
+        if not self.use_graphs:
+            return self.model.decode(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots),
+                                     self._dev(plan.block_tables), self._dev(plan.ctx_lens))
+        bb = _bucket(b, self.cfg.max_batch)
+        wb = _bucket(plan.max_pages, math.ceil(self.cfg.max_model_len / PAGE))
+        g = self._graphs.get((bb, wb)) or self._capture(bb, wb)
+        io = g["io"]
+        host = g["host"]
+        hn = g["host_np"]  # numpy views of the pinned staging buffers
+        hn["tokens"][:] = 0
+        hn["tokens"][:b] = plan.tokens
+        hn["positions"][:] = 0
+        hn["positions"][:b] = plan.positions
+        hn["slots"][:] = -1
+        hn["slots"][:b] = plan.slots
+        hn["ctx"][:] = 1
+        hn["ctx"][:b] = plan.ctx_lens
+        hn["bt"][:] = 0
+        hn["bt"][:b, :plan.max_pages] = plan.block_tables
+        for k in host:
+            io[k].copy_(host[k], non_blocking=True)
+        g["graph"].replay()
+        self.stats["graph_replays"] += 1
+        return g["logits"][:b]
+
+    def _capture(self, bb: int, wb: int):
+        """Capture one decode step for batch bucket bb and page-table width wb."""
+        def pinned(shape):
+            return torch.zeros(shape, dtype=torch.int32).pin_memory()
+
+        host = {"tokens": pinned(bb), "positions": pinned(bb), "slots": pinned(bb), "ctx": pinned(bb),
+                "bt": pinned((bb, wb))}
+        host["slots"][:] = -1
+        host["ctx"][:] = 1
+        io = {k: v.to(self.device) for k, v in host.items()}
+        run = lambda: self.model.decode(io["tokens"], io["positions"], io["slots"], io["bt"], io["ctx"])  # noqa: E731
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):  # warm up: workspaces and allocator pools settle before capture
+                run()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            logits = run()
+        g = {"graph": graph, "io": io, "host": host, "host_np": {k: v.numpy() for k, v in host.items()},
+             "logits": logits}
+        self._graphs[(bb, wb)] = g
+        self.stats["graph_captures"] += 1
+        return g
+
+    def warmup(self, batches=None, widths=None) -> None:
+        """Capture decode graphs ahead of traffic (otherwise captured on first use)."""
+        if not self.use_graphs:
+            return
+        maxw = math.ceil(self.cfg.max_model_len / PAGE)
+        for bb in batches or [1 << i for i in range(int(math.log2(self.cfg.max_batch)) + 1)]:
+            for wb in widths or [w for w in (8, 16, 32, 64, 128, 256) if w <= maxw]:
+                if (bb, wb) not in self._graphs:
+                    self._capture(bb, wb)
+
+    # -------------------------------------------------------------- sampling
+    def _sample(self, ids, logits: torch.Tensor) -> torch.Tensor:
+        ps = [self.requests[int(r)].params for r in ids]
+        if all(p.temperature <= 0 for p in ps):
+            return logits.argmax(dim=-1)
+        lf = logits.float()
+        temp = torch.tensor([max(p.temperature, 1e-5) for p in ps], device=lf.device)[:, None]
+        lf = lf / temp
+        ks = [p.top_k for p in ps]
+        if any(k > 0 for k in ks):
+            kmax = max(ks)
+            vals, _ = lf.topk(kmax, dim=-1)
+            kth = torch.tensor([k if k > 0 else kmax for k in ks], device=lf.device)[:, None] - 1
+            thr = vals.gather(1, kth)
+            full = torch.tensor([k <= 0 for k in ks], device=lf.device)[:, None]
+            lf = torch.where(full | (lf >= thr), lf, torch.full_like(lf, float("-inf")))
+        probs = torch.softmax(lf, dim=-1)
+        sampled = torch.multinomial(probs, 1, generator=self._gen).squeeze(1)
+        greedy = torch.tensor([p.temperature <= 0 for p in ps], device=lf.device)
+        return torch.where(greedy, logits.argmax(dim=-1), sampled)

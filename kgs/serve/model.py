@@ -1,0 +1,172 @@
+"""Paged-KV Llama model runner for :mod:`kgs.serve` (BASELINE config 5 stand-in:
+Llama-3-8B bf16, TP=1, one MI355X).
+
+Two step kinds, both driven by the native scheduler's plans
+(``native/serve/scheduler.cpp``):
+
+* **prefill** -- the prompts of newly admitted sequences, each padded to a
+  multiple of 128 tokens and concatenated: every projection is one
+  :func:`kgs.ops.gemm_nt` (256x256 MFMA pipeline), RoPE + the KV-cache scatter
+  is one :func:`kgs.ops.decode.rope_cache_` launch, attention is the
+  flash-attention forward per sequence, and only the last real token of each
+  sequence goes through the LM head;
+* **decode** -- one token per running sequence: projections on
+  :func:`kgs.ops.decode.skinny_gemm` over prepacked weights (batch <= 32; larger
+  decode batches use hipBLASLt, where it measured faster), attention is
+  :func:`kgs.ops.decode.paged_decode_attention` over the paged cache.
+
+``backend="ref"`` runs the same weights, cache layout and plans through plain
+PyTorch (CPU or GPU) -- the numerics reference for tests.
+
+Weights are random-init (no network, no checkpoint) with the same generator
+scheme as :class:`kgs.models.llama.LlamaModel`, whose ``forward`` (no cache) is
+the full-recompute oracle the tests compare generations against.
+"""
+from __future__ import annotations
+
+import torch
+
+from kgs.models.llama import LlamaConfig, LlamaModel, _rms_norm
+from kgs.ops import decode as D
+
+SKINNY_MAX_M = 32  # decode batches above this go to hipBLASLt (measured crossover, profiles/decode_kernels.md)
+
+
+class ServingModel:
+    def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
+                 num_pages: int = 1024, max_model_len: int = 8192):
+        if cfg.head_dim != D.HEAD_DIM:
+            raise ValueError(f"head_dim must be {D.HEAD_DIM}")
+        self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
+        base = LlamaModel(cfg, device=device, backend="torch" if backend == "ref" else "kgs", seed=seed)
+        self.oracle = base  # same weights, full-recompute forward (tests)
+        self.embed, self.norm = base.embed, base.norm
+        self.ln1 = [L["ln1"] for L in base.layers]
+        self.ln2 = [L["ln2"] for L in base.layers]
+        self.w = [{n: base.layers[i][n].w for n in ("qkv", "o", "gate_up", "down")} for i in range(cfg.layers)]
+        self.w_lm = base.lm_head.w
+        self.packed = None
+        if backend == "kgs":
+            self.packed = [{n: D.PackedWeight(w) for n, w in lw.items()} for lw in self.w]
+            self.packed_lm = D.PackedWeight(self.w_lm)
+            D.reserve_workspace(self.device)
+        self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device)
+        self.max_model_len = max_model_len
+        from kgs.ops.transformer import rope_tables
+
+        self.cos, self.sin = rope_tables(max_model_len + 256, cfg.head_dim, cfg.rope_theta, self.device)
+
+    # ------------------------------------------------------------------ utils
+    def weight_bytes(self) -> int:
+        n = sum(w.numel() for lw in self.w for w in lw.values()) + self.w_lm.numel()
+        return 2 * n
+
+    def _proj(self, x: torch.Tensor, layer: int | None, name: str, decode: bool) -> torch.Tensor:
+        w = self.w_lm if layer is None else self.w[layer][name]
+        if self.backend == "ref":
+            return (x.float() @ w.float().T).to(torch.bfloat16)
+        m = x.shape[0]
+        if decode and m <= SKINNY_MAX_M:
+            pw = self.packed_lm if layer is None else self.packed[layer][name]
+            return D.skinny_gemm(x, pw)
+        if decode:
+            return torch.matmul(x, w.T)
+        from kgs.ops import gemm_nt
+
+        return gemm_nt(x, w)
+
+    def _norm(self, x, d, w):
+        """x += d (in place, bf16) and return rmsnorm(x) * w."""
+        if self.backend == "ref":
+            if d is not None:
+                x.copy_((x.float() + d.float()).to(torch.bfloat16))
+            return _rms_norm(x, w, self.cfg.eps)
+        from kgs.ops.transformer import add_rmsnorm
+
+        return add_rmsnorm(x, d, w, self.cfg.eps)
+
+    def _silu_mul(self, gu):
+        if self.backend == "ref":
+            i = gu.shape[1] // 2
+            g, u = gu[:, :i].float(), gu[:, i:].float()
+            return (g * torch.sigmoid(g) * u).to(torch.bfloat16)
+        from kgs.ops.transformer import silu_mul
+
+        return silu_mul(gu)
+
+    def _rope_cache(self, qkv, layer, positions, slots):
+        c = self.cfg
+        if self.backend == "ref":
+            hq = c.heads + c.kv_heads
+            rot = D.ref_rope_rows(qkv, self.cos, self.sin, positions, hq)
+            qkv[:, :hq * D.HEAD_DIM] = rot.to(torch.bfloat16)
+            k = qkv[:, c.heads * D.HEAD_DIM:hq * D.HEAD_DIM].reshape(-1, c.kv_heads, D.HEAD_DIM)
+            v = qkv[:, hq * D.HEAD_DIM:(hq + c.kv_heads) * D.HEAD_DIM].reshape(-1, c.kv_heads, D.HEAD_DIM)
+            D.ref_cache_write(self.cache.layer(layer), k, v, slots)
+            return
+        D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(layer), c.heads, c.kv_heads)
+
+    # ---------------------------------------------------------------- prefill
+    @torch.no_grad()
+    def prefill(self, tokens, positions, slots, seq_starts, seq_lens, padded_lens) -> torch.Tensor:
+        """Flattened padded prompts -> logits of each sequence's last real token [S, vocab]."""
+        c = self.cfg
+        h, hd = c.hidden, c.head_dim
+        x = self.embed[tokens.long()].reshape(-1, h).contiguous()
+        y = self._norm(x, None, self.ln1[0])
+        for i in range(c.layers):
+            qkv = self._proj(y, i, "qkv", False)
+            self._rope_cache(qkv, i, positions, slots)
+            a = self._prefill_attention(qkv, seq_starts, seq_lens, padded_lens)
+            y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
+            act = self._silu_mul(self._proj(y, i, "gate_up", False))
+            nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
+            y = self._norm(x, self._proj(act, i, "down", False), nxt)
+        last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
+        yl = y[last].contiguous()
+        return self._proj(yl, None, "lm", True)
+
+    def _prefill_attention(self, qkv, seq_starts, seq_lens, padded_lens):
+        c = self.cfg
+        hd = c.head_dim
+        out = torch.empty((qkv.shape[0], c.heads * hd), dtype=torch.bfloat16, device=qkv.device)
+        for s0, n, p in zip(seq_starts, seq_lens, padded_lens):
+            s0, n, p = int(s0), int(n), int(p)
+            blk = qkv[s0:s0 + p]
+            if self.backend == "ref":
+                q = blk[:n, :c.heads * hd].float().reshape(n, c.heads, hd).transpose(0, 1)
+                k = blk[:n, c.heads * hd:(c.heads + c.kv_heads) * hd].float().reshape(n, c.kv_heads, hd).transpose(0, 1)
+                v = blk[:n, (c.heads + c.kv_heads) * hd:(c.heads + 2 * c.kv_heads) * hd].float().reshape(
+                    n, c.kv_heads, hd).transpose(0, 1)
+                rep = c.heads // c.kv_heads
+                k, v = k.repeat_interleave(rep, 0), v.repeat_interleave(rep, 0)
+                o = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=True)
+                out[s0:s0 + n] = o.transpose(0, 1).reshape(n, c.heads * hd).to(torch.bfloat16)
+                out[s0 + n:s0 + p] = 0
+            else:
+                from kgs.ops.transformer import attention_qkv
+
+                attention_qkv(blk, 1, p, c.heads, c.kv_heads, head_dim=hd, causal=True, out=out[s0:s0 + p])
+        return out
+
+    # ----------------------------------------------------------------- decode
+    @torch.no_grad()
+    def decode(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split=None) -> torch.Tensor:
+        """One token per sequence -> logits [B, vocab]."""
+        c = self.cfg
+        x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
+        y = self._norm(x, None, self.ln1[0])
+        for i in range(c.layers):
+            qkv = self._proj(y, i, "qkv", True)
+            self._rope_cache(qkv, i, positions, slots)
+            if self.backend == "ref":
+                a = D.ref_paged_decode(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads,
+                                       c.kv_heads).to(torch.bfloat16)
+            else:
+                a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
+                                             pages_per_split=pages_per_split)
+            y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
+            act = self._silu_mul(self._proj(y, i, "gate_up", True))
+            nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
+            y = self._norm(x, self._proj(act, i, "down", True), nxt)
+        return self._proj(y, None, "lm", True)

@@ -8,6 +8,8 @@ Builds, with the ROCm toolchain in ``/opt/rocm``:
 * ``kgs/_native/libkgs_gpuinfo.so`` + ``kgs/_native/kgs-gpuinfo`` -- the C++
   device-enumeration core (KFD sysfs topology + amd-smi) used by the device
   plugin, also as a standalone CLI.
+* ``kgs/_native/_serve*.so`` -- the continuous-batching scheduler and paged-KV
+  block allocator of ``kgs.serve`` (C++17, pybind11).
 * ``kgs/_native/kgs-rccl-bench`` -- single-process multi-GPU RCCL all-reduce
   sweep (ncclCommInitAll), the C++ twin of ``kgs.parallel.allreduce``.
 
@@ -93,6 +95,7 @@ def targets() -> list[Target]:
     kdir = NATIVE / "kernels"
     gdir = NATIVE / "gpuinfo"
     rdir = NATIVE / "rccl_bench"
+    sdir = NATIVE / "serve"
     k_headers = sorted(kdir.glob("*.h"))
     g_headers = sorted(gdir.glob("*.h"))
     amdsmi_ok = (ROCM / "include" / "amd_smi" / "amdsmi.h").exists()
@@ -135,6 +138,14 @@ def targets() -> list[Target]:
             link_flags=smi_link,
             shared=False,
             headers=g_headers,
+        ),
+        Target(
+            "serve-py",
+            OUT / f"_serve{_py_ext_suffix()}",
+            [sdir / "scheduler.cpp", sdir / "serve_py.cpp"],
+            CXX,
+            flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{sdir}"] + _pybind_includes(),
+            headers=sorted(sdir.glob("*.h")),
         ),
         Target(
             "rccl-bench",

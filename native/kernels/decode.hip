@@ -1,0 +1,520 @@
+// Decode-path kernels for gfx950: the memory-bound half of LLM serving (one new
+// token per sequence per step), written around layouts chosen for the MFMA
+// operand maps so that every hot load is a contiguous 1 KB wave access.
+//
+//   * skinny GEMM   y[M, N] = x[M, K] . W[N, K]^T for a decode batch M <= 256.
+//                   W is PREPACKED once (kgs/ops/decode.py pack_weight) into
+//                   16-row x 32-k MFMA A-fragments: [N/16][K/32][64 lanes][8],
+//                   so a wave streams its rows as back-to-back 1 KB loads
+//                   straight into registers (no LDS round trip for the weight
+//                   bytes). x (small, L2-resident) is staged through LDS in
+//                   fragment order, read from global in whole rows, and shared
+//                   by the 4 waves of a workgroup. Split-K across workgroups
+//                   when N alone cannot fill 256 CUs: the last workgroup of a
+//                   strip (agent-scope release/acquire ticket) reduces the fp32
+//                   slabs and writes bf16 -- one launch, graph-capturable.
+//   * rope_cache    rotate-half RoPE on the q and k heads of a fused QKV row and
+//                   scatter k, v into the paged KV cache (one launch for both).
+//   * paged decode attention: one wave per (sequence, KV head, context split);
+//                   the GQA group's query heads are the 16 columns of
+//                   S^T = K . Q^T (v_mfma_f32_16x16x32_bf16) and O^T = V^T . P^T
+//                   takes the S^T accumulator as its B operand with no lane
+//                   movement. The cache page layout is the MFMA fragment order
+//                   itself (kv_k_index / kv_v_index) -- 16 contiguous 1 KB loads
+//                   per 32-token page -- and splits are merged by a small
+//                   log-sum-exp reduction kernel.
+#include "kgs_common.h"
+
+namespace kgs {
+namespace dec {
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+constexpr int HD = 128;                // head_dim
+constexpr int PAGE = 32;               // tokens per KV-cache page
+constexpr int PAGE_ELEMS = PAGE * HD;  // per (page, kv head, K|V): 4096 bf16 = 8 KB
+
+// --- KV cache page layout (per page, per kv head: K region then V region) ---
+// K (token tau, dim d): S^T = K.Q^T A-fragments, 16-token halves t, k-steps ks
+__host__ __device__ __forceinline__ int kv_k_index(int tau, int d) {
+  const int t = tau >> 4, r = tau & 15, ks = d >> 5, g = (d >> 3) & 3, j = d & 7;
+  return (((t * 4 + ks) * 64) + g * 16 + r) * 8 + j;
+}
+// V (token tau, dim d): O^T = V^T.P^T A-fragments, 16-dim tiles dt; the k
+// (token) order within a fragment is the order S^T's accumulator hands P over:
+// lane group g holds tokens {4g..4g+3} of half 0 then {16+4g..16+4g+3}.
+__host__ __device__ __forceinline__ int kv_v_index(int tau, int d) {
+  const int dt = d >> 4, m = d & 15, g = (tau >> 2) & 3, j = (tau & 3) + 4 * (tau >> 4);
+  return ((dt * 64) + g * 16 + m) * 8 + j;
+}
+
+__device__ __forceinline__ float wmax16(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  return fmaxf(v, __shfl_xor(v, 32, 64));
+}
+__device__ __forceinline__ float wsum16(float v) {
+  v += __shfl_xor(v, 16, 64);
+  return v + __shfl_xor(v, 32, 64);
+}
+
+// ---------------------------------------------------------------------------
+// skinny GEMM
+// ---------------------------------------------------------------------------
+// Workgroup = 4 waves = a strip of 64*R rows of W (wave w: 16-row tiles
+// (strip*4 + w)*R .. +R-1) x all Mp = 16*MT columns, over one K range.
+// x chunk per stage: KC k-steps of 32 x Mp rows, double buffered in LDS. The
+// next chunk's x loads are issued a whole chunk (16 k-steps, ~2 us of weight
+// streaming) before they are needed -- shorter distances stall on L2 latency
+// (measured: KC 4 at Mp 64 ran 1.4x slower); W fragments stream through a
+// register ring PF k-steps deep. Mp > 64 keeps KC 2 (VGPR-bound; the serving
+// engine routes those batches to hipBLASLt, profiles/decode_kernels.md).
+template <int MT>
+struct SkinnyCfg {
+  static constexpr int KC = MT >= 8 ? 2 : 16;       // k-steps per x chunk
+  static constexpr int CHUNK_SLOTS = KC * MT * 64;  // 16-B slots per chunk
+  static constexpr int LOADS = CHUNK_SLOTS / 256;   // per thread per chunk
+};
+
+template <int R, int MT>
+__global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void skinny(const bf16x8* __restrict__ wp, const unsigned short* __restrict__ x,
+                                                 unsigned short* __restrict__ y, float* __restrict__ ws,
+                                                 int* __restrict__ cnt, int M, int N, int K, long ldx, long ldy,
+                                                 int ksplit, int chunks_per_split) {
+  using C = SkinnyCfg<MT>;
+  constexpr int KC = C::KC;
+  constexpr int PF = KC < 8 ? KC : 8;  // W ring depth in k-steps (divides KC)
+  // the only __shared__ object (a second one can make hipcc drain vmcnt before
+  // every ds_read, cdna_hip_programming.md s5 trap 4a); the split-K "last
+  // arriver" flag reuses its first word after the main loop
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][C::CHUNK_SLOTS];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nstrip = N / (64 * R);
+  const int strip = blockIdx.x % nstrip, split = blockIdx.x / nstrip;
+  const int nkk = K / 32;
+  const int kk0 = split * chunks_per_split * KC;
+  const int nsteps = chunks_per_split * KC;  // k-steps (of 32) for this workgroup
+  const int nt0 = (strip * 4 + w) * R;       // first 16-row tile of this wave
+  const bf16x8* wrow[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) wrow[r] = wp + ((long)(nt0 + r) * nkk + kk0) * 64 + lane;
+
+  // x chunk staging: element e = tid + 256 i of the chunk, row-major over
+  // (row m, 16-B column q) so global reads are whole-row runs; the LDS position
+  // is the fragment slot ((kk*MT + ct)*64 + g*16 + r). Rows >= M re-read row
+  // M-1 (their output columns are never stored).
+  constexpr int QPR = KC * 4;  // 16-B columns per row per chunk
+  bf16x8 xstage[C::LOADS];
+  auto load_x = [&](int chunk) {
+#pragma unroll
+    for (int i = 0; i < C::LOADS; ++i) {
+      const int e = tid + 256 * i, m = e / QPR, q = e - m * QPR;
+      const int mr = m < M ? m : M - 1;
+      xstage[i] = *(const bf16x8*)(x + (long)mr * ldx + (long)(kk0 + chunk * KC) * 32 + 8 * q);
+    }
+  };
+  auto store_x = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < C::LOADS; ++i) {
+      const int e = tid + 256 * i, m = e / QPR, q = e - m * QPR;
+      const int kk = q >> 2, g = q & 3, ct = m >> 4, r = m & 15;
+      xs[buf][(kk * MT + ct) * 64 + g * 16 + r] = xstage[i];
+    }
+  };
+
+  f32x4v acc[R][MT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int c = 0; c < MT; ++c) acc[r][c] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  // Every load below is unconditional (indices clamped to the last step /
+  // chunk: a few redundant L2-hit reloads at the tail) so hipcc can count
+  // vmcnt through the loop instead of draining the ring before each MFMA.
+  bf16x8 wf[PF][R];
+#pragma unroll
+  for (int p = 0; p < PF; ++p)
+#pragma unroll
+    for (int r = 0; r < R; ++r) wf[p][r] = __builtin_nontemporal_load(wrow[r] + (long)min(p, nsteps - 1) * 64);
+
+  load_x(0);
+  store_x(0);
+  __syncthreads();
+  const int nchunks = chunks_per_split;
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    load_x(min(chunk + 1, nchunks - 1));
+    const bf16x8* xb = xs[chunk & 1] + lane;
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      const int p = kk % PF;
+#pragma unroll
+      for (int c = 0; c < MT; ++c) {
+        const bf16x8 bfrag = xb[(kk * MT + c) * 64];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[p][r], bfrag, acc[r][c], 0, 0, 0);
+      }
+      const long sn = min(chunk * KC + kk + PF, nsteps - 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) wf[p][r] = __builtin_nontemporal_load(wrow[r] + sn * 64);
+    }
+    store_x((chunk + 1) & 1);
+    __syncthreads();
+  }
+
+  // C^T tile (r, c): lane holds column m = 16c + (lane & 15), rows n = 16*(nt0+r) + 4*(lane>>4) + i
+  const int g = lane >> 4, mc = lane & 15;
+  if (ksplit == 1) {
+#pragma unroll
+    for (int c = 0; c < MT; ++c) {
+      const int m = 16 * c + mc;
+      if (m < M) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int n = 16 * (nt0 + r) + 4 * g;
+          uint2 pk;
+          pk.x = pack_bf16x2(acc[r][c][0], acc[r][c][1]);
+          pk.y = pack_bf16x2(acc[r][c][2], acc[r][c][3]);
+          *(uint2*)(y + (long)m * ldy + n) = pk;
+        }
+      }
+    }
+    return;
+  }
+  // split-K: fp32 slabs ws[split][m][n]; the last arriver of the strip reduces.
+  // Publish = plain stores, vmcnt(0), barrier, agent-scope release, ticket
+  // (cdna_hip_programming.md s5 "In-launch split-K reduction").
+  const long mstride = N, sstride = (long)16 * MT * N;
+#pragma unroll
+  for (int c = 0; c < MT; ++c) {
+    const int m = 16 * c + mc;
+    if (m < M) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int n = 16 * (nt0 + r) + 4 * g;
+        *(f32x4v*)(ws + split * sstride + m * mstride + n) = acc[r][c];
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = (int*)&xs[0][0];
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(cnt + strip, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == ksplit - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      cnt[strip] = 0;  // re-arm the ticket for the next (stream-ordered) call
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return;
+#pragma unroll
+  for (int c = 0; c < MT; ++c) {
+    const int m = 16 * c + mc;
+    if (m < M) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int n = 16 * (nt0 + r) + 4 * g;
+        f32x4v t = f32x4v{0.f, 0.f, 0.f, 0.f};
+        for (int sp = 0; sp < ksplit; ++sp) t += *(const f32x4v*)(ws + sp * sstride + m * mstride + n);
+        uint2 pk;
+        pk.x = pack_bf16x2(t[0], t[1]);
+        pk.y = pack_bf16x2(t[2], t[3]);
+        *(uint2*)(y + (long)m * ldy + n) = pk;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// RoPE + KV-cache write
+// ---------------------------------------------------------------------------
+// qkv row t: [H q heads | HKV k heads | HKV v heads] x 128. Thread = (token,
+// head among H + 2 HKV, chunk c < 8): q/k heads rotate dims (8c.., 64+8c..) in
+// place; k and v heads are also written into page slot[t] (skipped when < 0).
+__global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ qkv, const float* __restrict__ cosv,
+                                                  const float* __restrict__ sinv, const int* __restrict__ pos,
+                                                  const int* __restrict__ slot, unsigned short* __restrict__ cache,
+                                                  long tokens, int H, int HKV, long ld) {
+  const int nh = H + 2 * HKV;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= tokens * nh * 8) return;
+  const long t = idx / (nh * 8);
+  const int rem = (int)(idx - t * nh * 8);
+  const int h = rem >> 3, c = rem & 7;
+  unsigned short* base = qkv + t * ld + (long)h * HD + 8 * c;
+  bf16x8* p1 = (bf16x8*)base;
+  bf16x8* p2 = (bf16x8*)(base + HD / 2);
+  bf16x8 a = *p1, b = *p2;
+  if (h < H + HKV) {
+    const int p = pos[t];
+    const f32x4* cp = (const f32x4*)(cosv + (long)p * (HD / 2) + 8 * c);
+    const f32x4* sp = (const f32x4*)(sinv + (long)p * (HD / 2) + 8 * c);
+    const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+    bf16x8 o1, o2;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float cs = e < 4 ? c0[e] : c1[e - 4];
+      const float sn = e < 4 ? s0[e] : s1[e - 4];
+      const float x1 = bf2f((unsigned short)a[e]), x2 = bf2f((unsigned short)b[e]);
+      o1[e] = (short)f2bf(x1 * cs - x2 * sn);
+      o2[e] = (short)f2bf(x2 * cs + x1 * sn);
+    }
+    *p1 = o1;
+    *p2 = o2;
+    a = o1;
+    b = o2;
+  }
+  if (h < H) return;
+  const int sl = slot[t];
+  if (sl < 0) return;
+  const int page = sl / PAGE, tau = sl - page * PAGE;
+  const bool isv = h >= H + HKV;
+  const int kvh = isv ? h - H - HKV : h - H;
+  unsigned short* pg = cache + (((long)page * HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
+  const int d1 = 8 * c, d2 = HD / 2 + 8 * c;
+  if (!isv) {
+    *(bf16x8*)(pg + kv_k_index(tau, d1)) = a;
+    *(bf16x8*)(pg + kv_k_index(tau, d2)) = b;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pg[kv_v_index(tau, d1 + e)] = (unsigned short)a[e];
+      pg[kv_v_index(tau, d2 + e)] = (unsigned short)b[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// paged decode attention
+// ---------------------------------------------------------------------------
+struct AttnArgs {
+  const unsigned short* q;      // [B, ldq]: head h at q + h*128
+  const unsigned short* cache;  // layer base: [pages][HKV][2][4096]
+  const int* block_tables;      // [B, max_pages]
+  const int* ctx_lens;          // [B] tokens in the cache (incl. the new one)
+  unsigned short* o;            // [B, ldo]
+  float* po;                    // [B, H, nsplit, 128] (nsplit > 1)
+  float* pml;                   // [B, H, nsplit, 2]
+  long ldq, ldo;
+  int B, H, HKV, max_pages, pages_per_split, nsplit;
+  float sl2;                    // scale * log2(e)
+};
+
+__global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
+  const int lane = threadIdx.x;
+  const int G = a.H / a.HKV;
+  int id = blockIdx.x;
+  const int sp = id % a.nsplit;
+  id /= a.nsplit;
+  const int kvh = id % a.HKV, b = id / a.HKV;
+  const int g = lane >> 4, n = lane & 15;
+  const int ctx = a.ctx_lens[b];
+  const int npages = (ctx + PAGE - 1) / PAGE;
+  const int p0 = sp * a.pages_per_split, p1 = min(npages, p0 + a.pages_per_split);
+  const int h = kvh * G + n;
+
+  float m = -INFINITY, lsum = 0.f;
+  f32x4v acc[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) acc[dt] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  if (p0 < p1) {
+    bf16x8 qf[4];
+    const unsigned short* qp = a.q + (long)b * a.ldq + (long)h * HD + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qp + 32 * ks) : bf16x8{};
+    const int* bt = a.block_tables + (long)b * a.max_pages;
+    for (int pi = p0; pi < p1; ++pi) {
+      const long pg = bt[pi];
+      const bf16x8* kp = (const bf16x8*)(a.cache + ((pg * a.HKV + kvh) * 2) * PAGE_ELEMS) + lane;
+      const bf16x8* vp = kp + PAGE_ELEMS / 8;
+      bf16x8 kf[8], vf[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kf[i] = __builtin_nontemporal_load(kp + 64 * i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(vp + 64 * i);
+      f32x4v s[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        s[t] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t * 4 + ks], qf[ks], s[t], 0, 0, 0);
+      }
+      // lane holds S^T[token 16t + 4g + i][head n]
+      const int tok0 = pi * PAGE + 4 * g;
+      float bm = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = (tok0 + 16 * t + i) < ctx ? s[t][i] * a.sl2 : -INFINITY;
+          s[t][i] = v;
+          bm = fmaxf(bm, v);
+        }
+      bm = wmax16(bm);
+      const float mn = fmaxf(m, bm);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      bf16x8 pf;
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = __builtin_amdgcn_exp2f(s[t][i] - mn);
+          ps += p;
+          pf[4 * t + i] = (short)f2bf(p);
+        }
+      lsum = lsum * alpha + ps;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) {
+        acc[dt] *= alpha;
+        acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, acc[dt], 0, 0, 0);
+      }
+    }
+  }
+  lsum = wsum16(lsum);
+  if (n >= G) return;
+  // lane holds O^T[dim 16dt + 4g + i][head n]
+  if (a.nsplit == 1) {
+    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+    unsigned short* op = a.o + (long)b * a.ldo + (long)h * HD + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) {
+      uint2 pk;
+      pk.x = pack_bf16x2(acc[dt][0] * inv, acc[dt][1] * inv);
+      pk.y = pack_bf16x2(acc[dt][2] * inv, acc[dt][3] * inv);
+      *(uint2*)(op + 16 * dt) = pk;
+    }
+    return;
+  }
+  const long row = ((long)b * a.H + h) * a.nsplit + sp;
+  float* po = a.po + row * HD + 4 * g;
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) *(f32x4v*)(po + 16 * dt) = acc[dt];
+  if (g == 0) {
+    a.pml[row * 2] = m;
+    a.pml[row * 2 + 1] = lsum;
+  }
+}
+
+// merge nsplit partials (m in log2 units, l, unnormalised O) of one (b, h)
+__global__ __launch_bounds__(64) void paged_reduce(const float* __restrict__ po, const float* __restrict__ pml,
+                                                   unsigned short* __restrict__ o, int H, int nsplit, long ldo) {
+  const int bh = blockIdx.x, lane = threadIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const float* ml = pml + (long)bh * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+  const float* pb = po + (long)bh * nsplit * HD + 2 * lane;
+  for (int s = 0; s < nsplit; ++s) {
+    const float l = ml[2 * s + 1];
+    if (l <= 0.f) continue;
+    const float f = __builtin_amdgcn_exp2f(ml[2 * s] - M);
+    L += f * l;
+    const float2 v = *(const float2*)(pb + (long)s * HD);
+    o0 += f * v.x;
+    o1 += f * v.y;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  *(unsigned*)(o + (long)b * ldo + (long)h * HD + 2 * lane) = pack_bf16x2(o0 * inv, o1 * inv);
+}
+
+}  // namespace dec
+}  // namespace kgs
+
+namespace {
+inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+template <int R, int MT>
+hipError_t launch_skinny(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx,
+                         long ldy, int ksplit, int cps, hipStream_t s) {
+  const int nstrip = N / (64 * R);
+  hipLaunchKernelGGL((kgs::dec::skinny<R, MT>), dim3(nstrip * ksplit), dim3(256), 0, s, (const bf16x8*)wp,
+                     (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps);
+  return hipGetLastError();
+}
+}  // namespace
+
+// Rows of W per workgroup strip, k elements per x chunk and padded batch for a
+// batch of M rows: lets the host size split-K and the workspace (kgs/ops/decode.py).
+KGS_EXPORT int kgs_skinny_geometry(int M, int* rows_per_strip, int* k_per_chunk, int* mpad) {
+  if (M <= 0 || M > 256) return KGS_ERR_SHAPE;
+  const int mt = M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  *mpad = 16 * mt;
+  *rows_per_strip = 64 * (mt >= 8 ? 2 : 1);
+  *k_per_chunk = 32 * (mt >= 8 ? 2 : 16);
+  return 0;
+}
+
+// y[M, N] (bf16, row stride ldy) = x[M, K] (row stride ldx) . W^T with W
+// prepacked ([N/16][K/32][64][8] bf16). ksplit must divide K / k_per_chunk;
+// with ksplit > 1, ws holds ksplit * mpad * N floats and cnt N / rows_per_strip
+// zero-initialised ints (left zeroed on return).
+KGS_EXPORT int kgs_skinny_gemm_bf16(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K,
+                                   long ldx, long ldy, int ksplit, hipStream_t s) {
+  int rps, kpc, mpad;
+  if (kgs_skinny_geometry(M, &rps, &kpc, &mpad)) return KGS_ERR_SHAPE;
+  if (N <= 0 || K <= 0 || N % rps || K % kpc || ldx < K || ldy < N) return KGS_ERR_SHAPE;
+  const int nchunks = K / kpc;
+  if (ksplit <= 0 || nchunks % ksplit) return KGS_ERR_ARG;
+  if (ksplit > 1 && (ws == nullptr || cnt == nullptr)) return KGS_ERR_ARG;
+  if (!al16(wp) || !al16(x) || ((uintptr_t)y & 7) || ((uintptr_t)ws & 15) || ldx % 8 || ldy % 4) return KGS_ERR_ALIGN;
+  const int cps = nchunks / ksplit;
+  switch (mpad / 16) {
+    case 1: return (int)launch_skinny<1, 1>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
+    case 2: return (int)launch_skinny<1, 2>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
+    case 4: return (int)launch_skinny<1, 4>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
+    case 8: return (int)launch_skinny<2, 8>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
+    case 16: return (int)launch_skinny<2, 16>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
+    default: return KGS_ERR_SHAPE;
+  }
+}
+
+// qkv: [tokens, ld] fused projection rows (H q heads, HKV k heads, HKV v heads
+// of 128); pos/slot: int32 [tokens]; cache: this layer's pages
+// [pages][HKV][2][4096] bf16. q and k are rotated in place; k, v land in the cache.
+KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* sinv, const int* pos, const int* slot,
+                                  void* cache, long tokens, int H, int HKV, int hd, long ld, hipStream_t s) {
+  if (tokens < 0 || H <= 0 || HKV <= 0 || H % HKV || hd != kgs::dec::HD) return KGS_ERR_SHAPE;
+  if (ld < (long)(H + 2 * HKV) * hd) return KGS_ERR_SHAPE;
+  if (!al16(qkv) || !al16(cosv) || !al16(sinv) || !al16(cache) || ld % 8) return KGS_ERR_ALIGN;
+  const long n = tokens * (H + 2 * HKV) * 8;
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(kgs::dec::rope_cache, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (unsigned short*)qkv,
+                     cosv, sinv, pos, slot, (unsigned short*)cache, tokens, H, HKV, ld);
+  return (int)hipGetLastError();
+}
+
+// Paged decode attention for one new query token per sequence. q: [B, ldq]
+// (query heads at 128-element blocks); cache: layer base; block_tables
+// [B, max_pages] int32; ctx_lens [B] int32 (>= 1). nsplit > 1 needs po
+// (B*H*nsplit*128 f32) and pml (B*H*nsplit*2 f32) and adds a reduce launch.
+KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int* block_tables, const int* ctx_lens,
+                                    void* o, float* po, float* pml, int B, int H, int HKV, int hd, int max_pages,
+                                    int pages_per_split, int nsplit, long ldq, long ldo, float scale, hipStream_t s) {
+  using namespace kgs::dec;
+  if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 16 || hd != HD) return KGS_ERR_SHAPE;
+  if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0) return KGS_ERR_SHAPE;
+  if ((long)pages_per_split * nsplit < max_pages) return KGS_ERR_ARG;
+  if (ldq < (long)H * HD || ldo < (long)H * HD) return KGS_ERR_SHAPE;
+  if (!al16(q) || !al16(cache) || !al16(o) || ldq % 8 || ldo % 8) return KGS_ERR_ALIGN;
+  if (nsplit > 1 && (po == nullptr || pml == nullptr || !al16(po))) return KGS_ERR_ARG;
+  const long nwg = (long)B * HKV * nsplit;
+  if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
+  AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
+             pml, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, scale * 1.4426950408889634f};
+  hipLaunchKernelGGL(paged_decode, dim3((unsigned)nwg), dim3(64), 0, s, a);
+  if (nsplit > 1)
+    hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
+                       ldo);
+  return (int)hipGetLastError();
+}

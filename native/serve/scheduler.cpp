@@ -1,0 +1,224 @@
+// kgs.serve native scheduler: see scheduler.h for the model.
+#include "scheduler.h"
+
+#include <algorithm>
+#include <sstream>
+
+namespace kgs {
+namespace serve {
+
+BlockAllocator::BlockAllocator(int num_pages) : num_pages_(num_pages), state_(num_pages > 0 ? num_pages : 0, 0) {
+  // page 0 is the null page: never handed out
+  if (num_pages_ > 0) state_[0] = 1;
+  free_.reserve(num_pages_);
+  for (int p = num_pages_ - 1; p >= 1; --p) free_.push_back(p);
+}
+
+int BlockAllocator::alloc() {
+  if (free_.empty()) return -1;
+  const int p = free_.back();
+  free_.pop_back();
+  state_[p] = 1;
+  return p;
+}
+
+void BlockAllocator::free(int page) {
+  if (page <= 0 || page >= num_pages_ || state_[page] == 0) return;  // double free / null page: ignore
+  state_[page] = 0;
+  free_.push_back(page);
+}
+
+Scheduler::Scheduler(const SchedulerConfig& cfg) : cfg_(cfg), alloc_(cfg.num_pages) {
+  // a (re-)prefill of any sequence up to max_model_len must fit one step
+  const int pad = std::max(1, cfg_.pad_multiple);
+  cfg_.pad_multiple = pad;
+  cfg_.max_prefill_tokens = std::max(cfg_.max_prefill_tokens, (cfg_.max_model_len + pad - 1) / pad * pad);
+}
+
+bool Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new_tokens) {
+  if (prompt.empty() || max_new_tokens < 1) return false;
+  if (seqs_.count(id)) return false;
+  const int total = (int)prompt.size() + max_new_tokens;
+  if ((int)prompt.size() >= cfg_.max_model_len || pages_for(std::min(total, cfg_.max_model_len)) > cfg_.num_pages - 1)
+    return false;
+  Sequence s;
+  s.id = id;
+  s.tokens = prompt;
+  s.prompt_len = (int)prompt.size();
+  s.max_new = max_new_tokens;
+  seqs_.emplace(id, std::move(s));
+  waiting_.push_back(id);
+  return true;
+}
+
+void Scheduler::free_pages(Sequence& s) {
+  for (int p : s.pages) alloc_.free(p);
+  s.pages.clear();
+  s.cached = 0;
+}
+
+bool Scheduler::abort(int64_t id) {
+  auto it = seqs_.find(id);
+  if (it == seqs_.end() || it->second.state == SeqState::kFinished) return false;
+  Sequence& s = it->second;
+  if (s.state == SeqState::kWaiting) {
+    waiting_.erase(std::remove(waiting_.begin(), waiting_.end(), id), waiting_.end());
+  } else {
+    running_.erase(std::remove(running_.begin(), running_.end(), id), running_.end());
+    free_pages(s);
+  }
+  s.state = SeqState::kFinished;
+  return true;
+}
+
+void Scheduler::preempt(Sequence& s, StepPlan& plan) {
+  free_pages(s);
+  s.state = SeqState::kWaiting;
+  s.preemptions++;
+  running_.erase(std::remove(running_.begin(), running_.end(), s.id), running_.end());
+  waiting_.push_front(s.id);
+  plan.preempted.push_back(s.id);
+}
+
+bool Scheduler::try_prefill(StepPlan& plan) {
+  const int ps = cfg_.page_size, pad = cfg_.pad_multiple;
+  // keep ~1% of the cache free after admission so running sequences can grow
+  const int watermark = std::max(1, (cfg_.num_pages - 1) / 100);
+  int budget = cfg_.max_prefill_tokens;
+  while (!waiting_.empty() && (int)running_.size() < cfg_.max_batch) {
+    Sequence& s = seqs_.at(waiting_.front());
+    const int len = (int)s.tokens.size();
+    const int padded = (len + pad - 1) / pad * pad;
+    const int need = pages_for(len + 1);
+    if (padded > budget) break;
+    if (alloc_.num_free() - need < (running_.empty() && plan.seq_ids.empty() ? 0 : watermark)) break;
+    waiting_.pop_front();
+    budget -= padded;
+    for (int i = 0; i < need; ++i) s.pages.push_back(alloc_.alloc());
+    const int start = (int)plan.tokens.size();
+    plan.seq_ids.push_back(s.id);
+    plan.seq_starts.push_back(start);
+    plan.seq_lens.push_back(len);
+    plan.padded_lens.push_back(padded);
+    for (int t = 0; t < padded; ++t) {
+      const bool real = t < len;
+      plan.tokens.push_back(real ? s.tokens[t] : 0);
+      plan.positions.push_back(t);
+      plan.slots.push_back(real ? s.pages[t / ps] * ps + t % ps : -1);
+    }
+    s.cached = len;
+    s.state = SeqState::kRunning;
+    s.arrival = next_arrival_++;
+    running_.push_back(s.id);
+  }
+  if (plan.seq_ids.empty()) return false;
+  plan.kind = 1;
+  return true;
+}
+
+void Scheduler::build_decode(StepPlan& plan) {
+  const int ps = cfg_.page_size;
+  // make sure every running sequence has a slot for one more token, preempting
+  // the newest sequences when the cache is full (oldest keep making progress)
+  for (size_t i = 0; i < running_.size();) {
+    Sequence& s = seqs_.at(running_[i]);
+    if (pages_for(s.cached + 1) <= (int)s.pages.size()) {
+      ++i;
+      continue;
+    }
+    int p = alloc_.alloc();
+    while (p < 0) {
+      Sequence& victim = seqs_.at(running_.back());
+      const bool self = victim.id == s.id;
+      preempt(victim, plan);
+      if (self) break;
+      p = alloc_.alloc();
+    }
+    if (p < 0) continue;  // s itself was preempted (running_ shrank)
+    s.pages.push_back(p);
+    ++i;
+  }
+  if (running_.empty()) return;
+  plan.kind = 2;
+  int maxp = 0;
+  for (int64_t id : running_) maxp = std::max(maxp, (int)seqs_.at(id).pages.size());
+  plan.max_pages = maxp;
+  plan.block_tables.assign(running_.size() * (size_t)maxp, 0);
+  for (size_t i = 0; i < running_.size(); ++i) {
+    Sequence& s = seqs_.at(running_[i]);
+    const int pos = s.cached;
+    plan.seq_ids.push_back(s.id);
+    plan.tokens.push_back(s.tokens.back());
+    plan.positions.push_back(pos);
+    plan.slots.push_back(s.pages[pos / ps] * ps + pos % ps);
+    plan.ctx_lens.push_back(pos + 1);
+    std::copy(s.pages.begin(), s.pages.end(), plan.block_tables.begin() + i * maxp);
+    s.cached = pos + 1;
+  }
+}
+
+StepPlan Scheduler::schedule() {
+  StepPlan plan;
+  if (!waiting_.empty() && try_prefill(plan)) return plan;
+  build_decode(plan);
+  return plan;
+}
+
+std::vector<int64_t> Scheduler::update(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks,
+                                       const std::vector<uint8_t>& eos) {
+  std::vector<int64_t> done;
+  for (size_t i = 0; i < ids.size() && i < toks.size(); ++i) {
+    auto it = seqs_.find(ids[i]);
+    if (it == seqs_.end() || it->second.state != SeqState::kRunning) continue;  // aborted / preempted meanwhile
+    Sequence& s = it->second;
+    s.tokens.push_back(toks[i]);
+    s.generated++;
+    const bool stop = (i < eos.size() && eos[i]) || s.generated >= s.max_new ||
+                      (int)s.tokens.size() >= cfg_.max_model_len;
+    if (stop) {
+      running_.erase(std::remove(running_.begin(), running_.end(), s.id), running_.end());
+      free_pages(s);
+      s.state = SeqState::kFinished;
+      done.push_back(s.id);
+    }
+  }
+  return done;
+}
+
+const Sequence* Scheduler::get(int64_t id) const {
+  auto it = seqs_.find(id);
+  return it == seqs_.end() ? nullptr : &it->second;
+}
+
+void Scheduler::release(int64_t id) {
+  auto it = seqs_.find(id);
+  if (it != seqs_.end() && it->second.state == SeqState::kFinished) seqs_.erase(it);
+}
+
+std::string Scheduler::check_invariants() const {
+  std::ostringstream err;
+  std::vector<int> owner(cfg_.num_pages, 0);
+  for (const auto& kv : seqs_) {
+    const Sequence& s = kv.second;
+    if (s.state != SeqState::kRunning && !s.pages.empty()) err << "seq " << s.id << " not running but holds pages; ";
+    if (s.state == SeqState::kRunning && pages_for(s.cached) > (int)s.pages.size())
+      err << "seq " << s.id << " cached " << s.cached << " beyond its pages; ";
+    for (int p : s.pages) {
+      if (p <= 0 || p >= cfg_.num_pages) err << "seq " << s.id << " holds bad page " << p << "; ";
+      else if (owner[p]++) err << "page " << p << " shared; ";
+      if (alloc_.is_free(p)) err << "page " << p << " both free and owned; ";
+    }
+  }
+  int owned = 0;
+  for (int c : owner) owned += c;
+  if (owned + alloc_.num_free() != cfg_.num_pages - 1) err << "page leak: owned " << owned << " free " << alloc_.num_free() << "; ";
+  if ((int)running_.size() > cfg_.max_batch) err << "running over max_batch; ";
+  for (int64_t id : running_)
+    if (seqs_.at(id).state != SeqState::kRunning) err << "running list has non-running " << id << "; ";
+  for (int64_t id : waiting_)
+    if (seqs_.at(id).state != SeqState::kWaiting) err << "waiting list has non-waiting " << id << "; ";
+  return err.str();
+}
+
+}  // namespace serve
+}  // namespace kgs

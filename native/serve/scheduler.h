@@ -1,0 +1,114 @@
+// Continuous-batching scheduler + paged-KV block allocator for kgs.serve (the
+// native runtime behind the Llama serving stand-in of BASELINE config 5).
+//
+// The model runner (kgs/serve/engine.py) asks for one step at a time:
+//   * PREFILL: admitted waiting sequences, each padded to a multiple of
+//     `pad_multiple` tokens (the flash-attention prefill kernel's q-block), with
+//     per-token positions and KV-cache slots (-1 for padding rows);
+//   * DECODE: every running sequence's last token, its position, the slot the
+//     new k/v goes to, its block table and context length.
+// Pages are PAGE_SIZE tokens; page 0 is reserved as the null page that padded
+// decode rows point at (never handed out). When a decode step cannot get a new
+// page, the most recently admitted running sequence is preempted: its pages are
+// freed and it goes back to the front of the waiting queue with its generated
+// tokens appended to the prompt (recompute on re-admission).
+#pragma once
+
+#include <cstdint>
+#include <deque>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace kgs {
+namespace serve {
+
+class BlockAllocator {
+ public:
+  explicit BlockAllocator(int num_pages);
+  int alloc();                   // -1 when exhausted
+  void free(int page);
+  int num_free() const { return (int)free_.size(); }
+  int num_pages() const { return num_pages_; }
+  bool is_free(int page) const { return page > 0 && page < num_pages_ && state_[page] == 0; }
+
+ private:
+  int num_pages_;
+  std::vector<int> free_;      // LIFO stack (recently freed pages are reused first: warm in L2/MALL)
+  std::vector<uint8_t> state_; // 0 free, 1 in use
+};
+
+enum class SeqState : int { kWaiting = 0, kRunning = 1, kFinished = 2 };
+
+struct Sequence {
+  int64_t id = 0;
+  std::vector<int32_t> tokens;  // prompt + generated
+  int prompt_len = 0;
+  int max_new = 0;
+  int generated = 0;
+  int64_t arrival = 0;          // admission order (preemption picks the newest)
+  std::vector<int32_t> pages;
+  int cached = 0;               // tokens whose k/v are in the cache
+  SeqState state = SeqState::kWaiting;
+  int preemptions = 0;
+};
+
+struct StepPlan {
+  int kind = 0;  // 0 idle, 1 prefill, 2 decode
+  std::vector<int64_t> seq_ids;
+  // prefill (flattened over sequences, each padded to pad_multiple)
+  std::vector<int32_t> tokens, positions, slots;
+  std::vector<int32_t> seq_starts, seq_lens, padded_lens;
+  // decode
+  std::vector<int32_t> block_tables;  // [B, max_pages]
+  std::vector<int32_t> ctx_lens;
+  int max_pages = 0;
+  std::vector<int64_t> preempted;
+};
+
+struct SchedulerConfig {
+  int num_pages = 1024;
+  int page_size = 32;
+  int max_batch = 256;            // decode sequences per step
+  int max_prefill_tokens = 16384; // padded tokens per prefill step
+  int max_model_len = 8192;
+  int pad_multiple = 128;
+};
+
+class Scheduler {
+ public:
+  explicit Scheduler(const SchedulerConfig& cfg);
+  // returns false if the request can never fit (prompt + max_new > max_model_len
+  // or more pages than the cache has)
+  bool add(int64_t id, const std::vector<int32_t>& prompt, int max_new_tokens);
+  bool abort(int64_t id);
+  StepPlan schedule();
+  // one sampled token per sequence of the last plan (same order); eos[i] != 0
+  // finishes sequence i early. Returns the ids that finished.
+  std::vector<int64_t> update(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks,
+                              const std::vector<uint8_t>& eos);
+  const Sequence* get(int64_t id) const;
+  void release(int64_t id);  // drop a finished sequence's record
+  int num_waiting() const { return (int)waiting_.size(); }
+  int num_running() const { return (int)running_.size(); }
+  int num_free_pages() const { return alloc_.num_free(); }
+  const SchedulerConfig& config() const { return cfg_; }
+  std::string check_invariants() const;  // "" when consistent (tests)
+
+ private:
+  int pages_for(int tokens) const { return (tokens + cfg_.page_size - 1) / cfg_.page_size; }
+  bool try_prefill(StepPlan& plan);
+  void build_decode(StepPlan& plan);
+  void preempt(Sequence& s, StepPlan& plan);
+  void free_pages(Sequence& s);
+
+  SchedulerConfig cfg_;
+  BlockAllocator alloc_;
+  std::unordered_map<int64_t, Sequence> seqs_;
+  std::deque<int64_t> waiting_;
+  std::vector<int64_t> running_;  // admission order
+  int64_t next_arrival_ = 0;
+};
+
+}  // namespace serve
+}  // namespace kgs

@@ -1,0 +1,232 @@
+"""kgs.serve on CPU: the native scheduler's bookkeeping (admission, paging,
+preemption, invariants under random traffic) and the engine's paged-KV
+generation through the plain-PyTorch reference backend, checked token by token
+against a full-recompute forward of the same weights."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+_serve = pytest.importorskip("kgs._native._serve")
+
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+
+def _sched(num_pages=64, max_batch=8, max_model_len=512, max_prefill=1024):
+    c = _serve.SchedulerConfig()
+    c.num_pages, c.page_size, c.max_batch = num_pages, 32, max_batch
+    c.max_prefill_tokens, c.max_model_len, c.pad_multiple = max_prefill, max_model_len, 128
+    return _serve.Scheduler(c)
+
+
+def test_allocator_reserves_null_page():
+    a = _serve.BlockAllocator(4)
+    got = {a.alloc() for _ in range(3)}
+    assert got == {1, 2, 3} and a.alloc() == -1
+    a.free(0)  # the null page is never freed into the pool
+    a.free(2)
+    a.free(2)  # double free ignored
+    assert a.num_free == 1 and a.alloc() == 2
+
+
+def test_prefill_then_decode_plan():
+    s = _sched()
+    assert s.add(10, np.arange(1, 41, dtype=np.int32), 5)
+    assert s.add(11, np.arange(1, 71, dtype=np.int32), 5)
+    p = s.schedule()
+    assert p.kind == 1 and list(p.seq_ids) == [10, 11]
+    assert list(p.seq_lens) == [40, 70] and list(p.padded_lens) == [128, 128]
+    assert list(p.seq_starts) == [0, 128]
+    slots = p.slots
+    assert (slots[40:128] == -1).all() and (slots[128 + 70:] == -1).all()
+    real = np.concatenate([slots[:40], slots[128:198]])
+    assert len(set(real.tolist())) == 110 and (real >= 32).all()  # page 0 never used
+    s.update(p.seq_ids, np.array([7, 8], np.int32), np.zeros(2, np.uint8))
+    d = s.schedule()
+    assert d.kind == 2 and list(d.tokens) == [7, 8]
+    assert list(d.positions) == [40, 70] and list(d.ctx_lens) == [41, 71]
+    bt = d.block_tables
+    assert bt.shape == (2, d.max_pages)
+    for row, slot, pos in zip(bt, d.slots, d.positions):
+        assert slot == row[pos // 32] * 32 + pos % 32
+    assert s.check_invariants() == ""
+
+
+def test_finish_frees_pages():
+    s = _sched(num_pages=16)
+    free0 = s.num_free_pages
+    s.add(1, np.ones(33, np.int32), 2)
+    p = s.schedule()
+    s.update(p.seq_ids, np.array([3], np.int32), np.zeros(1, np.uint8))
+    p = s.schedule()
+    done = s.update(p.seq_ids, np.array([4], np.int32), np.zeros(1, np.uint8))
+    assert list(done) == [1] and s.num_free_pages == free0
+    assert list(s.tokens(1)[-2:]) == [3, 4]
+    s.release(1)
+    with pytest.raises(KeyError):
+        s.tokens(1)
+
+
+def test_eos_and_abort():
+    s = _sched()
+    s.add(1, np.ones(5, np.int32), 100)
+    s.add(2, np.ones(5, np.int32), 100)
+    p = s.schedule()
+    done = s.update(p.seq_ids, np.array([9, 9], np.int32), np.array([1, 0], np.uint8))
+    assert list(done) == [1]
+    assert s.abort(2) and not s.abort(2)
+    assert s.num_running == 0 and s.check_invariants() == ""
+
+
+def test_rejects_impossible_requests():
+    s = _sched(num_pages=4, max_model_len=512)
+    assert not s.add(1, np.ones(600, np.int32), 1)      # longer than max_model_len
+    assert not s.add(2, np.ones(200, np.int32), 10)     # needs more pages than the cache has
+    assert not s.add(3, np.zeros(0, np.int32), 1)
+    assert s.add(4, np.ones(10, np.int32), 1) and not s.add(4, np.ones(10, np.int32), 1)  # duplicate id
+
+
+def test_preemption_recomputes_newest():
+    # 7 usable pages: two sequences of 3 pages each (+1% watermark), both growing past a page boundary
+    s = _sched(num_pages=8, max_model_len=512)
+    assert s.add(1, np.ones(64, np.int32), 120)
+    assert s.add(2, np.ones(64, np.int32), 120)
+    p = s.schedule()
+    assert p.kind == 1 and len(p.seq_ids) == 2
+    tok = 5
+    preempted = []
+    for _ in range(400):
+        s.update(p.seq_ids, np.full(len(p.seq_ids), tok, np.int32), np.zeros(len(p.seq_ids), np.uint8))
+        p = s.schedule()
+        preempted += list(p.preempted)
+        assert s.check_invariants() == ""
+        if p.kind == 0:
+            break
+    assert 2 in preempted  # the newest admitted sequence yields its pages
+    assert s.info(2)["preemptions"] >= 1
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.integers(1, 300), st.integers(1, 60), st.booleans()), min_size=1, max_size=25),
+       st.integers(8, 40), st.integers(1, 6))
+def test_random_traffic_invariants(reqs, pages, max_batch):
+    s = _sched(num_pages=pages, max_batch=max_batch, max_model_len=512)
+    live = set()
+    for i, (plen, new, _) in enumerate(reqs):
+        if s.add(i, np.full(plen, 3, np.int32), new):
+            live.add(i)
+    rng = np.random.default_rng(0)
+    for _ in range(2000):
+        p = s.schedule()
+        assert s.check_invariants() == "", s.check_invariants()
+        if p.kind == 0:
+            break
+        n = len(p.seq_ids)
+        eos = (rng.random(n) < 0.05).astype(np.uint8)
+        for d in s.update(p.seq_ids, np.full(n, 4, np.int32), eos):
+            live.discard(int(d))
+        if p.kind == 2:
+            assert (p.ctx_lens == p.positions + 1).all()
+    assert not live and s.num_running == 0 and s.num_waiting == 0
+    assert s.num_free_pages == pages - 1
+
+
+# ---------------------------------------------------------------- engine (ref backend)
+
+def _tiny():
+    from kgs.models.llama import LlamaConfig
+
+    return LlamaConfig(hidden=256, intermediate=512, heads=2, kv_heads=1, layers=2, vocab=512)
+
+
+def _check_against_oracle(eng, prompts, outs):
+    oracle = eng.model.oracle
+    for prompt, req in zip(prompts, outs):
+        seq = list(prompt)
+        for tok in req.output:
+            logits = oracle.forward(torch.tensor([seq]))[0, -1].float()
+            # the engine's token is the oracle's argmax up to bf16 rounding noise
+            assert logits[tok] >= logits.max() - 2e-2 * logits.abs().max(), (len(seq), tok, int(logits.argmax()))
+            seq.append(tok)
+
+
+def test_engine_ref_matches_full_recompute():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=64, max_batch=4, max_model_len=512, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    rng = np.random.default_rng(1)
+    prompts = [rng.integers(3, 512, size=n).tolist() for n in (5, 33, 64, 100, 17)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    assert all(len(r.output) == 6 and r.finish_reason == "length" for r in outs)
+    assert eng.stats["prefill_steps"] >= 2 and eng.stats["decode_steps"] >= 5  # max_batch 4 < 5 prompts
+    _check_against_oracle(eng, prompts, outs)
+
+
+def test_engine_ref_preemption_is_transparent():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    # 5 usable pages for 3 sequences that grow across page boundaries: forces preemption + recompute
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=6, max_batch=3, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    rng = np.random.default_rng(2)
+    prompts = [rng.integers(3, 512, size=n).tolist() for n in (30, 28, 31)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=12, ignore_eos=True))
+    assert eng.stats["preemptions"] >= 1
+    _check_against_oracle(eng, prompts, outs)
+
+
+def test_engine_sampling_and_eos():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False,
+                                          eos_token_id=-1), device="cpu", backend="ref")
+    outs = eng.generate([[5, 6, 7], [8, 9]], [SamplingParams(max_tokens=4, temperature=1.0, top_k=5),
+                                              SamplingParams(max_tokens=3)])
+    assert len(outs[0].output) == 4 and len(outs[1].output) == 3
+    first = outs[1].output[0]
+    eng2 = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False,
+                                           eos_token_id=first), device="cpu", backend="ref")
+    r = eng2.generate([[8, 9]], SamplingParams(max_tokens=3))[0]
+    assert r.output == [first] and r.finish_reason == "stop"
+
+
+def test_http_api_completions_and_stream():
+    from fastapi.testclient import TestClient
+
+    from kgs.serve import EngineConfig, LLMEngine
+    from kgs.serve.api import ByteTokenizer, EngineLoop, create_app
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    runner = EngineLoop(eng)
+    try:
+        client = TestClient(create_app(runner, model_name="tiny"))
+        assert client.get("/health").json() == {"status": "ok"}
+        assert client.get("/v1/models").json()["data"][0]["id"] == "tiny"
+        r = client.post("/v1/completions", json={"prompt": "hello", "max_tokens": 5, "ignore_eos": True}).json()
+        ch = r["choices"][0]
+        assert len(ch["token_ids"]) == 5 and ch["finish_reason"] == "length"
+        assert r["usage"] == {"prompt_tokens": 6, "completion_tokens": 5, "total_tokens": 11}
+        # same prompt as token ids gives the same greedy continuation
+        r2 = client.post("/v1/completions", json={"prompt": ByteTokenizer().encode("hello"), "max_tokens": 5,
+                                                  "ignore_eos": True}).json()
+        assert r2["choices"][0]["token_ids"] == ch["token_ids"]
+        with client.stream("POST", "/v1/completions",
+                           json={"prompt": [5, 6, 7], "max_tokens": 4, "stream": True, "ignore_eos": True}) as s:
+            events = [ln for ln in s.iter_lines() if ln.startswith("data: ")]
+        assert events[-1] == "data: [DONE]" and len(events) == 5
+        bad = client.post("/v1/completions", json={"prompt": [3] * 300, "max_tokens": 4})
+        assert bad.status_code == 400
+        m = client.get("/metrics").text
+        assert "kgs_requests_total 3" in m and "kgs_requests_rejected_total 1" in m
+    finally:
+        runner.shutdown()
+
+
+def test_byte_tokenizer_roundtrip():
+    from kgs.serve.api import ByteTokenizer
+
+    t = ByteTokenizer()
+    ids = t.encode("héllo ✓")
+    assert ids[0] == t.BOS and t.decode(ids) == "héllo ✓"
