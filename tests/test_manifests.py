@@ -105,3 +105,19 @@ def test_smoke_pod():
     doc = _load("rocm-gpu-smoke-pod.yaml")
     assert doc == manifests.gpu_test_pod("localhost:5000/kgs-rocm-test:dev", gpus=1, name="gpu-rocm-smoke",
                                          command=["python3", "-m", "kgs.workload.entrypoint", "--smoke", "--pod"])
+
+
+def test_kgs_serve_pod():
+    doc = _load("kgs-serve-pod.yaml")
+    vllm = _load("vllm-rocm-pod.yaml")
+    ctr, vctr = doc["spec"]["containers"][0], vllm["spec"]["containers"][0]
+    assert ctr["command"] == ["python3", "-m", "kgs.serve", "serve"]
+    assert "--port=8000" in ctr["args"] and {"containerPort": 8000} in ctr["ports"]
+    # same layout as the vLLM pod it stands in for
+    for key in ("resources", "volumeMounts", "securityContext"):
+        assert ctr[key] == vctr[key]
+    for key in ("nodeSelector", "tolerations", "volumes", "restartPolicy"):
+        assert doc["spec"][key] == vllm["spec"][key]
+    from kgs.serve.api import main  # the entrypoint the pod runs exists
+
+    assert callable(main)
