@@ -82,6 +82,49 @@ def bench_gemm(iters, ms, ring_bytes=3 << 30):
         torch.cuda.empty_cache()
 
 
+def tune_gemm(iters, ms, ring_bytes=2 << 30):
+    """Time every (variant, split-K) of the skinny GEMM per Llama shape and batch
+    bucket with HBM-streamed weights; print the best and a TUNED table."""
+    from kgs.ops.decode import PackedWeight, _mt, skinny_gemm, skinny_geometry, skinny_variants
+
+    table = {}
+    for name, (n, k) in SHAPES.items():
+        copies = max(2, min(32, ring_bytes // (n * k * 2)))
+        ws = [(torch.randn(n, k, device="cuda") * k ** -0.5).to(torch.bfloat16) for _ in range(copies)]
+        pws = [PackedWeight(w) for w in ws]
+        for m in ms:
+            x = (torch.rand(m, k, device="cuda") * 2 - 1).to(torch.bfloat16)
+            out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            it = {"i": 0}
+
+            def torch_call():
+                it["i"] = (it["i"] + 1) % copies
+                torch.matmul(x, ws[it["i"]].T, out=out)
+
+            t_t = _time(torch_call, iters)
+            res = {}
+            for v in skinny_variants(m):
+                rps, kpc, mpad = skinny_geometry(m, v)
+                if n % rps or k % kpc:
+                    continue
+                nch, nstrip = k // kpc, n // rps
+                for ks in [d for d in range(1, nch + 1) if nch % d == 0 and nstrip * d <= 2048 and
+                           (d == 1 or d * mpad * n * 4 <= (64 << 20))]:
+                    def call(v=v, ks=ks):
+                        it["i"] = (it["i"] + 1) % copies
+                        skinny_gemm(x, pws[it["i"]], out=out, ksplit=ks, variant=v)
+                    res[(v, ks)] = _time(call, iters)
+            (bv, bks), bt = min(res.items(), key=lambda kv: kv[1])
+            table[(_mt(m), n, k)] = (bv, bks)
+            print(json.dumps({"op": "skinny_tune", "shape": name, "m": m, "n": n, "k": k, "best_variant": bv,
+                              "best_ksplit": bks, "us": round(bt, 2), "tbps": round(n * k * 2 / bt / 1e6, 2),
+                              "torch_us": round(t_t, 2), "speedup": round(t_t / bt, 3),
+                              "all": {f"{v}/{ks}": round(t, 1) for (v, ks), t in sorted(res.items())}}), flush=True)
+        del ws, pws
+        torch.cuda.empty_cache()
+    print("TUNED = " + repr(table), flush=True)
+
+
 def bench_attn(iters):
     from kgs.ops.decode import PagedKVCache, decode_splits, paged_decode_attention
 
@@ -111,9 +154,13 @@ def main(argv=None) -> int:
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--ms", default="1,16,32,64,128,256")
     ap.add_argument("--sweep", action="store_true", help="time every valid split-K factor")
+    ap.add_argument("--tune", action="store_true", help="time every tile variant x split-K; print a TUNED table")
     a = ap.parse_args(argv)
     global SWEEP
     SWEEP = a.sweep
+    if a.tune:
+        tune_gemm(a.iters, [int(v) for v in a.ms.split(",")])
+        return 0
     both = not (a.gemm or a.attn)
     if a.gemm or both:
         bench_gemm(a.iters, [int(v) for v in a.ms.split(",")])

@@ -48,33 +48,100 @@ def unpack_weight(p: torch.Tensor) -> torch.Tensor:
     return p.reshape(nt, kk, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, kk * 32)
 
 
+def pack_swiglu(w: torch.Tensor) -> torch.Tensor:
+    """Fused gate|up weight ``[2I, K]`` (gate rows first) -> packed fragments whose
+    16-row tile ``t`` holds gate rows ``8t..8t+7`` then up rows ``8t..8t+7``: the
+    skinny GEMM's SwiGLU epilogue pairs them lane-to-lane (``lane ^ 32``)."""
+    n2, k = w.shape
+    if n2 % 32:
+        raise ValueError("fused gate|up weight needs 2I % 32 == 0")
+    inter = n2 // 2
+    inter_w = w.reshape(2, inter // 8, 8, k).permute(1, 0, 2, 3).reshape(n2, k)
+    return pack_weight(inter_w)
+
+
 class PackedWeight:
-    """A projection weight in skinny-GEMM fragment order (plus its shape)."""
+    """A projection weight in skinny-GEMM fragment order (plus its shape).
+    ``swiglu=True``: a fused gate|up weight whose GEMM emits ``silu(g) * u``."""
 
-    __slots__ = ("data", "n", "k")
+    __slots__ = ("data", "n", "k", "swiglu")
 
-    def __init__(self, w: torch.Tensor):
+    def __init__(self, w: torch.Tensor, swiglu: bool = False, fold: torch.Tensor | None = None):
+        """``fold``: an RMSNorm weight ``[K]`` folded into the columns (``W * fold``),
+        for GEMMs that apply the norm in their epilogue (``epi="rms"``)."""
         self.n, self.k = w.shape
-        self.data = pack_weight(w.to(torch.bfloat16))
+        self.swiglu = swiglu
+        if fold is not None:
+            w = w.float() * fold.float()[None, :]
+        w = w.to(torch.bfloat16)
+        self.data = pack_swiglu(w) if swiglu else pack_weight(w)
+
+    @property
+    def n_out(self) -> int:
+        return self.n // 2 if self.swiglu else self.n
 
     def unpacked(self) -> torch.Tensor:
+        if self.swiglu:
+            p = unpack_weight(self.data)
+            inter = self.n // 2
+            return p.reshape(inter // 8, 2, 8, self.k).permute(1, 0, 2, 3).reshape(self.n, self.k)
         return unpack_weight(self.data)
 
 
-def skinny_geometry(m: int) -> tuple[int, int, int]:
-    """(rows of W per workgroup strip, k per x chunk, padded batch) -- mirrors
-    ``kgs_skinny_geometry`` in decode.hip."""
+# tile variants of native/kernels/decode.hip (id -> (R W-row tiles per wave,
+# MT 16-column x tiles, KC k-steps per x chunk)); 0 = default for the batch size
+SKINNY_VARIANTS = {
+    1: (1, 1, 16), 2: (1, 1, 8), 3: (2, 1, 16),
+    4: (1, 2, 16), 5: (1, 2, 8), 6: (2, 2, 8), 7: (2, 2, 16),
+    8: (1, 4, 16), 9: (1, 4, 4), 10: (1, 4, 8), 11: (2, 4, 4), 12: (2, 4, 8),
+    13: (2, 8, 2), 14: (2, 8, 4), 15: (4, 8, 2), 16: (1, 8, 4),
+    17: (2, 16, 2), 18: (1, 16, 4), 19: (1, 16, 2),
+}
+_DEFAULT_VARIANT = {1: 1, 2: 4, 4: 8, 8: 13, 16: 17}
+
+# Measured routing per (MT, N, K) on MI355X with weights streamed from HBM
+# (bench/decode_bench.py --tune, profiles/decode_tune.md): (variant, ksplit) of
+# the skinny GEMM where it beat hipBLASLt, None where hipBLASLt won. Shapes:
+# Llama-3-8B qkv 6144x4096, o 4096x4096, gate|up 28672x4096, down 4096x14336,
+# lm_head 128256x4096.
+_QKV, _O, _GU, _DOWN, _LM = (6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)
+TUNED: dict = {
+    (1, *_QKV): (1, 1), (1, *_O): (1, 2), (1, *_GU): (2, 1), (1, *_DOWN): (1, 4), (1, *_LM): (1, 1),
+    (2, *_QKV): (6, 4), (2, *_O): (6, 4), (2, *_GU): (6, 1), (2, *_DOWN): (4, 4), (2, *_LM): (5, 1),
+    (4, *_QKV): None, (4, *_O): None, (4, *_GU): (12, 1), (4, *_DOWN): (10, 4), (4, *_LM): (11, 1),
+    (8, *_QKV): None, (8, *_O): None, (8, *_GU): None, (8, *_DOWN): (16, 4), (8, *_LM): None,
+    (16, *_QKV): None, (16, *_O): None, (16, *_GU): None, (16, *_DOWN): None, (16, *_LM): None,
+}
+SKINNY_DEFAULT_MAX_M = 32  # untuned shapes: skinny GEMM up to this batch, hipBLASLt above
+
+
+def _mt(m: int) -> int:
     if not 0 < m <= 256:
         raise ValueError(f"skinny GEMM batch must be 1..256, got {m}")
-    mt = 1 if m <= 16 else 2 if m <= 32 else 4 if m <= 64 else 8 if m <= 128 else 16
-    return 64 * (2 if mt >= 8 else 1), 32 * (2 if mt >= 8 else 16), 16 * mt
+    return 1 if m <= 16 else 2 if m <= 32 else 4 if m <= 64 else 8 if m <= 128 else 16
 
 
-def choose_ksplit(m: int, n: int, k: int, cus: int = CUS) -> int:
+def skinny_variants(m: int) -> list[int]:
+    mt = _mt(m)
+    return [v for v, (_, vmt, _) in SKINNY_VARIANTS.items() if vmt == mt]
+
+
+def skinny_geometry(m: int, variant: int = 0) -> tuple[int, int, int]:
+    """(rows of W per workgroup strip, k per x chunk, padded batch) -- mirrors
+    ``kgs_skinny_variant_geometry`` in decode.hip."""
+    mt = _mt(m)
+    v = variant or _DEFAULT_VARIANT[mt]
+    r, vmt, kc = SKINNY_VARIANTS[v]
+    if vmt != mt:
+        raise ValueError(f"variant {variant} is for {16 * vmt}-column batches, not M={m}")
+    return 64 * r, 32 * kc, 16 * mt
+
+
+def choose_ksplit(m: int, n: int, k: int, cus: int = CUS, variant: int = 0) -> int:
     """Largest divisor of the k-chunk count that keeps the grid within one
     workgroup per CU (measured best: long-running streaming workgroups,
     profiles/decode_kernels.md) and the fp32 slabs within 64 MB (1 = no split)."""
-    rps, kpc, mpad = skinny_geometry(m)
+    rps, kpc, mpad = skinny_geometry(m, variant)
     nstrip, nchunks = n // rps, k // kpc
     best = 1
     for d in range(2, nchunks + 1):
@@ -84,6 +151,25 @@ def choose_ksplit(m: int, n: int, k: int, cus: int = CUS) -> int:
             break
         best = d
     return best
+
+
+def skinny_config(m: int, n: int, k: int) -> tuple[int, int]:
+    """(variant, ksplit) for a skinny-GEMM call: the tuned entry, else the defaults."""
+    hit = TUNED.get((_mt(m), n, k))
+    if hit is not None:
+        return hit
+    v = _DEFAULT_VARIANT[_mt(m)]
+    return v, choose_ksplit(m, n, k, variant=v)
+
+
+def use_skinny(m: int, n: int, k: int) -> bool:
+    """Decode routing: True = skinny GEMM, False = the library GEMM (hipBLASLt)."""
+    if not 0 < m <= 256:
+        return False
+    key = (_mt(m), n, k)
+    if key in TUNED:
+        return TUNED[key] is not None
+    return m <= SKINNY_DEFAULT_MAX_M
 
 
 _WS: dict = {}
@@ -102,25 +188,52 @@ def _workspace(device: torch.device, floats: int, ints: int):
     return ws, cnt
 
 
+EPI_SWIGLU, EPI_RMS, EPI_RESID = 1, 2, 4
+
+
 def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = None,
-                ksplit: int | None = None) -> torch.Tensor:
-    """``x @ W^T`` (bf16, fp32 accumulate) for ``x: [M <= 256, K]`` row-major."""
+                ksplit: int | None = None, variant: int = 0, rms: torch.Tensor | None = None,
+                resid_ss: torch.Tensor | None = None, zero: torch.Tensor | None = None,
+                eps: float = 1e-5) -> torch.Tensor:
+    """``x @ W^T`` (bf16, fp32 accumulate) for ``x: [M <= 256, K]`` row-major;
+    ``silu(x @ Wg^T) * (x @ Wu^T)`` for a ``swiglu`` weight. Fused epilogues:
+
+    * ``rms`` (fp32 ``[M]`` row sums of squares of x): RMSNorm folded in -- the
+      rows are scaled by ``rsqrt(rms / K + eps)`` (the norm weight must be folded
+      into W, ``PackedWeight(..., fold=w)``);
+    * ``resid_ss`` (fp32 ``[M]``): ``out`` is the residual stream, updated in
+      place (``out += x @ W^T``), and the new rows' sums of squares are added
+      into ``resid_ss`` (for the next ``rms`` consumer);
+    * ``zero`` (fp32 ``[M]``): cleared at kernel start (a consumed statistic)."""
     if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1:
         raise ValueError("x must be a row-major bf16 GPU matrix")
     m, k = x.shape
     if k != w.k:
         raise ValueError(f"inner dims differ: x {tuple(x.shape)} vs W [{w.n}, {w.k}]")
-    rps, kpc, mpad = skinny_geometry(m)
+    if variant == 0 and ksplit is None:
+        variant, ks = skinny_config(m, w.n, k)
+    else:
+        ks = ksplit if ksplit is not None else choose_ksplit(m, w.n, k, variant=variant)
+    rps, kpc, mpad = skinny_geometry(m, variant)
     if w.n % rps or k % kpc:
         raise ValueError(f"skinny GEMM needs N % {rps} == 0 and K % {kpc} == 0 (N={w.n}, K={k})")
+    epi = (EPI_SWIGLU if w.swiglu else 0) | (EPI_RMS if rms is not None else 0) | \
+        (EPI_RESID if resid_ss is not None else 0)
+    for t, name in ((rms, "rms"), (resid_ss, "resid_ss"), (zero, "zero")):
+        if t is not None and (t.dtype != torch.float32 or t.numel() < m or not t.is_contiguous()):
+            raise ValueError(f"{name} must be a contiguous fp32 vector of >= M elements")
+    if resid_ss is not None:
+        if w.swiglu or out is None or tuple(out.shape) != (m, w.n):
+            raise ValueError("resid_ss needs the residual stream as out [M, N] (and no swiglu)")
     if out is None:
-        out = torch.empty((m, w.n), dtype=torch.bfloat16, device=x.device)
-    ks = choose_ksplit(m, w.n, k) if ksplit is None else ksplit
+        out = torch.empty((m, w.n_out), dtype=torch.bfloat16, device=x.device)
     ws, cnt = _workspace(x.device, ks * mpad * w.n if ks > 1 else 0, w.n // rps)
-    rc = _lib.lib().kgs_skinny_gemm_bf16(w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(),
-                                         cnt.data_ptr(), m, w.n, k, x.stride(0), out.stride(0), ks,
-                                         _lib.stream_handle(x.device))
-    _lib.check(rc, f"skinny_gemm[{m}x{w.n}x{k}, ksplit={ks}]")
+    rc = _lib.lib().kgs_skinny_gemm_bf16_fused(
+        w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(), cnt.data_ptr(), m, w.n, k, x.stride(0),
+        out.stride(0), ks, variant, epi, rms.data_ptr() if rms is not None else None,
+        resid_ss.data_ptr() if resid_ss is not None else None, zero.data_ptr() if zero is not None else None,
+        1.0 / k, float(eps), _lib.stream_handle(x.device))
+    _lib.check(rc, f"skinny_gemm[{m}x{w.n}x{k}, variant={variant}, ksplit={ks}, epi={epi}]")
     return out
 
 
@@ -185,11 +298,13 @@ def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positio
     return qkv
 
 
-def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS) -> tuple[int, int]:
+def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS, min_pages: int = 4) -> tuple[int, int]:
     """(pages_per_split, nsplit): split each sequence's context so the grid has
-    about 8 waves per CU."""
+    about 8 waves per CU, but give every split at least ``min_pages`` pages (a
+    one-page split is all launch and merge overhead: 52 us for batch 1 x 4096
+    tokens with 1-page splits, profiles/decode_kernels.md)."""
     want = max(1, math.ceil(8 * cus / max(1, batch * kv_heads)))
-    nsplit = max(1, min(max_pages, want))
+    nsplit = max(1, min(math.ceil(max_pages / min_pages), want))
     pps = math.ceil(max_pages / nsplit)
     return pps, math.ceil(max_pages / pps)
 

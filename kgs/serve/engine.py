@@ -58,6 +58,7 @@ class EngineConfig:
     max_model_len: int = 8192
     eos_token_id: int = 2
     cuda_graphs: bool = True
+    fused_max_batch: int = 32         # decode batches up to this use the fused skinny-GEMM layer (measured crossover)
     seed: int = 0
 
 
@@ -77,7 +78,7 @@ class LLMEngine:
         self.backend = backend
         num_pages = cfg.num_pages or self._pages_from_memory(model_cfg)
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
-                                  max_model_len=cfg.max_model_len)
+                                  max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128

@@ -10,10 +10,15 @@ Two step kinds, both driven by the native scheduler's plans
   is one :func:`kgs.ops.decode.rope_cache_` launch, attention is the
   flash-attention forward per sequence, and only the last real token of each
   sequence goes through the LM head;
-* **decode** -- one token per running sequence: projections on
-  :func:`kgs.ops.decode.skinny_gemm` over prepacked weights (batch <= 32; larger
-  decode batches use hipBLASLt, where it measured faster), attention is
-  :func:`kgs.ops.decode.paged_decode_attention` over the paged cache.
+* **decode** -- one token per running sequence; attention is
+  :func:`kgs.ops.decode.paged_decode_attention` over the paged cache. Batches up
+  to ``fused_max_batch`` run the FUSED layer: five
+  :func:`kgs.ops.decode.skinny_gemm` launches over prepacked weights whose
+  epilogues carry the RMSNorms (norm weights folded into the weights, row
+  scales from sums of squares the residual-updating GEMMs accumulate), the
+  residual adds and SwiGLU -- no elementwise kernels. Larger batches use
+  add_rmsnorm/silu_mul and hipBLASLt, with the skinny GEMM where it measured
+  faster (:func:`kgs.ops.decode.use_skinny`).
 
 ``backend="ref"`` runs the same weights, cache layout and plans through plain
 PyTorch (CPU or GPU) -- the numerics reference for tests.
@@ -29,12 +34,11 @@ import torch
 from kgs.models.llama import LlamaConfig, LlamaModel, _rms_norm
 from kgs.ops import decode as D
 
-SKINNY_MAX_M = 32  # decode batches above this go to hipBLASLt (measured crossover, profiles/decode_kernels.md)
 
 
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
-                 num_pages: int = 1024, max_model_len: int = 8192):
+                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 32):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -46,9 +50,16 @@ class ServingModel:
         self.w = [{n: base.layers[i][n].w for n in ("qkv", "o", "gate_up", "down")} for i in range(cfg.layers)]
         self.w_lm = base.lm_head.w
         self.packed = None
+        self.fused_max_batch = fused_max_batch
         if backend == "kgs":
-            self.packed = [{n: D.PackedWeight(w) for n, w in lw.items()} for lw in self.w]
-            self.packed_lm = D.PackedWeight(self.w_lm)
+            # decode copies in skinny-GEMM fragment order; the RMSNorm weights
+            # in front of qkv / gate|up / lm_head are folded into them (their
+            # GEMMs apply the norm in the epilogue), gate|up is SwiGLU-packed
+            self.packed = [{"qkv": D.PackedWeight(lw["qkv"], fold=self.ln1[i]),
+                            "o": D.PackedWeight(lw["o"]),
+                            "gate_up": D.PackedWeight(lw["gate_up"], swiglu=True, fold=self.ln2[i]),
+                            "down": D.PackedWeight(lw["down"])} for i, lw in enumerate(self.w)]
+            self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm)
             D.reserve_workspace(self.device)
         self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device)
         self.max_model_len = max_model_len
@@ -66,9 +77,8 @@ class ServingModel:
         if self.backend == "ref":
             return (x.float() @ w.float().T).to(torch.bfloat16)
         m = x.shape[0]
-        if decode and m <= SKINNY_MAX_M:
-            pw = self.packed_lm if layer is None else self.packed[layer][name]
-            return D.skinny_gemm(x, pw)
+        if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]):
+            return D.skinny_gemm(x, self.packed[layer][name])
         if decode:
             return torch.matmul(x, w.T)
         from kgs.ops import gemm_nt
@@ -154,6 +164,8 @@ class ServingModel:
     def decode(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split=None) -> torch.Tensor:
         """One token per sequence -> logits [B, vocab]."""
         c = self.cfg
+        if self.backend == "kgs" and tokens.shape[0] <= self.fused_max_batch:
+            return self._decode_fused(tokens, positions, slots, block_tables, ctx_lens, pages_per_split)
         x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
         y = self._norm(x, None, self.ln1[0])
         for i in range(c.layers):
@@ -170,3 +182,24 @@ class ServingModel:
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             y = self._norm(x, self._proj(act, i, "down", True), nxt)
         return self._proj(y, None, "lm", True)
+
+    def _decode_fused(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split):
+        """Decode with every norm / SwiGLU / residual add inside the skinny GEMMs:
+        5 GEMMs + RoPE/KV-write + attention per layer, no elementwise launches.
+        ss_a / ss_b carry the residual rows' sums of squares between the
+        producing GEMM (residual update) and the consuming one (folded RMSNorm)."""
+        c = self.cfg
+        eps = c.eps
+        x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()  # residual stream
+        ss_b = x.float().pow(2).sum(-1)  # statistic for layer 0's qkv
+        ss_a = torch.zeros_like(ss_b)
+        for i in range(c.layers):
+            P = self.packed[i]
+            qkv = D.skinny_gemm(x, P["qkv"], rms=ss_b, eps=eps)
+            self._rope_cache(qkv, i, positions, slots)
+            a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
+                                         pages_per_split=pages_per_split)
+            D.skinny_gemm(a, P["o"], out=x, resid_ss=ss_a, zero=ss_b)
+            act = D.skinny_gemm(x, P["gate_up"], rms=ss_a, eps=eps)
+            D.skinny_gemm(act, P["down"], out=x, resid_ss=ss_b, zero=ss_a)
+        return D.skinny_gemm(x, self.packed_lm, rms=ss_b, eps=eps)

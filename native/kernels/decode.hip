@@ -68,19 +68,44 @@ __device__ __forceinline__ float wsum16(float v) {
 // (measured: KC 4 at Mp 64 ran 1.4x slower); W fragments stream through a
 // register ring PF k-steps deep. Mp > 64 keeps KC 2 (VGPR-bound; the serving
 // engine routes those batches to hipBLASLt, profiles/decode_kernels.md).
-template <int MT>
+template <int MT, int KC_>
 struct SkinnyCfg {
-  static constexpr int KC = MT >= 8 ? 2 : 16;       // k-steps per x chunk
+  static constexpr int KC = KC_;                    // k-steps per x chunk
   static constexpr int CHUNK_SLOTS = KC * MT * 64;  // 16-B slots per chunk
   static constexpr int LOADS = CHUNK_SLOTS / 256;   // per thread per chunk
 };
 
-template <int R, int MT>
-__global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void skinny(const bf16x8* __restrict__ wp, const unsigned short* __restrict__ x,
+// Fused epilogues (runtime flags in SkinnyEpi::mode, uniform per launch):
+//   EPI_SWIGLU  W is the fused gate|up weight packed so that 16-row tile t holds
+//               gate rows 8t..8t+7 then up rows 8t..8t+7 (kgs/ops/decode.py
+//               pack_swiglu); lane l (gate) pairs with lane l ^ 32 (up) and
+//               writes silu(g) * u, so y is [M, N/2].
+//   EPI_RMS     RMSNorm folded into the GEMM: x is the raw residual stream,
+//               the norm weight is folded into W, and each output row m is
+//               scaled by rsqrt(ss_in[m] * inv_k + eps) -- ss_in being the
+//               row's sum of squares, accumulated by the producer of x.
+//   EPI_RESID   residual update y[m, n] += acc (y = the residual stream, in
+//               place) and ss_out[m] += sum over n of the new y^2 (fp32
+//               atomics), the statistic the next EPI_RMS consumer needs.
+//   ss_zero     zeroed by workgroup 0 at kernel start (the sum-of-squares
+//               buffer of the previous layer boundary, already consumed).
+// Together they remove both add_rmsnorm launches and the SwiGLU launch from a
+// decode layer (kgs/serve/model.py fused decode path).
+enum { EPI_SWIGLU = 1, EPI_RMS = 2, EPI_RESID = 4 };
+struct SkinnyEpi {
+  int mode;
+  const float* ss_in;
+  float* ss_out;
+  float* ss_zero;
+  float inv_k, eps;
+};
+
+template <int R, int MT, int KC_>
+__global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void skinny(const bf16x8* __restrict__ wp, const unsigned short* __restrict__ x,
                                                  unsigned short* __restrict__ y, float* __restrict__ ws,
                                                  int* __restrict__ cnt, int M, int N, int K, long ldx, long ldy,
-                                                 int ksplit, int chunks_per_split) {
-  using C = SkinnyCfg<MT>;
+                                                 int ksplit, int chunks_per_split, SkinnyEpi ep) {
+  using C = SkinnyCfg<MT, KC_>;
   constexpr int KC = C::KC;
   constexpr int PF = KC < 8 ? KC : 8;  // W ring depth in k-steps (divides KC)
   // the only __shared__ object (a second one can make hipcc drain vmcnt before
@@ -91,6 +116,7 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void skinny(const bf16x8* __r
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nstrip = N / (64 * R);
   const int strip = blockIdx.x % nstrip, split = blockIdx.x / nstrip;
+  if (ep.ss_zero != nullptr && blockIdx.x == 0 && tid < M) ep.ss_zero[tid] = 0.f;
   const int nkk = K / 32;
   const int kk0 = split * chunks_per_split * KC;
   const int nsteps = chunks_per_split * KC;  // k-steps (of 32) for this workgroup
@@ -164,21 +190,53 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void skinny(const bf16x8* __r
 
   // C^T tile (r, c): lane holds column m = 16c + (lane & 15), rows n = 16*(nt0+r) + 4*(lane>>4) + i
   const int g = lane >> 4, mc = lane & 15;
+  // store one lane's 4 consecutive outputs; every lane of the wave calls it
+  // (the SWIGLU / RESID exchanges are cross-lane)
+  auto emit = [&](f32x4v v, int m, int r) {
+    const int ms = m < M ? m : M - 1;
+    if (ep.mode & EPI_RMS) v *= rsqrtf(ep.ss_in[ms] * ep.inv_k + ep.eps);
+    if (ep.mode & EPI_SWIGLU) {
+      f32x4v u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32, 64);
+      if (m < M && g < 2) {
+        f32x4v o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = v[i] / (1.0f + __expf(-v[i])) * u[i];
+        uint2 pk;
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
+        *(uint2*)(y + (long)m * ldy + 8 * (nt0 + r) + 4 * g) = pk;
+      }
+    } else if (ep.mode & EPI_RESID) {
+      float sq = 0.f;
+      if (m < M) {
+        uint2* yp = (uint2*)(y + (long)m * ldy + 16 * (nt0 + r) + 4 * g);
+        const uint2 old = *yp;
+        float o[4] = {bf2f(old.x & 0xffff) + v[0], bf2f(old.x >> 16) + v[1], bf2f(old.y & 0xffff) + v[2],
+                      bf2f(old.y >> 16) + v[3]};
+        uint2 pk;
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
+        *yp = pk;
+        // statistic of the stored (bf16-rounded) values, as add_rmsnorm computes it
+        const float r0 = bf2f(pk.x & 0xffff), r1 = bf2f(pk.x >> 16), r2 = bf2f(pk.y & 0xffff), r3 = bf2f(pk.y >> 16);
+        sq = r0 * r0 + r1 * r1 + r2 * r2 + r3 * r3;
+      }
+      sq = wsum16(sq);  // lanes of one column m (g = 0..3)
+      if (m < M && g == 0) atomicAdd(ep.ss_out + m, sq);
+    } else if (m < M) {
+      uint2 pk;
+      pk.x = pack_bf16x2(v[0], v[1]);
+      pk.y = pack_bf16x2(v[2], v[3]);
+      *(uint2*)(y + (long)m * ldy + 16 * (nt0 + r) + 4 * g) = pk;
+    }
+  };
   if (ksplit == 1) {
 #pragma unroll
-    for (int c = 0; c < MT; ++c) {
-      const int m = 16 * c + mc;
-      if (m < M) {
+    for (int c = 0; c < MT; ++c)
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int n = 16 * (nt0 + r) + 4 * g;
-          uint2 pk;
-          pk.x = pack_bf16x2(acc[r][c][0], acc[r][c][1]);
-          pk.y = pack_bf16x2(acc[r][c][2], acc[r][c][3]);
-          *(uint2*)(y + (long)m * ldy + n) = pk;
-        }
-      }
-    }
+      for (int r = 0; r < R; ++r) emit(acc[r][c], 16 * c + mc, r);
     return;
   }
   // split-K: fp32 slabs ws[split][m][n]; the last arriver of the strip reduces.
@@ -216,17 +274,13 @@ __global__ __launch_bounds__(256, MT >= 4 ? 1 : 2) void skinny(const bf16x8* __r
 #pragma unroll
   for (int c = 0; c < MT; ++c) {
     const int m = 16 * c + mc;
-    if (m < M) {
+    const int ms = m < M ? m : M - 1;  // every lane joins the epilogue exchanges
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int n = 16 * (nt0 + r) + 4 * g;
-        f32x4v t = f32x4v{0.f, 0.f, 0.f, 0.f};
-        for (int sp = 0; sp < ksplit; ++sp) t += *(const f32x4v*)(ws + sp * sstride + m * mstride + n);
-        uint2 pk;
-        pk.x = pack_bf16x2(t[0], t[1]);
-        pk.y = pack_bf16x2(t[2], t[3]);
-        *(uint2*)(y + (long)m * ldy + n) = pk;
-      }
+    for (int r = 0; r < R; ++r) {
+      const int n = 16 * (nt0 + r) + 4 * g;
+      f32x4v t = f32x4v{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < ksplit; ++sp) t += *(const f32x4v*)(ws + sp * sstride + ms * mstride + n);
+      emit(t, m, r);
     }
   }
 }
@@ -415,6 +469,7 @@ __global__ __launch_bounds__(64) void paged_reduce(const float* __restrict__ po,
   for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
   float L = 0.f, o0 = 0.f, o1 = 0.f;
   const float* pb = po + (long)bh * nsplit * HD + 2 * lane;
+#pragma unroll 4
   for (int s = 0; s < nsplit; ++s) {
     const float l = ml[2 * s + 1];
     if (l <= 0.f) continue;
@@ -434,49 +489,105 @@ __global__ __launch_bounds__(64) void paged_reduce(const float* __restrict__ po,
 namespace {
 inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
-template <int R, int MT>
+// Tile variants (R = 16-row W tiles per wave, MT = 16-column x tiles, KC =
+// k-steps per x chunk). 0 = the measured default for the batch size.
+struct SkinnyVariant {
+  int r, mt, kc;
+};
+constexpr SkinnyVariant kVariants[] = {
+    {0, 0, 0},                                      // 0: auto
+    {1, 1, 16}, {1, 1, 8}, {2, 1, 16},              // 1-3:  M <= 16
+    {1, 2, 16}, {1, 2, 8}, {2, 2, 8}, {2, 2, 16},   // 4-7:  M <= 32
+    {1, 4, 16}, {1, 4, 4}, {1, 4, 8}, {2, 4, 4}, {2, 4, 8},  // 8-12: M <= 64
+    {2, 8, 2}, {2, 8, 4}, {4, 8, 2}, {1, 8, 4},     // 13-16: M <= 128
+    {2, 16, 2}, {1, 16, 4}, {1, 16, 2},             // 17-19: M <= 256
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+int mt_for(int M) { return M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : M <= 128 ? 8 : 16; }
+int default_variant(int mt) { return mt == 1 ? 1 : mt == 2 ? 4 : mt == 4 ? 8 : mt == 8 ? 13 : 17; }
+
+template <int R, int MT, int KC>
 hipError_t launch_skinny(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx,
-                         long ldy, int ksplit, int cps, hipStream_t s) {
+                         long ldy, int ksplit, int cps, const kgs::dec::SkinnyEpi& ep, hipStream_t s) {
   const int nstrip = N / (64 * R);
-  hipLaunchKernelGGL((kgs::dec::skinny<R, MT>), dim3(nstrip * ksplit), dim3(256), 0, s, (const bf16x8*)wp,
-                     (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps);
+  hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC>), dim3(nstrip * ksplit), dim3(256), 0, s, (const bf16x8*)wp,
+                     (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
   return hipGetLastError();
 }
 }  // namespace
 
-// Rows of W per workgroup strip, k elements per x chunk and padded batch for a
-// batch of M rows: lets the host size split-K and the workspace (kgs/ops/decode.py).
-KGS_EXPORT int kgs_skinny_geometry(int M, int* rows_per_strip, int* k_per_chunk, int* mpad) {
+// Geometry of tile variant `variant` (0 = default) for a batch of M rows:
+// rows of W per workgroup strip, k elements per x chunk, padded batch. Lets the
+// host size split-K and the workspace (kgs/ops/decode.py). Returns
+// KGS_ERR_ARG when the variant does not cover M's column-tile count.
+KGS_EXPORT int kgs_skinny_variant_geometry(int variant, int M, int* rows_per_strip, int* k_per_chunk, int* mpad) {
   if (M <= 0 || M > 256) return KGS_ERR_SHAPE;
-  const int mt = M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : M <= 128 ? 8 : 16;
+  const int mt = mt_for(M);
+  if (variant == 0) variant = default_variant(mt);
+  if (variant < 0 || variant >= kNumVariants || kVariants[variant].mt != mt) return KGS_ERR_ARG;
   *mpad = 16 * mt;
-  *rows_per_strip = 64 * (mt >= 8 ? 2 : 1);
-  *k_per_chunk = 32 * (mt >= 8 ? 2 : 16);
+  *rows_per_strip = 64 * kVariants[variant].r;
+  *k_per_chunk = 32 * kVariants[variant].kc;
   return 0;
+}
+
+KGS_EXPORT int kgs_skinny_geometry(int M, int* rows_per_strip, int* k_per_chunk, int* mpad) {
+  return kgs_skinny_variant_geometry(0, M, rows_per_strip, k_per_chunk, mpad);
 }
 
 // y[M, N] (bf16, row stride ldy) = x[M, K] (row stride ldx) . W^T with W
 // prepacked ([N/16][K/32][64][8] bf16). ksplit must divide K / k_per_chunk;
 // with ksplit > 1, ws holds ksplit * mpad * N floats and cnt N / rows_per_strip
-// zero-initialised ints (left zeroed on return).
-KGS_EXPORT int kgs_skinny_gemm_bf16(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K,
-                                   long ldx, long ldy, int ksplit, hipStream_t s) {
+// zero-initialised ints (left zeroed on return). epi: EPI_* flags (SWIGLU: y is
+// [M, N/2]; RMS needs ss_in[M]; RESID accumulates into y and ss_out[M]);
+// ss_zero (optional, [M] floats) is cleared at kernel start.
+KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
+                                         int K, long ldx, long ldy, int ksplit, int variant, int epi,
+                                         const float* ss_in, float* ss_out, float* ss_zero, float inv_k, float eps,
+                                         hipStream_t s) {
+  using namespace kgs::dec;
   int rps, kpc, mpad;
-  if (kgs_skinny_geometry(M, &rps, &kpc, &mpad)) return KGS_ERR_SHAPE;
-  if (N <= 0 || K <= 0 || N % rps || K % kpc || ldx < K || ldy < N) return KGS_ERR_SHAPE;
+  const int rc = kgs_skinny_variant_geometry(variant, M, &rps, &kpc, &mpad);
+  if (rc) return rc;
+  if (variant == 0) variant = default_variant(mt_for(M));
+  if (epi & ~(EPI_SWIGLU | EPI_RMS | EPI_RESID) || ((epi & EPI_SWIGLU) && (epi & EPI_RESID))) return KGS_ERR_ARG;
+  if (((epi & EPI_RMS) && ss_in == nullptr) || ((epi & EPI_RESID) && ss_out == nullptr)) return KGS_ERR_ARG;
+  if (N <= 0 || K <= 0 || N % rps || K % kpc || ldx < K || ldy < ((epi & EPI_SWIGLU) ? N / 2 : N))
+    return KGS_ERR_SHAPE;
   const int nchunks = K / kpc;
   if (ksplit <= 0 || nchunks % ksplit) return KGS_ERR_ARG;
   if (ksplit > 1 && (ws == nullptr || cnt == nullptr)) return KGS_ERR_ARG;
   if (!al16(wp) || !al16(x) || ((uintptr_t)y & 7) || ((uintptr_t)ws & 15) || ldx % 8 || ldy % 4) return KGS_ERR_ALIGN;
   const int cps = nchunks / ksplit;
-  switch (mpad / 16) {
-    case 1: return (int)launch_skinny<1, 1>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
-    case 2: return (int)launch_skinny<1, 2>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
-    case 4: return (int)launch_skinny<1, 4>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
-    case 8: return (int)launch_skinny<2, 8>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
-    case 16: return (int)launch_skinny<2, 16>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, s);
-    default: return KGS_ERR_SHAPE;
+  const SkinnyEpi ep{epi, ss_in, ss_out, ss_zero, inv_k, eps};
+  switch (variant) {
+#define KGS_SKV(id, R, MT, KC) \
+  case id: return (int)launch_skinny<R, MT, KC>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
+    KGS_SKV(1, 1, 1, 16) KGS_SKV(2, 1, 1, 8) KGS_SKV(3, 2, 1, 16)
+    KGS_SKV(4, 1, 2, 16) KGS_SKV(5, 1, 2, 8) KGS_SKV(6, 2, 2, 8) KGS_SKV(7, 2, 2, 16)
+    KGS_SKV(8, 1, 4, 16) KGS_SKV(9, 1, 4, 4) KGS_SKV(10, 1, 4, 8) KGS_SKV(11, 2, 4, 4) KGS_SKV(12, 2, 4, 8)
+    KGS_SKV(13, 2, 8, 2) KGS_SKV(14, 2, 8, 4) KGS_SKV(15, 4, 8, 2) KGS_SKV(16, 1, 8, 4)
+    KGS_SKV(17, 2, 16, 2) KGS_SKV(18, 1, 16, 4) KGS_SKV(19, 1, 16, 2)
+#undef KGS_SKV
+    default: return KGS_ERR_ARG;
   }
+}
+
+KGS_EXPORT int kgs_skinny_gemm_bf16_ex(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
+                                      int K, long ldx, long ldy, int ksplit, int variant, int epi, hipStream_t s) {
+  return kgs_skinny_gemm_bf16_fused(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, variant, epi, nullptr, nullptr,
+                                    nullptr, 0.f, 0.f, s);
+}
+
+KGS_EXPORT int kgs_skinny_gemm_bf16_v(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K,
+                                     long ldx, long ldy, int ksplit, int variant, hipStream_t s) {
+  return kgs_skinny_gemm_bf16_ex(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, variant, 0, s);
+}
+
+KGS_EXPORT int kgs_skinny_gemm_bf16(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K,
+                                   long ldx, long ldy, int ksplit, hipStream_t s) {
+  return kgs_skinny_gemm_bf16_v(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, 0, s);
 }
 
 // qkv: [tokens, ld] fused projection rows (H q heads, HKV k heads, HKV v heads

@@ -29,13 +29,36 @@ def test_geometry_matches_native():
     import ctypes
 
     from kgs.ops import _lib
-    from kgs.ops.decode import skinny_geometry
+    from kgs.ops.decode import SKINNY_VARIANTS, skinny_geometry, skinny_variants
 
     so = _lib.lib()
     for m in (1, 5, 16, 17, 32, 33, 64, 65, 128, 129, 256):
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         assert so.kgs_skinny_geometry(m, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)) == 0
         assert (a.value, b.value, c.value) == skinny_geometry(m)
+        for v in SKINNY_VARIANTS:
+            rc = so.kgs_skinny_variant_geometry(v, m, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+            if v in skinny_variants(m):
+                assert rc == 0 and (a.value, b.value, c.value) == skinny_geometry(m, v)
+            else:
+                assert rc == -3
+
+
+@pytest.mark.parametrize("m", [9, 30, 64, 128, 200])
+def test_skinny_gemm_every_variant(m):
+    from kgs.ops.decode import PackedWeight, choose_ksplit, skinny_gemm, skinny_variants
+
+    n, k = 512, 1024
+    x = _bf(m, k)
+    w = _bf(n, k, scale=k ** -0.5)
+    pw = PackedWeight(w)
+    ref = x.float() @ w.float().T
+    for v in skinny_variants(m):
+        for ks in sorted({1, choose_ksplit(m, n, k, variant=v)}):
+            y = skinny_gemm(x, pw, ksplit=ks, variant=v)
+            torch.cuda.synchronize()
+            err = (y.float() - ref).abs().max().item()
+            assert err <= 2e-2 * ref.abs().max().item() + 1e-3, (v, ks, err)
 
 
 @pytest.mark.parametrize("m", [1, 7, 16, 24, 64, 100, 256])
@@ -154,3 +177,64 @@ def test_paged_decode_long_context():
     o = paged_decode_attention(q, cache.layer(0), bt, ctx_t, heads, hkv)
     torch.cuda.synchronize()
     assert (o.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("m", [1, 20, 64, 150])
+def test_skinny_swiglu_epilogue(m):
+    from kgs.ops.decode import PackedWeight, choose_ksplit, skinny_gemm, skinny_variants
+
+    inter, k = 512, 1024
+    x = _bf(m, k)
+    w = _bf(2 * inter, k, scale=k ** -0.5)  # fused gate|up, gate rows first
+    pw = PackedWeight(w, swiglu=True)
+    g = x.float() @ w[:inter].float().T
+    u = x.float() @ w[inter:].float().T
+    ref = g * torch.sigmoid(g) * u
+    for v in skinny_variants(m):
+        for ks in sorted({1, choose_ksplit(m, 2 * inter, k, variant=v)}):
+            y = skinny_gemm(x, pw, ksplit=ks, variant=v)
+            torch.cuda.synchronize()
+            assert y.shape == (m, inter)
+            assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item() + 1e-3, (v, ks)
+
+
+@pytest.mark.parametrize("m", [3, 32, 64])
+def test_skinny_fused_rms_and_residual_epilogues(m):
+    """The fused decode layer's GEMMs: RMSNorm folded into W + row scale from a
+    sum of squares (qkv / gate|up / lm_head) and the in-place residual update that
+    accumulates the next sums of squares (o / down)."""
+    from kgs.ops.decode import PackedWeight, skinny_gemm
+    from kgs.ops.transformer import ref_add_rmsnorm
+
+    h, n = 1024, 1536
+    x = _bf(m, h)
+    lnw = (_bf(h, scale=0.2) + 1).contiguous()
+    w = _bf(n, h, scale=h ** -0.5)
+    # rms: rmsnorm(x) * lnw @ W^T
+    ss = x.float().pow(2).sum(-1)
+    _, y_ref = ref_add_rmsnorm(x, None, lnw)
+    ref = y_ref.float() @ w.float().T
+    got = skinny_gemm(x, PackedWeight(w, fold=lnw), rms=ss, eps=1e-5)
+    torch.cuda.synchronize()
+    assert (got.float() - ref).abs().max().item() <= 3e-2 * ref.abs().max().item()
+    # swiglu + rms
+    wgu = _bf(2 * n, h, scale=h ** -0.5)
+    g, u = y_ref.float() @ wgu[:n].float().T, y_ref.float() @ wgu[n:].float().T
+    ref2 = g * torch.sigmoid(g) * u
+    got2 = skinny_gemm(x, PackedWeight(wgu, swiglu=True, fold=lnw), rms=ss, eps=1e-5)
+    torch.cuda.synchronize()
+    assert (got2.float() - ref2).abs().max().item() <= 3e-2 * ref2.abs().max().item()
+    # residual: res += a @ Wo^T, ss_out += rowsum(res^2), zero cleared
+    wo = _bf(h, n, scale=n ** -0.5)
+    a = _bf(m, n)
+    for ks in (1, None):
+        res = _bf(m, h)
+        res0 = res.clone()
+        ss_out = torch.full((m,), 0.0, device=DEV)
+        junk = torch.full((m,), 7.0, device=DEV)
+        skinny_gemm(a, PackedWeight(wo), out=res, resid_ss=ss_out, zero=junk, ksplit=ks)
+        torch.cuda.synchronize()
+        new_ref = (res0.float() + a.float() @ wo.float().T)
+        assert (res.float() - new_ref).abs().max().item() <= 2e-2 * new_ref.abs().max().item()
+        assert torch.allclose(ss_out, res.float().pow(2).sum(-1), rtol=1e-4, atol=1e-3)
+        assert junk.abs().max().item() == 0

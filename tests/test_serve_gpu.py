@@ -59,14 +59,27 @@ def test_graphs_equal_eager():
     assert a == b
 
 
-def test_large_decode_batch_routes_to_library_gemm():
+def test_large_decode_batch_unfused_path():
     from kgs.serve import SamplingParams
-    from kgs.serve.model import SKINNY_MAX_M
 
-    n = SKINNY_MAX_M + 8
-    eng = _engine(True, max_batch=64)
+    n = 72  # above fused_max_batch 64: add_rmsnorm / silu_mul + hipBLASLt / skinny routing
+    eng = _engine(True, max_batch=128)
     rng = np.random.default_rng(2)
     prompts = [rng.integers(3, 1024, size=20).tolist() for _ in range(n)]
     outs = eng.generate(prompts, SamplingParams(max_tokens=3, ignore_eos=True))
     assert all(len(r.output) == 3 for r in outs)
     _oracle_check(eng, prompts[:4], outs[:4])
+
+
+def test_fused_and_unfused_decode_agree():
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(3)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (50, 9, 140)]
+    p = SamplingParams(max_tokens=12, ignore_eos=True)
+    fused = _engine(False, fused_max_batch=64)
+    unfused = _engine(False, fused_max_batch=0)
+    a = fused.generate(prompts, p)
+    b = unfused.generate(prompts, p)
+    _oracle_check(fused, prompts, a)
+    _oracle_check(unfused, prompts, b)
