@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Per-kernel breakdown of one decode step from a rocprofv3 kernel trace of
+``python -m kgs.serve bench`` (steps are delimited by the sampler's argmax).
+
+  python bench/decode_step_breakdown.py gpurun_out/prof_decode/b1/d_kernel_trace.csv [--step -3]
+"""
+import argparse
+import collections
+import csv
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--step", type=int, default=-3, help="which argmax-delimited step (python index)")
+    a = ap.parse_args(argv)
+    rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
+    idx = [i for i, r in enumerate(rows) if "ArgMax" in r["Kernel_Name"]]
+    s0, s1 = idx[a.step - 1], idx[a.step]
+    seg = rows[s0 + 1:s1 + 1]
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in seg:
+        name = r["Kernel_Name"].split("(")[0][:72]
+        agg[name][0] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        agg[name][1] += 1
+    busy = sum(v[0] for v in agg.values())
+    span = int(seg[-1]["End_Timestamp"]) - int(rows[s0]["End_Timestamp"])
+    print(f"step span {span / 1e3:.1f} us, kernels busy {busy / 1e3:.1f} us ({100 * busy / span:.0f} %), "
+          f"{len(seg)} kernels, idle between kernels {(span - busy) / 1e3:.1f} us")
+    print("| kernel | us / step | share | launches | us / launch |")
+    print("|---|---:|---:|---:|---:|")
+    for name, (t, c) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+        print(f"| `{name}` | {t / 1e3:.1f} | {100 * t / busy:.1f}% | {c} | {t / c / 1e3:.2f} |")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -140,6 +140,13 @@ class ServingModel:
         c = self.cfg
         hd = c.head_dim
         out = torch.empty((qkv.shape[0], c.heads * hd), dtype=torch.bfloat16, device=qkv.device)
+        if self.backend != "ref" and len(set(int(p) for p in padded_lens)) == 1:
+            # equal padded lengths, packed back to back: one batched launch
+            from kgs.ops.transformer import attention_qkv
+
+            p = int(padded_lens[0])
+            attention_qkv(qkv, len(padded_lens), p, c.heads, c.kv_heads, head_dim=hd, causal=True, out=out)
+            return out
         for s0, n, p in zip(seq_starts, seq_lens, padded_lens):
             s0, n, p = int(s0), int(n), int(p)
             blk = qkv[s0:s0 + p]

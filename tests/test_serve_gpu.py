@@ -83,3 +83,13 @@ def test_fused_and_unfused_decode_agree():
     b = unfused.generate(prompts, p)
     _oracle_check(fused, prompts, a)
     _oracle_check(unfused, prompts, b)
+
+
+def test_equal_length_prefill_batched_attention():
+    from kgs.serve import SamplingParams
+
+    eng = _engine(True)
+    rng = np.random.default_rng(4)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (90, 120, 128, 100)]  # all pad to 128
+    outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
+    _oracle_check(eng, prompts, outs)
