@@ -82,7 +82,7 @@ def bench_gemm(iters, ms, ring_bytes=3 << 30):
         torch.cuda.empty_cache()
 
 
-def tune_gemm(iters, ms, ring_bytes=2 << 30):
+def tune_gemm(iters, ms, ring_bytes=2 << 30, fp8=False):
     """Time every (variant, split-K) of the skinny GEMM per Llama shape and batch
     bucket with HBM-streamed weights; print the best and a TUNED table."""
     from kgs.ops.decode import PackedWeight, _mt, skinny_gemm, skinny_geometry, skinny_variants
@@ -91,7 +91,7 @@ def tune_gemm(iters, ms, ring_bytes=2 << 30):
     for name, (n, k) in SHAPES.items():
         copies = max(2, min(32, ring_bytes // (n * k * 2)))
         ws = [(torch.randn(n, k, device="cuda") * k ** -0.5).to(torch.bfloat16) for _ in range(copies)]
-        pws = [PackedWeight(w) for w in ws]
+        pws = [PackedWeight(w, fp8=fp8) for w in ws]
         for m in ms:
             x = (torch.rand(m, k, device="cuda") * 2 - 1).to(torch.bfloat16)
             out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
@@ -116,7 +116,7 @@ def tune_gemm(iters, ms, ring_bytes=2 << 30):
                     res[(v, ks)] = _time(call, iters)
             (bv, bks), bt = min(res.items(), key=lambda kv: kv[1])
             table[(_mt(m), n, k)] = (bv, bks)
-            print(json.dumps({"op": "skinny_tune", "shape": name, "m": m, "n": n, "k": k, "best_variant": bv,
+            print(json.dumps({"op": "skinny_tune_fp8" if fp8 else "skinny_tune", "shape": name, "m": m, "n": n, "k": k, "best_variant": bv,
                               "best_ksplit": bks, "us": round(bt, 2), "tbps": round(n * k * 2 / bt / 1e6, 2),
                               "torch_us": round(t_t, 2), "speedup": round(t_t / bt, 3),
                               "all": {f"{v}/{ks}": round(t, 1) for (v, ks), t in sorted(res.items())}}), flush=True)
@@ -155,11 +155,12 @@ def main(argv=None) -> int:
     ap.add_argument("--ms", default="1,16,32,64,128,256")
     ap.add_argument("--sweep", action="store_true", help="time every valid split-K factor")
     ap.add_argument("--tune", action="store_true", help="time every tile variant x split-K; print a TUNED table")
+    ap.add_argument("--fp8", action="store_true", help="--tune the weight-only fp8 (W8A16) kernels")
     a = ap.parse_args(argv)
     global SWEEP
     SWEEP = a.sweep
     if a.tune:
-        tune_gemm(a.iters, [int(v) for v in a.ms.split(",")])
+        tune_gemm(a.iters, [int(v) for v in a.ms.split(",")], fp8=a.fp8)
         return 0
     both = not (a.gemm or a.attn)
     if a.gemm or both:

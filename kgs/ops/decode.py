@@ -12,7 +12,7 @@ half of LLM serving, which is HBM-bound on the weights and the KV cache.
 * :func:`rope_cache_` -- RoPE on the q/k heads of fused QKV rows + scatter of k/v
   into their cache slots, one launch.
 * :func:`paged_decode_attention` -- GQA decode attention over the paged cache
-  (context split across waves, log-sum-exp merge).
+  (context split across waves, log-sum-exp merge by the last split, one launch).
 
 Every op raises :class:`kgs.ops.NativeUnavailable` when the native library is
 missing; the ``ref_*`` functions are the plain-PyTorch fp32 references (they run
@@ -48,44 +48,68 @@ def unpack_weight(p: torch.Tensor) -> torch.Tensor:
     return p.reshape(nt, kk, 4, 16, 8).permute(0, 3, 1, 2, 4).reshape(nt * 16, kk * 32)
 
 
-def pack_swiglu(w: torch.Tensor) -> torch.Tensor:
-    """Fused gate|up weight ``[2I, K]`` (gate rows first) -> packed fragments whose
+def swiglu_rows(n2: int) -> torch.Tensor:
+    """Row order of a fused gate|up weight ``[2I, K]`` (gate rows first) in which
     16-row tile ``t`` holds gate rows ``8t..8t+7`` then up rows ``8t..8t+7``: the
     skinny GEMM's SwiGLU epilogue pairs them lane-to-lane (``lane ^ 32``)."""
-    n2, k = w.shape
     if n2 % 32:
         raise ValueError("fused gate|up weight needs 2I % 32 == 0")
     inter = n2 // 2
-    inter_w = w.reshape(2, inter // 8, 8, k).permute(1, 0, 2, 3).reshape(n2, k)
-    return pack_weight(inter_w)
+    return torch.arange(n2).reshape(2, inter // 8, 8).permute(1, 0, 2).reshape(n2)
+
+
+def pack_swiglu(w: torch.Tensor) -> torch.Tensor:
+    return pack_weight(w[swiglu_rows(w.shape[0]).to(w.device)])
+
+
+FP8 = torch.float8_e4m3fn
+FP8_MAX = 448.0
 
 
 class PackedWeight:
     """A projection weight in skinny-GEMM fragment order (plus its shape).
-    ``swiglu=True``: a fused gate|up weight whose GEMM emits ``silu(g) * u``."""
 
-    __slots__ = ("data", "n", "k", "swiglu")
+    * ``swiglu=True``: a fused gate|up weight whose GEMM emits ``silu(g) * u``;
+    * ``fold``: an RMSNorm weight ``[K]`` folded into the columns (``W * fold``),
+      for GEMMs that apply the norm in their epilogue (``rms=``);
+    * ``fp8=True``: weight-only fp8 (W8A16): OCP e4m3 with one scale per output
+      row, dequantised to bf16 in registers (half the HBM bytes per step)."""
 
-    def __init__(self, w: torch.Tensor, swiglu: bool = False, fold: torch.Tensor | None = None):
-        """``fold``: an RMSNorm weight ``[K]`` folded into the columns (``W * fold``),
-        for GEMMs that apply the norm in their epilogue (``epi="rms"``)."""
+    __slots__ = ("data", "n", "k", "swiglu", "fp8", "wscale")
+
+    def __init__(self, w: torch.Tensor, swiglu: bool = False, fold: torch.Tensor | None = None, fp8: bool = False):
         self.n, self.k = w.shape
-        self.swiglu = swiglu
+        self.swiglu, self.fp8 = swiglu, fp8
+        rows = swiglu_rows(self.n).to(w.device) if swiglu else None
         if fold is not None:
             w = w.float() * fold.float()[None, :]
-        w = w.to(torch.bfloat16)
-        self.data = pack_swiglu(w) if swiglu else pack_weight(w)
+        if fp8:
+            wf = w.float()
+            scale = wf.abs().amax(1).clamp(min=1e-12) / FP8_MAX
+            q = (wf / scale[:, None]).clamp(-FP8_MAX, FP8_MAX).to(FP8).view(torch.uint8)
+            if rows is not None:
+                q, scale = q[rows], scale[rows]
+            self.data = pack_weight(q)
+            self.wscale = scale.float().contiguous()
+        else:
+            w = w.to(torch.bfloat16)
+            self.data = pack_weight(w[rows] if rows is not None else w)
+            self.wscale = None
 
     @property
     def n_out(self) -> int:
         return self.n // 2 if self.swiglu else self.n
 
     def unpacked(self) -> torch.Tensor:
+        """The weight as the kernel sees it (dequantised for fp8), in original row order."""
+        p = unpack_weight(self.data)
+        if self.fp8:
+            p = (p.view(FP8).float() * self.wscale[:, None]).to(torch.bfloat16)
         if self.swiglu:
-            p = unpack_weight(self.data)
-            inter = self.n // 2
-            return p.reshape(inter // 8, 2, 8, self.k).permute(1, 0, 2, 3).reshape(self.n, self.k)
-        return unpack_weight(self.data)
+            inv = torch.empty(self.n, dtype=torch.long, device=p.device)
+            inv[swiglu_rows(self.n).to(p.device)] = torch.arange(self.n, device=p.device)
+            p = p[inv]
+        return p
 
 
 # tile variants of native/kernels/decode.hip (id -> (R W-row tiles per wave,
@@ -210,6 +234,8 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
     m, k = x.shape
     if k != w.k:
         raise ValueError(f"inner dims differ: x {tuple(x.shape)} vs W [{w.n}, {w.k}]")
+    if w.fp8 and _mt(m) > 4:
+        raise ValueError("fp8 (W8A16) skinny GEMM covers batches <= 64")
     if variant == 0 and ksplit is None:
         variant, ks = skinny_config(m, w.n, k)
     else:
@@ -232,8 +258,8 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
         w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(), cnt.data_ptr(), m, w.n, k, x.stride(0),
         out.stride(0), ks, variant, epi, rms.data_ptr() if rms is not None else None,
         resid_ss.data_ptr() if resid_ss is not None else None, zero.data_ptr() if zero is not None else None,
-        1.0 / k, float(eps), _lib.stream_handle(x.device))
-    _lib.check(rc, f"skinny_gemm[{m}x{w.n}x{k}, variant={variant}, ksplit={ks}, epi={epi}]")
+        1.0 / k, float(eps), w.wscale.data_ptr() if w.fp8 else None, _lib.stream_handle(x.device))
+    _lib.check(rc, f"skinny_gemm[{m}x{w.n}x{k}, variant={variant}, ksplit={ks}, epi={epi}, fp8={w.fp8}]")
     return out
 
 
@@ -333,19 +359,21 @@ def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tab
         pps, nsplit = pages_per_split, math.ceil(max_pages / pages_per_split)
     if out is None:
         out = torch.empty((b, heads * HEAD_DIM), dtype=torch.bfloat16, device=q.device)
-    po = pml = None
+    po = pml = cnt = None
     if nsplit > 1:
         need = b * heads * nsplit
         key = q.device.index
-        po, pml = _AWS.get(key, (None, None))
-        if po is None or po.numel() < need * HEAD_DIM:
-            po = torch.empty(need * HEAD_DIM, dtype=torch.float32, device=q.device)
-            pml = torch.empty(need * 2, dtype=torch.float32, device=q.device)
-            _AWS[key] = (po, pml)
+        po, pml, cnt = _AWS.get(key, (None, None, None))
+        if po is None or po.numel() < need * HEAD_DIM or cnt.numel() < b * kv_heads:
+            po = torch.empty(max(need, 1 << 14) * HEAD_DIM, dtype=torch.float32, device=q.device)
+            pml = torch.empty(max(need, 1 << 14) * 2, dtype=torch.float32, device=q.device)
+            cnt = torch.zeros(max(b * kv_heads, 4096), dtype=torch.int32, device=q.device)
+            _AWS[key] = (po, pml, cnt)
     scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
     rc = _lib.lib().kgs_paged_decode_bf16(q.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(),
                                           ctx_lens.data_ptr(), out.data_ptr(), po.data_ptr() if po is not None else None,
-                                          pml.data_ptr() if pml is not None else None, b, heads, kv_heads, HEAD_DIM,
+                                          pml.data_ptr() if pml is not None else None,
+                                          cnt.data_ptr() if cnt is not None else None, b, heads, kv_heads, HEAD_DIM,
                                           max_pages, pps, nsplit, q.stride(0), out.stride(0), float(scale),
                                           _lib.stream_handle(q.device))
     _lib.check(rc, "paged_decode_attention")

@@ -32,7 +32,8 @@ def run_engine(a) -> dict:
 
     mc = LlamaConfig.llama3_8b(layers=a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
-                      max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch)
+                      max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
+                      decode_weights=a.decode_weights)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -62,7 +63,7 @@ def run_engine(a) -> dict:
         "metric": "offline serving throughput (kgs.serve, Llama-3-8B arch, random init)",
         "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
-        "fused_max_batch": a.fused_max_batch,
+        "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
@@ -115,6 +116,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--fused-max-batch", type=int, default=32,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
+    ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")
     ap.add_argument("--hf-only", action="store_true")
     a = ap.parse_args(argv)

@@ -59,6 +59,7 @@ class EngineConfig:
     eos_token_id: int = 2
     cuda_graphs: bool = True
     fused_max_batch: int = 32         # decode batches up to this use the fused skinny-GEMM layer (measured crossover)
+    decode_weights: str = "bf16"      # "fp8": weight-only fp8 decode copies (W8A16)
     seed: int = 0
 
 
@@ -78,7 +79,8 @@ class LLMEngine:
         self.backend = backend
         num_pages = cfg.num_pages or self._pages_from_memory(model_cfg)
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
-                                  max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch)
+                                  max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
+                                  decode_weights=cfg.decode_weights)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
@@ -100,7 +102,7 @@ class LLMEngine:
         per_layer = h * (h + 2 * kvd) + h * h + 2 * h * i + i * h
         weights = 2 * (mc.layers * per_layer + 2 * mc.vocab * h)
         # the kgs backend keeps prefill-order and prepacked decode copies of every projection
-        resident = weights * (2 if self.backend == "kgs" else 1)
+        resident = weights * ((1.5 if self.cfg.decode_weights == "fp8" else 2) if self.backend == "kgs" else 1)
         avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
         return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads)))
 

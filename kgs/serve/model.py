@@ -20,6 +20,10 @@ Two step kinds, both driven by the native scheduler's plans
   add_rmsnorm/silu_mul and hipBLASLt, with the skinny GEMM where it measured
   faster (:func:`kgs.ops.decode.use_skinny`).
 
+``decode_weights="fp8"``: the decode copies are weight-only fp8 (W8A16, one
+scale per output row, dequantised in registers), halving the weight bytes a
+decode step streams; prefill and batches above the fused path stay bf16.
+
 ``backend="ref"`` runs the same weights, cache layout and plans through plain
 PyTorch (CPU or GPU) -- the numerics reference for tests.
 
@@ -38,7 +42,8 @@ from kgs.ops import decode as D
 
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
-                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 32):
+                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 32,
+                 decode_weights: str = "bf16"):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -51,15 +56,21 @@ class ServingModel:
         self.w_lm = base.lm_head.w
         self.packed = None
         self.fused_max_batch = fused_max_batch
+        if decode_weights not in ("bf16", "fp8"):
+            raise ValueError(f"decode_weights must be bf16 or fp8, got {decode_weights!r}")
+        self.decode_fp8 = decode_weights == "fp8"
+        if self.decode_fp8:
+            self.fused_max_batch = min(fused_max_batch, 64)  # the W8A16 skinny GEMM covers M <= 64
         if backend == "kgs":
+            f8 = self.decode_fp8
             # decode copies in skinny-GEMM fragment order; the RMSNorm weights
             # in front of qkv / gate|up / lm_head are folded into them (their
             # GEMMs apply the norm in the epilogue), gate|up is SwiGLU-packed
-            self.packed = [{"qkv": D.PackedWeight(lw["qkv"], fold=self.ln1[i]),
-                            "o": D.PackedWeight(lw["o"]),
-                            "gate_up": D.PackedWeight(lw["gate_up"], swiglu=True, fold=self.ln2[i]),
-                            "down": D.PackedWeight(lw["down"])} for i, lw in enumerate(self.w)]
-            self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm)
+            self.packed = [{"qkv": D.PackedWeight(lw["qkv"], fold=self.ln1[i], fp8=f8),
+                            "o": D.PackedWeight(lw["o"], fp8=f8),
+                            "gate_up": D.PackedWeight(lw["gate_up"], swiglu=True, fold=self.ln2[i], fp8=f8),
+                            "down": D.PackedWeight(lw["down"], fp8=f8)} for i, lw in enumerate(self.w)]
+            self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm, fp8=f8)
             D.reserve_workspace(self.device)
         self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device)
         self.max_model_len = max_model_len
@@ -77,7 +88,8 @@ class ServingModel:
         if self.backend == "ref":
             return (x.float() @ w.float().T).to(torch.bfloat16)
         m = x.shape[0]
-        if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]):
+        if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]) and \
+                not (self.decode_fp8 and m > 64):
             return D.skinny_gemm(x, self.packed[layer][name])
         if decode:
             return torch.matmul(x, w.T)

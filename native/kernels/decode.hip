@@ -21,9 +21,12 @@
 //                   takes the S^T accumulator as its B operand with no lane
 //                   movement. The cache page layout is the MFMA fragment order
 //                   itself (kv_k_index / kv_v_index) -- 16 contiguous 1 KB loads
-//                   per 32-token page -- and splits are merged by a small
-//                   log-sum-exp reduction kernel.
+//                   per 32-token page, the next page's loads in flight under
+//                   the current page's math -- and context splits are merged
+//                   (log-sum-exp) by the split that finishes last, in-launch.
 #include "kgs_common.h"
+
+#include <type_traits>
 
 namespace kgs {
 namespace dec {
@@ -98,16 +101,41 @@ struct SkinnyEpi {
   float* ss_out;
   float* ss_zero;
   float inv_k, eps;
+  const float* wscale;  // W8: per packed row dequant scale
 };
 
-template <int R, int MT, int KC_>
-__global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void skinny(const bf16x8* __restrict__ wp, const unsigned short* __restrict__ x,
+// W8 (weight-only fp8, "W8A16"): W is OCP e4m3 in the same fragment order, 8 B
+// per lane per fragment (512 B wave loads: half the HBM bytes), dequantised to
+// bf16 in registers (v_cvt_pk_f32_fp8, times the lane's row scale, RNE to
+// bf16); x, the MFMA and every epilogue stay bf16/fp32.
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <bool W8>
+using WFrag = typename std::conditional<W8, u32x2, bf16x8>::type;
+
+__device__ __forceinline__ bf16x8 dequant8(u32x2 v, float s) {
+  bf16x8 o;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[w], false);  // bytes 0, 1
+    const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v[w], true);   // bytes 2, 3
+    o[4 * w + 0] = (short)f2bf(lo[0] * s);
+    o[4 * w + 1] = (short)f2bf(lo[1] * s);
+    o[4 * w + 2] = (short)f2bf(hi[0] * s);
+    o[4 * w + 3] = (short)f2bf(hi[1] * s);
+  }
+  return o;
+}
+
+template <int R, int MT, int KC_, bool W8 = false>
+__global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void skinny(const void* __restrict__ wpv, const unsigned short* __restrict__ x,
                                                  unsigned short* __restrict__ y, float* __restrict__ ws,
                                                  int* __restrict__ cnt, int M, int N, int K, long ldx, long ldy,
                                                  int ksplit, int chunks_per_split, SkinnyEpi ep) {
   using C = SkinnyCfg<MT, KC_>;
   constexpr int KC = C::KC;
-  constexpr int PF = KC < 8 ? KC : 8;  // W ring depth in k-steps (divides KC)
+  // W ring depth in k-steps (divides KC); fp8 fragments are half the bytes, so
+  // twice the depth keeps the same bytes in flight
+  constexpr int PF = KC < (W8 ? 16 : 8) ? KC : (W8 ? 16 : 8);
   // the only __shared__ object (a second one can make hipcc drain vmcnt before
   // every ds_read, cdna_hip_programming.md s5 trap 4a); the split-K "last
   // arriver" flag reuses its first word after the main loop
@@ -121,9 +149,14 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   const int kk0 = split * chunks_per_split * KC;
   const int nsteps = chunks_per_split * KC;  // k-steps (of 32) for this workgroup
   const int nt0 = (strip * 4 + w) * R;       // first 16-row tile of this wave
-  const bf16x8* wrow[R];
+  const WFrag<W8>* wp = (const WFrag<W8>*)wpv;
+  const WFrag<W8>* wrow[R];
+  float wsc[R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) wrow[r] = wp + ((long)(nt0 + r) * nkk + kk0) * 64 + lane;
+  for (int r = 0; r < R; ++r) {
+    wrow[r] = wp + ((long)(nt0 + r) * nkk + kk0) * 64 + lane;
+    wsc[r] = W8 ? ep.wscale[16 * (nt0 + r) + (lane & 15)] : 1.f;
+  }
 
   // x chunk staging: element e = tid + 256 i of the chunk, row-major over
   // (row m, 16-B column q) so global reads are whole-row runs; the LDS position
@@ -157,7 +190,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   // Every load below is unconditional (indices clamped to the last step /
   // chunk: a few redundant L2-hit reloads at the tail) so hipcc can count
   // vmcnt through the loop instead of draining the ring before each MFMA.
-  bf16x8 wf[PF][R];
+  WFrag<W8> wf[PF][R];
 #pragma unroll
   for (int p = 0; p < PF; ++p)
 #pragma unroll
@@ -173,12 +206,18 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       const int p = kk % PF;
+      bf16x8 wdq[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (W8) wdq[r] = dequant8(wf[p][r], wsc[r]);
+        else wdq[r] = wf[p][r];
+      }
 #pragma unroll
       for (int c = 0; c < MT; ++c) {
         const bf16x8 bfrag = xb[(kk * MT + c) * 64];
 #pragma unroll
         for (int r = 0; r < R; ++r)
-          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[p][r], bfrag, acc[r][c], 0, 0, 0);
+          acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wdq[r], bfrag, acc[r][c], 0, 0, 0);
       }
       const long sn = min(chunk * KC + kk + PF, nsteps - 1);
 #pragma unroll
@@ -355,11 +394,28 @@ struct AttnArgs {
   unsigned short* o;            // [B, ldo]
   float* po;                    // [B, H, nsplit, 128] (nsplit > 1)
   float* pml;                   // [B, H, nsplit, 2]
+  int* cnt;                     // [B * HKV] split tickets (nsplit > 1), zero / re-armed
   long ldq, ldo;
   int B, H, HKV, max_pages, pages_per_split, nsplit;
   float sl2;                    // scale * log2(e)
 };
 
+// store O^T[dim 16dt + 4g + i][head] * inv for the lane's head
+__device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, float inv) {
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) {
+    uint2 pk;
+    pk.x = pack_bf16x2(acc[dt][0] * inv, acc[dt][1] * inv);
+    pk.y = pack_bf16x2(acc[dt][2] * inv, acc[dt][3] * inv);
+    *(uint2*)(op + 16 * dt) = pk;
+  }
+}
+
+// One wave per (sequence, KV head, context split). The page loop is software
+// pipelined: the next page's 16 K/V fragment loads are in flight while the
+// current page's MFMAs and softmax run. With nsplit > 1 the partial (m, l, O)
+// go to a workspace and the split that arrives last (agent-scope ticket per
+// (sequence, KV head)) merges them -- no separate reduction launch.
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int lane = threadIdx.x;
   const int G = a.H / a.HKV;
@@ -384,15 +440,24 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qp + 32 * ks) : bf16x8{};
     const int* bt = a.block_tables + (long)b * a.max_pages;
-    for (int pi = p0; pi < p1; ++pi) {
-      const long pg = bt[pi];
-      const bf16x8* kp = (const bf16x8*)(a.cache + ((pg * a.HKV + kvh) * 2) * PAGE_ELEMS) + lane;
-      const bf16x8* vp = kp + PAGE_ELEMS / 8;
-      bf16x8 kf[8], vf[8];
+    auto page_ptr = [&](int pi) {
+      return (const bf16x8*)(a.cache + (((long)bt[pi] * a.HKV + kvh) * 2) * PAGE_ELEMS) + lane;
+    };
+    bf16x8 kf[8], vf[8], kn[8], vn[8];
+    {
+      const bf16x8* kp = page_ptr(p0);
 #pragma unroll
       for (int i = 0; i < 8; ++i) kf[i] = __builtin_nontemporal_load(kp + 64 * i);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(vp + 64 * i);
+      for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
+    }
+    for (int pi = p0; pi < p1; ++pi) {
+      // prefetch page pi+1 (clamped: the last iteration re-reads its own page, an L2 hit)
+      const bf16x8* kp = page_ptr(min(pi + 1, p1 - 1));
+#pragma unroll
+      for (int i = 0; i < 8; ++i) kn[i] = __builtin_nontemporal_load(kp + 64 * i);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) vn[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
       f32x4v s[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -432,55 +497,63 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
         acc[dt] *= alpha;
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, acc[dt], 0, 0, 0);
       }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        kf[i] = kn[i];
+        vf[i] = vn[i];
+      }
     }
   }
   lsum = wsum16(lsum);
-  if (n >= G) return;
   // lane holds O^T[dim 16dt + 4g + i][head n]
+  unsigned short* op = a.o + (long)b * a.ldo + (long)h * HD + 4 * g;
   if (a.nsplit == 1) {
-    const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-    unsigned short* op = a.o + (long)b * a.ldo + (long)h * HD + 4 * g;
-#pragma unroll
-    for (int dt = 0; dt < 8; ++dt) {
-      uint2 pk;
-      pk.x = pack_bf16x2(acc[dt][0] * inv, acc[dt][1] * inv);
-      pk.y = pack_bf16x2(acc[dt][2] * inv, acc[dt][3] * inv);
-      *(uint2*)(op + 16 * dt) = pk;
-    }
+    if (n < G) store_o(op, acc, lsum > 0.f ? 1.f / lsum : 0.f);
     return;
   }
-  const long row = ((long)b * a.H + h) * a.nsplit + sp;
-  float* po = a.po + row * HD + 4 * g;
+  const long row = ((long)b * a.H + h) * a.nsplit;  // this head's first split slot
+  if (n < G) {
+    float* po = a.po + (row + sp) * HD + 4 * g;
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) *(f32x4v*)(po + 16 * dt) = acc[dt];
-  if (g == 0) {
-    a.pml[row * 2] = m;
-    a.pml[row * 2 + 1] = lsum;
+    for (int dt = 0; dt < 8; ++dt) *(f32x4v*)(po + 16 * dt) = acc[dt];
+    if (g == 0) {
+      a.pml[(row + sp) * 2] = m;
+      a.pml[(row + sp) * 2 + 1] = lsum;
+    }
   }
-}
-
-// merge nsplit partials (m in log2 units, l, unnormalised O) of one (b, h)
-__global__ __launch_bounds__(64) void paged_reduce(const float* __restrict__ po, const float* __restrict__ pml,
-                                                   unsigned short* __restrict__ o, int H, int nsplit, long ldo) {
-  const int bh = blockIdx.x, lane = threadIdx.x;
-  const int b = bh / H, h = bh - b * H;
-  const float* ml = pml + (long)bh * nsplit * 2;
+  // publish the partial, take a ticket; the last split of (b, kvh) merges
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int last = 0;
+  if (lane == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(a.cnt + (long)b * a.HKV + kvh, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == a.nsplit - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      a.cnt[(long)b * a.HKV + kvh] = 0;  // re-arm for the next (stream-ordered) call
+    }
+  }
+  last = __shfl(last, 0, 64);
+  if (!last || n >= G) return;
   float M = -INFINITY;
-  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
-  float L = 0.f, o0 = 0.f, o1 = 0.f;
-  const float* pb = po + (long)bh * nsplit * HD + 2 * lane;
-#pragma unroll 4
-  for (int s = 0; s < nsplit; ++s) {
-    const float l = ml[2 * s + 1];
+  for (int s2 = 0; s2 < a.nsplit; ++s2) M = fmaxf(M, a.pml[(row + s2) * 2]);
+  float L = 0.f;
+  f32x4v o[8];
+#pragma unroll
+  for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4v{0.f, 0.f, 0.f, 0.f};
+  for (int s2 = 0; s2 < a.nsplit; ++s2) {
+    const float l = a.pml[(row + s2) * 2 + 1];
     if (l <= 0.f) continue;
-    const float f = __builtin_amdgcn_exp2f(ml[2 * s] - M);
+    const float f = __builtin_amdgcn_exp2f(a.pml[(row + s2) * 2] - M);
     L += f * l;
-    const float2 v = *(const float2*)(pb + (long)s * HD);
-    o0 += f * v.x;
-    o1 += f * v.y;
+    const float* ps = a.po + (row + s2) * HD + 4 * g;
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] += f * *(const f32x4v*)(ps + 16 * dt);
   }
-  const float inv = L > 0.f ? 1.f / L : 0.f;
-  *(unsigned*)(o + (long)b * ldo + (long)h * HD + 2 * lane) = pack_bf16x2(o0 * inv, o1 * inv);
+  store_o(op, o, L > 0.f ? 1.f / L : 0.f);
 }
 
 }  // namespace dec
@@ -507,11 +580,11 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 int mt_for(int M) { return M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : M <= 128 ? 8 : 16; }
 int default_variant(int mt) { return mt == 1 ? 1 : mt == 2 ? 4 : mt == 4 ? 8 : mt == 8 ? 13 : 17; }
 
-template <int R, int MT, int KC>
+template <int R, int MT, int KC, bool W8>
 hipError_t launch_skinny(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx,
                          long ldy, int ksplit, int cps, const kgs::dec::SkinnyEpi& ep, hipStream_t s) {
   const int nstrip = N / (64 * R);
-  hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC>), dim3(nstrip * ksplit), dim3(256), 0, s, (const bf16x8*)wp,
+  hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, W8>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
                      (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
   return hipGetLastError();
 }
@@ -545,7 +618,7 @@ KGS_EXPORT int kgs_skinny_geometry(int M, int* rows_per_strip, int* k_per_chunk,
 KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
                                          int K, long ldx, long ldy, int ksplit, int variant, int epi,
                                          const float* ss_in, float* ss_out, float* ss_zero, float inv_k, float eps,
-                                         hipStream_t s) {
+                                         const float* wscale, hipStream_t s) {
   using namespace kgs::dec;
   int rps, kpc, mpad;
   const int rc = kgs_skinny_variant_geometry(variant, M, &rps, &kpc, &mpad);
@@ -560,10 +633,16 @@ KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y
   if (ksplit > 1 && (ws == nullptr || cnt == nullptr)) return KGS_ERR_ARG;
   if (!al16(wp) || !al16(x) || ((uintptr_t)y & 7) || ((uintptr_t)ws & 15) || ldx % 8 || ldy % 4) return KGS_ERR_ALIGN;
   const int cps = nchunks / ksplit;
-  const SkinnyEpi ep{epi, ss_in, ss_out, ss_zero, inv_k, eps};
-  switch (variant) {
-#define KGS_SKV(id, R, MT, KC) \
-  case id: return (int)launch_skinny<R, MT, KC>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
+  const SkinnyEpi ep{epi, ss_in, ss_out, ss_zero, inv_k, eps, wscale};
+  const bool w8 = wscale != nullptr;
+  if (w8 && variant > 12) return KGS_ERR_ARG;  // fp8 weights: batch buckets <= 64 (variants 1-12)
+  switch (variant * 2 + (w8 ? 1 : 0)) {
+#define KGS_SKV(id, R, MT, KC)                                                                                       \
+  case 2 * id: return (int)launch_skinny<R, MT, KC, false>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s); \
+  case 2 * id + 1:                                                                                                    \
+    if constexpr (id <= 12) return (int)launch_skinny<R, MT, KC, true>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit,  \
+                                                                        cps, ep, s);                                  \
+    return KGS_ERR_ARG;
     KGS_SKV(1, 1, 1, 16) KGS_SKV(2, 1, 1, 8) KGS_SKV(3, 2, 1, 16)
     KGS_SKV(4, 1, 2, 16) KGS_SKV(5, 1, 2, 8) KGS_SKV(6, 2, 2, 8) KGS_SKV(7, 2, 2, 16)
     KGS_SKV(8, 1, 4, 16) KGS_SKV(9, 1, 4, 4) KGS_SKV(10, 1, 4, 8) KGS_SKV(11, 2, 4, 4) KGS_SKV(12, 2, 4, 8)
@@ -577,7 +656,7 @@ KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y
 KGS_EXPORT int kgs_skinny_gemm_bf16_ex(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
                                       int K, long ldx, long ldy, int ksplit, int variant, int epi, hipStream_t s) {
   return kgs_skinny_gemm_bf16_fused(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, variant, epi, nullptr, nullptr,
-                                    nullptr, 0.f, 0.f, s);
+                                    nullptr, 0.f, 0.f, nullptr, s);
 }
 
 KGS_EXPORT int kgs_skinny_gemm_bf16_v(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K,
@@ -608,24 +687,23 @@ KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* si
 // Paged decode attention for one new query token per sequence. q: [B, ldq]
 // (query heads at 128-element blocks); cache: layer base; block_tables
 // [B, max_pages] int32; ctx_lens [B] int32 (>= 1). nsplit > 1 needs po
-// (B*H*nsplit*128 f32) and pml (B*H*nsplit*2 f32) and adds a reduce launch.
+// (B*H*nsplit*128 f32), pml (B*H*nsplit*2 f32) and cnt (B*HKV zeroed ints, left
+// zeroed); the splits are merged in the same launch.
 KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int* block_tables, const int* ctx_lens,
-                                    void* o, float* po, float* pml, int B, int H, int HKV, int hd, int max_pages,
-                                    int pages_per_split, int nsplit, long ldq, long ldo, float scale, hipStream_t s) {
+                                    void* o, float* po, float* pml, int* cnt, int B, int H, int HKV, int hd,
+                                    int max_pages, int pages_per_split, int nsplit, long ldq, long ldo, float scale,
+                                    hipStream_t s) {
   using namespace kgs::dec;
   if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 16 || hd != HD) return KGS_ERR_SHAPE;
   if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0) return KGS_ERR_SHAPE;
   if ((long)pages_per_split * nsplit < max_pages) return KGS_ERR_ARG;
   if (ldq < (long)H * HD || ldo < (long)H * HD) return KGS_ERR_SHAPE;
   if (!al16(q) || !al16(cache) || !al16(o) || ldq % 8 || ldo % 8) return KGS_ERR_ALIGN;
-  if (nsplit > 1 && (po == nullptr || pml == nullptr || !al16(po))) return KGS_ERR_ARG;
+  if (nsplit > 1 && (po == nullptr || pml == nullptr || cnt == nullptr || !al16(po))) return KGS_ERR_ARG;
   const long nwg = (long)B * HKV * nsplit;
   if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
-             pml, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, scale * 1.4426950408889634f};
+             pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, scale * 1.4426950408889634f};
   hipLaunchKernelGGL(paged_decode, dim3((unsigned)nwg), dim3(64), 0, s, a);
-  if (nsplit > 1)
-    hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
-                       ldo);
   return (int)hipGetLastError();
 }

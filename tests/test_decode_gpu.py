@@ -238,3 +238,35 @@ def test_skinny_fused_rms_and_residual_epilogues(m):
         assert (res.float() - new_ref).abs().max().item() <= 2e-2 * new_ref.abs().max().item()
         assert torch.allclose(ss_out, res.float().pow(2).sum(-1), rtol=1e-4, atol=1e-3)
         assert junk.abs().max().item() == 0
+
+
+@pytest.mark.parametrize("m", [1, 30, 64])
+def test_skinny_fp8_weights(m):
+    """W8A16: e4m3 weights with per-row scales, dequantised in registers; with and
+    without the fused epilogues, against fp32 math on the dequantised weight."""
+    from kgs.ops.decode import PackedWeight, choose_ksplit, skinny_gemm, skinny_variants
+
+    n, k = 768, 2048
+    x = _bf(m, k)
+    w = _bf(n, k, scale=k ** -0.5)
+    pw = PackedWeight(w, fp8=True)
+    wd = pw.unpacked().float()
+    assert (wd - w.float()).abs().max().item() <= 0.07 * w.float().abs().max().item()
+    ref = x.float() @ wd.T
+    for v in skinny_variants(m):
+        for ks in sorted({1, choose_ksplit(m, n, k, variant=v)}):
+            y = skinny_gemm(x, pw, ksplit=ks, variant=v)
+            torch.cuda.synchronize()
+            assert (y.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item() + 1e-3, (v, ks)
+    # SwiGLU + folded RMSNorm on fp8 weights
+    lnw = (_bf(k, scale=0.2) + 1).contiguous()
+    wgu = _bf(2 * n, k, scale=k ** -0.5)
+    pgu = PackedWeight(wgu, swiglu=True, fold=lnw, fp8=True)
+    wgd = pgu.unpacked().float()  # folded + dequantised, original row order
+    ss = x.float().pow(2).sum(-1)
+    xn = x.float() * torch.rsqrt(ss / k + 1e-5)[:, None]
+    g, u = xn @ wgd[:n].T, xn @ wgd[n:].T
+    ref2 = g * torch.sigmoid(g) * u
+    y2 = skinny_gemm(x, pgu, rms=ss)
+    torch.cuda.synchronize()
+    assert (y2.float() - ref2).abs().max().item() <= 3e-2 * ref2.abs().max().item()

@@ -230,3 +230,26 @@ def test_byte_tokenizer_roundtrip():
     t = ByteTokenizer()
     ids = t.encode("héllo ✓")
     assert ids[0] == t.BOS and t.decode(ids) == "héllo ✓"
+
+
+def test_decode_routing_tables_cpu():
+    """The decode GEMM routing/geometry helpers (pure Python, mirrored by decode.hip)."""
+    from kgs.ops import decode as D
+
+    for m in (1, 16, 17, 32, 33, 64, 65, 128, 129, 256):
+        vs = D.skinny_variants(m)
+        assert vs and all(D.SKINNY_VARIANTS[v][1] == D._mt(m) for v in vs)
+        for v in vs:
+            rps, kpc, mpad = D.skinny_geometry(m, v)
+            assert rps % 64 == 0 and kpc % 32 == 0 and mpad >= m
+    for key, val in D.TUNED.items():
+        if val is not None:
+            v, ks = val
+            assert D.SKINNY_VARIANTS[v][1] == key[0]
+            _, kpc, _ = D.skinny_geometry(16 * key[0], v)
+            assert (key[2] // kpc) % ks == 0, key
+    assert D.use_skinny(1, 6144, 4096) and not D.use_skinny(256, 6144, 4096)
+    assert D.use_skinny(20, 512, 1024) and not D.use_skinny(40, 512, 1024)
+    assert D.skinny_config(16, 4096, 4096) == D.TUNED[(1, 4096, 4096)]
+    pps, ns = D.decode_splits(1, 8, 128)
+    assert pps >= 4 and pps * ns >= 128

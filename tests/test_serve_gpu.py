@@ -93,3 +93,15 @@ def test_equal_length_prefill_batched_attention():
     prompts = [rng.integers(3, 1024, size=n).tolist() for n in (90, 120, 128, 100)]  # all pad to 128
     outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
     _oracle_check(eng, prompts, outs)
+
+
+def test_fp8_decode_weights_engine():
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(5)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (40, 70)]
+    eng = _engine(True, decode_weights="fp8")
+    outs = eng.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    assert all(len(r.output) == 6 for r in outs)
+    # weight-only fp8: the chosen tokens stay near the bf16 oracle's top logit
+    _oracle_check(eng, prompts, outs, tol=0.12)
