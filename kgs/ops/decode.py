@@ -136,6 +136,14 @@ TUNED: dict = {
     (8, *_QKV): None, (8, *_O): None, (8, *_GU): None, (8, *_DOWN): (16, 4), (8, *_LM): None,
     (16, *_QKV): None, (16, *_O): None, (16, *_GU): None, (16, *_DOWN): None, (16, *_LM): None,
 }
+# the same sweep for weight-only fp8 (--tune --fp8): (variant, ksplit) per (MT, N, K)
+TUNED_FP8: dict = {
+    (1, *_QKV): (1, 2), (2, *_QKV): (7, 4), (4, *_QKV): (12, 4),
+    (1, *_O): (1, 4), (2, *_O): (5, 4), (4, *_O): (9, 4),
+    (1, *_GU): (1, 1), (2, *_GU): (7, 1), (4, *_GU): (12, 1),
+    (1, *_DOWN): (1, 4), (2, *_DOWN): (7, 7), (4, *_DOWN): (12, 8),
+    (1, *_LM): (1, 1), (2, *_LM): (6, 1), (4, *_LM): (11, 1),
+}
 SKINNY_DEFAULT_MAX_M = 32  # untuned shapes: skinny GEMM up to this batch, hipBLASLt above
 
 
@@ -177,9 +185,9 @@ def choose_ksplit(m: int, n: int, k: int, cus: int = CUS, variant: int = 0) -> i
     return best
 
 
-def skinny_config(m: int, n: int, k: int) -> tuple[int, int]:
+def skinny_config(m: int, n: int, k: int, fp8: bool = False) -> tuple[int, int]:
     """(variant, ksplit) for a skinny-GEMM call: the tuned entry, else the defaults."""
-    hit = TUNED.get((_mt(m), n, k))
+    hit = (TUNED_FP8 if fp8 else TUNED).get((_mt(m), n, k))
     if hit is not None:
         return hit
     v = _DEFAULT_VARIANT[_mt(m)]
@@ -237,7 +245,7 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
     if w.fp8 and _mt(m) > 4:
         raise ValueError("fp8 (W8A16) skinny GEMM covers batches <= 64")
     if variant == 0 and ksplit is None:
-        variant, ks = skinny_config(m, w.n, k)
+        variant, ks = skinny_config(m, w.n, k, fp8=w.fp8)
     else:
         ks = ksplit if ksplit is not None else choose_ksplit(m, w.n, k, variant=variant)
     rps, kpc, mpad = skinny_geometry(m, variant)

@@ -60,6 +60,30 @@ __device__ __forceinline__ float wsum16(float v) {
   return v + __shfl_xor(v, 32, 64);
 }
 
+// In-launch hand-offs (split-K slabs, attention split partials): producers store
+// WRITE-THROUGH (sc1 buffer stores) and drain, so they need no release fence (a
+// release is a buffer_wbl2 of the whole XCD L2 per wave: decode attention ran
+// 8x slower with one per split); the single consumer (last arriver) takes ONE
+// agent-scope acquire before reading -- without it a reader on another XCD sees
+// stale lines of a reused workspace (measured: wrong merges whenever splits
+// landed on different XCDs). cdna_hip_programming.md Guideline 16, recipe R1.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4v v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);
+}
+__device__ __forceinline__ f32x4v ld_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+__device__ __forceinline__ void st1_sc1(__amdgpu_buffer_rsrc_t r, unsigned off, float a) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, a), r, off, 0, 16);
+}
+__device__ __forceinline__ float ld1_sc1(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16));
+}
+
 // ---------------------------------------------------------------------------
 // skinny GEMM
 // ---------------------------------------------------------------------------
@@ -278,10 +302,11 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
       for (int r = 0; r < R; ++r) emit(acc[r][c], 16 * c + mc, r);
     return;
   }
-  // split-K: fp32 slabs ws[split][m][n]; the last arriver of the strip reduces.
-  // Publish = plain stores, vmcnt(0), barrier, agent-scope release, ticket
-  // (cdna_hip_programming.md s5 "In-launch split-K reduction").
+  // split-K: fp32 slabs ws[split][m][n] stored write-through (sc1); every wave
+  // drains, the workgroup takes a ticket; the last arriver of the strip reads
+  // every slab with sc1 loads and reduces -- no release/acquire fences.
   const long mstride = N, sstride = (long)16 * MT * N;
+  const __amdgpu_buffer_rsrc_t wr = rsrc(ws, (unsigned)(ksplit * sstride * 4));
 #pragma unroll
   for (int c = 0; c < MT; ++c) {
     const int m = 16 * c + mc;
@@ -289,7 +314,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int n = 16 * (nt0 + r) + 4 * g;
-        *(f32x4v*)(ws + split * sstride + m * mstride + n) = acc[r][c];
+        st_sc1(wr, (unsigned)((split * sstride + m * mstride + n) * 4), acc[r][c]);
       }
     }
   }
@@ -297,14 +322,12 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   __syncthreads();
   int* flag = (int*)&xs[0][0];
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(cnt + strip, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == ksplit - 1;
     if (last) {
+      __hip_atomic_store(cnt + strip, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      cnt[strip] = 0;  // re-arm the ticket for the next (stream-ordered) call
     }
     *flag = last;
   }
@@ -318,7 +341,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     for (int r = 0; r < R; ++r) {
       const int n = 16 * (nt0 + r) + 4 * g;
       f32x4v t = f32x4v{0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < ksplit; ++sp) t += *(const f32x4v*)(ws + sp * sstride + ms * mstride + n);
+      for (int sp = 0; sp < ksplit; ++sp) t += ld_sc1(wr, (unsigned)((sp * sstride + ms * mstride + n) * 4));
       emit(t, m, r);
     }
   }
@@ -443,21 +466,14 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
     auto page_ptr = [&](int pi) {
       return (const bf16x8*)(a.cache + (((long)bt[pi] * a.HKV + kvh) * 2) * PAGE_ELEMS) + lane;
     };
-    bf16x8 kf[8], vf[8], kn[8], vn[8];
-    {
-      const bf16x8* kp = page_ptr(p0);
+    auto load_page = [&](bf16x8 (&kf)[8], bf16x8 (&vf)[8], int pi) {
+      const bf16x8* kp = page_ptr(pi);
 #pragma unroll
       for (int i = 0; i < 8; ++i) kf[i] = __builtin_nontemporal_load(kp + 64 * i);
 #pragma unroll
       for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
-    }
-    for (int pi = p0; pi < p1; ++pi) {
-      // prefetch page pi+1 (clamped: the last iteration re-reads its own page, an L2 hit)
-      const bf16x8* kp = page_ptr(min(pi + 1, p1 - 1));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) kn[i] = __builtin_nontemporal_load(kp + 64 * i);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) vn[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
+    };
+    auto page = [&](const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], int pi) {
       f32x4v s[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -497,11 +513,16 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
         acc[dt] *= alpha;
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, acc[dt], 0, 0, 0);
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        kf[i] = kn[i];
-        vf[i] = vn[i];
-      }
+    };
+    // two register sets alternate: one page's loads fly while the other's math runs
+    bf16x8 ka[8], va[8], kb[8], vb[8];
+    load_page(ka, va, p0);
+    for (int pi = p0; pi < p1; pi += 2) {
+      load_page(kb, vb, min(pi + 1, p1 - 1));  // clamped: a last odd page re-reads itself (L2 hit)
+      page(ka, va, pi);
+      if (pi + 1 >= p1) break;
+      load_page(ka, va, min(pi + 2, p1 - 1));
+      page(kb, vb, pi + 1);
     }
   }
   lsum = wsum16(lsum);
@@ -512,46 +533,46 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
     return;
   }
   const long row = ((long)b * a.H + h) * a.nsplit;  // this head's first split slot
+  const long nrows = (long)a.B * a.H * a.nsplit;
+  const __amdgpu_buffer_rsrc_t por = rsrc(a.po, (unsigned)(nrows * HD * 4));
+  const __amdgpu_buffer_rsrc_t mlr = rsrc(a.pml, (unsigned)(nrows * 8));
   if (n < G) {
-    float* po = a.po + (row + sp) * HD + 4 * g;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) *(f32x4v*)(po + 16 * dt) = acc[dt];
+    for (int dt = 0; dt < 8; ++dt) st_sc1(por, (unsigned)(((row + sp) * HD + 16 * dt + 4 * g) * 4), acc[dt]);
     if (g == 0) {
-      a.pml[(row + sp) * 2] = m;
-      a.pml[(row + sp) * 2 + 1] = lsum;
+      st1_sc1(mlr, (unsigned)((row + sp) * 8), m);
+      st1_sc1(mlr, (unsigned)((row + sp) * 8 + 4), lsum);
     }
   }
-  // publish the partial, take a ticket; the last split of (b, kvh) merges
+  // publish (write-through stores drained), take a ticket; the last split of
+  // (b, kvh) merges with sc1 loads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int last = 0;
   if (lane == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int prev = __hip_atomic_fetch_add(a.cnt + (long)b * a.HKV + kvh, 1, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == a.nsplit - 1;
+    int* c = a.cnt + (long)b * a.HKV + kvh;
+    last = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == a.nsplit - 1;
     if (last) {
+      __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      a.cnt[(long)b * a.HKV + kvh] = 0;  // re-arm for the next (stream-ordered) call
     }
   }
   last = __shfl(last, 0, 64);
   if (!last || n >= G) return;
   float M = -INFINITY;
-  for (int s2 = 0; s2 < a.nsplit; ++s2) M = fmaxf(M, a.pml[(row + s2) * 2]);
+  for (int s2 = 0; s2 < a.nsplit; ++s2) M = fmaxf(M, ld1_sc1(mlr, (unsigned)((row + s2) * 8)));
   float L = 0.f;
   f32x4v o[8];
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4v{0.f, 0.f, 0.f, 0.f};
   for (int s2 = 0; s2 < a.nsplit; ++s2) {
-    const float l = a.pml[(row + s2) * 2 + 1];
-    if (l <= 0.f) continue;
-    const float f = __builtin_amdgcn_exp2f(a.pml[(row + s2) * 2] - M);
-    L += f * l;
-    const float* ps = a.po + (row + s2) * HD + 4 * g;
+    const float ms = ld1_sc1(mlr, (unsigned)((row + s2) * 8));
+    const float ls = ld1_sc1(mlr, (unsigned)((row + s2) * 8 + 4));
+    if (ls <= 0.f) continue;
+    const float f = __builtin_amdgcn_exp2f(ms - M);
+    L += f * ls;
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) o[dt] += f * *(const f32x4v*)(ps + 16 * dt);
+    for (int dt = 0; dt < 8; ++dt) o[dt] += f * ld_sc1(por, (unsigned)(((row + s2) * HD + 16 * dt + 4 * g) * 4));
   }
   store_o(op, o, L > 0.f ? 1.f / L : 0.f);
 }

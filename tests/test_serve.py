@@ -253,3 +253,13 @@ def test_decode_routing_tables_cpu():
     assert D.skinny_config(16, 4096, 4096) == D.TUNED[(1, 4096, 4096)]
     pps, ns = D.decode_splits(1, 8, 128)
     assert pps >= 4 and pps * ns >= 128
+
+
+def test_fp8_routing_table_cpu():
+    from kgs.ops import decode as D
+
+    for key, (v, ks) in D.TUNED_FP8.items():
+        assert v <= 12 and D.SKINNY_VARIANTS[v][1] == key[0]  # fp8 kernels exist for variants 1-12
+        _, kpc, _ = D.skinny_geometry(16 * key[0], v)
+        assert (key[2] // kpc) % ks == 0
+    assert D.skinny_config(1, 28672, 4096, fp8=True) == D.TUNED_FP8[(1, 28672, 4096)]
