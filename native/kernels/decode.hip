@@ -21,8 +21,7 @@
 //                   takes the S^T accumulator as its B operand with no lane
 //                   movement. The cache page layout is the MFMA fragment order
 //                   itself (kv_k_index / kv_v_index) -- 16 contiguous 1 KB loads
-//                   per 32-token page, the next page's loads in flight under
-//                   the current page's math -- and context splits are merged
+//                   per 32-token page -- and context splits are merged
 //                   (log-sum-exp) by the split that finishes last, in-launch.
 #include "kgs_common.h"
 
@@ -417,9 +416,10 @@ struct AttnArgs {
   unsigned short* o;            // [B, ldo]
   float* po;                    // [B, H, nsplit, 128] (nsplit > 1)
   float* pml;                   // [B, H, nsplit, 2]
-  int* cnt;                     // [B * HKV] split tickets (nsplit > 1), zero / re-armed
+  int* cnt;                     // [B * HKV] split tickets (in-launch merge), zero / re-armed
   long ldq, ldo;
   int B, H, HKV, max_pages, pages_per_split, nsplit;
+  int merge;                    // nsplit > 1: 1 = last split merges in-launch, 0 = paged_reduce follows
   float sl2;                    // scale * log2(e)
 };
 
@@ -434,9 +434,7 @@ __device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, f
   }
 }
 
-// One wave per (sequence, KV head, context split). The page loop is software
-// pipelined: the next page's 16 K/V fragment loads are in flight while the
-// current page's MFMAs and softmax run. With nsplit > 1 the partial (m, l, O)
+// One wave per (sequence, KV head, context split). With nsplit > 1 the partial (m, l, O)
 // go to a workspace and the split that arrives last (agent-scope ticket per
 // (sequence, KV head)) merges them -- no separate reduction launch.
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
@@ -514,15 +512,13 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, acc[dt], 0, 0, 0);
       }
     };
-    // two register sets alternate: one page's loads fly while the other's math runs
-    bf16x8 ka[8], va[8], kb[8], vb[8];
-    load_page(ka, va, p0);
-    for (int pi = p0; pi < p1; pi += 2) {
-      load_page(kb, vb, min(pi + 1, p1 - 1));  // clamped: a last odd page re-reads itself (L2 hit)
-      page(ka, va, pi);
-      if (pi + 1 >= p1) break;
-      load_page(ka, va, min(pi + 2, p1 - 1));
-      page(kb, vb, pi + 1);
+    // one page at a time: the loads of other waves on the SIMD hide this one's
+    // latency (a two-register-set pipeline measured slower: 208 VGPRs cost a
+    // wave of occupancy, 47 -> 59 us at batch 64 x 1024)
+    for (int pi = p0; pi < p1; ++pi) {
+      bf16x8 kf[8], vf[8];
+      load_page(kf, vf, pi);
+      page(kf, vf, pi);
     }
   }
   lsum = wsum16(lsum);
@@ -544,6 +540,7 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
       st1_sc1(mlr, (unsigned)((row + sp) * 8 + 4), lsum);
     }
   }
+  if (!a.merge) return;  // paged_reduce merges after the kernel boundary
   // publish (write-through stores drained), take a ticket; the last split of
   // (b, kvh) merges with sc1 loads
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -575,6 +572,34 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
     for (int dt = 0; dt < 8; ++dt) o[dt] += f * ld_sc1(por, (unsigned)(((row + s2) * HD + 16 * dt + 4 * g) * 4));
   }
   store_o(op, o, L > 0.f ? 1.f / L : 0.f);
+}
+
+// merge nsplit partials (m in log2 units, l, unnormalised O) of one (b, h):
+// the launch-boundary variant, for batches with many (sequence, KV head)
+// groups -- there an in-launch last-arriver merge costs one L2-invalidating
+// acquire per group (measured 47 -> 58 us at batch 64 x 1024)
+__global__ __launch_bounds__(64) void paged_reduce(const float* __restrict__ po, const float* __restrict__ pml,
+                                                   unsigned short* __restrict__ o, int H, int nsplit, long ldo) {
+  const int bh = blockIdx.x, lane = threadIdx.x;
+  const int b = bh / H, h = bh - b * H;
+  const float* ml = pml + (long)bh * nsplit * 2;
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, ml[2 * s]);
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+  // the writer stores O^T in 16-dim tiles: lane's dims d = 2*lane, 2*lane + 1
+  const float* pb = po + (long)bh * nsplit * HD + 2 * lane;
+#pragma unroll 4
+  for (int s = 0; s < nsplit; ++s) {
+    const float l = ml[2 * s + 1];
+    if (l <= 0.f) continue;
+    const float f = __builtin_amdgcn_exp2f(ml[2 * s] - M);
+    L += f * l;
+    const float2 v = *(const float2*)(pb + (long)s * HD);
+    o0 += f * v.x;
+    o1 += f * v.y;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  *(unsigned*)(o + (long)b * ldo + (long)h * HD + 2 * lane) = pack_bf16x2(o0 * inv, o1 * inv);
 }
 
 }  // namespace dec
@@ -720,11 +745,17 @@ KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int
   if ((long)pages_per_split * nsplit < max_pages) return KGS_ERR_ARG;
   if (ldq < (long)H * HD || ldo < (long)H * HD) return KGS_ERR_SHAPE;
   if (!al16(q) || !al16(cache) || !al16(o) || ldq % 8 || ldo % 8) return KGS_ERR_ALIGN;
-  if (nsplit > 1 && (po == nullptr || pml == nullptr || cnt == nullptr || !al16(po))) return KGS_ERR_ARG;
+  if (nsplit > 1 && (po == nullptr || pml == nullptr || !al16(po))) return KGS_ERR_ARG;
   const long nwg = (long)B * HKV * nsplit;
   if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
+  // in-launch merge only when there are few (sequence, KV head) groups: it saves
+  // the reduce launch but costs each group's last split an acquire
+  const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
-             pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, scale * 1.4426950408889634f};
+             pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
   hipLaunchKernelGGL(paged_decode, dim3((unsigned)nwg), dim3(64), 0, s, a);
+  if (nsplit > 1 && !merge)
+    hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
+                       ldo);
   return (int)hipGetLastError();
 }
