@@ -130,18 +130,18 @@ _DEFAULT_VARIANT = {1: 1, 2: 4, 4: 8, 8: 13, 16: 17}
 # lm_head 128256x4096.
 _QKV, _O, _GU, _DOWN, _LM = (6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)
 TUNED: dict = {
-    (1, *_QKV): (1, 1), (1, *_O): (1, 2), (1, *_GU): (2, 1), (1, *_DOWN): (1, 4), (1, *_LM): (1, 1),
-    (2, *_QKV): (6, 4), (2, *_O): (6, 4), (2, *_GU): (6, 1), (2, *_DOWN): (4, 4), (2, *_LM): (5, 1),
-    (4, *_QKV): None, (4, *_O): None, (4, *_GU): (12, 1), (4, *_DOWN): (10, 4), (4, *_LM): (11, 1),
+    (1, *_QKV): (1, 2), (1, *_O): (1, 4), (1, *_GU): (3, 1), (1, *_DOWN): (1, 4), (1, *_LM): (1, 1),
+    (2, *_QKV): (4, 2), (2, *_O): (4, 4), (2, *_GU): (6, 1), (2, *_DOWN): (4, 4), (2, *_LM): (6, 1),
+    (4, *_QKV): None, (4, *_O): (9, 4), (4, *_GU): (11, 1), (4, *_DOWN): (10, 4), (4, *_LM): (11, 1),
     (8, *_QKV): None, (8, *_O): None, (8, *_GU): None, (8, *_DOWN): (16, 4), (8, *_LM): None,
     (16, *_QKV): None, (16, *_O): None, (16, *_GU): None, (16, *_DOWN): None, (16, *_LM): None,
 }
 # the same sweep for weight-only fp8 (--tune --fp8): (variant, ksplit) per (MT, N, K)
 TUNED_FP8: dict = {
-    (1, *_QKV): (1, 2), (2, *_QKV): (7, 4), (4, *_QKV): (12, 4),
-    (1, *_O): (1, 4), (2, *_O): (5, 4), (4, *_O): (9, 4),
-    (1, *_GU): (1, 1), (2, *_GU): (7, 1), (4, *_GU): (12, 1),
-    (1, *_DOWN): (1, 4), (2, *_DOWN): (7, 7), (4, *_DOWN): (12, 8),
+    (1, *_QKV): (1, 4), (2, *_QKV): (5, 4), (4, *_QKV): (9, 4),
+    (1, *_O): (1, 4), (2, *_O): (5, 4), (4, *_O): (10, 4),
+    (1, *_GU): (1, 1), (2, *_GU): (7, 1), (4, *_GU): (12, 2),
+    (1, *_DOWN): (1, 7), (2, *_DOWN): (5, 8), (4, *_DOWN): (9, 8),
     (1, *_LM): (1, 1), (2, *_LM): (6, 1), (4, *_LM): (11, 1),
 }
 SKINNY_DEFAULT_MAX_M = 32  # untuned shapes: skinny GEMM up to this batch, hipBLASLt above
@@ -294,19 +294,26 @@ def kv_index_tables(device="cpu") -> tuple[torch.Tensor, torch.Tensor]:
 
 class PagedKVCache:
     """All layers' KV pages in one allocation: ``[layers, pages, kv_heads, 2, 4096]``
-    bf16 (2 = K then V region of a 32-token page). Page 0.. are handed out by the
+    (2 = K then V region of a 32-token page) in bf16, or in OCP e4m3
+    (``dtype="fp8"``: scale 1, saturating -- half the bytes the decode attention
+    streams and twice the tokens per GB). Pages are handed out by the
     scheduler's block allocator (kgs.serve)."""
 
-    def __init__(self, layers: int, pages: int, kv_heads: int, device, dtype=torch.bfloat16):
+    def __init__(self, layers: int, pages: int, kv_heads: int, device, dtype="bf16"):
         self.layers, self.pages, self.kv_heads = layers, pages, kv_heads
-        self.data = torch.zeros(layers, pages, kv_heads, 2, PAGE * HEAD_DIM, dtype=dtype, device=device)
+        tdt = {"bf16": torch.bfloat16, torch.bfloat16: torch.bfloat16, "fp8": FP8, FP8: FP8}[dtype]
+        self.data = torch.zeros(layers, pages, kv_heads, 2, PAGE * HEAD_DIM, dtype=tdt, device=device)
 
     def layer(self, i: int) -> torch.Tensor:
         return self.data[i]
 
+    @property
+    def fp8(self) -> bool:
+        return self.data.dtype == FP8
+
     @staticmethod
-    def bytes_per_page(layers: int, kv_heads: int) -> int:
-        return layers * kv_heads * 2 * PAGE * HEAD_DIM * 2
+    def bytes_per_page(layers: int, kv_heads: int, dtype="bf16") -> int:
+        return layers * kv_heads * 2 * PAGE * HEAD_DIM * (1 if dtype == "fp8" else 2)
 
 
 def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positions: torch.Tensor,
@@ -323,11 +330,12 @@ def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positio
     for v in (cos, sin):
         if v.dtype != torch.float32 or not v.is_contiguous() or v.shape[-1] != HEAD_DIM // 2:
             raise ValueError("cos/sin must be contiguous fp32 [max_pos, 64]")
-    if cache_layer.dtype != torch.bfloat16 or not cache_layer.is_contiguous():
-        raise ValueError("cache_layer must be a contiguous bf16 page array")
+    if cache_layer.dtype not in (torch.bfloat16, FP8) or not cache_layer.is_contiguous():
+        raise ValueError("cache_layer must be a contiguous bf16 or e4m3 page array")
     rc = _lib.lib().kgs_rope_cache_bf16(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), positions.data_ptr(),
                                         slots.data_ptr(), cache_layer.data_ptr(), t, heads, kv_heads, HEAD_DIM,
-                                        qkv.stride(0), _lib.stream_handle(qkv.device))
+                                        qkv.stride(0), 1 if cache_layer.dtype == FP8 else 0,
+                                        _lib.stream_handle(qkv.device))
     _lib.check(rc, "rope_cache")
     return qkv
 
@@ -383,7 +391,7 @@ def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tab
                                           pml.data_ptr() if pml is not None else None,
                                           cnt.data_ptr() if cnt is not None else None, b, heads, kv_heads, HEAD_DIM,
                                           max_pages, pps, nsplit, q.stride(0), out.stride(0), float(scale),
-                                          _lib.stream_handle(q.device))
+                                          1 if cache_layer.dtype == FP8 else 0, _lib.stream_handle(q.device))
     _lib.check(rc, "paged_decode_attention")
     return out
 
@@ -399,9 +407,15 @@ def ref_cache_write(cache_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
     k, v = k[keep], v[keep]
     page, tau = slots // PAGE, slots % PAGE
     hkv = cache_layer.shape[1]
+
+    def cvt(t):
+        if cache_layer.dtype == FP8:  # saturating, like the kernel
+            return t.float().clamp(-FP8_MAX, FP8_MAX).to(FP8)
+        return t.to(cache_layer.dtype)
+
     for h in range(hkv):
-        cache_layer[page[:, None], h, 0, k_idx[tau]] = k[:, h].to(cache_layer.dtype)
-        cache_layer[page[:, None], h, 1, v_idx[tau]] = v[:, h].to(cache_layer.dtype)
+        cache_layer[page[:, None], h, 0, k_idx[tau]] = cvt(k[:, h])
+        cache_layer[page[:, None], h, 1, v_idx[tau]] = cvt(v[:, h])
 
 
 def ref_gather_kv(cache_layer: torch.Tensor, pages: torch.Tensor, ctx: int) -> tuple[torch.Tensor, torch.Tensor]:

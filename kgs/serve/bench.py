@@ -33,7 +33,7 @@ def run_engine(a) -> dict:
     mc = LlamaConfig.llama3_8b(layers=a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
-                      decode_weights=a.decode_weights)
+                      decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -64,6 +64,7 @@ def run_engine(a) -> dict:
         "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
+        "kv_cache_dtype": a.kv_cache_dtype,
         "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
@@ -118,6 +119,8 @@ def main(argv=None) -> int:
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")
+    ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8 = e4m3 KV pages (half the attention bytes); the headline is bf16")
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")
     ap.add_argument("--hf-only", action="store_true")
     a = ap.parse_args(argv)

@@ -60,6 +60,7 @@ class EngineConfig:
     cuda_graphs: bool = True
     fused_max_batch: int = 32         # decode batches up to this use the fused skinny-GEMM layer (measured crossover)
     decode_weights: str = "bf16"      # "fp8": weight-only fp8 decode copies (W8A16)
+    kv_cache_dtype: str = "bf16"      # "fp8": e4m3 KV pages
     seed: int = 0
 
 
@@ -80,7 +81,7 @@ class LLMEngine:
         num_pages = cfg.num_pages or self._pages_from_memory(model_cfg)
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
                                   max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
-                                  decode_weights=cfg.decode_weights)
+                                  decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
@@ -104,7 +105,7 @@ class LLMEngine:
         # the kgs backend keeps prefill-order and prepacked decode copies of every projection
         resident = weights * ((1.5 if self.cfg.decode_weights == "fp8" else 2) if self.backend == "kgs" else 1)
         avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
-        return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads)))
+        return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, self.cfg.kv_cache_dtype)))
 
     # ----------------------------------------------------------------- API
     def add_request(self, prompt: list[int], params: SamplingParams | None = None) -> int:

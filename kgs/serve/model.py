@@ -24,6 +24,9 @@ Two step kinds, both driven by the native scheduler's plans
 scale per output row, dequantised in registers), halving the weight bytes a
 decode step streams; prefill and batches above the fused path stay bf16.
 
+``kv_cache_dtype="fp8"``: e4m3 KV pages (scale 1), dequantised in the decode
+attention's registers -- half the KV bytes per decode step.
+
 ``backend="ref"`` runs the same weights, cache layout and plans through plain
 PyTorch (CPU or GPU) -- the numerics reference for tests.
 
@@ -43,7 +46,7 @@ from kgs.ops import decode as D
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 32,
-                 decode_weights: str = "bf16"):
+                 decode_weights: str = "bf16", kv_cache_dtype: str = "bf16"):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -72,7 +75,7 @@ class ServingModel:
                             "down": D.PackedWeight(lw["down"], fp8=f8)} for i, lw in enumerate(self.w)]
             self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm, fp8=f8)
             D.reserve_workspace(self.device)
-        self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device)
+        self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device, dtype=kv_cache_dtype)
         self.max_model_len = max_model_len
         from kgs.ops.transformer import rope_tables
 

@@ -135,6 +135,18 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 template <bool W8>
 using WFrag = typename std::conditional<W8, u32x2, bf16x8>::type;
 
+// 8 floats -> 8 OCP e4m3 bytes (saturating at +-448, RNE)
+__device__ __forceinline__ uint2 tfm_e4m3x8(const float* v) {
+  float c[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) c[e] = fminf(fmaxf(v[e], -448.f), 448.f);
+  unsigned lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], lo, true);
+  unsigned hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[4], c[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(c[6], c[7], hi, true);
+  return make_uint2(lo, hi);
+}
+
 __device__ __forceinline__ bf16x8 dequant8(u32x2 v, float s) {
   bf16x8 o;
 #pragma unroll
@@ -352,9 +364,12 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 // qkv row t: [H q heads | HKV k heads | HKV v heads] x 128. Thread = (token,
 // head among H + 2 HKV, chunk c < 8): q/k heads rotate dims (8c.., 64+8c..) in
 // place; k and v heads are also written into page slot[t] (skipped when < 0).
+// KV8: the cache holds OCP e4m3 bytes (scale 1, saturating) in the same
+// element order -- a page region is 4 KB instead of 8 KB.
+template <bool KV8>
 __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ qkv, const float* __restrict__ cosv,
                                                   const float* __restrict__ sinv, const int* __restrict__ pos,
-                                                  const int* __restrict__ slot, unsigned short* __restrict__ cache,
+                                                  const int* __restrict__ slot, void* __restrict__ cache,
                                                   long tokens, int H, int HKV, long ld) {
   const int nh = H + 2 * HKV;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
@@ -391,16 +406,38 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
   const int page = sl / PAGE, tau = sl - page * PAGE;
   const bool isv = h >= H + HKV;
   const int kvh = isv ? h - H - HKV : h - H;
-  unsigned short* pg = cache + (((long)page * HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
+  const long region = (((long)page * HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
   const int d1 = 8 * c, d2 = HD / 2 + 8 * c;
-  if (!isv) {
-    *(bf16x8*)(pg + kv_k_index(tau, d1)) = a;
-    *(bf16x8*)(pg + kv_k_index(tau, d2)) = b;
-  } else {
+  if constexpr (KV8) {
+    unsigned char* pg = (unsigned char*)cache + region;
+    float fa[8], fb[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      pg[kv_v_index(tau, d1 + e)] = (unsigned short)a[e];
-      pg[kv_v_index(tau, d2 + e)] = (unsigned short)b[e];
+      fa[e] = bf2f((unsigned short)a[e]);
+      fb[e] = bf2f((unsigned short)b[e]);
+    }
+    if (!isv) {
+      *(uint2*)(pg + kv_k_index(tau, d1)) = tfm_e4m3x8(fa);
+      *(uint2*)(pg + kv_k_index(tau, d2)) = tfm_e4m3x8(fb);
+    } else {
+      const uint2 qa = tfm_e4m3x8(fa), qb = tfm_e4m3x8(fb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pg[kv_v_index(tau, d1 + e)] = (unsigned char)(((e < 4 ? qa.x : qa.y) >> (8 * (e & 3))) & 0xff);
+        pg[kv_v_index(tau, d2 + e)] = (unsigned char)(((e < 4 ? qb.x : qb.y) >> (8 * (e & 3))) & 0xff);
+      }
+    }
+  } else {
+    unsigned short* pg = (unsigned short*)cache + region;
+    if (!isv) {
+      *(bf16x8*)(pg + kv_k_index(tau, d1)) = a;
+      *(bf16x8*)(pg + kv_k_index(tau, d2)) = b;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pg[kv_v_index(tau, d1 + e)] = (unsigned short)a[e];
+        pg[kv_v_index(tau, d2 + e)] = (unsigned short)b[e];
+      }
     }
   }
 }
@@ -437,6 +474,7 @@ __device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, f
 // One wave per (sequence, KV head, context split). With nsplit > 1 the partial (m, l, O)
 // go to a workspace and the split that arrives last (agent-scope ticket per
 // (sequence, KV head)) merges them -- no separate reduction launch.
+template <bool KV8>
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int lane = threadIdx.x;
   const int G = a.H / a.HKV;
@@ -461,15 +499,27 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qp + 32 * ks) : bf16x8{};
     const int* bt = a.block_tables + (long)b * a.max_pages;
-    auto page_ptr = [&](int pi) {
-      return (const bf16x8*)(a.cache + (((long)bt[pi] * a.HKV + kvh) * 2) * PAGE_ELEMS) + lane;
-    };
     auto load_page = [&](bf16x8 (&kf)[8], bf16x8 (&vf)[8], int pi) {
-      const bf16x8* kp = page_ptr(pi);
+      const long region = ((long)bt[pi] * a.HKV + kvh) * 2 * PAGE_ELEMS;  // elements of the K region
+      if constexpr (KV8) {  // e4m3 pages: 8 B per lane per fragment, dequantised in registers
+        const u32x2* kp = (const u32x2*)((const unsigned char*)a.cache + region) + lane;
+        u32x2 kr[8], vr[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) kf[i] = __builtin_nontemporal_load(kp + 64 * i);
+        for (int i = 0; i < 8; ++i) kr[i] = __builtin_nontemporal_load(kp + 64 * i);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
+        for (int i = 0; i < 8; ++i) vr[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          kf[i] = dequant8(kr[i], 1.f);
+          vf[i] = dequant8(vr[i], 1.f);
+        }
+      } else {
+        const bf16x8* kp = (const bf16x8*)(a.cache + region) + lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) kf[i] = __builtin_nontemporal_load(kp + 64 * i);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) vf[i] = __builtin_nontemporal_load(kp + PAGE_ELEMS / 8 + 64 * i);
+      }
     };
     auto page = [&](const bf16x8 (&kf)[8], const bf16x8 (&vf)[8], int pi) {
       f32x4v s[2];
@@ -718,15 +768,21 @@ KGS_EXPORT int kgs_skinny_gemm_bf16(const void* wp, const void* x, void* y, floa
 // qkv: [tokens, ld] fused projection rows (H q heads, HKV k heads, HKV v heads
 // of 128); pos/slot: int32 [tokens]; cache: this layer's pages
 // [pages][HKV][2][4096] bf16. q and k are rotated in place; k, v land in the cache.
+// kv8: the cache holds e4m3 bytes ([pages][HKV][2][4096] B) instead of bf16.
 KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* sinv, const int* pos, const int* slot,
-                                  void* cache, long tokens, int H, int HKV, int hd, long ld, hipStream_t s) {
+                                  void* cache, long tokens, int H, int HKV, int hd, long ld, int kv8, hipStream_t s) {
   if (tokens < 0 || H <= 0 || HKV <= 0 || H % HKV || hd != kgs::dec::HD) return KGS_ERR_SHAPE;
   if (ld < (long)(H + 2 * HKV) * hd) return KGS_ERR_SHAPE;
   if (!al16(qkv) || !al16(cosv) || !al16(sinv) || !al16(cache) || ld % 8) return KGS_ERR_ALIGN;
   const long n = tokens * (H + 2 * HKV) * 8;
   if (n == 0) return 0;
-  hipLaunchKernelGGL(kgs::dec::rope_cache, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (unsigned short*)qkv,
-                     cosv, sinv, pos, slot, (unsigned short*)cache, tokens, H, HKV, ld);
+  const dim3 g((unsigned)((n + 255) / 256)), b(256);
+  if (kv8)
+    hipLaunchKernelGGL(kgs::dec::rope_cache<true>, g, b, 0, s, (unsigned short*)qkv, cosv, sinv, pos, slot, cache,
+                       tokens, H, HKV, ld);
+  else
+    hipLaunchKernelGGL(kgs::dec::rope_cache<false>, g, b, 0, s, (unsigned short*)qkv, cosv, sinv, pos, slot, cache,
+                       tokens, H, HKV, ld);
   return (int)hipGetLastError();
 }
 
@@ -738,7 +794,7 @@ KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* si
 KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int* block_tables, const int* ctx_lens,
                                     void* o, float* po, float* pml, int* cnt, int B, int H, int HKV, int hd,
                                     int max_pages, int pages_per_split, int nsplit, long ldq, long ldo, float scale,
-                                    hipStream_t s) {
+                                    int kv8, hipStream_t s) {
   using namespace kgs::dec;
   if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 16 || hd != HD) return KGS_ERR_SHAPE;
   if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0) return KGS_ERR_SHAPE;
@@ -753,7 +809,10 @@ KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int
   const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
              pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
-  hipLaunchKernelGGL(paged_decode, dim3((unsigned)nwg), dim3(64), 0, s, a);
+  if (kv8)
+    hipLaunchKernelGGL(paged_decode<true>, dim3((unsigned)nwg), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(paged_decode<false>, dim3((unsigned)nwg), dim3(64), 0, s, a);
   if (nsplit > 1 && !merge)
     hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
                        ldo);

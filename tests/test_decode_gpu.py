@@ -270,3 +270,41 @@ def test_skinny_fp8_weights(m):
     y2 = skinny_gemm(x, pgu, rms=ss)
     torch.cuda.synchronize()
     assert (y2.float() - ref2).abs().max().item() <= 3e-2 * ref2.abs().max().item()
+
+
+@pytest.mark.parametrize("pps", [None, 1, 100])
+def test_fp8_kv_cache(pps):
+    """e4m3 KV pages: the fused RoPE/KV write stores what the reference quantiser
+    stores, and the attention over them matches fp32 math on the dequantised cache."""
+    from kgs.ops.decode import (PAGE, PagedKVCache, paged_decode_attention, ref_cache_write, ref_paged_decode,
+                                rope_cache_)
+    from kgs.ops.transformer import rope_tables
+
+    heads, hkv, hd = 32, 8, 128
+    ctxs = [5, 64, 200]
+    b = len(ctxs)
+    cache = PagedKVCache(1, 32, hkv, DEV, dtype="fp8")
+    ref_cache = torch.zeros_like(cache.layer(0))
+    bt = _setup_cache(b, ctxs, hkv, 32, seed=3).to(DEV)
+    cos, sin = rope_tables(4096, hd, 500000.0, DEV)
+    pos, slots = [], []
+    for i, c in enumerate(ctxs):
+        for t in range(c):
+            pos.append(t)
+            slots.append(int(bt[i, t // PAGE]) * PAGE + t % PAGE)
+    qkv = _bf(len(pos), (heads + 2 * hkv) * hd)
+    pos_t = torch.tensor(pos, dtype=torch.int32, device=DEV)
+    slot_t = torch.tensor(slots, dtype=torch.int32, device=DEV)
+    rope_cache_(qkv, cos, sin, pos_t, slot_t, cache.layer(0), heads, hkv)
+    torch.cuda.synchronize()
+    k = qkv[:, heads * hd:(heads + hkv) * hd].reshape(-1, hkv, hd)
+    v = qkv[:, (heads + hkv) * hd:].reshape(-1, hkv, hd)
+    ref_cache_write(ref_cache, k, v, slot_t)
+    assert torch.equal(cache.layer(0).view(torch.uint8), ref_cache.view(torch.uint8))
+    last = torch.tensor([sum(ctxs[:i + 1]) - 1 for i in range(b)], device=DEV)
+    q = qkv[last].contiguous()
+    ctx_t = torch.tensor(ctxs, dtype=torch.int32, device=DEV)
+    ref = ref_paged_decode(q, cache.layer(0), bt, ctx_t, heads, hkv)
+    o = paged_decode_attention(q, cache.layer(0), bt, ctx_t, heads, hkv, pages_per_split=pps)
+    torch.cuda.synchronize()
+    assert (o.float() - ref).abs().max().item() < 2e-2

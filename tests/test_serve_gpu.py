@@ -105,3 +105,14 @@ def test_fp8_decode_weights_engine():
     assert all(len(r.output) == 6 for r in outs)
     # weight-only fp8: the chosen tokens stay near the bf16 oracle's top logit
     _oracle_check(eng, prompts, outs, tol=0.12)
+
+
+def test_fp8_kv_cache_engine():
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(6)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (40, 130)]
+    eng = _engine(True, kv_cache_dtype="fp8")
+    assert eng.model.cache.fp8
+    outs = eng.generate(prompts, SamplingParams(max_tokens=6, ignore_eos=True))
+    _oracle_check(eng, prompts, outs, tol=0.12)
