@@ -45,7 +45,7 @@ from kgs.ops import decode as D
 
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
-                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 32,
+                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 64,
                  decode_weights: str = "bf16", kv_cache_dtype: str = "bf16"):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
