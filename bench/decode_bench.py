@@ -82,6 +82,37 @@ def bench_gemm(iters, ms, ring_bytes=3 << 30):
         torch.cuda.empty_cache()
 
 
+def bench_wide(iters, ms, ring_bytes=3 << 30):
+    """Large decode batches (M >= 128): the kgs 256x256 prefill GEMM (gemm_nt)
+    against hipBLASLt, weights HBM-streamed as in bench_gemm."""
+    from kgs.ops.gemm import gemm_nt
+
+    for name, (n, k) in SHAPES.items():
+        copies = max(2, min(64, ring_bytes // (n * k * 2)))
+        ws = [(torch.randn(n, k, device="cuda") * k ** -0.5).to(torch.bfloat16) for _ in range(copies)]
+        for m in ms:
+            x = (torch.rand(m, k, device="cuda") * 2 - 1).to(torch.bfloat16)
+            out = torch.empty(m, n, dtype=torch.bfloat16, device="cuda")
+            it = {"i": 0}
+
+            def kgs_call():
+                it["i"] = (it["i"] + 1) % copies
+                gemm_nt(x, ws[it["i"]], out=out)
+
+            def torch_call():
+                it["i"] = (it["i"] + 1) % copies
+                torch.matmul(x, ws[it["i"]].T, out=out)
+
+            t_k = _time(kgs_call, iters)
+            t_t = _time(torch_call, iters)
+            byts = n * k * 2 + m * k * 2 + m * n * 2
+            print(json.dumps({"op": "gemm_nt_wide", "shape": name, "m": m, "n": n, "k": k, "copies": copies,
+                              "us": round(t_k, 2), "tbps": round(byts / t_k / 1e6, 2), "torch_us": round(t_t, 2),
+                              "speedup": round(t_t / t_k, 3)}), flush=True)
+        del ws
+        torch.cuda.empty_cache()
+
+
 def tune_gemm(iters, ms, ring_bytes=2 << 30, fp8=False):
     """Time every (variant, split-K) of the skinny GEMM per Llama shape and batch
     bucket with HBM-streamed weights; print the best and a TUNED table."""
@@ -156,11 +187,15 @@ def main(argv=None) -> int:
     ap.add_argument("--sweep", action="store_true", help="time every valid split-K factor")
     ap.add_argument("--tune", action="store_true", help="time every tile variant x split-K; print a TUNED table")
     ap.add_argument("--fp8", action="store_true", help="--tune the weight-only fp8 (W8A16) kernels")
+    ap.add_argument("--wide", action="store_true", help="kgs 256x256 GEMM vs hipBLASLt at M >= 128")
     a = ap.parse_args(argv)
     global SWEEP
     SWEEP = a.sweep
     if a.tune:
         tune_gemm(a.iters, [int(v) for v in a.ms.split(",")], fp8=a.fp8)
+        return 0
+    if a.wide:
+        bench_wide(a.iters, [int(v) for v in a.ms.split(",")])
         return 0
     both = not (a.gemm or a.attn)
     if a.gemm or both:

@@ -94,7 +94,10 @@ class ServingModel:
         if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]) and \
                 not (self.decode_fp8 and m > 64):
             return D.skinny_gemm(x, self.packed[layer][name])
-        if decode:
+        # the LM head (N = 128256) from batch 128 up runs faster on the kgs
+        # 256x256 GEMM than on hipBLASLt (1.09x at 128, 1.21x at 256,
+        # profiles/decode_wide_gemm.jsonl); the other decode shapes do not
+        if decode and (layer is not None or m < 128):
             return torch.matmul(x, w.T)
         from kgs.ops import gemm_nt
 
