@@ -85,7 +85,7 @@ def bench_gemm(iters, ms, ring_bytes=3 << 30):
 def bench_wide(iters, ms, ring_bytes=3 << 30):
     """Large decode batches (M >= 128): the kgs 256x256 prefill GEMM (gemm_nt)
     against hipBLASLt, weights HBM-streamed as in bench_gemm."""
-    from kgs.ops.gemm import gemm_nt
+    from kgs.ops.gemm import gemm_nt, gemm_nt_splitk
 
     for name, (n, k) in SHAPES.items():
         copies = max(2, min(64, ring_bytes // (n * k * 2)))
@@ -105,8 +105,19 @@ def bench_wide(iters, ms, ring_bytes=3 << 30):
 
             t_k = _time(kgs_call, iters)
             t_t = _time(torch_call, iters)
+            splits = {}
+            for ns in (2, 4, 8, 16):
+                if k % ns or (k // ns) % 128:
+                    continue
+
+                def sk_call(ns=ns):
+                    it["i"] = (it["i"] + 1) % copies
+                    gemm_nt_splitk(x, ws[it["i"]], ns, out=out)
+                splits[ns] = round(_time(sk_call, iters), 2)
+            ref = x.float() @ ws[0].float().T
+            err = ((gemm_nt_splitk(x, ws[0], 4).float() - ref).abs().max() / ref.abs().max()).item()
             byts = n * k * 2 + m * k * 2 + m * n * 2
-            print(json.dumps({"op": "gemm_nt_wide", "shape": name, "m": m, "n": n, "k": k, "copies": copies,
+            print(json.dumps({"op": "gemm_nt_wide", "splitk_us": splits, "splitk_rel_err": round(err, 5), "shape": name, "m": m, "n": n, "k": k, "copies": copies,
                               "us": round(t_k, 2), "tbps": round(byts / t_k / 1e6, 2), "torch_us": round(t_t, 2),
                               "speedup": round(t_t / t_k, 3)}), flush=True)
         del ws

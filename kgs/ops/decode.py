@@ -144,6 +144,27 @@ TUNED_FP8: dict = {
     (1, *_DOWN): (1, 7), (2, *_DOWN): (5, 8), (4, *_DOWN): (9, 8),
     (1, *_LM): (1, 1), (2, *_LM): (6, 1), (4, *_LM): (11, 1),
 }
+# Decode batches above the fused range: K slices of the split-K 256x256 GEMM
+# (kgs.ops.gemm.gemm_nt_splitk) per (batch bucket, N, K) where it beat both
+# hipBLASLt and the skinny GEMM (bench/decode_bench.py --wide,
+# profiles/decode_wide_gemm.jsonl): down 1.89x / 1.14x / 1.48x at 128 / 256 /
+# 512, qkv 1.22x at 256, o 1.07x at 128. gate|up (fp32 partials too large) and
+# the rest stay on hipBLASLt.
+SPLITK_TUNED: dict = {
+    (128, *_DOWN): 16, (128, *_O): 8,
+    (256, *_QKV): 8, (256, *_DOWN): 8,
+    (512, *_DOWN): 8,
+}
+SPLITK_WS_FLOATS = 8 * 512 * 4096  # the largest entry above (M x N x slices)
+
+
+def splitk_slices(m: int, n: int, k: int) -> int | None:
+    """K slices for a decode GEMM of batch m (bucketed to a power of two), or
+    None when the split-K kernel is not the measured winner."""
+    mb = 1 << max(0, (m - 1).bit_length())
+    return SPLITK_TUNED.get((mb, n, k))
+
+
 SKINNY_DEFAULT_MAX_M = 32  # untuned shapes: skinny GEMM up to this batch, hipBLASLt above
 
 
@@ -272,9 +293,13 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
 
 
 def reserve_workspace(device) -> None:
-    """Allocate the largest split-K slab buffer :func:`choose_ksplit` can ask
-    for (64 MB) up front, e.g. before hipGraph capture."""
+    """Allocate the largest split-K slab buffers the decode GEMMs can ask for up
+    front (skinny: 64 MB; the 256x256 split-K kernel: SPLITK_WS_FLOATS), e.g.
+    before hipGraph capture."""
+    from .gemm import reserve_splitk_workspace
+
     _workspace(torch.device(device), 16 << 20, 1 << 16)
+    reserve_splitk_workspace(torch.device(device), SPLITK_WS_FLOATS)
 
 
 # ----------------------------------------------------------------------------

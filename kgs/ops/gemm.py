@@ -88,6 +88,44 @@ def gemm_nt(
     return out
 
 
+_SPLITK_WS: dict = {}
+
+
+def reserve_splitk_workspace(device: torch.device, floats: int) -> None:
+    """Allocate the fp32 partial-tile buffer up front (before hipGraph capture:
+    a buffer first allocated inside a capture would belong to the graph's pool)."""
+    ws = _SPLITK_WS.get(device)
+    if ws is None or ws.numel() < floats:
+        _SPLITK_WS[device] = torch.empty(floats, dtype=torch.float32, device=device)
+
+
+def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b.T`` (bf16, f32 accumulation) over ``nslice`` K-slices: the 256x256
+    pipeline writes fp32 partial tiles, a reduce kernel sums them. For short-M
+    (decode-batch) GEMMs whose N / 256 tiles leave most CUs idle.
+    ``(K / nslice) % 8 == 0``; % 128 with M, N % 256 == 0 takes the aligned path."""
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    need = nslice * M * N
+    ws = _SPLITK_WS.get(a.device)
+    if ws is None or ws.numel() < need:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gemm_nt_splitk: reserve_splitk_workspace() before hipGraph capture")
+        reserve_splitk_workspace(a.device, need)
+        ws = _SPLITK_WS[a.device]
+    rc = _lib.lib().kgs_gemm_bf16_nt_splitk(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws.data_ptr(), M, N, K,
+                                            a.stride(0), b.stride(0), out.stride(0), nslice,
+                                            _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_splitk[{M}x{N}x{K}/{nslice}]")
+    return out
+
+
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
 FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16, "gm8": 17, "gm16": 18, "gm2": 19}  # gm*: experiments

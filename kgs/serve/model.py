@@ -17,8 +17,10 @@ Two step kinds, both driven by the native scheduler's plans
   epilogues carry the RMSNorms (norm weights folded into the weights, row
   scales from sums of squares the residual-updating GEMMs accumulate), the
   residual adds and SwiGLU -- no elementwise kernels. Larger batches use
-  add_rmsnorm/silu_mul and hipBLASLt, with the skinny GEMM where it measured
-  faster (:func:`kgs.ops.decode.use_skinny`).
+  add_rmsnorm/silu_mul and hipBLASLt, with the split-K 256x256 GEMM
+  (:func:`kgs.ops.decode.splitk_slices`), the skinny GEMM
+  (:func:`kgs.ops.decode.use_skinny`) or the 256x256 GEMM (LM head) where
+  those measured faster.
 
 ``decode_weights="fp8"``: the decode copies are weight-only fp8 (W8A16, one
 scale per output row, dequantised in registers), halving the weight bytes a
@@ -91,6 +93,12 @@ class ServingModel:
         if self.backend == "ref":
             return (x.float() @ w.float().T).to(torch.bfloat16)
         m = x.shape[0]
+        if decode:
+            ns = D.splitk_slices(m, w.shape[0], w.shape[1])
+            if ns is not None:
+                from kgs.ops.gemm import gemm_nt_splitk
+
+                return gemm_nt_splitk(x, w, ns)
         if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]) and \
                 not (self.decode_fp8 and m > 64):
             return D.skinny_gemm(x, self.packed[layer][name])

@@ -436,6 +436,64 @@ hipError_t launch_layout(int ta, int tb, const unsigned short* A, const unsigned
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// split-K for short-M GEMMs (decode batches of 128-256 rows): the 256x256
+// pipeline over nslice K-slices (gemm_nt_256 S bit 20) writes fp32 partial
+// tiles, splitk_reduce sums them into bf16 C. With N / 256 tiles alone such a
+// GEMM fills a fraction of the 256 CUs (the Llama-3-8B down projection has 16
+// tiles); the slices fill the rest.
+// ---------------------------------------------------------------------------
+namespace kgs {
+__global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ P, unsigned short* __restrict__ C,
+                                                     int M, int N, int ldc, int nslice) {
+  const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 8;  // 8 consecutive columns of one row
+  const long MN = (long)M * N;
+  if (e >= MN) return;
+  const int row = (int)(e / N), col = (int)(e - (long)row * N);
+  f32x4 a = *(const f32x4*)(P + e), b = *(const f32x4*)(P + e + 4);
+  for (int s = 1; s < nslice; ++s) {
+    a += *(const f32x4*)(P + s * MN + e);
+    b += *(const f32x4*)(P + s * MN + e + 4);
+  }
+  uint4 o;
+  o.x = pack_bf16x2(a[0], a[1]);
+  o.y = pack_bf16x2(a[2], a[3]);
+  o.z = pack_bf16x2(b[0], b[1]);
+  o.w = pack_bf16x2(b[2], b[3]);
+  *(uint4*)(C + (long)row * ldc + col) = o;
+}
+}  // namespace kgs
+
+// C[M, N] (bf16) = A[M, K] . B[N, K]^T over nslice K-slices; ws holds nslice *
+// M * N floats. K / nslice must be a multiple of 128 (aligned M % 256 == 0,
+// N % 256 == 0) or of 8 (any M, N % 8 == 0: the bounded pipeline).
+KGS_EXPORT int kgs_gemm_bf16_nt_splitk(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
+                                       int ldb, int ldc, int nslice, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
+  if (lda < K || ldb < K || ldc < N || N % 8 || ldc % 8) return KGS_ERR_SHAPE;
+  if (ws == nullptr) return KGS_ERR_ARG;
+  const int ks = K / nslice;
+  if ((uintptr_t)ws % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  const bool fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, ks, lda, ldb, ldc) && ks % 128 == 0;
+  const bool bounded = kgs_gemm_bf16_nt_bounded_ok(A, B, C, M, N, ks, lda, ldb, ldc);
+  if (!fast && !bounded) return KGS_ERR_ALIGN;
+  using namespace kgs;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  const int ntm = (M + g256::BM - 1) / g256::BM, ntn = (N + g256::BN - 1) / g256::BN;
+  const dim3 grid(ntm * ntn * nslice);
+  if (fast)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 7 + 1048576>), grid, dim3(512), 0, stream, a, b,
+                       (unsigned short*)ws, nullptr, M, N, ks, lda, ldb, N, 1.0f, nullptr);
+  else
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 7 + 512 + 1048576>), grid, dim3(512), 0, stream, a, b,
+                       (unsigned short*)ws, nullptr, M, N, ks, lda, ldb, N, 1.0f, nullptr);
+  const long groups = ((long)M * N / 8 + 255) / 256;
+  hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)groups), dim3(256), 0, stream, ws, (unsigned short*)C, M, N, ldc,
+                     nslice);
+  return (int)hipGetLastError();
+}
+
 KGS_EXPORT int kgs_gemm_bf16_layout_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
                                        int ldb, int ldc, int ta, int tb) {
   if (M <= 0 || N <= 0 || K <= 0) return 0;

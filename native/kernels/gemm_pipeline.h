@@ -461,6 +461,29 @@ __device__ __forceinline__ void store_tile(const Ctx& c, const Regs& R, unsigned
     }
 }
 
+// split-K partial tile: fp32, row-major [M][N], one 16-B store per lane per
+// fragment (the lane holds 4 consecutive columns of one row)
+template <bool BND>
+__device__ __forceinline__ void store_tile_f32(const Ctx& c, const Regs& R, float* __restrict__ P, int M, int N,
+                                               int tm, int tn, int lane) {
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = tm * BM + mh * 128 + c.wr * 64 + i * 16 + fr;
+      if (BND && row >= M) continue;
+      float* prow = P + (long)row * N;
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          const int col = tn * BN + nh * 128 + c.wc * 32 + n * 16 + fq * 4;
+          if (!BND || col < N) *(f32x4*)(prow + col) = R.acc[mh][i][nh][n];
+        }
+    }
+}
+
 template <int EPI, int S>
 __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restrict__ A,
                                                    const unsigned short* __restrict__ B,
@@ -471,10 +494,20 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
 
   constexpr bool BND = (S & 512) != 0;
+  // S bit 20: split-K -- the grid is nwg tiles x gridDim.x / nwg K-slices of K
+  // columns each (K is the slice length, lda/ldb the full row strides); slice
+  // s reads columns [s K, (s+1) K) and stores its fp32 partial tile to
+  // ((float*)C)[s][M][N] (ldc ignored); kgs_splitk_reduce sums the slices.
+  constexpr bool SPLITK = (S & 1048576) != 0;
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntm = BND ? (M + BM - 1) / BM : M / BM, ntn = BND ? (N + BN - 1) / BN : N / BN, nwg = ntm * ntn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  // split-K: remap over the whole grid, so the blocks of one XCD share a slice
+  // (its x panel stays in that XCD's L2) and walk neighbouring weight tiles
+  const int nslice = SPLITK ? gridDim.x / nwg : 1;
+  const int wga = SPLITK ? xcd_remap(blockIdx.x, nwg * nslice) : 0;
+  const int slice = SPLITK ? wga / nwg : 0;
+  const int wg = SPLITK ? wga - slice * nwg : xcd_remap(blockIdx.x, nwg);
   // S bits 2-3 select the tile-group height (experiment knob): 8, 4, 16, 2
   constexpr int GM = ((S >> 2) & 3) == 0 ? GROUP_M : ((S >> 2) & 3) == 1 ? 4 : ((S >> 2) & 3) == 2 ? 16 : 2;
   const int per_group = GM * ntn;
@@ -496,6 +529,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   // S bit 5: timing probe -- every block loads tile (0,0) (L2-resident operands)
   c.Ag = ((S & 2048) && !(S & 16384)) ? A + (long)tm * BM : A + (long)((S & 32) ? 0 : tm) * BM * lda;
   c.Bg = (S & 4096) ? B + (long)tn * BN : B + (long)((S & 32) ? 0 : tn) * BN * ldb;
+  if constexpr (SPLITK) {
+    c.Ag += (long)slice * K;
+    c.Bg += (long)slice * K;
+  }
   c.a_kstride = lda;
   c.b_kstride = ldb;
   c.a_half = 128L * lda;
@@ -637,6 +674,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   // fp8: the dequant scale, times a device-resident factor (dynamic activation scale)
   if constexpr ((S & 1024) && !(S & 524288)) {
     if (alpha_ptr) alpha *= *alpha_ptr;
+  }
+  if constexpr (SPLITK) {
+    store_tile_f32<BND>(c, R, (float*)C + (long)slice * M * N, M, N, tm, tn, lane);
+    return;
   }
   store_tile<EPI, S>(c, R, C, bias, M, N, ldc, alpha, tm, tn, lane, alpha_ptr);
   if constexpr (S & 65536) {

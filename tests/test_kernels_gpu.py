@@ -170,6 +170,23 @@ def test_gemm_bounded_ragged(M, N, K):
         assert torch.equal(gemm_nt(a, b, variant="bounded"), c)
 
 
+@pytest.mark.parametrize("M,N,K,nslice", [(256, 1024, 4096, 1), (256, 1024, 4096, 4), (256, 768, 14336, 14),
+                                          (128, 512, 4096, 8), (200, 264, 2048, 2), (64, 4096, 1024, 8)])
+def test_gemm_splitk(M, N, K, nslice):
+    """Split-K 256x256 pipeline (fp32 partial tiles + reduce) against fp32 torch;
+    an asymmetric B and a strided A view catch swapped or shifted slices."""
+    from kgs.ops.gemm import gemm_nt_splitk
+
+    a_full = (torch.rand(M, K + 64, device=DEV) * 2 - 1).bfloat16()
+    a = a_full[:, 32:32 + K]  # row stride K + 64, 64-B offset
+    b = ((torch.rand(N, K, device=DEV) * 2 - 1) * torch.linspace(0.5, 1.5, K, device=DEV)).bfloat16()
+    c = gemm_nt_splitk(a, b, nslice)
+    ref = _ref_nt(a, b)
+    assert _rel_err(c, ref) < 1e-2
+    # slices are summed in a fixed order: repeatable bit for bit
+    assert torch.equal(gemm_nt_splitk(a, b, nslice), c)
+
+
 def test_gemm_bounded_matches_fast_on_aligned():
     from kgs.ops import gemm_nt
 
