@@ -3,8 +3,10 @@ replacement for the vLLM process of ``pods/vllm-rocm-pod.yaml`` (same port
 8000, same ``/v1/completions`` request shape; see ``pods/kgs-serve-pod.yaml``).
 
 Endpoints: ``POST /v1/completions`` (prompt as text or token ids; ``stream``
-gives server-sent events), ``GET /v1/models``, ``GET /health``, ``GET /metrics``
-(Prometheus). One background thread owns the engine (it is not thread-safe) and
+gives server-sent events), ``POST /v1/chat/completions`` (messages rendered by
+a plain role-tagged template), ``GET /v1/models``, ``GET /health``,
+``GET /metrics`` (Prometheus). Sampling: temperature, top_k, top_p,
+stop strings, stop_token_ids, ignore_eos. One background thread owns the engine (it is not thread-safe) and
 runs :meth:`LLMEngine.step` whenever there is work; request handlers only talk to
 it through a queue.
 
@@ -27,14 +29,69 @@ from pydantic import BaseModel
 from .engine import SamplingParams
 
 
-class CompletionRequest(BaseModel):
+class _SamplingFields(BaseModel):
     model: str | None = None
-    prompt: str | list[int]
     max_tokens: int = 16
     temperature: float = 0.0
     top_k: int = 0
+    top_p: float = 1.0
+    stop: str | list[str] | None = None
+    stop_token_ids: list[int] | None = None
     stream: bool = False
     ignore_eos: bool = False
+
+    def params(self) -> SamplingParams:
+        return SamplingParams(max_tokens=self.max_tokens, temperature=self.temperature, top_k=self.top_k,
+                              top_p=self.top_p, ignore_eos=self.ignore_eos,
+                              stop_token_ids=tuple(self.stop_token_ids or ()))
+
+    def stops(self) -> list[str]:
+        return [self.stop] if isinstance(self.stop, str) else [t for t in (self.stop or []) if t]
+
+
+class CompletionRequest(_SamplingFields):
+    prompt: str | list[int]
+
+
+class ChatMessage(BaseModel):
+    role: str
+    content: str
+
+
+class ChatRequest(_SamplingFields):
+    messages: list[ChatMessage]
+
+
+def render_chat(messages) -> str:
+    """Role-tagged transcript ending with an open assistant turn (the weights are
+    random-init, so there is no model-specific chat template to honour)."""
+    return "".join(f"<|{m.role}|>\n{m.content}\n" for m in messages) + "<|assistant|>\n"
+
+
+class StopText:
+    """Incremental detokenisation with OpenAI-style stop strings: text is
+    released only once it can no longer be the start of a stop string; a match
+    truncates the output before the stop string."""
+
+    def __init__(self, tok, stops: list[str]):
+        self.tok, self.stops = tok, stops
+        self.ids: list[int] = []
+        self.sent = 0
+        self.hold = max((len(t) for t in stops), default=1) - 1
+
+    def push(self, t: int, final: bool) -> tuple[str, bool]:
+        """Add a token; returns (text to emit now, stop string hit)."""
+        self.ids.append(t)
+        text = self.tok.decode(self.ids)
+        if self.stops:
+            hits = [i for i in (text.find(st, max(0, self.sent - self.hold)) for st in self.stops) if i >= 0]
+            if hits:
+                cut = min(hits)
+                out, self.sent = text[self.sent:cut], cut
+                return out, True
+        end = len(text) if final or not self.stops else max(self.sent, len(text) - self.hold)
+        out, self.sent = text[self.sent:end], end
+        return out, False
 
 
 class ByteTokenizer:
@@ -159,50 +216,77 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 
-    @app.post("/v1/completions")
-    async def completions(req: CompletionRequest):
-        ids = tok.encode(req.prompt) if isinstance(req.prompt, str) else list(req.prompt)
+    async def _start(ids, params):
         if not ids:
             raise HTTPException(400, "empty prompt")
-        params = SamplingParams(max_tokens=req.max_tokens, temperature=req.temperature, top_k=req.top_k,
-                                ignore_eos=req.ignore_eos)
         q: asyncio.Queue = asyncio.Queue()
         loop_runner.submit(ids, params, asyncio.get_running_loop(), q)
         first = await q.get()
         if first[0] == "error":
             raise HTTPException(400, first[1])
-        rid = first[1]
-        cid, created = f"cmpl-{uuid.uuid4().hex[:16]}", int(time.time())
+        return first[1], q
+
+    async def _tokens(rid, q, stop: StopText):
+        """(token id, text, finished, finish reason) until the request ends; a
+        stop-string hit aborts the request in the engine."""
+        try:
+            while True:
+                _, t, fin, reason = await q.get()
+                text, hit = stop.push(t, fin)
+                if hit:
+                    loop_runner.cancel(rid)
+                    yield t, text, True, "stop"
+                    return
+                yield t, text, fin, reason
+                if fin:
+                    return
+        except asyncio.CancelledError:  # client went away
+            loop_runner.cancel(rid)
+            raise
+
+    async def _serve(req, ids, chat: bool):
+        params = req.params()
+        rid, q = await _start(ids, params)
+        cid, created = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex[:16]}", int(time.time())
         name = req.model or model_name
+        obj = "chat.completion" if chat else "text_completion"
+        stop = StopText(tok, req.stops())
+
+        def choice(text, ids_, reason, delta):
+            if not chat:
+                return {"index": 0, "text": text, "token_ids": ids_, "finish_reason": reason}
+            msg = {"role": "assistant", "content": text}
+            return {"index": 0, ("delta" if delta else "message"): msg, "finish_reason": reason}
 
         if req.stream:
             async def events():
-                try:
-                    while True:
-                        _, t, fin, reason = await q.get()
-                        chunk = {"id": cid, "object": "text_completion", "created": created, "model": name,
-                                 "choices": [{"index": 0, "text": tok.decode([t]), "token_ids": [t],
-                                              "finish_reason": reason}]}
-                        yield f"data: {json.dumps(chunk)}\n\n"
-                        if fin:
-                            break
-                    yield "data: [DONE]\n\n"
-                except asyncio.CancelledError:  # client went away
-                    loop_runner.cancel(rid)
-                    raise
+                async for t, text, fin, reason in _tokens(rid, q, stop):
+                    chunk = {"id": cid, "object": obj + (".chunk" if chat else ""), "created": created,
+                             "model": name, "choices": [choice(text, [t], reason, True)]}
+                    yield f"data: {json.dumps(chunk)}\n\n"
+                yield "data: [DONE]\n\n"
 
             return StreamingResponse(events(), media_type="text/event-stream")
 
-        out, reason = [], None
-        while True:
-            _, t, fin, reason = await q.get()
+        out, parts, reason = [], [], None
+        async for t, text, fin, reason in _tokens(rid, q, stop):
             out.append(t)
-            if fin:
-                break
-        return {"id": cid, "object": "text_completion", "created": created, "model": name,
-                "choices": [{"index": 0, "text": tok.decode(out), "token_ids": out, "finish_reason": reason}],
+            parts.append(text)
+        return {"id": cid, "object": obj, "created": created, "model": name,
+                "choices": [choice("".join(parts), out, reason, False)],
                 "usage": {"prompt_tokens": len(ids), "completion_tokens": len(out),
                           "total_tokens": len(ids) + len(out)}}
+
+    @app.post("/v1/completions")
+    async def completions(req: CompletionRequest):
+        ids = tok.encode(req.prompt) if isinstance(req.prompt, str) else list(req.prompt)
+        return await _serve(req, ids, chat=False)
+
+    @app.post("/v1/chat/completions")
+    async def chat_completions(req: ChatRequest):
+        if not req.messages:
+            raise HTTPException(400, "no messages")
+        return await _serve(req, tok.encode(render_chat(req.messages)), chat=True)
 
     return app
 

@@ -32,6 +32,7 @@ class SamplingParams:
     max_tokens: int = 16
     temperature: float = 0.0   # 0 = greedy
     top_k: int = 0             # 0 = full vocabulary
+    top_p: float = 1.0         # nucleus: smallest set of tokens whose probability reaches top_p
     ignore_eos: bool = False
     stop_token_ids: tuple = ()
 
@@ -263,6 +264,16 @@ class LLMEngine:
             thr = vals.gather(1, kth)
             full = torch.tensor([k <= 0 for k in ks], device=lf.device)[:, None]
             lf = torch.where(full | (lf >= thr), lf, torch.full_like(lf, float("-inf")))
+        tp = [p.top_p for p in ps]
+        if any(0.0 < t < 1.0 for t in tp):
+            # nucleus: keep the highest-probability tokens until their mass reaches
+            # top_p (the token that crosses it included); rows with top_p >= 1 keep all
+            srt, idx = torch.sort(lf, dim=-1, descending=True)
+            cum = torch.softmax(srt, dim=-1).cumsum(dim=-1)
+            tpv = torch.tensor([t if 0.0 < t < 1.0 else 1.0 for t in tp], device=lf.device)[:, None]
+            drop = (cum - torch.softmax(srt, dim=-1)) >= tpv  # mass before this token already reached top_p
+            srt = srt.masked_fill(drop, float("-inf"))
+            lf = torch.full_like(lf, float("-inf")).scatter(1, idx, srt)
         probs = torch.softmax(lf, dim=-1)
         sampled = torch.multinomial(probs, 1, generator=self._gen).squeeze(1)
         greedy = torch.tensor([p.temperature <= 0 for p in ps], device=lf.device)

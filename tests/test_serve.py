@@ -224,6 +224,81 @@ def test_http_api_completions_and_stream():
         runner.shutdown()
 
 
+def test_http_api_chat_stop_strings_and_top_p():
+    from fastapi.testclient import TestClient
+
+    from kgs.serve import EngineConfig, LLMEngine
+    from kgs.serve.api import EngineLoop, create_app, render_chat
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    runner = EngineLoop(eng)
+    try:
+        client = TestClient(create_app(runner, model_name="tiny"))
+        msgs = [{"role": "system", "content": "be brief"}, {"role": "user", "content": "hi"}]
+        r = client.post("/v1/chat/completions", json={"messages": msgs, "max_tokens": 6, "ignore_eos": True}).json()
+        assert r["object"] == "chat.completion"
+        msg = r["choices"][0]["message"]
+        assert msg["role"] == "assistant" and r["usage"]["completion_tokens"] == 6
+        # the chat endpoint is the completion of the rendered transcript
+        from types import SimpleNamespace as NS
+        prompt = render_chat([NS(**m) for m in msgs])
+        c = client.post("/v1/completions", json={"prompt": prompt, "max_tokens": 6, "ignore_eos": True}).json()
+        assert c["choices"][0]["text"] == msg["content"]
+        # a stop token id ends generation at its first occurrence (greedy: deterministic)
+        ids = c["choices"][0]["token_ids"]
+        r3 = client.post("/v1/completions", json={"prompt": prompt, "max_tokens": 6, "stop_token_ids": [ids[2]]}).json()
+        assert r3["choices"][0]["token_ids"] == ids[:ids.index(ids[2]) + 1]
+        assert r3["choices"][0]["finish_reason"] == "stop"
+        # streamed chat: role-tagged deltas, [DONE]
+        with client.stream("POST", "/v1/chat/completions",
+                           json={"messages": msgs, "max_tokens": 3, "stream": True, "ignore_eos": True}) as s:
+            events = [ln for ln in s.iter_lines() if ln.startswith("data: ")]
+        assert events[-1] == "data: [DONE]" and len(events) == 4
+        import json as _json
+        assert _json.loads(events[0][6:])["object"] == "chat.completion.chunk"
+        # top_p runs (sampling path) and respects max_tokens
+        r4 = client.post("/v1/completions", json={"prompt": "abc", "max_tokens": 4, "temperature": 1.0,
+                                                  "top_p": 0.5, "ignore_eos": True}).json()
+        assert r4["usage"]["completion_tokens"] == 4
+    finally:
+        runner.shutdown()
+
+
+def test_stop_text_truncates_and_holds_back():
+    from kgs.serve.api import ByteTokenizer, StopText
+
+    tok = ByteTokenizer()
+    ids = tok.encode("hello world, bye")[1:]
+    st = StopText(tok, ["wor", "xyz"])
+    out, hit = "", False
+    for i, t in enumerate(ids):
+        text, hit = st.push(t, i == len(ids) - 1)
+        out += text
+        if hit:
+            break
+    assert hit and out == "hello "
+    st2 = StopText(tok, ["zzz"])  # never hits: everything comes out by the final token
+    out2 = "".join(st2.push(t, i == len(ids) - 1)[0] for i, t in enumerate(ids))
+    assert out2 == "hello world, bye"
+
+
+def test_top_p_sampling_keeps_nucleus():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    rid = eng.add_request([5, 6, 7], SamplingParams(max_tokens=1, temperature=1.0, top_p=0.3))
+    eng.abort(rid)
+    # one dominant token (p ~ 0.9) -> top_p 0.3 always picks it; top_p 1.0 can pick others
+    logits = torch.full((2, 64), -5.0)
+    logits[:, 7] = 5.0
+    eng.requests[rid].params = SamplingParams(temperature=1.0, top_p=0.3)
+    rid2 = eng.add_request([5, 6], SamplingParams(max_tokens=1, temperature=1.0, top_p=1.0))
+    picks = {int(eng._sample([rid, rid2], logits)[0]) for _ in range(50)}
+    assert picks == {7}
+
+
 def test_byte_tokenizer_roundtrip():
     from kgs.serve.api import ByteTokenizer
 
