@@ -226,16 +226,33 @@ def use_skinny(m: int, n: int, k: int) -> bool:
 
 
 _WS: dict = {}
+# Workspaces replaced by larger ones. hipGraphs captured before the growth still
+# hold the old device pointers, so the old buffers must outlive them: they are
+# kept here for the life of the process instead of going back to the caching
+# allocator (where they could be reused, or released to the driver and fault).
+_RETIRED: list = []
+
+
+def device_key(device: torch.device) -> int:
+    """Normalised per-GPU cache key: torch.device("cuda") and "cuda:0" differ as
+    dict keys but name the same workspace."""
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def retire(*bufs) -> None:
+    _RETIRED.extend(b for b in bufs if b is not None)
 
 
 def _workspace(device: torch.device, floats: int, ints: int):
     """Per-device split-K slab buffer and zeroed ticket counters (the kernel
     re-arms the counters it uses). GEMMs of one device are stream-ordered."""
-    key = device.index if device.index is not None else torch.cuda.current_device()
+    key = device_key(device)
     ws, cnt = _WS.get(key, (None, None))
     if ws is None or ws.numel() < floats:
+        retire(ws)
         ws = torch.empty(max(floats, 1 << 20), dtype=torch.float32, device=device)
     if cnt is None or cnt.numel() < ints:
+        retire(cnt)
         cnt = torch.zeros(max(ints, 4096), dtype=torch.int32, device=device)
     _WS[key] = (ws, cnt)
     return ws, cnt
@@ -403,9 +420,10 @@ def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tab
     po = pml = cnt = None
     if nsplit > 1:
         need = b * heads * nsplit
-        key = q.device.index
+        key = device_key(q.device)
         po, pml, cnt = _AWS.get(key, (None, None, None))
         if po is None or po.numel() < need * HEAD_DIM or cnt.numel() < b * kv_heads:
+            retire(po, pml, cnt)
             po = torch.empty(max(need, 1 << 14) * HEAD_DIM, dtype=torch.float32, device=q.device)
             pml = torch.empty(max(need, 1 << 14) * 2, dtype=torch.float32, device=q.device)
             cnt = torch.zeros(max(b * kv_heads, 4096), dtype=torch.int32, device=q.device)

@@ -91,12 +91,19 @@ def gemm_nt(
 _SPLITK_WS: dict = {}
 
 
-def reserve_splitk_workspace(device: torch.device, floats: int) -> None:
-    """Allocate the fp32 partial-tile buffer up front (before hipGraph capture:
-    a buffer first allocated inside a capture would belong to the graph's pool)."""
-    ws = _SPLITK_WS.get(device)
+def reserve_splitk_workspace(device: torch.device, floats: int) -> torch.Tensor:
+    """The per-GPU fp32 partial-tile buffer, grown to at least ``floats``. Call
+    it up front (before hipGraph capture: a buffer first allocated inside a
+    capture would belong to the graph's pool). A buffer it replaces is retired,
+    not freed -- graphs captured earlier still point at it."""
+    from .decode import device_key, retire
+
+    key = device_key(device)
+    ws = _SPLITK_WS.get(key)
     if ws is None or ws.numel() < floats:
-        _SPLITK_WS[device] = torch.empty(floats, dtype=torch.float32, device=device)
+        retire(ws)
+        ws = _SPLITK_WS[key] = torch.empty(floats, dtype=torch.float32, device=device)
+    return ws
 
 
 def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Tensor | None = None) -> torch.Tensor:
@@ -113,12 +120,13 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     need = nslice * M * N
-    ws = _SPLITK_WS.get(a.device)
+    from .decode import device_key
+
+    ws = _SPLITK_WS.get(device_key(a.device))
     if ws is None or ws.numel() < need:
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("gemm_nt_splitk: reserve_splitk_workspace() before hipGraph capture")
-        reserve_splitk_workspace(a.device, need)
-        ws = _SPLITK_WS[a.device]
+        ws = reserve_splitk_workspace(a.device, need)
     rc = _lib.lib().kgs_gemm_bf16_nt_splitk(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws.data_ptr(), M, N, K,
                                             a.stride(0), b.stride(0), out.stride(0), nslice,
                                             _lib.stream_handle(a.device))

@@ -8,7 +8,7 @@ Optional baseline (``--hf``): the same architecture in HF ``transformers``
 on the same GPU -- what a PyTorch user gets without a serving engine.
 
   python -m kgs.serve bench [--requests 256] [--input-len 512] [--output-len 256]
-                            [--max-batch 256] [--layers 32] [--hf]
+                            [--max-batch 256] [--layers 32] [--hf] [--request-rate R]
 """
 from __future__ import annotations
 
@@ -25,6 +25,13 @@ def _prompts(n, length, vocab, seed=0):
     return [rng.integers(3, vocab, size=length).tolist() for _ in range(n)]
 
 
+def _graph_widths(a):
+    """Page-table width buckets a run with these lengths can hit (captured up front)."""
+    widths = sorted({w for w in (8, 16, 32, 64, 128, 256)
+                     if w >= (a.input_len + 32) // 32 and w <= 2 * ((a.input_len + a.output_len) // 32 + 1)})
+    return widths or None
+
+
 def run_engine(a) -> dict:
     from kgs.models.llama import LlamaConfig
 
@@ -39,9 +46,7 @@ def run_engine(a) -> dict:
     t_load = time.perf_counter() - t0
     t0 = time.perf_counter()
     if not a.no_graphs:
-        widths = sorted({w for w in (8, 16, 32, 64, 128, 256)
-                         if w >= (a.input_len + 32) // 32 and w <= 2 * ((a.input_len + a.output_len) // 32 + 1)})
-        eng.warmup(widths=widths or None)
+        eng.warmup(widths=_graph_widths(a))
     # one short request end to end (prefill + decode paths compiled/allocated)
     eng.generate(_prompts(1, 16, mc.vocab, seed=9), SamplingParams(max_tokens=4, ignore_eos=True))
     torch.cuda.synchronize()
@@ -69,6 +74,77 @@ def run_engine(a) -> dict:
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
         "load_s": round(t_load, 1), "warmup_s": round(t_warm, 1), "stats": dict(eng.stats),
+    }
+
+
+def _pct(v, q):
+    v = sorted(v)
+    return v[min(len(v) - 1, int(q * len(v)))] if v else float("nan")
+
+
+def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
+    """Online serving: requests arrive as a Poisson process at --request-rate
+    req/s (the arrival schedule is drawn up front, seeded), the engine runs
+    continuously and admits each request once its arrival time has passed.
+    Latencies are measured from the scheduled arrival: TTFT, TPOT (per request,
+    (t_done - t_first) / (tokens - 1)), ITL (every gap between two tokens of a
+    request) and end-to-end latency, p50/p99 -- the metrics of vLLM's
+    benchmark_serving, without the HTTP hop."""
+    from kgs.models.llama import LlamaConfig
+
+    from .engine import EngineConfig, LLMEngine, SamplingParams
+
+    mc = mc or LlamaConfig.llama3_8b(layers=a.layers)
+    ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
+                      max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
+                      decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
+                      **({"num_pages": 256} if device == "cpu" else {}))
+    eng = LLMEngine(mc, ec, device=device, backend=backend)
+    if not a.no_graphs:
+        eng.warmup(widths=_graph_widths(a))
+    eng.generate(_prompts(1, 16, mc.vocab, seed=9), SamplingParams(max_tokens=4, ignore_eos=True))
+    if device != "cpu":
+        torch.cuda.synchronize()
+    rng = np.random.default_rng(1)
+    arrivals = np.cumsum(rng.exponential(1.0 / a.request_rate, size=a.requests))
+    prompts = _prompts(a.requests, a.input_len, mc.vocab)
+    params = SamplingParams(max_tokens=a.output_len, ignore_eos=True)
+    tok_times: dict = {}
+    done = []
+    t0 = time.perf_counter()
+    i = 0
+    while i < a.requests or eng.has_work():
+        now = time.perf_counter() - t0
+        while i < a.requests and arrivals[i] <= now:
+            rid = eng.add_request(prompts[i], params)
+            eng.requests[rid].t_arrival = t0 + arrivals[i]
+            tok_times[rid] = []
+            i += 1
+        if not eng.has_work():
+            time.sleep(max(0.0, min(0.01, arrivals[i] - now)))
+            continue
+        for rid, _tok, fin in eng.step():
+            tok_times[rid].append(time.perf_counter())
+            if fin:
+                done.append(eng.requests.pop(rid))
+    dt = time.perf_counter() - t0
+    ttft = [r.t_first - r.t_arrival for r in done]
+    tpot = [(r.t_done - r.t_first) / max(1, len(r.output) - 1) for r in done]
+    e2e = [r.t_done - r.t_arrival for r in done]
+    itl = [b - c for ts in tok_times.values() for c, b in zip(ts, ts[1:])]
+    n_out = sum(len(r.output) for r in done)
+    ms = lambda v: round(1e3 * v, 2)  # noqa: E731
+    return {
+        "metric": "online serving (kgs.serve, Poisson arrivals, Llama-3-8B arch, random init)",
+        "backend": "kgs", "requests": a.requests, "request_rate": a.request_rate, "input_len": a.input_len,
+        "output_len": a.output_len, "max_batch": a.max_batch, "layers": a.layers,
+        "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
+        "requests_per_s": round(len(done) / dt, 3),
+        "ttft_ms": {"p50": ms(_pct(ttft, .5)), "p99": ms(_pct(ttft, .99)), "mean": ms(float(np.mean(ttft)))},
+        "tpot_ms": {"p50": ms(_pct(tpot, .5)), "p99": ms(_pct(tpot, .99)), "mean": ms(float(np.mean(tpot)))},
+        "itl_ms": {"p50": ms(_pct(itl, .5)), "p99": ms(_pct(itl, .99))},
+        "e2e_ms": {"p50": ms(_pct(e2e, .5)), "p99": ms(_pct(e2e, .99))},
+        "stats": dict(eng.stats),
     }
 
 
@@ -121,9 +197,14 @@ def main(argv=None) -> int:
                     help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = e4m3 KV pages (half the attention bytes); the headline is bf16")
+    ap.add_argument("--request-rate", type=float, default=0.0,
+                    help="> 0: online mode, Poisson arrivals at this many requests/s (TTFT/TPOT/ITL p50/p99)")
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")
     ap.add_argument("--hf-only", action="store_true")
     a = ap.parse_args(argv)
+    if a.request_rate > 0:
+        print(json.dumps(run_online(a)), flush=True)
+        return 0
     if not a.hf_only:
         print(json.dumps(run_engine(a)), flush=True)
         torch.cuda.empty_cache()

@@ -187,6 +187,23 @@ def test_gemm_splitk(M, N, K, nslice):
     assert torch.equal(gemm_nt_splitk(a, b, nslice), c)
 
 
+def test_splitk_workspace_is_stable_for_graphs():
+    """The partial-tile buffer reserved under torch.device("cuda") is the one
+    calls on "cuda:0" use (no silent second allocation), and a growth retires the
+    old buffer instead of freeing it (hipGraphs captured earlier point at it)."""
+    from kgs.ops import decode as D
+    from kgs.ops.gemm import gemm_nt_splitk, reserve_splitk_workspace
+
+    ws = reserve_splitk_workspace(torch.device("cuda"), D.SPLITK_WS_FLOATS)
+    a = (torch.rand(256, 4096, device="cuda:0") * 2 - 1).bfloat16()
+    for n, ns in ((4096, 8), (6144, 8), (4096, 16)):
+        b = (torch.rand(n, 4096, device=DEV) * 2 - 1).bfloat16()
+        gemm_nt_splitk(a, b, ns)
+        assert reserve_splitk_workspace(torch.device("cuda", 0), 1).data_ptr() == ws.data_ptr()
+    big = reserve_splitk_workspace(torch.device("cuda"), ws.numel() + 1024)
+    assert big.data_ptr() != ws.data_ptr() and any(r is ws for r in D._RETIRED)
+
+
 def test_gemm_bounded_matches_fast_on_aligned():
     from kgs.ops import gemm_nt
 

@@ -299,6 +299,22 @@ def test_top_p_sampling_keeps_nucleus():
     assert picks == {7}
 
 
+def test_online_bench_poisson_cpu():
+    """bench --request-rate: Poisson arrivals through the engine loop (ref backend
+    on CPU); every request completes and the latency percentiles are ordered."""
+    from kgs.serve import bench
+
+    a = bench.main.__globals__["argparse"].Namespace(
+        requests=6, input_len=20, output_len=5, max_batch=4, max_model_len=256, max_prefill_tokens=4096,
+        layers=2, no_graphs=True, fused_max_batch=0, decode_weights="bf16", kv_cache_dtype="bf16",
+        request_rate=200.0)
+    r = bench.run_online(a, mc=_tiny(), device="cpu", backend="ref")
+    assert r["requests_per_s"] > 0 and r["stats"]["decode_tokens"] + r["stats"]["prefill_steps"] > 0
+    for k in ("ttft_ms", "tpot_ms", "itl_ms", "e2e_ms"):
+        assert 0 <= r[k]["p50"] <= r[k]["p99"]
+    assert r["output_tok_per_s"] > 0 and r["e2e_ms"]["p99"] >= r["ttft_ms"]["p50"]
+
+
 def test_byte_tokenizer_roundtrip():
     from kgs.serve.api import ByteTokenizer
 
