@@ -63,6 +63,8 @@ _SIGS = {
     "kgs_silu_mul_fp8": ([_c_void_p] * 3 + [_c_long, _c_int, _c_long, _c_long, _c_void_p], _c_int),
     "kgs_gemm_fp8_nt_rows": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 +
                              [ctypes.c_float, _c_void_p, _c_int, _c_int, _c_void_p], _c_int),
+    "kgs_attn_fwd_bf16_ex": ([_c_void_p] * 4 + [_c_int] * 6 + [_c_long] * 4 + [ctypes.c_float, _c_int, _c_void_p],
+                             _c_int),
     "kgs_attn_fwd_bf16": ([_c_void_p] * 4 + [_c_int] * 5 + [_c_long] * 4 + [ctypes.c_float, _c_int, _c_void_p],
                           _c_int),
     # decode path (native/kernels/decode.hip)

@@ -461,6 +461,35 @@ def ref_cache_write(cache_layer: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
         cache_layer[page[:, None], h, 1, v_idx[tau]] = cvt(v[:, h])
 
 
+_KV_IDX: dict = {}
+
+
+def gather_kv(cache_layer: torch.Tensor, pages: torch.Tensor, ctx: int, rows: int | None = None
+              ) -> tuple[torch.Tensor, torch.Tensor]:
+    """The first ``ctx`` cached tokens of one sequence as contiguous row-major
+    ``k``, ``v`` ``[rows, kv_heads * 128]`` bf16 (rows ``ctx .. rows-1`` zero) --
+    the keys/values a prefill chunk attends to (``rows`` pads them to the
+    chunk's q-blocks). Vectorised torch gathers through the page layout's index
+    tables; an fp8 cache is widened to bf16."""
+    rows = ctx if rows is None else rows
+    dev = cache_layer.device
+    key = (dev.type, dev.index)
+    if key not in _KV_IDX:
+        _KV_IDX[key] = kv_index_tables(dev)
+    k_idx, v_idx = _KV_IDX[key]
+    hkv = cache_layer.shape[1]
+    npg = (ctx + PAGE - 1) // PAGE
+    sel = cache_layer[pages[:npg].long()]  # [npg, hkv, 2, 4096]
+    out = []
+    for region, idx in ((0, k_idx), (1, v_idx)):
+        t = sel[:, :, region][..., idx]  # [npg, hkv, 32, 128]
+        t = t.permute(0, 2, 1, 3).reshape(npg * PAGE, hkv * HEAD_DIM)[:ctx].to(torch.bfloat16)
+        if rows > ctx:
+            t = torch.cat([t, t.new_zeros(rows - ctx, hkv * HEAD_DIM)])
+        out.append(t.contiguous())
+    return out[0], out[1]
+
+
 def ref_gather_kv(cache_layer: torch.Tensor, pages: torch.Tensor, ctx: int) -> tuple[torch.Tensor, torch.Tensor]:
     """The first ``ctx`` tokens of one sequence: ``(k, v)``, each ``[ctx, HKV, 128]`` fp32."""
     k_idx, v_idx = kv_index_tables(cache_layer.device)

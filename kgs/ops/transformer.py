@@ -170,6 +170,40 @@ def attention_qkv(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_heads:
     return out
 
 
+def attention_chunk(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, heads: int, kv_heads: int,
+                    head_dim: int = 128, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """Causal flash attention of one sequence's prefill CHUNK over its whole
+    context: ``q`` rows ``[S, >= heads*128]`` are the last S positions (S % 128
+    == 0), ``k``/``v`` ``[Sk, >= kv_heads*128]`` every key up to and including
+    them (Sk - S % 64 == 0) -- row i sees keys 0 .. Sk - S + i. Any row strides."""
+    for t, n in ((q, "q"), (k, "k"), (v, "v")):
+        _need(t, n)
+    S, Sk = q.shape[0], k.shape[0]
+    if v.shape[0] != Sk:
+        raise ValueError("k and v differ in length")
+    out = torch.empty((S, heads * head_dim), dtype=torch.bfloat16, device=q.device) if out is None else out
+    _need(out, "out")
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    rc = _lib.lib().kgs_attn_fwd_bf16_ex(q.data_ptr(), k.data_ptr(), v.data_ptr(), out.data_ptr(), 1, S, Sk, heads,
+                                         kv_heads, head_dim, q.stride(0), k.stride(0), v.stride(0), out.stride(0),
+                                         float(scale), 1, _lib.stream_handle(q.device))
+    _lib.check(rc, "attention_chunk")
+    return out
+
+
+def ref_attention_chunk(q, k, v, heads, kv_heads, head_dim=128, scale=None):
+    """fp32 reference of :func:`attention_chunk` (bottom-right causal)."""
+    S, Sk = q.shape[0], k.shape[0]
+    qf = q[:, :heads * head_dim].float().reshape(S, heads, head_dim).transpose(0, 1)
+    kf = k[:, :kv_heads * head_dim].float().reshape(Sk, kv_heads, head_dim).transpose(0, 1)
+    vf = v[:, :kv_heads * head_dim].float().reshape(Sk, kv_heads, head_dim).transpose(0, 1)
+    rep = heads // kv_heads
+    kf, vf = kf.repeat_interleave(rep, 0), vf.repeat_interleave(rep, 0)
+    mask = torch.arange(Sk, device=q.device)[None, :] <= (Sk - S + torch.arange(S, device=q.device))[:, None]
+    o = torch.nn.functional.scaled_dot_product_attention(qf, kf, vf, attn_mask=mask, scale=scale)
+    return o.transpose(0, 1).reshape(S, heads * head_dim)
+
+
 # ----------------------------------------------------------------------------
 # fp32 PyTorch references (tests, the "torch" model backend)
 

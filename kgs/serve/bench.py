@@ -40,7 +40,8 @@ def run_engine(a) -> dict:
     mc = LlamaConfig.llama3_8b(layers=a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
-                      decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype)
+                      decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
+                      chunked_prefill=a.chunked_prefill)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -69,7 +70,7 @@ def run_engine(a) -> dict:
         "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
-        "kv_cache_dtype": a.kv_cache_dtype,
+        "kv_cache_dtype": a.kv_cache_dtype, "chunked_prefill": a.chunked_prefill,
         "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
@@ -98,6 +99,7 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
+                      chunked_prefill=getattr(a, "chunked_prefill", 0),
                       **({"num_pages": 256} if device == "cpu" else {}))
     eng = LLMEngine(mc, ec, device=device, backend=backend)
     if not a.no_graphs:
@@ -138,7 +140,7 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
         "metric": "online serving (kgs.serve, Poisson arrivals, Llama-3-8B arch, random init)",
         "backend": "kgs", "requests": a.requests, "request_rate": a.request_rate, "input_len": a.input_len,
         "output_len": a.output_len, "max_batch": a.max_batch, "layers": a.layers,
-        "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
+        "chunked_prefill": getattr(a, "chunked_prefill", 0), "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "requests_per_s": round(len(done) / dt, 3),
         "ttft_ms": {"p50": ms(_pct(ttft, .5)), "p99": ms(_pct(ttft, .99)), "mean": ms(float(np.mean(ttft)))},
         "tpot_ms": {"p50": ms(_pct(tpot, .5)), "p99": ms(_pct(tpot, .99)), "mean": ms(float(np.mean(tpot)))},
@@ -197,6 +199,8 @@ def main(argv=None) -> int:
                     help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = e4m3 KV pages (half the attention bytes); the headline is bf16")
+    ap.add_argument("--chunked-prefill", type=int, default=0,
+                    help="> 0: mixed steps of at most this many rows (prompt chunks + decodes)")
     ap.add_argument("--request-rate", type=float, default=0.0,
                     help="> 0: online mode, Poisson arrivals at this many requests/s (TTFT/TPOT/ITL p50/p99)")
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")

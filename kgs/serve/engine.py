@@ -62,6 +62,7 @@ class EngineConfig:
     fused_max_batch: int = 64         # decode batches up to this use the fused skinny-GEMM layer (measured crossover)
     decode_weights: str = "bf16"      # "fp8": weight-only fp8 decode copies (W8A16)
     kv_cache_dtype: str = "bf16"      # "fp8": e4m3 KV pages
+    chunked_prefill: int = 0          # > 0: mixed steps of at most this many rows (prompt chunks + decodes)
     seed: int = 0
 
 
@@ -86,6 +87,7 @@ class LLMEngine:
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
+        sc.chunk_tokens = cfg.chunked_prefill
         self.sched = _serve.Scheduler(sc)
         self.num_pages = num_pages
         self.requests: dict[int, Request] = {}
@@ -93,7 +95,7 @@ class LLMEngine:
         self._graphs: dict = {}
         self._gen = torch.Generator(device=self.device).manual_seed(cfg.seed)
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
-                      "preemptions": 0, "graph_replays": 0, "graph_captures": 0}
+                      "mixed_steps": 0, "preemptions": 0, "graph_replays": 0, "graph_captures": 0}
         self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs"
 
     def _pages_from_memory(self, mc: LlamaConfig) -> int:
@@ -134,7 +136,17 @@ class LLMEngine:
             return []
         self.stats["preemptions"] += len(plan.preempted)
         ids = plan.seq_ids
-        if plan.kind == 1:
+        if plan.kind == 3:
+            logits = self._run_mixed(plan)
+            npf = plan.n_prefill
+            # only chunks that complete their prompt produce a token
+            ids = np.concatenate([ids[:npf][plan.last_chunk.astype(bool)], ids[npf:]])
+            self.stats["mixed_steps"] += 1
+            self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
+            self.stats["decode_tokens"] += len(plan.seq_ids) - npf
+            if len(ids) == 0:
+                return []
+        elif plan.kind == 1:
             logits = self._run_prefill(plan)
             self.stats["prefill_steps"] += 1
             self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
@@ -184,6 +196,16 @@ class LLMEngine:
     def _run_prefill(self, plan) -> torch.Tensor:
         return self.model.prefill(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots),
                                   plan.seq_starts.tolist(), plan.seq_lens.tolist(), plan.padded_lens.tolist())
+
+    def _run_mixed(self, plan) -> torch.Tensor:
+        npf = plan.n_prefill
+        pf_bt = self._dev(plan.pf_block_tables) if npf else None
+        chunks = [(int(plan.seq_starts[j]), int(plan.seq_lens[j]), int(plan.padded_lens[j]), int(plan.ctx_starts[j]),
+                   pf_bt[j], bool(plan.last_chunk[j])) for j in range(npf)]
+        nd = len(plan.seq_ids) - npf
+        return self.model.mixed(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots), chunks,
+                                self._dev(plan.block_tables) if nd else None,
+                                self._dev(plan.ctx_lens) if nd else None)
 
     def _run_decode(self, plan) -> torch.Tensor:
         b = len(plan.seq_ids)

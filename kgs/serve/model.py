@@ -192,6 +192,72 @@ class ServingModel:
                 attention_qkv(blk, 1, p, c.heads, c.kv_heads, head_dim=hd, causal=True, out=out[s0:s0 + p])
         return out
 
+    # ------------------------------------------------------------------ mixed
+    @torch.no_grad()
+    def mixed(self, tokens, positions, slots, chunks, dec_block_tables=None, dec_ctx_lens=None) -> torch.Tensor:
+        """Chunked-prefill step: prompt chunks (rows first) plus decode rows in ONE
+        pass through the projections. ``chunks``: per prefill sequence
+        ``(row0, n, padded, ctx0, pages, last)`` -- rows ``row0 .. row0+padded``
+        hold prompt positions ``ctx0 .. ctx0+n-1`` (then padding), ``pages`` its
+        block table, ``last`` whether the chunk ends the prompt. Decode rows
+        follow. Returns logits for the last row of every ``last`` chunk, then
+        for every decode row."""
+        c = self.cfg
+        hd = c.head_dim
+        x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
+        n_pf = sum(ch[2] for ch in chunks)
+        nd = x.shape[0] - n_pf
+        y = self._norm(x, None, self.ln1[0])
+        for i in range(c.layers):
+            qkv = self._proj(y, i, "qkv", False)
+            self._rope_cache(qkv, i, positions, slots)
+            a = torch.empty((x.shape[0], c.heads * hd), dtype=torch.bfloat16, device=x.device)
+            for row0, n, p, ctx0, pages, _ in chunks:
+                a[row0:row0 + p] = self._chunk_attention(qkv[row0:row0 + p], i, n, p, ctx0, pages)
+            if nd:
+                qd = qkv[n_pf:]
+                if self.backend == "ref":
+                    a[n_pf:] = D.ref_paged_decode(qd, self.cache.layer(i), dec_block_tables, dec_ctx_lens, c.heads,
+                                                  c.kv_heads).to(torch.bfloat16)
+                else:
+                    D.paged_decode_attention(qd, self.cache.layer(i), dec_block_tables, dec_ctx_lens, c.heads,
+                                             c.kv_heads, out=a[n_pf:])
+            y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
+            act = self._silu_mul(self._proj(y, i, "gate_up", False))
+            nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
+            y = self._norm(x, self._proj(act, i, "down", False), nxt)
+        rows = [row0 + n - 1 for row0, n, _, _, _, last in chunks if last] + list(range(n_pf, n_pf + nd))
+        if not rows:
+            return torch.empty((0, c.vocab), dtype=torch.bfloat16, device=x.device)
+        yl = y[torch.as_tensor(rows, device=y.device)].contiguous()
+        return self._proj(yl, None, "lm", True)
+
+    def _chunk_attention(self, blk, layer, n, p, ctx0, pages):
+        """Causal attention of one prompt chunk (rows = positions ctx0 .. ctx0+p-1,
+        n real) over everything cached before it plus itself; padded rows out 0."""
+        c = self.cfg
+        hd = c.head_dim
+        if ctx0 == 0:  # first chunk: the whole-prompt path
+            out = torch.empty((p, c.heads * hd), dtype=torch.bfloat16, device=blk.device)
+            if self.backend == "ref":
+                return self._prefill_attention(blk, [0], [n], [p])
+            from kgs.ops.transformer import attention_qkv
+
+            return attention_qkv(blk, 1, p, c.heads, c.kv_heads, head_dim=hd, causal=True, out=out)
+        # keys/values of positions 0 .. ctx0+n-1 (this chunk's rows were just
+        # written to the cache by rope_cache), zero-padded to ctx0 + p rows
+        if self.backend == "ref":
+            from kgs.ops.transformer import ref_attention_chunk
+
+            k, v = D.gather_kv(self.cache.layer(layer), pages, ctx0 + n)
+            o = torch.zeros((p, c.heads * hd), dtype=torch.bfloat16, device=blk.device)
+            o[:n] = ref_attention_chunk(blk[:n], k, v, c.heads, c.kv_heads, hd).to(torch.bfloat16)
+            return o
+        from kgs.ops.transformer import attention_chunk
+
+        k, v = D.gather_kv(self.cache.layer(layer), pages, ctx0 + n, rows=ctx0 + p)
+        return attention_chunk(blk, k, v, c.heads, c.kv_heads, hd)
+
     # ----------------------------------------------------------------- decode
     @torch.no_grad()
     def decode(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split=None) -> torch.Tensor:

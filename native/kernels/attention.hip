@@ -50,6 +50,8 @@ struct Args {
   int B, S, H, HKV;
   float sl2;  // softmax scale * log2(e)
   int causal;
+  int Sk;    // keys per sequence (= S, or S + qoff for a chunk over a cached context)
+  int qoff;  // position of query row 0 among the keys: causal row i sees keys <= qoff + i
 };
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -91,7 +93,9 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
   const int q0 = qb * QB;
   const int qw = q0 + 32 * w;       // this wave's first query row
   const int qrow = qw + l32;        // this lane's query row
-  const long tok0 = (long)b * a.S;  // first token of the sequence
+  const long tok0 = (long)b * a.S;     // first query token of the sequence
+  const long ktok0 = (long)b * a.Sk;   // its first key token
+  const int qoff = a.qoff;
 
   // Q fragments (B operand of S^T = K.Q^T): lane holds Q[qrow][16ks + 8hh .. +7]
   bf16x8 qf[8];
@@ -101,8 +105,8 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
     for (int ks = 0; ks < 8; ++ks) qf[ks] = qp[2 * ks];
   }
 
-  const unsigned short* kbase = a.k + tok0 * a.ldk + (long)kvh * HD;
-  const unsigned short* vbase = a.v + tok0 * a.ldv + (long)kvh * HD;
+  const unsigned short* kbase = a.k + ktok0 * a.ldk + (long)kvh * HD;
+  const unsigned short* vbase = a.v + ktok0 * a.ldv + (long)kvh * HD;
   // staging: thread moves 16-B chunks id = tid + 256 i (i < 4) of each tile
   uint4 sk0, sk1, sk2, sk3, sv0, sv1, sv2, sv3;
 #define KGS_ATT_LD(i, SK, SV)                                              \
@@ -121,7 +125,7 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
 #define KGS_ATT_LOAD() KGS_ATT_LD(0, sk0, sv0) KGS_ATT_LD(1, sk1, sv1) KGS_ATT_LD(2, sk2, sv2) KGS_ATT_LD(3, sk3, sv3)
 #define KGS_ATT_STORE() KGS_ATT_ST(0, sk0, sv0) KGS_ATT_ST(1, sk1, sv1) KGS_ATT_ST(2, sk2, sv2) KGS_ATT_ST(3, sk3, sv3)
 
-  const int ntile = a.causal ? (q0 + QB) / KB : a.S / KB;
+  const int ntile = a.causal ? (qoff + q0 + QB) / KB : a.Sk / KB;
   {
     const int jn = 0, sb = 0;
     KGS_ATT_LOAD()
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
       KGS_ATT_LOAD()
     }
     const int kv0 = j * KB;
-    if (!a.causal || kv0 <= qw + 31) {
+    if (!a.causal || kv0 <= qoff + qw + 31) {
       const char* Ks = smem[buf][0];
       const char* Vs = smem[buf][1];
       f32x16 s[2];
@@ -158,13 +162,13 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
           s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
         }
       }
-      if (a.causal && kv0 + KB - 1 > qw) {
+      if (a.causal && kv0 + KB - 1 > qoff + qw) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int kv = kv0 + 32 * t + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            if (kv > qrow) s[t][r] = NEG;
+            if (kv > qoff + qrow) s[t][r] = NEG;
           }
       }
       float mx = m;
@@ -238,19 +242,29 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
 // q/k/v/o point at head 0 of token 0 ([B*S, ld] token-major); heads of one
 // token are contiguous 128-element blocks. Requires head_dim 128, S % 128 == 0,
 // H % HKV == 0, 16-B aligned pointers and ld % 8 == 0.
-KGS_EXPORT int kgs_attn_fwd_bf16(const void* q, const void* k, const void* v, void* o, int B, int S, int H, int HKV,
-                                int hd, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
-                                hipStream_t s) {
+//
+// _ex: Sk keys per sequence ([B*Sk, ld] k/v), Sk >= S, Sk - S a multiple of 64:
+// the S query rows are the LAST S positions of the sequence (a prefill chunk
+// over Sk - S cached tokens), so causal row i sees keys 0 .. Sk - S + i.
+KGS_EXPORT int kgs_attn_fwd_bf16_ex(const void* q, const void* k, const void* v, void* o, int B, int S, int Sk, int H,
+                                   int HKV, int hd, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
+                                   hipStream_t s) {
   using namespace kgs::attn;
   if (B <= 0 || S <= 0 || H <= 0 || HKV <= 0 || H % HKV) return KGS_ERR_SHAPE;
-  if (hd != HD || S % QB) return KGS_ERR_SHAPE;
+  if (hd != HD || S % QB || Sk < S || (Sk - S) % KB) return KGS_ERR_SHAPE;
   if (ldq < (long)H * HD || ldk < (long)HKV * HD || ldv < (long)HKV * HD || ldo < (long)H * HD) return KGS_ERR_SHAPE;
   const uintptr_t al = (uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o;
   if ((al & 15) || (ldq | ldk | ldv | ldo) & 7) return KGS_ERR_ALIGN;
   const long nwg = (long)B * H * (S / QB);
   if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
   Args a{(const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o,
-         ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0};
+         ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0, Sk, Sk - S};
   hipLaunchKernelGGL(fwd, dim3((unsigned)nwg), dim3(256), 0, s, a);
   return (int)hipGetLastError();
+}
+
+KGS_EXPORT int kgs_attn_fwd_bf16(const void* q, const void* k, const void* v, void* o, int B, int S, int H, int HKV,
+                                int hd, long ldq, long ldk, long ldv, long ldo, float scale, int causal,
+                                hipStream_t s) {
+  return kgs_attn_fwd_bf16_ex(q, k, v, o, B, S, S, H, HKV, hd, ldq, ldk, ldv, ldo, scale, causal, s);
 }

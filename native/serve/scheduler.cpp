@@ -33,6 +33,8 @@ Scheduler::Scheduler(const SchedulerConfig& cfg) : cfg_(cfg), alloc_(cfg.num_pag
   const int pad = std::max(1, cfg_.pad_multiple);
   cfg_.pad_multiple = pad;
   cfg_.max_prefill_tokens = std::max(cfg_.max_prefill_tokens, (cfg_.max_model_len + pad - 1) / pad * pad);
+  // a mixed step always has room for one padded chunk
+  if (cfg_.chunk_tokens > 0) cfg_.chunk_tokens = std::max(cfg_.chunk_tokens, pad);
 }
 
 bool Scheduler::add(int64_t id, const std::vector<int32_t>& prompt, int max_new_tokens) {
@@ -157,7 +159,121 @@ void Scheduler::build_decode(StepPlan& plan) {
   }
 }
 
+StepPlan Scheduler::schedule_mixed() {
+  StepPlan plan;
+  const int ps = cfg_.page_size, pad = cfg_.pad_multiple;
+  // 1) every decode-ready sequence gets a slot for one more token (preempting
+  //    the newest sequences when the cache is full, as build_decode does)
+  for (size_t i = 0; i < running_.size();) {
+    Sequence& s = seqs_.at(running_[i]);
+    if (!decode_ready(s) || pages_for(s.cached + 1) <= (int)s.pages.size()) {
+      ++i;
+      continue;
+    }
+    int p = alloc_.alloc();
+    while (p < 0) {
+      Sequence& victim = seqs_.at(running_.back());
+      const bool self = victim.id == s.id;
+      preempt(victim, plan);
+      if (self) break;
+      p = alloc_.alloc();
+    }
+    if (p < 0) continue;
+    s.pages.push_back(p);
+    ++i;
+  }
+  std::vector<int64_t> dec;
+  for (int64_t id : running_)
+    if (decode_ready(seqs_.at(id))) dec.push_back(id);
+  // 2) prompt chunks within the remaining row budget: sequences already
+  //    prefilling (admission order), then newly admitted ones
+  int budget = std::max(pad, cfg_.chunk_tokens - (int)dec.size());
+  const int watermark = std::max(1, (cfg_.num_pages - 1) / 100);
+  std::vector<int64_t> pf;
+  auto add_chunk = [&](Sequence& s) -> bool {
+    const int len = (int)s.tokens.size(), rem = len - s.cached;
+    const bool last = rem <= budget;
+    const int n = last ? rem : budget / pad * pad;  // non-final chunks: whole q-blocks
+    if (n <= 0) return false;
+    const int padded = (n + pad - 1) / pad * pad;
+    const int need = pages_for(s.cached + n + (last ? 1 : 0)) - (int)s.pages.size();
+    if (need > 0 && alloc_.num_free() - need < (dec.empty() && pf.empty() ? 0 : watermark)) return false;
+    for (int i = 0; i < need; ++i) s.pages.push_back(alloc_.alloc());
+    const int start = (int)plan.tokens.size();
+    plan.seq_ids.push_back(s.id);
+    plan.seq_starts.push_back(start);
+    plan.seq_lens.push_back(n);
+    plan.padded_lens.push_back(padded);
+    plan.ctx_starts.push_back(s.cached);
+    plan.last_chunk.push_back(last ? 1 : 0);
+    for (int t = 0; t < padded; ++t) {
+      const int pos = s.cached + t;
+      const bool real = t < n;
+      plan.tokens.push_back(real ? s.tokens[pos] : 0);
+      plan.positions.push_back(pos);
+      plan.slots.push_back(real ? s.pages[pos / ps] * ps + pos % ps : -1);
+    }
+    s.cached += n;
+    budget -= padded;
+    pf.push_back(s.id);
+    return true;
+  };
+  auto fill = [&]() {
+    for (int64_t id : running_) {
+      Sequence& s = seqs_.at(id);
+      if (budget < pad) break;
+      if (!decode_ready(s) && s.cached < (int)s.tokens.size()) add_chunk(s);
+    }
+    while (!waiting_.empty() && budget >= pad && (int)running_.size() < cfg_.max_batch) {
+      Sequence& s = seqs_.at(waiting_.front());
+      if (!add_chunk(s)) break;
+      waiting_.pop_front();
+      s.state = SeqState::kRunning;
+      s.arrival = next_arrival_++;
+      running_.push_back(s.id);
+    }
+  };
+  fill();
+  // every running sequence is mid-prompt and none can get pages for its next
+  // chunk: free the newest (recompute later) so the others progress
+  while (dec.empty() && pf.empty() && !running_.empty()) {
+    preempt(seqs_.at(running_.back()), plan);
+    fill();
+  }
+  plan.n_prefill = (int)pf.size();
+  // 3) decode rows after the chunks
+  if (!pf.empty()) {
+    int maxp = 0;
+    for (int64_t id : pf) maxp = std::max(maxp, (int)seqs_.at(id).pages.size());
+    plan.pf_max_pages = maxp;
+    plan.pf_block_tables.assign(pf.size() * (size_t)maxp, 0);
+    for (size_t i = 0; i < pf.size(); ++i) {
+      const Sequence& s = seqs_.at(pf[i]);
+      std::copy(s.pages.begin(), s.pages.end(), plan.pf_block_tables.begin() + i * maxp);
+    }
+  }
+  int maxp = 0;
+  for (int64_t id : dec) maxp = std::max(maxp, (int)seqs_.at(id).pages.size());
+  plan.max_pages = maxp;
+  plan.block_tables.assign(dec.size() * (size_t)maxp, 0);
+  for (size_t i = 0; i < dec.size(); ++i) {
+    Sequence& s = seqs_.at(dec[i]);
+    const int pos = s.cached;
+    plan.seq_ids.push_back(s.id);
+    plan.tokens.push_back(s.tokens.back());
+    plan.positions.push_back(pos);
+    plan.slots.push_back(s.pages[pos / ps] * ps + pos % ps);
+    plan.ctx_lens.push_back(pos + 1);
+    std::copy(s.pages.begin(), s.pages.end(), plan.block_tables.begin() + i * maxp);
+    s.cached = pos + 1;
+  }
+  // no chunk this step: a plain decode plan (the engine replays its hipGraph)
+  plan.kind = plan.seq_ids.empty() ? 0 : pf.empty() ? 2 : 3;
+  return plan;
+}
+
 StepPlan Scheduler::schedule() {
+  if (cfg_.chunk_tokens > 0) return schedule_mixed();
   StepPlan plan;
   if (!waiting_.empty() && try_prefill(plan)) return plan;
   build_decode(plan);

@@ -7,6 +7,11 @@
 //     per-token positions and KV-cache slots (-1 for padding rows);
 //   * DECODE: every running sequence's last token, its position, the slot the
 //     new k/v goes to, its block table and context length.
+//   * MIXED (SchedulerConfig::chunk_tokens > 0, chunked prefill): every
+//     decode-ready sequence's token PLUS prompt chunks of sequences still
+//     prefilling, within a per-step token budget -- a long prompt is split over
+//     steps (chunks are multiples of pad_multiple except the last), so decode
+//     steps never wait behind a whole prefill. Prefill rows come first.
 // Pages are PAGE_SIZE tokens; page 0 is reserved as the null page that padded
 // decode rows point at (never handed out). When a decode step cannot get a new
 // page, the most recently admitted running sequence is preempted: its pages are
@@ -54,7 +59,7 @@ struct Sequence {
 };
 
 struct StepPlan {
-  int kind = 0;  // 0 idle, 1 prefill, 2 decode
+  int kind = 0;  // 0 idle, 1 prefill, 2 decode, 3 mixed (chunked prefill + decode)
   std::vector<int64_t> seq_ids;
   // prefill (flattened over sequences, each padded to pad_multiple)
   std::vector<int32_t> tokens, positions, slots;
@@ -64,6 +69,16 @@ struct StepPlan {
   std::vector<int32_t> ctx_lens;
   int max_pages = 0;
   std::vector<int64_t> preempted;
+  // mixed: seq_ids[0 .. n_prefill) are prefill chunks (rows first, with
+  // seq_starts / seq_lens / padded_lens), the rest decode rows (block_tables /
+  // ctx_lens); ctx_starts = tokens cached before the chunk, last_chunk = the
+  // chunk completes the prompt (its last row is sampled), pf_block_tables
+  // [n_prefill, pf_max_pages] the chunk sequences' pages
+  int n_prefill = 0;
+  std::vector<int32_t> ctx_starts;
+  std::vector<uint8_t> last_chunk;
+  std::vector<int32_t> pf_block_tables;
+  int pf_max_pages = 0;
 };
 
 struct SchedulerConfig {
@@ -73,6 +88,7 @@ struct SchedulerConfig {
   int max_prefill_tokens = 16384; // padded tokens per prefill step
   int max_model_len = 8192;
   int pad_multiple = 128;
+  int chunk_tokens = 0;           // > 0: mixed steps of at most this many rows (chunked prefill)
 };
 
 class Scheduler {
@@ -99,6 +115,8 @@ class Scheduler {
   int pages_for(int tokens) const { return (tokens + cfg_.page_size - 1) / cfg_.page_size; }
   bool try_prefill(StepPlan& plan);
   void build_decode(StepPlan& plan);
+  StepPlan schedule_mixed();
+  bool decode_ready(const Sequence& s) const { return s.cached == (int)s.tokens.size() - 1; }
   void preempt(Sequence& s, StepPlan& plan);
   void free_pages(Sequence& s);
 

@@ -36,7 +36,8 @@ PYBIND11_MODULE(_serve, m) {
       .def_readwrite("max_batch", &SchedulerConfig::max_batch)
       .def_readwrite("max_prefill_tokens", &SchedulerConfig::max_prefill_tokens)
       .def_readwrite("max_model_len", &SchedulerConfig::max_model_len)
-      .def_readwrite("pad_multiple", &SchedulerConfig::pad_multiple);
+      .def_readwrite("pad_multiple", &SchedulerConfig::pad_multiple)
+      .def_readwrite("chunk_tokens", &SchedulerConfig::chunk_tokens);
 
   py::class_<StepPlan>(m, "StepPlan")
       .def_readonly("kind", &StepPlan::kind)
@@ -55,7 +56,16 @@ PYBIND11_MODULE(_serve, m) {
                                return a;
                              })
       .def_property_readonly("ctx_lens", [](const StepPlan& p) { return arr(p.ctx_lens); })
-      .def_property_readonly("preempted", [](const StepPlan& p) { return arr(p.preempted); });
+      .def_property_readonly("preempted", [](const StepPlan& p) { return arr(p.preempted); })
+      .def_readonly("n_prefill", &StepPlan::n_prefill)
+      .def_readonly("pf_max_pages", &StepPlan::pf_max_pages)
+      .def_property_readonly("ctx_starts", [](const StepPlan& p) { return arr(p.ctx_starts); })
+      .def_property_readonly("last_chunk", [](const StepPlan& p) { return arr(p.last_chunk); })
+      .def_property_readonly("pf_block_tables", [](const StepPlan& p) {
+        auto a = arr(p.pf_block_tables);
+        if (p.pf_max_pages > 0) a.resize({(py::ssize_t)p.n_prefill, (py::ssize_t)p.pf_max_pages});
+        return a;
+      });
 
   py::class_<Scheduler>(m, "Scheduler")
       .def(py::init<const SchedulerConfig&>(), py::arg("config"))

@@ -12,10 +12,11 @@ from hypothesis import given, settings  # noqa: E402
 from hypothesis import strategies as st  # noqa: E402
 
 
-def _sched(num_pages=64, max_batch=8, max_model_len=512, max_prefill=1024):
+def _sched(num_pages=64, max_batch=8, max_model_len=512, max_prefill=1024, chunk_tokens=0):
     c = _serve.SchedulerConfig()
     c.num_pages, c.page_size, c.max_batch = num_pages, 32, max_batch
     c.max_prefill_tokens, c.max_model_len, c.pad_multiple = max_prefill, max_model_len, 128
+    c.chunk_tokens = chunk_tokens
     return _serve.Scheduler(c)
 
 
@@ -106,11 +107,14 @@ def test_preemption_recomputes_newest():
     assert s.info(2)["preemptions"] >= 1
 
 
-@settings(max_examples=40, deadline=None)
+@settings(max_examples=60, deadline=None)
 @given(st.lists(st.tuples(st.integers(1, 300), st.integers(1, 60), st.booleans()), min_size=1, max_size=25),
-       st.integers(8, 40), st.integers(1, 6))
-def test_random_traffic_invariants(reqs, pages, max_batch):
-    s = _sched(num_pages=pages, max_batch=max_batch, max_model_len=512)
+       st.integers(8, 40), st.integers(1, 6), st.sampled_from([0, 0, 128, 256, 512]))
+def test_random_traffic_invariants(reqs, pages, max_batch, chunk):
+    """Random traffic through both scheduling modes (whole-prompt prefill and
+    chunked prefill): invariants hold every step, every request finishes, no
+    page leaks."""
+    s = _sched(num_pages=pages, max_batch=max_batch, max_model_len=512, chunk_tokens=chunk)
     live = set()
     for i, (plen, new, _) in enumerate(reqs):
         if s.add(i, np.full(plen, 3, np.int32), new):
@@ -121,9 +125,12 @@ def test_random_traffic_invariants(reqs, pages, max_batch):
         assert s.check_invariants() == "", s.check_invariants()
         if p.kind == 0:
             break
-        n = len(p.seq_ids)
+        ids = p.seq_ids
+        if p.kind == 3:  # only completed prompts and decodes sample
+            ids = np.concatenate([ids[:p.n_prefill][p.last_chunk.astype(bool)], ids[p.n_prefill:]])
+        n = len(ids)
         eos = (rng.random(n) < 0.05).astype(np.uint8)
-        for d in s.update(p.seq_ids, np.full(n, 4, np.int32), eos):
+        for d in s.update(ids, np.full(n, 4, np.int32), eos):
             live.discard(int(d))
         if p.kind == 2:
             assert (p.ctx_lens == p.positions + 1).all()
@@ -161,6 +168,58 @@ def test_engine_ref_matches_full_recompute():
     assert all(len(r.output) == 6 and r.finish_reason == "length" for r in outs)
     assert eng.stats["prefill_steps"] >= 2 and eng.stats["decode_steps"] >= 5  # max_batch 4 < 5 prompts
     _check_against_oracle(eng, prompts, outs)
+
+
+def test_engine_ref_chunked_prefill_matches_full_recompute():
+    """Chunked prefill (mixed steps, 256-row budget): long prompts split over
+    steps and attend to their own cached chunks; decodes of shorter sequences run
+    in the same steps. Generations equal the full-recompute oracle's."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=96, max_batch=4, max_model_len=1024, cuda_graphs=False,
+                                          chunked_prefill=256), device="cpu", backend="ref")
+    rng = np.random.default_rng(5)
+    prompts = [rng.integers(3, 512, size=n).tolist() for n in (40, 700, 300, 129, 5)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
+    assert all(len(r.output) == 5 for r in outs)
+    assert eng.stats["mixed_steps"] >= 4  # the 700-token prompt alone needs 3 chunks
+    assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts)
+    _check_against_oracle(eng, prompts, outs)
+    assert eng.sched.check_invariants() == ""
+
+
+def test_scheduler_chunked_plans():
+    """Mixed plans: decode rows after the chunks, non-final chunks whole
+    q-blocks, ctx_starts advancing, every prompt token scheduled exactly once."""
+    from kgs._native import _serve
+
+    cfg = _serve.SchedulerConfig()
+    cfg.num_pages, cfg.page_size, cfg.max_batch, cfg.max_model_len, cfg.pad_multiple = 200, 32, 8, 2048, 128
+    cfg.chunk_tokens = 384
+    s = _serve.Scheduler(cfg)
+    assert s.add(1, list(range(3, 1003)), 4) and s.add(2, [5, 6, 7], 4)
+    seen = {1: 0, 2: 0}
+    kinds = []
+    for _ in range(12):
+        p = s.schedule()
+        if p.kind == 0:
+            break
+        kinds.append(p.kind)
+        assert s.check_invariants() == ""
+        npf = p.n_prefill if p.kind == 3 else 0
+        ids = list(p.seq_ids)
+        for j in range(npf):
+            assert p.ctx_starts[j] == seen[ids[j]] and p.ctx_starts[j] % 128 == 0
+            if not p.last_chunk[j]:
+                assert p.seq_lens[j] % 128 == 0
+            seen[ids[j]] += int(p.seq_lens[j])
+        assert len(p.tokens) == sum(p.padded_lens[:npf]) + len(ids) - npf if p.kind == 3 else True
+        assert sum(p.padded_lens[:npf]) + len(ids) - npf <= 384 + 128
+        sampled = [ids[j] for j in range(npf) if p.last_chunk[j]] + ids[npf:]
+        s.update(np.array(sampled, dtype=np.int64), np.full(len(sampled), 9, dtype=np.int32),
+                 np.zeros(len(sampled), dtype=np.uint8))
+    assert seen == {1: 1000, 2: 3}
+    assert 3 in kinds and 2 in kinds  # mixed steps while prompt 1 prefills, then plain decode plans
 
 
 def test_engine_ref_preemption_is_transparent():
