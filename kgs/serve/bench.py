@@ -20,9 +20,12 @@ import numpy as np
 import torch
 
 
-def _prompts(n, length, vocab, seed=0):
+def _prompts(n, length, vocab, seed=0, shared=0):
+    """n random prompts of `length` tokens; the first `shared` tokens are one
+    common prefix (a system prompt) when shared > 0."""
     rng = np.random.default_rng(seed)
-    return [rng.integers(3, vocab, size=length).tolist() for _ in range(n)]
+    head = rng.integers(3, vocab, size=min(shared, length)).tolist()
+    return [head + rng.integers(3, vocab, size=length - len(head)).tolist() for _ in range(n)]
 
 
 def _graph_widths(a):
@@ -41,7 +44,7 @@ def run_engine(a) -> dict:
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
-                      chunked_prefill=a.chunked_prefill)
+                      chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -52,7 +55,7 @@ def run_engine(a) -> dict:
     eng.generate(_prompts(1, 16, mc.vocab, seed=9), SamplingParams(max_tokens=4, ignore_eos=True))
     torch.cuda.synchronize()
     t_warm = time.perf_counter() - t0
-    prompts = _prompts(a.requests, a.input_len, mc.vocab)
+    prompts = _prompts(a.requests, a.input_len, mc.vocab, shared=a.shared_prefix)
     params = SamplingParams(max_tokens=a.output_len, ignore_eos=True)
     for k in eng.stats:
         eng.stats[k] = 0
@@ -71,6 +74,8 @@ def run_engine(a) -> dict:
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "kv_cache_dtype": a.kv_cache_dtype, "chunked_prefill": a.chunked_prefill,
+        "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
+        "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
         "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
@@ -100,6 +105,7 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=getattr(a, "chunked_prefill", 0),
+                      prefix_caching=getattr(a, "prefix_caching", False),
                       **({"num_pages": 256} if device == "cpu" else {}))
     eng = LLMEngine(mc, ec, device=device, backend=backend)
     if not a.no_graphs:
@@ -109,7 +115,7 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
         torch.cuda.synchronize()
     rng = np.random.default_rng(1)
     arrivals = np.cumsum(rng.exponential(1.0 / a.request_rate, size=a.requests))
-    prompts = _prompts(a.requests, a.input_len, mc.vocab)
+    prompts = _prompts(a.requests, a.input_len, mc.vocab, shared=getattr(a, "shared_prefix", 0))
     params = SamplingParams(max_tokens=a.output_len, ignore_eos=True)
     tok_times: dict = {}
     done = []
@@ -140,7 +146,9 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
         "metric": "online serving (kgs.serve, Poisson arrivals, Llama-3-8B arch, random init)",
         "backend": "kgs", "requests": a.requests, "request_rate": a.request_rate, "input_len": a.input_len,
         "output_len": a.output_len, "max_batch": a.max_batch, "layers": a.layers,
-        "chunked_prefill": getattr(a, "chunked_prefill", 0), "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
+        "chunked_prefill": getattr(a, "chunked_prefill", 0), "prefix_caching": getattr(a, "prefix_caching", False),
+        "shared_prefix": getattr(a, "shared_prefix", 0), "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
+        "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
         "requests_per_s": round(len(done) / dt, 3),
         "ttft_ms": {"p50": ms(_pct(ttft, .5)), "p99": ms(_pct(ttft, .99)), "mean": ms(float(np.mean(ttft)))},
         "tpot_ms": {"p50": ms(_pct(tpot, .5)), "p99": ms(_pct(tpot, .99)), "mean": ms(float(np.mean(tpot)))},
@@ -201,6 +209,9 @@ def main(argv=None) -> int:
                     help="fp8 = e4m3 KV pages (half the attention bytes); the headline is bf16")
     ap.add_argument("--chunked-prefill", type=int, default=0,
                     help="> 0: mixed steps of at most this many rows (prompt chunks + decodes)")
+    ap.add_argument("--prefix-caching", action="store_true", help="reuse cached pages of shared prompt prefixes")
+    ap.add_argument("--shared-prefix", type=int, default=0,
+                    help="the first N prompt tokens are common to every request (a system prompt)")
     ap.add_argument("--request-rate", type=float, default=0.0,
                     help="> 0: online mode, Poisson arrivals at this many requests/s (TTFT/TPOT/ITL p50/p99)")
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")

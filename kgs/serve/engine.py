@@ -63,6 +63,7 @@ class EngineConfig:
     decode_weights: str = "bf16"      # "fp8": weight-only fp8 decode copies (W8A16)
     kv_cache_dtype: str = "bf16"      # "fp8": e4m3 KV pages
     chunked_prefill: int = 0          # > 0: mixed steps of at most this many rows (prompt chunks + decodes)
+    prefix_caching: bool = False      # reuse cached KV pages of shared prompt prefixes (runs on mixed steps)
     seed: int = 0
 
 
@@ -88,6 +89,7 @@ class LLMEngine:
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
         sc.chunk_tokens = cfg.chunked_prefill
+        sc.prefix_caching = cfg.prefix_caching
         self.sched = _serve.Scheduler(sc)
         self.num_pages = num_pages
         self.requests: dict[int, Request] = {}

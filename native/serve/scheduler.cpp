@@ -7,25 +7,136 @@
 namespace kgs {
 namespace serve {
 
-BlockAllocator::BlockAllocator(int num_pages) : num_pages_(num_pages), state_(num_pages > 0 ? num_pages : 0, 0) {
+BlockAllocator::BlockAllocator(int num_pages)
+    : num_pages_(num_pages), ref_(num_pages > 0 ? num_pages : 0, 0), lru_pos_(num_pages > 0 ? num_pages : 0),
+      in_lru_(num_pages > 0 ? num_pages : 0, 0), hash_(num_pages > 0 ? num_pages : 0, 0),
+      parent_(num_pages > 0 ? num_pages : 0, 0), hashed_(num_pages > 0 ? num_pages : 0, 0),
+      toks_(num_pages > 0 ? num_pages : 0) {
   // page 0 is the null page: never handed out
-  if (num_pages_ > 0) state_[0] = 1;
+  if (num_pages_ > 0) ref_[0] = 1;
   free_.reserve(num_pages_);
   for (int p = num_pages_ - 1; p >= 1; --p) free_.push_back(p);
 }
 
+void BlockAllocator::forget(int page) {
+  if (!hashed_[page]) return;
+  auto it = by_hash_.find(hash_[page]);
+  if (it != by_hash_.end() && it->second == page) by_hash_.erase(it);
+  hashed_[page] = 0;
+  toks_[page].clear();
+}
+
 int BlockAllocator::alloc() {
-  if (free_.empty()) return -1;
-  const int p = free_.back();
-  free_.pop_back();
-  state_[p] = 1;
+  int p;
+  if (!free_.empty()) {
+    p = free_.back();
+    free_.pop_back();
+  } else if (!lru_.empty()) {  // evict the least recently released cached page
+    p = lru_.back();
+    lru_.pop_back();
+    in_lru_[p] = 0;
+    forget(p);
+  } else {
+    return -1;
+  }
+  ref_[p] = 1;
   return p;
 }
 
 void BlockAllocator::free(int page) {
-  if (page <= 0 || page >= num_pages_ || state_[page] == 0) return;  // double free / null page: ignore
-  state_[page] = 0;
-  free_.push_back(page);
+  if (page <= 0 || page >= num_pages_ || ref_[page] == 0) return;  // double free / null page: ignore
+  if (--ref_[page] > 0) return;
+  if (hashed_[page]) {
+    lru_.push_front(page);
+    lru_pos_[page] = lru_.begin();
+    in_lru_[page] = 1;
+  } else {
+    free_.push_back(page);
+  }
+}
+
+void BlockAllocator::acquire(int page) {
+  if (page <= 0 || page >= num_pages_) return;
+  if (in_lru_[page]) {
+    lru_.erase(lru_pos_[page]);
+    in_lru_[page] = 0;
+  }
+  ++ref_[page];
+}
+
+void BlockAllocator::register_page(int page, uint64_t hash, uint64_t parent, const int32_t* tokens, int n) {
+  if (page <= 0 || page >= num_pages_ || hashed_[page] || by_hash_.count(hash)) return;
+  by_hash_[hash] = page;
+  hash_[page] = hash;
+  parent_[page] = parent;
+  hashed_[page] = 1;
+  toks_[page].assign(tokens, tokens + n);
+}
+
+int BlockAllocator::lookup(uint64_t hash, uint64_t parent, const int32_t* tokens, int n) const {
+  auto it = by_hash_.find(hash);
+  if (it == by_hash_.end()) return -1;
+  const int p = it->second;
+  // exact check: the same parent chain and the same tokens (no trust in the hash alone)
+  if (parent_[p] != parent || (int)toks_[p].size() != n || !std::equal(tokens, tokens + n, toks_[p].begin()))
+    return -1;
+  return p;
+}
+
+namespace {
+// FNV-1a over (parent hash, the page's token ids)
+uint64_t page_hash(uint64_t parent, const int32_t* t, int n) {
+  uint64_t h = 1469598103934665603ull ^ parent;
+  h *= 1099511628211ull;
+  for (int i = 0; i < n; ++i) {
+    uint32_t v = (uint32_t)t[i];
+    for (int b = 0; b < 4; ++b) {
+      h ^= (v >> (8 * b)) & 0xff;
+      h *= 1099511628211ull;
+    }
+  }
+  return h;
+}
+}  // namespace
+
+int Scheduler::match_prefix(Sequence& s) {
+  // leading full pages already cached; keep the last token to compute (its
+  // logits), and an even page count: a chunk's context must be a multiple of
+  // the attention kernel's 64-key tile
+  const int ps = cfg_.page_size, len = (int)s.tokens.size();
+  uint64_t h = 0;
+  std::vector<int> hit;
+  std::vector<uint64_t> hs;
+  for (int j = 0; (j + 1) * ps <= len - 1; ++j) {
+    const int32_t* t = s.tokens.data() + j * ps;
+    const uint64_t hj = page_hash(h, t, ps);
+    const int p = alloc_.lookup(hj, h, t, ps);
+    if (p < 0) break;
+    hit.push_back(p);
+    hs.push_back(hj);
+    h = hj;
+  }
+  const int keep = (int)hit.size() / 2 * 2;
+  if (keep == 0) return 0;
+  for (int j = 0; j < keep; ++j) {
+    alloc_.acquire(hit[j]);
+    s.pages.push_back(hit[j]);
+  }
+  s.hashed = keep;
+  s.tail_hash = hs[keep - 1];
+  s.cached = keep * ps;
+  return s.cached;
+}
+
+void Scheduler::register_full_pages(Sequence& s) {
+  const int ps = cfg_.page_size;
+  while ((s.hashed + 1) * ps <= s.cached && s.hashed < (int)s.pages.size()) {
+    const int32_t* t = s.tokens.data() + s.hashed * ps;
+    const uint64_t h = page_hash(s.tail_hash, t, ps);
+    alloc_.register_page(s.pages[s.hashed], h, s.tail_hash, t, ps);
+    s.tail_hash = h;
+    s.hashed++;
+  }
 }
 
 Scheduler::Scheduler(const SchedulerConfig& cfg) : cfg_(cfg), alloc_(cfg.num_pages) {
@@ -33,6 +144,9 @@ Scheduler::Scheduler(const SchedulerConfig& cfg) : cfg_(cfg), alloc_(cfg.num_pag
   const int pad = std::max(1, cfg_.pad_multiple);
   cfg_.pad_multiple = pad;
   cfg_.max_prefill_tokens = std::max(cfg_.max_prefill_tokens, (cfg_.max_model_len + pad - 1) / pad * pad);
+  // prefix caching skips cached leading pages with a chunk over the cached
+  // context: it runs on mixed steps
+  if (cfg_.prefix_caching && cfg_.chunk_tokens <= 0) cfg_.chunk_tokens = cfg_.max_prefill_tokens;
   // a mixed step always has room for one padded chunk
   if (cfg_.chunk_tokens > 0) cfg_.chunk_tokens = std::max(cfg_.chunk_tokens, pad);
 }
@@ -57,6 +171,8 @@ void Scheduler::free_pages(Sequence& s) {
   for (int p : s.pages) alloc_.free(p);
   s.pages.clear();
   s.cached = 0;
+  s.hashed = 0;
+  s.tail_hash = 0;
 }
 
 bool Scheduler::abort(int64_t id) {
@@ -191,13 +307,20 @@ StepPlan Scheduler::schedule_mixed() {
   const int watermark = std::max(1, (cfg_.num_pages - 1) / 100);
   std::vector<int64_t> pf;
   auto add_chunk = [&](Sequence& s) -> bool {
+    int matched = 0;
+    if (cfg_.prefix_caching && s.cached == 0 && s.pages.empty()) matched = match_prefix(s);
+    auto undo = [&]() {
+      if (matched) free_pages(s);
+      return false;
+    };
     const int len = (int)s.tokens.size(), rem = len - s.cached;
     const bool last = rem <= budget;
     const int n = last ? rem : budget / pad * pad;  // non-final chunks: whole q-blocks
-    if (n <= 0) return false;
+    if (n <= 0) return undo();
     const int padded = (n + pad - 1) / pad * pad;
     const int need = pages_for(s.cached + n + (last ? 1 : 0)) - (int)s.pages.size();
-    if (need > 0 && alloc_.num_free() - need < (dec.empty() && pf.empty() ? 0 : watermark)) return false;
+    if (need > 0 && alloc_.num_free() - need < (dec.empty() && pf.empty() ? 0 : watermark)) return undo();
+    prefix_hits_ += matched;
     for (int i = 0; i < need; ++i) s.pages.push_back(alloc_.alloc());
     const int start = (int)plan.tokens.size();
     plan.seq_ids.push_back(s.id);
@@ -214,6 +337,7 @@ StepPlan Scheduler::schedule_mixed() {
       plan.slots.push_back(real ? s.pages[pos / ps] * ps + pos % ps : -1);
     }
     s.cached += n;
+    if (cfg_.prefix_caching) register_full_pages(s);  // written by this step, before any later step reads them
     budget -= padded;
     pf.push_back(s.id);
     return true;
@@ -313,20 +437,30 @@ void Scheduler::release(int64_t id) {
 
 std::string Scheduler::check_invariants() const {
   std::ostringstream err;
-  std::vector<int> owner(cfg_.num_pages, 0);
+  std::vector<int> owners(cfg_.num_pages, 0);
   for (const auto& kv : seqs_) {
     const Sequence& s = kv.second;
     if (s.state != SeqState::kRunning && !s.pages.empty()) err << "seq " << s.id << " not running but holds pages; ";
     if (s.state == SeqState::kRunning && pages_for(s.cached) > (int)s.pages.size())
       err << "seq " << s.id << " cached " << s.cached << " beyond its pages; ";
+    std::vector<int> mine(s.pages);
+    std::sort(mine.begin(), mine.end());
+    if (std::adjacent_find(mine.begin(), mine.end()) != mine.end()) err << "seq " << s.id << " holds a page twice; ";
     for (int p : s.pages) {
-      if (p <= 0 || p >= cfg_.num_pages) err << "seq " << s.id << " holds bad page " << p << "; ";
-      else if (owner[p]++) err << "page " << p << " shared; ";
+      if (p <= 0 || p >= cfg_.num_pages) {
+        err << "seq " << s.id << " holds bad page " << p << "; ";
+        continue;
+      }
+      owners[p]++;
       if (alloc_.is_free(p)) err << "page " << p << " both free and owned; ";
     }
   }
   int owned = 0;
-  for (int c : owner) owned += c;
+  for (int p = 1; p < cfg_.num_pages; ++p) {
+    if (owners[p] != alloc_.refs(p)) err << "page " << p << " refs " << alloc_.refs(p) << " owners " << owners[p] << "; ";
+    if (!cfg_.prefix_caching && owners[p] > 1) err << "page " << p << " shared without prefix caching; ";
+    owned += owners[p] > 0;
+  }
   if (owned + alloc_.num_free() != cfg_.num_pages - 1) err << "page leak: owned " << owned << " free " << alloc_.num_free() << "; ";
   if ((int)running_.size() > cfg_.max_batch) err << "running over max_batch; ";
   for (int64_t id : running_)

@@ -21,6 +21,7 @@
 
 #include <cstdint>
 #include <deque>
+#include <list>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -28,19 +29,39 @@
 namespace kgs {
 namespace serve {
 
+// Pages carry a reference count: with prefix caching, sequences whose prompts
+// share leading pages share those pages. A page whose count drops to zero goes
+// back to the free stack -- or, if it holds a registered (hashed) full prompt
+// page, to an LRU list of evictable cached pages that a later prompt with the
+// same prefix can re-acquire. alloc() takes free pages first, then evicts the
+// least recently released cached page.
 class BlockAllocator {
  public:
   explicit BlockAllocator(int num_pages);
   int alloc();                   // -1 when exhausted
-  void free(int page);
-  int num_free() const { return (int)free_.size(); }
+  void free(int page);           // drop one reference
+  void acquire(int page);        // one more reference (revives an evictable cached page)
+  int num_free() const { return (int)free_.size() + (int)lru_.size(); }  // allocatable
   int num_pages() const { return num_pages_; }
-  bool is_free(int page) const { return page > 0 && page < num_pages_ && state_[page] == 0; }
+  int refs(int page) const { return page > 0 && page < num_pages_ ? ref_[page] : 0; }
+  bool is_free(int page) const { return page > 0 && page < num_pages_ && ref_[page] == 0; }
+  // prefix cache: a full page's content key (chained hash + its tokens)
+  void register_page(int page, uint64_t hash, uint64_t parent, const int32_t* tokens, int n);
+  int lookup(uint64_t hash, uint64_t parent, const int32_t* tokens, int n) const;  // -1 if absent
+  int num_cached() const { return (int)by_hash_.size(); }
 
  private:
+  void forget(int page);
   int num_pages_;
   std::vector<int> free_;      // LIFO stack (recently freed pages are reused first: warm in L2/MALL)
-  std::vector<uint8_t> state_; // 0 free, 1 in use
+  std::vector<int> ref_;
+  std::list<int> lru_;         // evictable cached pages, most recently released first
+  std::vector<std::list<int>::iterator> lru_pos_;
+  std::vector<uint8_t> in_lru_;
+  std::unordered_map<uint64_t, int> by_hash_;
+  std::vector<uint64_t> hash_, parent_;
+  std::vector<uint8_t> hashed_;
+  std::vector<std::vector<int32_t>> toks_;
 };
 
 enum class SeqState : int { kWaiting = 0, kRunning = 1, kFinished = 2 };
@@ -56,6 +77,8 @@ struct Sequence {
   int cached = 0;               // tokens whose k/v are in the cache
   SeqState state = SeqState::kWaiting;
   int preemptions = 0;
+  int hashed = 0;               // leading pages registered in the prefix cache
+  uint64_t tail_hash = 0;       // chained hash of those pages
 };
 
 struct StepPlan {
@@ -89,6 +112,7 @@ struct SchedulerConfig {
   int max_model_len = 8192;
   int pad_multiple = 128;
   int chunk_tokens = 0;           // > 0: mixed steps of at most this many rows (chunked prefill)
+  bool prefix_caching = false;    // share full prompt pages across sequences (implies chunked prefill)
 };
 
 class Scheduler {
@@ -108,6 +132,8 @@ class Scheduler {
   int num_waiting() const { return (int)waiting_.size(); }
   int num_running() const { return (int)running_.size(); }
   int num_free_pages() const { return alloc_.num_free(); }
+  int64_t prefix_hit_tokens() const { return prefix_hits_; }
+  int num_cached_pages() const { return alloc_.num_cached(); }
   const SchedulerConfig& config() const { return cfg_; }
   std::string check_invariants() const;  // "" when consistent (tests)
 
@@ -126,6 +152,9 @@ class Scheduler {
   std::deque<int64_t> waiting_;
   std::vector<int64_t> running_;  // admission order
   int64_t next_arrival_ = 0;
+  int64_t prefix_hits_ = 0;
+  int match_prefix(Sequence& s);     // acquire cached leading pages; returns tokens matched
+  void register_full_pages(Sequence& s);
 };
 
 }  // namespace serve

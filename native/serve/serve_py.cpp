@@ -37,7 +37,8 @@ PYBIND11_MODULE(_serve, m) {
       .def_readwrite("max_prefill_tokens", &SchedulerConfig::max_prefill_tokens)
       .def_readwrite("max_model_len", &SchedulerConfig::max_model_len)
       .def_readwrite("pad_multiple", &SchedulerConfig::pad_multiple)
-      .def_readwrite("chunk_tokens", &SchedulerConfig::chunk_tokens);
+      .def_readwrite("chunk_tokens", &SchedulerConfig::chunk_tokens)
+      .def_readwrite("prefix_caching", &SchedulerConfig::prefix_caching);
 
   py::class_<StepPlan>(m, "StepPlan")
       .def_readonly("kind", &StepPlan::kind)
@@ -110,5 +111,7 @@ PYBIND11_MODULE(_serve, m) {
       .def_property_readonly("num_waiting", &Scheduler::num_waiting)
       .def_property_readonly("num_running", &Scheduler::num_running)
       .def_property_readonly("num_free_pages", &Scheduler::num_free_pages)
+      .def_property_readonly("prefix_hit_tokens", &Scheduler::prefix_hit_tokens)
+      .def_property_readonly("num_cached_pages", &Scheduler::num_cached_pages)
       .def("check_invariants", &Scheduler::check_invariants);
 }

@@ -222,6 +222,89 @@ def test_scheduler_chunked_plans():
     assert 3 in kinds and 2 in kinds  # mixed steps while prompt 1 prefills, then plain decode plans
 
 
+def test_scheduler_prefix_caching_shares_pages():
+    from kgs._native import _serve
+
+    c = _serve.SchedulerConfig()
+    c.num_pages, c.page_size, c.max_batch, c.max_model_len, c.pad_multiple = 64, 32, 8, 1024, 128
+    c.max_prefill_tokens, c.prefix_caching = 1024, True
+    s = _serve.Scheduler(c)
+    shared = list(range(10, 10 + 200))  # 6 full pages
+    assert s.add(1, shared + [7, 8, 9], 3)
+    p = s.schedule()
+    assert p.kind == 3 and list(p.ctx_starts) == [0]
+    s.update(np.array([1]), np.array([5], np.int32), np.zeros(1, np.uint8))
+    assert s.num_cached_pages == 6
+    # same 200-token prefix: its 6 full pages are cached and reused (an even
+    # count: the chunk context must be a multiple of 64 keys), the rest computed
+    assert s.add(2, shared + [1, 2], 3)
+    p = s.schedule()
+    assert list(p.seq_ids[:p.n_prefill]) == [2] and p.ctx_starts[0] == 192 and p.seq_lens[0] == 202 - 192
+    assert s.prefix_hit_tokens == 192 and s.check_invariants() == ""
+    bt1, bt2 = s.info(1), s.info(2)
+    assert bt1["pages"] >= 7 and bt2["pages"] == 7
+    # finishing both releases the shared pages into the evictable cache, no leak
+    for _ in range(10):
+        p = s.schedule()
+        if p.kind == 0:
+            break
+        ids = p.seq_ids
+        if p.kind == 3:
+            ids = np.concatenate([ids[:p.n_prefill][p.last_chunk.astype(bool)], ids[p.n_prefill:]])
+        s.update(ids, np.full(len(ids), 4, np.int32), np.zeros(len(ids), np.uint8))
+        assert s.check_invariants() == ""
+    assert s.num_running == 0 and s.num_free_pages == 63 and s.num_cached_pages >= 6
+    # eviction: a large prompt reclaims cached pages
+    assert s.add(3, list(range(600, 600 + 1000)), 2)
+    s.schedule()
+    assert s.check_invariants() == ""
+
+
+@settings(max_examples=40, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 2), st.integers(1, 200), st.integers(1, 40)), min_size=1, max_size=20),
+       st.integers(12, 48), st.integers(1, 6), st.sampled_from([128, 256, 0]))
+def test_prefix_caching_random_traffic(reqs, pages, max_batch, chunk):
+    """Prompts built on three shared prefixes, random lengths, EOS and cache
+    pressure: refcounts match the owners every step, all requests finish, every
+    page is free or evictable at the end."""
+    c = _serve.SchedulerConfig()
+    c.num_pages, c.page_size, c.max_batch, c.max_model_len, c.pad_multiple = pages, 32, max_batch, 512, 128
+    c.max_prefill_tokens, c.chunk_tokens, c.prefix_caching = 1024, chunk, True
+    s = _serve.Scheduler(c)
+    prefixes = [list(range(100 + 300 * k, 100 + 300 * k + 160)) for k in range(3)]
+    live = set()
+    for i, (k, extra, new) in enumerate(reqs):
+        if s.add(i, prefixes[k] + [3] * extra, new):
+            live.add(i)
+    rng = np.random.default_rng(0)
+    for _ in range(3000):
+        p = s.schedule()
+        assert s.check_invariants() == "", s.check_invariants()
+        if p.kind == 0:
+            break
+        ids = p.seq_ids
+        if p.kind == 3:
+            ids = np.concatenate([ids[:p.n_prefill][p.last_chunk.astype(bool)], ids[p.n_prefill:]])
+        eos = (rng.random(len(ids)) < 0.05).astype(np.uint8)
+        for d in s.update(ids, np.full(len(ids), 4, np.int32), eos):
+            live.discard(int(d))
+    assert not live and s.num_running == 0 and s.num_free_pages == pages - 1
+
+
+def test_engine_ref_prefix_caching_matches_full_recompute():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=96, max_batch=4, max_model_len=1024, cuda_graphs=False,
+                                          prefix_caching=True, chunked_prefill=256), device="cpu", backend="ref")
+    rng = np.random.default_rng(7)
+    system = rng.integers(3, 512, size=300).tolist()
+    prompts = [system + rng.integers(3, 512, size=n).tolist() for n in (5, 40, 77)]
+    first = eng.generate(prompts[:1], SamplingParams(max_tokens=4, ignore_eos=True))
+    rest = eng.generate(prompts[1:], SamplingParams(max_tokens=4, ignore_eos=True))
+    assert eng.sched.prefix_hit_tokens >= 2 * 256
+    _check_against_oracle(eng, prompts, first + rest)
+
+
 def test_engine_ref_preemption_is_transparent():
     from kgs.serve import EngineConfig, LLMEngine, SamplingParams
 

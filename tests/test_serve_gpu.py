@@ -150,3 +150,20 @@ def test_chunked_prefill_engine_matches_oracle(graphs):
     assert eng.stats["mixed_steps"] >= 4 and all(len(r.output) == 6 for r in outs)
     _oracle_check(eng, prompts, outs)
     assert eng.sched.check_invariants() == ""
+
+
+def test_prefix_caching_engine_matches_oracle():
+    """Shared 300-token system prompt: later requests reuse its cached pages
+    (their first chunk attends to the gathered prefix) and still generate what
+    the oracle generates."""
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(11)
+    system = rng.integers(3, 1024, size=300).tolist()
+    prompts = [system + rng.integers(3, 1024, size=n).tolist() for n in (5, 40, 77, 130)]
+    eng = _engine(True, prefix_caching=True, chunked_prefill=512)
+    p = SamplingParams(max_tokens=5, ignore_eos=True)
+    outs = eng.generate(prompts[:1], p) + eng.generate(prompts[1:], p)
+    assert eng.sched.prefix_hit_tokens >= 3 * 256
+    _oracle_check(eng, prompts, outs)
+    assert eng.sched.check_invariants() == ""
