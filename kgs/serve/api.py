@@ -303,6 +303,11 @@ def main(argv=None) -> int:
     ap.add_argument("--backend", choices=("kgs", "ref"), default="kgs")
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--chunked-prefill", type=int, default=2048,
+                    help="rows per mixed prompt-chunk + decode step (0 = whole-prompt prefill steps)")
+    ap.add_argument("--prefix-caching", action="store_true", help="reuse cached pages of shared prompt prefixes")
+    ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16")
+    ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16")
     a = ap.parse_args(argv)
     import uvicorn
 
@@ -311,7 +316,9 @@ def main(argv=None) -> int:
     from .engine import EngineConfig, LLMEngine
 
     eng = LLMEngine(LlamaConfig.llama3_8b(layers=a.layers),
-                    EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs),
+                    EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
+                                 chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
+                                 kv_cache_dtype=a.kv_cache_dtype, decode_weights=a.decode_weights),
                     device=a.device, backend=a.backend)
     eng.warmup(widths=[8, 32])
     runner = EngineLoop(eng)
