@@ -167,3 +167,20 @@ def test_prefix_caching_engine_matches_oracle():
     assert eng.sched.prefix_hit_tokens >= 3 * 256
     _oracle_check(eng, prompts, outs)
     assert eng.sched.check_invariants() == ""
+
+
+def test_fp8_kv_with_chunked_prefill_and_prefix_caching():
+    """fp8 (e4m3) KV pages under chunked prefill + prefix caching: the chunk
+    context is gathered from fp8 pages (widened to bf16). Tokens stay close to
+    the bf16 engine's (fp8 KV rounding may flip near-ties, so compare the
+    oracle with a wider margin)."""
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(13)
+    system = rng.integers(3, 1024, size=260).tolist()
+    prompts = [system + rng.integers(3, 1024, size=n).tolist() for n in (9, 300)]
+    eng = _engine(True, prefix_caching=True, chunked_prefill=256, kv_cache_dtype="fp8")
+    p = SamplingParams(max_tokens=4, ignore_eos=True)
+    outs = eng.generate(prompts[:1], p) + eng.generate(prompts[1:], p)
+    assert eng.sched.prefix_hit_tokens >= 256 and eng.stats["mixed_steps"] >= 2
+    _oracle_check(eng, prompts, outs, tol=0.12)
