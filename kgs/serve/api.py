@@ -40,10 +40,13 @@ class _SamplingFields(BaseModel):
     stream: bool = False
     ignore_eos: bool = False
 
+    def n_logprobs(self) -> int | None:
+        return None
+
     def params(self) -> SamplingParams:
         return SamplingParams(max_tokens=self.max_tokens, temperature=self.temperature, top_k=self.top_k,
                               top_p=self.top_p, ignore_eos=self.ignore_eos,
-                              stop_token_ids=tuple(self.stop_token_ids or ()))
+                              stop_token_ids=tuple(self.stop_token_ids or ()), logprobs=self.n_logprobs())
 
     def stops(self) -> list[str]:
         return [self.stop] if isinstance(self.stop, str) else [t for t in (self.stop or []) if t]
@@ -51,6 +54,10 @@ class _SamplingFields(BaseModel):
 
 class CompletionRequest(_SamplingFields):
     prompt: str | list[int]
+    logprobs: int | None = None  # OpenAI completions: sampled token + this many alternatives
+
+    def n_logprobs(self) -> int | None:
+        return self.logprobs
 
 
 class ChatMessage(BaseModel):
@@ -60,6 +67,11 @@ class ChatMessage(BaseModel):
 
 class ChatRequest(_SamplingFields):
     messages: list[ChatMessage]
+    logprobs: bool = False
+    top_logprobs: int = 0
+
+    def n_logprobs(self) -> int | None:
+        return self.top_logprobs if self.logprobs else None
 
 
 def render_chat(messages) -> str:
@@ -177,8 +189,10 @@ class EngineLoop:
                 st = self.streams.get(rid)
                 if st is None:
                     continue
-                reason = eng.requests[rid].finish_reason if fin else None
-                self._push(st[0], st[1], ("token", tok, fin, reason))
+                req = eng.requests[rid]
+                reason = req.finish_reason if fin else None
+                lp = req.logprobs[-1] if req.params.logprobs is not None and req.logprobs else None
+                self._push(st[0], st[1], ("token", tok, fin, reason, lp))
                 if fin:
                     self.streams.pop(rid, None)
                     eng.requests.pop(rid, None)
@@ -231,13 +245,13 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
         stop-string hit aborts the request in the engine."""
         try:
             while True:
-                _, t, fin, reason = await q.get()
+                _, t, fin, reason, lp = await q.get()
                 text, hit = stop.push(t, fin)
                 if hit:
                     loop_runner.cancel(rid)
-                    yield t, text, True, "stop"
+                    yield t, text, True, "stop", lp
                     return
-                yield t, text, fin, reason
+                yield t, text, fin, reason, lp
                 if fin:
                     return
         except asyncio.CancelledError:  # client went away
@@ -252,28 +266,48 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
         obj = "chat.completion" if chat else "text_completion"
         stop = StopText(tok, req.stops())
 
-        def choice(text, ids_, reason, delta):
+        want_lp = params.logprobs is not None
+
+        def logprobs_obj(ids_, lps):
+            """OpenAI shapes: completions {tokens, token_logprobs, top_logprobs};
+            chat {content: [{token, logprob, top_logprobs: [{token, logprob}]}]}."""
+            if not want_lp:
+                return None
+            toks = [tok.decode([t]) for t in ids_]
+            if chat:
+                return {"content": [{"token": s_, "logprob": lp[0],
+                                     "top_logprobs": [{"token": tok.decode([i]), "logprob": v} for i, v in lp[1]]}
+                                    for s_, lp in zip(toks, lps)]}
+            return {"tokens": toks, "token_logprobs": [lp[0] for lp in lps],
+                    "top_logprobs": [{tok.decode([i]): v for i, v in lp[1]} for lp in lps]}
+
+        def choice(text, ids_, reason, delta, lps):
             if not chat:
-                return {"index": 0, "text": text, "token_ids": ids_, "finish_reason": reason}
-            msg = {"role": "assistant", "content": text}
-            return {"index": 0, ("delta" if delta else "message"): msg, "finish_reason": reason}
+                c = {"index": 0, "text": text, "token_ids": ids_, "finish_reason": reason}
+            else:
+                c = {"index": 0, ("delta" if delta else "message"): {"role": "assistant", "content": text},
+                     "finish_reason": reason}
+            if want_lp:
+                c["logprobs"] = logprobs_obj(ids_, lps)
+            return c
 
         if req.stream:
             async def events():
-                async for t, text, fin, reason in _tokens(rid, q, stop):
+                async for t, text, fin, reason, lp in _tokens(rid, q, stop):
                     chunk = {"id": cid, "object": obj + (".chunk" if chat else ""), "created": created,
-                             "model": name, "choices": [choice(text, [t], reason, True)]}
+                             "model": name, "choices": [choice(text, [t], reason, True, [lp])]}
                     yield f"data: {json.dumps(chunk)}\n\n"
                 yield "data: [DONE]\n\n"
 
             return StreamingResponse(events(), media_type="text/event-stream")
 
-        out, parts, reason = [], [], None
-        async for t, text, fin, reason in _tokens(rid, q, stop):
+        out, parts, lps, reason = [], [], [], None
+        async for t, text, fin, reason, lp in _tokens(rid, q, stop):
             out.append(t)
             parts.append(text)
+            lps.append(lp)
         return {"id": cid, "object": obj, "created": created, "model": name,
-                "choices": [choice("".join(parts), out, reason, False)],
+                "choices": [choice("".join(parts), out, reason, False, lps)],
                 "usage": {"prompt_tokens": len(ids), "completion_tokens": len(out),
                           "total_tokens": len(ids) + len(out)}}
 

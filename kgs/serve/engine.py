@@ -35,6 +35,7 @@ class SamplingParams:
     top_p: float = 1.0         # nucleus: smallest set of tokens whose probability reaches top_p
     ignore_eos: bool = False
     stop_token_ids: tuple = ()
+    logprobs: int | None = None  # None: off; k >= 0: the sampled token's logprob + the k most likely
 
 
 @dataclass
@@ -48,6 +49,9 @@ class Request:
     t_arrival: float = 0.0
     t_first: float | None = None
     t_done: float | None = None
+    # per output token, when params.logprobs is set: (logprob, [(token, logprob)] top-k),
+    # from the model's distribution before temperature / top-k / top-p
+    logprobs: list = field(default_factory=list)
 
 
 @dataclass
@@ -156,7 +160,9 @@ class LLMEngine:
             logits = self._run_decode(plan)
             self.stats["decode_steps"] += 1
             self.stats["decode_tokens"] += len(ids)
-        toks = self._sample(ids, logits).cpu().numpy().astype(np.int32)
+        toks_dev = self._sample(ids, logits)
+        lps = self._logprobs(ids, logits, toks_dev)
+        toks = toks_dev.cpu().numpy().astype(np.int32)
         eos = np.zeros(len(ids), dtype=np.uint8)
         now = time.perf_counter()
         for j, rid in enumerate(ids):
@@ -170,6 +176,8 @@ class LLMEngine:
             rid = int(rid)
             r = self.requests[rid]
             r.output.append(int(toks[j]))
+            if lps is not None and j in lps:
+                r.logprobs.append(lps[j])
             if r.t_first is None:
                 r.t_first = now
             fin = rid in done
@@ -273,6 +281,24 @@ class LLMEngine:
                     self._capture(bb, wb)
 
     # -------------------------------------------------------------- sampling
+    def _logprobs(self, ids, logits: torch.Tensor, toks: torch.Tensor):
+        """{row: (logprob of the sampled token, [(token, logprob)] top-k)} for the
+        rows whose request asked for logprobs; None when none did."""
+        rows = [j for j, r in enumerate(ids) if self.requests[int(r)].params.logprobs is not None]
+        if not rows:
+            return None
+        sel = torch.as_tensor(rows, device=logits.device)
+        lp = torch.log_softmax(logits[sel].float(), dim=-1)
+        chosen = lp.gather(1, toks[sel].long()[:, None])[:, 0].cpu().tolist()
+        k = max(self.requests[int(ids[j])].params.logprobs for j in rows)
+        top_v, top_i = (lp.topk(k, dim=-1) if k > 0 else (lp[:, :0], lp[:, :0].long()))
+        top_v, top_i = top_v.cpu().tolist(), top_i.cpu().tolist()
+        out = {}
+        for n, j in enumerate(rows):
+            kj = self.requests[int(ids[j])].params.logprobs
+            out[j] = (chosen[n], list(zip(top_i[n][:kj], top_v[n][:kj])))
+        return out
+
     def _sample(self, ids, logits: torch.Tensor) -> torch.Tensor:
         ps = [self.requests[int(r)].params for r in ids]
         if all(p.temperature <= 0 for p in ps):

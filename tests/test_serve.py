@@ -407,6 +407,46 @@ def test_http_api_chat_stop_strings_and_top_p():
         runner.shutdown()
 
 
+def test_logprobs_engine_and_api():
+    from fastapi.testclient import TestClient
+
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+    from kgs.serve.api import EngineLoop, create_app
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    prompt = [5, 6, 7, 8]
+    r = eng.generate([prompt], SamplingParams(max_tokens=3, ignore_eos=True, logprobs=3))[0]
+    assert len(r.logprobs) == 3
+    seq = list(prompt)
+    for tok, (lp, top) in zip(r.output, r.logprobs):
+        ref = torch.log_softmax(eng.model.oracle.forward(torch.tensor([seq]))[0, -1].float(), -1)
+        assert abs(lp - float(ref[tok])) < 5e-2 and len(top) == 3
+        # greedy: the sampled token is a top-1 (bf16 logits can tie)
+        assert abs(top[0][1] - lp) < 1e-6 and top[0][1] >= top[1][1] >= top[2][1]
+        seq.append(tok)
+    # no logprobs requested: nothing recorded
+    r2 = eng.generate([prompt], SamplingParams(max_tokens=2, ignore_eos=True))[0]
+    assert r2.logprobs == []
+    runner = EngineLoop(eng)
+    try:
+        client = TestClient(create_app(runner, model_name="tiny"))
+        c = client.post("/v1/completions", json={"prompt": prompt, "max_tokens": 3, "ignore_eos": True,
+                                                 "logprobs": 2}).json()["choices"][0]
+        lp = c["logprobs"]
+        assert len(lp["tokens"]) == 3 and len(lp["token_logprobs"]) == 3
+        assert all(len(t) <= 2 for t in lp["top_logprobs"]) and all(v <= 0 for v in lp["token_logprobs"])
+        ch = client.post("/v1/chat/completions", json={"messages": [{"role": "user", "content": "hi"}],
+                                                       "max_tokens": 2, "ignore_eos": True, "logprobs": True,
+                                                       "top_logprobs": 1}).json()["choices"][0]
+        content = ch["logprobs"]["content"]
+        assert len(content) == 2 and len(content[0]["top_logprobs"]) == 1
+        plain = client.post("/v1/completions", json={"prompt": prompt, "max_tokens": 1}).json()["choices"][0]
+        assert "logprobs" not in plain
+    finally:
+        runner.shutdown()
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 
