@@ -155,6 +155,12 @@ class EngineLoop:
         self.wake.set()
         self.thread.join(timeout=10)
 
+    def gauges(self) -> dict:
+        eng = self.engine
+        return {"running": eng.sched.num_running, "waiting": eng.sched.num_waiting,
+                "free_kv_pages": eng.sched.num_free_pages, "preemptions": eng.stats["preemptions"],
+                "prefix_hit_tokens": eng.sched.prefix_hit_tokens}
+
     def _push(self, loop, q, item) -> None:
         loop.call_soon_threadsafe(q.put_nowait, item)
 
@@ -216,17 +222,18 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
 
     @app.get("/metrics")
     def metrics():
-        eng = loop_runner.engine
         c = loop_runner.counters
+        g = loop_runner.gauges()
         lines = [
             "# TYPE kgs_requests_total counter", f"kgs_requests_total {c['requests']}",
             "# TYPE kgs_requests_rejected_total counter", f"kgs_requests_rejected_total {c['rejected']}",
             "# TYPE kgs_generated_tokens_total counter", f"kgs_generated_tokens_total {c['tokens']}",
             "# TYPE kgs_engine_steps_total counter", f"kgs_engine_steps_total {c['steps']}",
-            "# TYPE kgs_running gauge", f"kgs_running {eng.sched.num_running}",
-            "# TYPE kgs_waiting gauge", f"kgs_waiting {eng.sched.num_waiting}",
-            "# TYPE kgs_free_kv_pages gauge", f"kgs_free_kv_pages {eng.sched.num_free_pages}",
-            "# TYPE kgs_preemptions_total counter", f"kgs_preemptions_total {eng.stats['preemptions']}",
+            "# TYPE kgs_running gauge", f"kgs_running {g['running']}",
+            "# TYPE kgs_waiting gauge", f"kgs_waiting {g['waiting']}",
+            "# TYPE kgs_free_kv_pages gauge", f"kgs_free_kv_pages {g['free_kv_pages']}",
+            "# TYPE kgs_preemptions_total counter", f"kgs_preemptions_total {g['preemptions']}",
+            "# TYPE kgs_prefix_cache_hit_tokens_total counter", f"kgs_prefix_cache_hit_tokens_total {g['prefix_hit_tokens']}",
         ]
         return PlainTextResponse("\n".join(lines) + "\n")
 
@@ -342,6 +349,8 @@ def main(argv=None) -> int:
     ap.add_argument("--prefix-caching", action="store_true", help="reuse cached pages of shared prompt prefixes")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16")
+    ap.add_argument("--data-parallel", type=int, default=1,
+                    help="replicas, one engine process per GPU (cuda:0 .. N-1) behind this front end")
     a = ap.parse_args(argv)
     import uvicorn
 
@@ -349,13 +358,21 @@ def main(argv=None) -> int:
 
     from .engine import EngineConfig, LLMEngine
 
-    eng = LLMEngine(LlamaConfig.llama3_8b(layers=a.layers),
-                    EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
-                                 chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
-                                 kv_cache_dtype=a.kv_cache_dtype, decode_weights=a.decode_weights),
-                    device=a.device, backend=a.backend)
-    eng.warmup(widths=[8, 32])
-    runner = EngineLoop(eng)
+    mc = LlamaConfig.llama3_8b(layers=a.layers)
+    ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
+                      chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
+                      kv_cache_dtype=a.kv_cache_dtype, decode_weights=a.decode_weights)
+    if a.data_parallel > 1:
+        import dataclasses
+
+        from .dp import DPEngineLoop
+
+        runner = DPEngineLoop(a.data_parallel, dataclasses.asdict(mc), ec, device=a.device, backend=a.backend,
+                              warmup_widths=[8, 32])
+    else:
+        eng = LLMEngine(mc, ec, device=a.device, backend=a.backend)
+        eng.warmup(widths=[8, 32])
+        runner = EngineLoop(eng)
     app = create_app(runner, HFTokenizer(a.tokenizer) if a.tokenizer else None, a.model_name)
     try:
         uvicorn.run(app, host=a.host, port=a.port, log_level="info")

@@ -121,3 +121,12 @@ def test_kgs_serve_pod():
     from kgs.serve.api import main  # the entrypoint the pod runs exists
 
     assert callable(main)
+
+
+def test_kgs_serve_8gpu_pod():
+    one, eight = _load("kgs-serve-pod.yaml"), _load("kgs-serve-8gpu-pod.yaml")
+    c1, c8 = one["spec"]["containers"][0], eight["spec"]["containers"][0]
+    assert c8["resources"]["limits"]["amd.com/gpu"] == 8 and "--data-parallel=8" in c8["args"]
+    assert c8["command"] == c1["command"] and {"containerPort": 8000} in c8["ports"]
+    for key in ("nodeSelector", "tolerations", "restartPolicy"):
+        assert eight["spec"][key] == one["spec"][key]

@@ -447,6 +447,51 @@ def test_logprobs_engine_and_api():
         runner.shutdown()
 
 
+def test_data_parallel_replicas_cpu():
+    """--data-parallel: two engine processes (ref backend on CPU) behind the
+    EngineLoop interface; concurrent requests spread over both replicas and each
+    generates what one engine generates; the HTTP layer works on top."""
+    import asyncio
+    import dataclasses
+
+    from fastapi.testclient import TestClient
+
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+    from kgs.serve.api import create_app
+    from kgs.serve.dp import DPEngineLoop
+
+    ec = EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False)
+    runner = DPEngineLoop(2, dataclasses.asdict(_tiny()), ec, device="cpu", backend="ref", start_timeout=300)
+    prompts = [[5, 6, 7], [9, 10], [11, 12, 13, 14], [3, 4]]
+    p = SamplingParams(max_tokens=4, ignore_eos=True)
+    try:
+        async def one(prompt):
+            q: asyncio.Queue = asyncio.Queue()
+            runner.submit(prompt, p, asyncio.get_running_loop(), q)
+            kind, _ = await q.get()
+            assert kind == "id"
+            out = []
+            while True:
+                _, t, fin, _, _ = await q.get()
+                out.append(t)
+                if fin:
+                    return out
+
+        async def all_():
+            return await asyncio.gather(*(one(pr) for pr in prompts))
+
+        got = asyncio.run(all_())
+        assert runner.assigned == [2, 2]
+        ref = LLMEngine(_tiny(), ec, device="cpu", backend="ref").generate(prompts, p)
+        assert got == [r.output for r in ref]
+        client = TestClient(create_app(runner, model_name="tiny"))
+        r = client.post("/v1/completions", json={"prompt": prompts[0], "max_tokens": 4, "ignore_eos": True}).json()
+        assert r["choices"][0]["token_ids"] == got[0]
+        assert "kgs_requests_total 5" in client.get("/metrics").text
+    finally:
+        runner.shutdown()
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 

@@ -184,3 +184,40 @@ def test_fp8_kv_with_chunked_prefill_and_prefix_caching():
     outs = eng.generate(prompts[:1], p) + eng.generate(prompts[1:], p)
     assert eng.sched.prefix_hit_tokens >= 256 and eng.stats["mixed_steps"] >= 2
     _oracle_check(eng, prompts, outs, tol=0.12)
+
+
+def test_data_parallel_replica_on_gpu():
+    """One replica process on cuda:0 (the --data-parallel worker path on a GPU:
+    spawn, its own HIP context, hipGraphs) generates what the in-process engine
+    generates."""
+    import asyncio
+    import dataclasses
+
+    from kgs.serve import EngineConfig, SamplingParams
+    from kgs.serve.dp import DPEngineLoop
+
+    ec = EngineConfig(num_pages=256, max_batch=8, max_model_len=1024, cuda_graphs=True)
+    rng = np.random.default_rng(21)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (30, 200)]
+    p = SamplingParams(max_tokens=5, ignore_eos=True)
+    runner = DPEngineLoop(1, dataclasses.asdict(_cfg()), ec, device="cuda", backend="kgs", start_timeout=240)
+    try:
+        async def one(prompt):
+            q: asyncio.Queue = asyncio.Queue()
+            runner.submit(prompt, p, asyncio.get_running_loop(), q)
+            assert (await q.get())[0] == "id"
+            out = []
+            while True:
+                _, t, fin, _, _ = await q.get()
+                out.append(t)
+                if fin:
+                    return out
+
+        async def all_():
+            return await asyncio.gather(*(one(pr) for pr in prompts))
+
+        got = asyncio.run(all_())
+    finally:
+        runner.shutdown()
+    ref = _engine(True).generate(prompts, p)
+    assert got == [r.output for r in ref]
