@@ -44,6 +44,16 @@ class LlamaConfig:
     def llama3_8b(cls, layers: int = 32) -> "LlamaConfig":
         return cls(layers=layers)
 
+    @classmethod
+    def llama3_70b(cls, layers: int = 80) -> "LlamaConfig":
+        """141 GB of bf16 weights: fits one 288 GB MI355X with room for the KV cache."""
+        return cls(hidden=8192, intermediate=28672, heads=64, kv_heads=8, layers=layers)
+
+    @classmethod
+    def named(cls, name: str, layers: int | None = None) -> "LlamaConfig":
+        f = {"llama3-8b": cls.llama3_8b, "llama3-70b": cls.llama3_70b}[name]
+        return f() if layers is None else f(layers=layers)
+
     def params(self) -> int:
         h, i, kv = self.hidden, self.intermediate, self.kv_heads * self.head_dim
         per_layer = h * (h + 2 * kv) + h * h + 2 * h * i + i * h

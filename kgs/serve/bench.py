@@ -40,11 +40,12 @@ def run_engine(a) -> dict:
 
     from .engine import EngineConfig, LLMEngine, SamplingParams
 
-    mc = LlamaConfig.llama3_8b(layers=a.layers)
+    mc = LlamaConfig.named(a.model, a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
-                      chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching)
+                      chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
+                      packed_decode=not a.no_packed_decode)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -69,7 +70,7 @@ def run_engine(a) -> dict:
     ttft = sorted(r.t_first - r.t_arrival for r in outs)
     tpot = sorted((r.t_done - r.t_first) / max(1, len(r.output) - 1) for r in outs)
     return {
-        "metric": "offline serving throughput (kgs.serve, Llama-3-8B arch, random init)",
+        "metric": f"offline serving throughput (kgs.serve, {a.model} arch, random init)", "model": a.model,
         "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
@@ -100,12 +101,13 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
 
     from .engine import EngineConfig, LLMEngine, SamplingParams
 
-    mc = mc or LlamaConfig.llama3_8b(layers=a.layers)
+    mc = mc or LlamaConfig.named(getattr(a, "model", "llama3-8b"), a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=getattr(a, "chunked_prefill", 0),
                       prefix_caching=getattr(a, "prefix_caching", False),
+                      packed_decode=not getattr(a, "no_packed_decode", False),
                       **({"num_pages": 256} if device == "cpu" else {}))
     eng = LLMEngine(mc, ec, device=device, backend=backend)
     if not a.no_graphs:
@@ -199,7 +201,10 @@ def main(argv=None) -> int:
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--max-prefill-tokens", type=int, default=16384)
-    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--model", choices=("llama3-8b", "llama3-70b"), default="llama3-8b")
+    ap.add_argument("--layers", type=int, default=None, help="default: the model's (32 / 80)")
+    ap.add_argument("--no-packed-decode", action="store_true",
+                    help="one weight copy: decode on hipBLASLt / split-K (needed for llama3-70b on one GPU)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--fused-max-batch", type=int, default=64,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
@@ -217,6 +222,10 @@ def main(argv=None) -> int:
     ap.add_argument("--hf", action="store_true", help="also run the HF transformers baseline")
     ap.add_argument("--hf-only", action="store_true")
     a = ap.parse_args(argv)
+    if a.layers is None:
+        a.layers = 80 if a.model == "llama3-70b" else 32
+    if a.model == "llama3-70b" and not a.no_packed_decode and a.decode_weights == "bf16":
+        a.no_packed_decode = True  # two bf16 copies of 70B (282 GB) leave no room for the KV cache
     if a.request_rate > 0:
         print(json.dumps(run_online(a)), flush=True)
         return 0

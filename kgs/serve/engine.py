@@ -68,6 +68,7 @@ class EngineConfig:
     kv_cache_dtype: str = "bf16"      # "fp8": e4m3 KV pages
     chunked_prefill: int = 0          # > 0: mixed steps of at most this many rows (prompt chunks + decodes)
     prefix_caching: bool = False      # reuse cached KV pages of shared prompt prefixes (runs on mixed steps)
+    packed_decode: bool = True        # prepacked skinny-GEMM decode copies (False: one weight copy, e.g. 70B)
     seed: int = 0
 
 
@@ -88,7 +89,8 @@ class LLMEngine:
         num_pages = cfg.num_pages or self._pages_from_memory(model_cfg)
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
                                   max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
-                                  decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype)
+                                  decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype,
+                                  packed_decode=cfg.packed_decode)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
@@ -112,7 +114,8 @@ class LLMEngine:
         per_layer = h * (h + 2 * kvd) + h * h + 2 * h * i + i * h
         weights = 2 * (mc.layers * per_layer + 2 * mc.vocab * h)
         # the kgs backend keeps prefill-order and prepacked decode copies of every projection
-        resident = weights * ((1.5 if self.cfg.decode_weights == "fp8" else 2) if self.backend == "kgs" else 1)
+        copies = (1.5 if self.cfg.decode_weights == "fp8" else 2) if self.cfg.packed_decode else 1
+        resident = weights * (copies if self.backend == "kgs" else 1)
         avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
         return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, self.cfg.kv_cache_dtype)))
 

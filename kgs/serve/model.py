@@ -48,7 +48,7 @@ from kgs.ops import decode as D
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 64,
-                 decode_weights: str = "bf16", kv_cache_dtype: str = "bf16"):
+                 decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -66,7 +66,14 @@ class ServingModel:
         self.decode_fp8 = decode_weights == "fp8"
         if self.decode_fp8:
             self.fused_max_batch = min(fused_max_batch, 64)  # the W8A16 skinny GEMM covers M <= 64
-        if backend == "kgs":
+        if backend == "kgs" and not packed_decode:
+            # no prepacked decode copies (e.g. Llama-3-70B: one bf16 copy of the
+            # weights is 141 GB): decode runs on the library/split-K GEMMs
+            if self.decode_fp8:
+                raise ValueError("decode_weights='fp8' needs the packed decode copies")
+            self.fused_max_batch = 0
+            D.reserve_workspace(self.device)
+        elif backend == "kgs":
             f8 = self.decode_fp8
             # decode copies in skinny-GEMM fragment order; the RMSNorm weights
             # in front of qkv / gate|up / lm_head are folded into them (their
@@ -99,7 +106,7 @@ class ServingModel:
                 from kgs.ops.gemm import gemm_nt_splitk
 
                 return gemm_nt_splitk(x, w, ns)
-        if decode and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]) and \
+        if decode and self.packed is not None and name in ("o", "down") and D.use_skinny(m, w.shape[0], w.shape[1]) and \
                 not (self.decode_fp8 and m > 64):
             return D.skinny_gemm(x, self.packed[layer][name])
         # the LM head (N = 128256) from batch 128 up runs faster on the kgs

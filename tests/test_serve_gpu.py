@@ -221,3 +221,19 @@ def test_data_parallel_replica_on_gpu():
         runner.shutdown()
     ref = _engine(True).generate(prompts, p)
     assert got == [r.output for r in ref]
+
+
+def test_unpacked_decode_gqa8_engine_matches_oracle():
+    """packed_decode=False (one weight copy, the Llama-3-70B layout on one GPU):
+    decode on hipBLASLt / split-K GEMMs, GQA 8:1 attention; matches the oracle."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    cfg = LlamaConfig(hidden=1024, intermediate=2048, heads=8, kv_heads=1, layers=2, vocab=1024)
+    eng = LLMEngine(cfg, EngineConfig(num_pages=256, max_batch=8, max_model_len=1024, packed_decode=False),
+                    device="cuda", backend="kgs")
+    assert eng.model.packed is None and eng.model.fused_max_batch == 0
+    rng = np.random.default_rng(23)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (20, 150, 300)]
+    outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
+    _oracle_check(eng, prompts, outs)
