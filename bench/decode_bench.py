@@ -21,6 +21,8 @@ import torch  # noqa: E402
 SWEEP = False
 SHAPES = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
           "lm_head": (128256, 4096)}
+SHAPES_70B = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672),
+              "lm_head": (128256, 8192)}
 
 
 def _time(fn, iters):
@@ -199,7 +201,11 @@ def main(argv=None) -> int:
     ap.add_argument("--tune", action="store_true", help="time every tile variant x split-K; print a TUNED table")
     ap.add_argument("--fp8", action="store_true", help="--tune the weight-only fp8 (W8A16) kernels")
     ap.add_argument("--wide", action="store_true", help="kgs 256x256 GEMM vs hipBLASLt at M >= 128")
+    ap.add_argument("--model", choices=("llama3-8b", "llama3-70b"), default="llama3-8b")
     a = ap.parse_args(argv)
+    if a.model == "llama3-70b":
+        SHAPES.clear()
+        SHAPES.update(SHAPES_70B)
     global SWEEP
     SWEEP = a.sweep
     if a.tune:

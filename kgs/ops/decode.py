@@ -154,8 +154,14 @@ SPLITK_TUNED: dict = {
     (128, *_DOWN): 16, (128, *_O): 8,
     (256, *_QKV): 8, (256, *_DOWN): 8,
     (512, *_DOWN): 8,
+    # Llama-3-70B (decode without packed copies, `--model llama3-70b`; bench/decode_bench.py --wide
+    # --model llama3-70b): down 1.55x / 1.83x / 2.3x at 64 / 128 / 256, qkv 1.40x and o 1.47x at 256;
+    # 1 = the plain 256x256 GEMM (gate|up at 256: 1.22x)
+    (64, 8192, 28672): 8,
+    (128, 10240, 8192): 4, (128, 8192, 8192): 8, (128, 8192, 28672): 8,
+    (256, 10240, 8192): 4, (256, 8192, 8192): 8, (256, 8192, 28672): 8, (256, 57344, 8192): 1,
 }
-SPLITK_WS_FLOATS = 8 * 512 * 4096  # the largest entry above (M x N x slices)
+SPLITK_WS_FLOATS = 8 * 256 * 8192  # the largest entry above (M x N x slices)
 
 
 def splitk_slices(m: int, n: int, k: int) -> int | None:

@@ -102,6 +102,10 @@ class ServingModel:
         m = x.shape[0]
         if decode:
             ns = D.splitk_slices(m, w.shape[0], w.shape[1])
+            if ns == 1:
+                from kgs.ops import gemm_nt
+
+                return gemm_nt(x, w)
             if ns is not None:
                 from kgs.ops.gemm import gemm_nt_splitk
 
