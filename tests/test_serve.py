@@ -573,6 +573,19 @@ def test_decode_routing_tables_cpu():
     assert pps >= 4 and pps * ns >= 128
 
 
+def test_splitk_routing_table_cpu():
+    """Every split-K entry is launchable (K slices of whole 128-deep K-tiles) and
+    fits the workspace reserved before graph capture."""
+    from kgs.ops import decode as D
+
+    for (m, n, k), ns in D.SPLITK_TUNED.items():
+        assert m & (m - 1) == 0 and n % 256 == 0, (m, n, k)
+        assert k % ns == 0 and (k // ns) % 128 == 0, (m, n, k, ns)
+        assert ns * m * n <= D.SPLITK_WS_FLOATS, (m, n, k, ns)
+        assert D.splitk_slices(m, n, k) == ns and D.splitk_slices(m // 2 + 1, n, k) == ns
+    assert D.splitk_slices(256, 28672, 4096) is None  # gate|up stays on hipBLASLt
+
+
 def test_fp8_routing_table_cpu():
     from kgs.ops import decode as D
 
