@@ -23,6 +23,18 @@ import threading
 
 
 def _worker(index: int, spec: dict, inq, outq) -> None:
+    """Replica main: any exception is reported to the front end (which fails
+    that replica's requests and stops routing to it) instead of leaving them
+    waiting forever."""
+    try:
+        _serve_replica(index, spec, inq, outq)
+    except BaseException:  # noqa: BLE001 -- report everything, then exit
+        import traceback
+
+        outq.put(("fatal", index, traceback.format_exc()))
+
+
+def _serve_replica(index: int, spec: dict, inq, outq) -> None:
     from kgs.models.llama import LlamaConfig
 
     from .engine import LLMEngine
@@ -104,18 +116,22 @@ class DPEngineLoop:
         ready = set()
         while len(ready) < replicas:
             try:
-                kind, idx, _ = self.outq.get(timeout=start_timeout)
+                kind, idx, payload = self.outq.get(timeout=start_timeout)
             except queue.Empty:
                 self.shutdown()
                 raise RuntimeError(f"data-parallel replicas not ready after {start_timeout} s")
             if kind == "ready":
                 ready.add(idx)
+            elif kind == "fatal":
+                self.shutdown()
+                raise RuntimeError(f"replica {idx} failed to start:\n{payload}")
         self.counters = {"requests": 0, "rejected": 0, "tokens": 0, "steps": 0}
         self.assigned = [0] * replicas  # requests routed to each replica (tests, logs)
         self._inflight = [0] * replicas
         self._gauges = [{"running": 0, "waiting": 0, "free_kv_pages": 0, "preemptions": 0,
                          "prefix_hit_tokens": 0} for _ in range(replicas)]
         self._streams: dict = {}
+        self._dead: set = set()
         self._ids = itertools.count()
         self._lock = threading.Lock()
         self._stop = threading.Event()
@@ -126,7 +142,11 @@ class DPEngineLoop:
     def submit(self, prompt, params, loop, q) -> None:
         with self._lock:
             gid = next(self._ids)
-            w = min(range(self.n), key=lambda i: (self._inflight[i], i))
+            live = [i for i in range(self.n) if i not in self._dead]
+            if not live:
+                loop.call_soon_threadsafe(q.put_nowait, ("error", "no live replica"))
+                return
+            w = min(live, key=lambda i: (self._inflight[i], i))
             self._inflight[w] += 1
             self.assigned[w] += 1
             self._streams[gid] = (loop, q, w)
@@ -178,6 +198,14 @@ class DPEngineLoop:
                     if st is not None:
                         self._inflight[st[2]] -= 1
                         self._push(st, ("error", msg))
+                elif kind == "fatal":
+                    # the replica died: fail its requests, route around it
+                    self._dead.add(idx)
+                    for gid, st in list(self._streams.items()):
+                        if st[2] == idx:
+                            self._streams.pop(gid)
+                            self._inflight[idx] -= 1
+                            self._push(st, ("error", f"replica {idx} failed"))
                 elif kind == "step":
                     batch, gauges = payload
                     self._gauges[idx] = gauges

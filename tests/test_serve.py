@@ -492,6 +492,18 @@ def test_data_parallel_replicas_cpu():
         runner.shutdown()
 
 
+def test_data_parallel_replica_failure_is_reported():
+    import dataclasses
+
+    from kgs.serve import EngineConfig
+    from kgs.serve.dp import DPEngineLoop
+
+    bad = dict(dataclasses.asdict(_tiny()), heads=3)  # hidden 256 / 3 heads: engine construction fails
+    with pytest.raises(RuntimeError, match="failed to start"):
+        DPEngineLoop(1, bad, EngineConfig(num_pages=32, max_batch=2, max_model_len=256, cuda_graphs=False),
+                     device="cpu", backend="ref", start_timeout=120)
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 
