@@ -390,6 +390,9 @@ StepPlan Scheduler::schedule_mixed() {
     plan.ctx_lens.push_back(pos + 1);
     std::copy(s.pages.begin(), s.pages.end(), plan.block_tables.begin() + i * maxp);
     s.cached = pos + 1;
+    // a page filled by generated tokens is cacheable too (multi-turn chat:
+    // the next turn's prompt starts with this one's prompt + answer)
+    if (cfg_.prefix_caching && s.cached % ps == 0) register_full_pages(s);
   }
   // no chunk this step: a plain decode plan (the engine replays its hipGraph)
   plan.kind = plan.seq_ids.empty() ? 0 : pf.empty() ? 2 : 3;

@@ -260,6 +260,26 @@ def test_scheduler_prefix_caching_shares_pages():
     assert s.check_invariants() == ""
 
 
+def test_prefix_caching_reuses_generated_pages():
+    """Multi-turn: the second prompt = first prompt + first answer + more; pages
+    filled during decode are registered, so the match extends past the first
+    prompt into the generated tokens."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=64, max_batch=2, max_model_len=1024, cuda_graphs=False,
+                                          prefix_caching=True, chunked_prefill=256), device="cpu", backend="ref")
+    rng = np.random.default_rng(9)
+    turn1 = rng.integers(3, 512, size=100).tolist()
+    r1 = eng.generate([turn1], SamplingParams(max_tokens=60, ignore_eos=True))[0]
+    turn2 = turn1 + r1.output + rng.integers(3, 512, size=20).tolist()  # 180 tokens
+    before = eng.sched.prefix_hit_tokens
+    r2 = eng.generate([turn2], SamplingParams(max_tokens=4, ignore_eos=True))[0]
+    # 5 full pages (160 tokens) of turn 2 are cached, 128 of them reused (even page count);
+    # turn 1's prompt alone covers only 3 full pages
+    assert eng.sched.prefix_hit_tokens - before == 128
+    _check_against_oracle(eng, [turn2], [r2])
+
+
 @settings(max_examples=40, deadline=None)
 @given(st.lists(st.tuples(st.integers(0, 2), st.integers(1, 200), st.integers(1, 40)), min_size=1, max_size=20),
        st.integers(12, 48), st.integers(1, 6), st.sampled_from([128, 256, 0]))
