@@ -39,6 +39,7 @@ class _SamplingFields(BaseModel):
     stop_token_ids: list[int] | None = None
     stream: bool = False
     ignore_eos: bool = False
+    n: int = 1  # independent samples of the prompt (choices 0 .. n-1)
 
     def n_logprobs(self) -> int | None:
         return None
@@ -267,19 +268,25 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
 
     async def _serve(req, ids, chat: bool):
         params = req.params()
-        rid, q = await _start(ids, params)
+        n = max(1, req.n)
+        # n samples of one prompt are n engine requests (with prefix caching they
+        # share the prompt's KV pages); choice i is request i
+        started = []
+        try:
+            for _ in range(n):
+                started.append(await _start(ids, params))
+        except HTTPException:
+            for rid, _q in started:  # do not leave the samples that did start running
+                loop_runner.cancel(rid)
+            raise
         cid, created = f"{'chatcmpl' if chat else 'cmpl'}-{uuid.uuid4().hex[:16]}", int(time.time())
         name = req.model or model_name
         obj = "chat.completion" if chat else "text_completion"
-        stop = StopText(tok, req.stops())
-
         want_lp = params.logprobs is not None
 
         def logprobs_obj(ids_, lps):
             """OpenAI shapes: completions {tokens, token_logprobs, top_logprobs};
             chat {content: [{token, logprob, top_logprobs: [{token, logprob}]}]}."""
-            if not want_lp:
-                return None
             toks = [tok.decode([t]) for t in ids_]
             if chat:
                 return {"content": [{"token": s_, "logprob": lp[0],
@@ -288,11 +295,11 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
             return {"tokens": toks, "token_logprobs": [lp[0] for lp in lps],
                     "top_logprobs": [{tok.decode([i]): v for i, v in lp[1]} for lp in lps]}
 
-        def choice(text, ids_, reason, delta, lps):
+        def choice(i, text, ids_, reason, delta, lps):
             if not chat:
-                c = {"index": 0, "text": text, "token_ids": ids_, "finish_reason": reason}
+                c = {"index": i, "text": text, "token_ids": ids_, "finish_reason": reason}
             else:
-                c = {"index": 0, ("delta" if delta else "message"): {"role": "assistant", "content": text},
+                c = {"index": i, ("delta" if delta else "message"): {"role": "assistant", "content": text},
                      "finish_reason": reason}
             if want_lp:
                 c["logprobs"] = logprobs_obj(ids_, lps)
@@ -300,23 +307,47 @@ def create_app(loop_runner: EngineLoop, tokenizer=None, model_name: str = "meta-
 
         if req.stream:
             async def events():
-                async for t, text, fin, reason, lp in _tokens(rid, q, stop):
-                    chunk = {"id": cid, "object": obj + (".chunk" if chat else ""), "created": created,
-                             "model": name, "choices": [choice(text, [t], reason, True, [lp])]}
-                    yield f"data: {json.dumps(chunk)}\n\n"
-                yield "data: [DONE]\n\n"
+                merged: asyncio.Queue = asyncio.Queue()
+
+                async def feed(i, rid, q):
+                    async for item in _tokens(rid, q, StopText(tok, req.stops())):
+                        await merged.put((i, item))
+                    await merged.put((i, None))
+
+                tasks = [asyncio.ensure_future(feed(i, rid, q)) for i, (rid, q) in enumerate(started)]
+                try:
+                    live = n
+                    while live:
+                        i, item = await merged.get()
+                        if item is None:
+                            live -= 1
+                            continue
+                        t, text, fin, reason, lp = item
+                        chunk = {"id": cid, "object": obj + (".chunk" if chat else ""), "created": created,
+                                 "model": name, "choices": [choice(i, text, [t], reason, True, [lp])]}
+                        yield f"data: {json.dumps(chunk)}\n\n"
+                    yield "data: [DONE]\n\n"
+                finally:
+                    for tsk in tasks:
+                        tsk.cancel()
 
             return StreamingResponse(events(), media_type="text/event-stream")
 
-        out, parts, lps, reason = [], [], [], None
-        async for t, text, fin, reason, lp in _tokens(rid, q, stop):
-            out.append(t)
-            parts.append(text)
-            lps.append(lp)
+        async def collect(rid, q):
+            out, parts, lps, reason = [], [], [], None
+            async for t, text, fin, reason, lp in _tokens(rid, q, StopText(tok, req.stops())):
+                out.append(t)
+                parts.append(text)
+                lps.append(lp)
+            return out, "".join(parts), lps, reason
+
+        results = await asyncio.gather(*(collect(rid, q) for rid, q in started))
+        completion = sum(len(r[0]) for r in results)
         return {"id": cid, "object": obj, "created": created, "model": name,
-                "choices": [choice("".join(parts), out, reason, False, lps)],
-                "usage": {"prompt_tokens": len(ids), "completion_tokens": len(out),
-                          "total_tokens": len(ids) + len(out)}}
+                "choices": [choice(i, text, out, reason, False, lps)
+                            for i, (out, text, lps, reason) in enumerate(results)],
+                "usage": {"prompt_tokens": len(ids), "completion_tokens": completion,
+                          "total_tokens": len(ids) + completion}}
 
     @app.post("/v1/completions")
     async def completions(req: CompletionRequest):

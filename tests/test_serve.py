@@ -524,6 +524,34 @@ def test_data_parallel_replica_failure_is_reported():
                      device="cpu", backend="ref", start_timeout=120)
 
 
+def test_http_n_samples():
+    from fastapi.testclient import TestClient
+
+    from kgs.serve import EngineConfig, LLMEngine
+    from kgs.serve.api import EngineLoop, create_app
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False,
+                                          prefix_caching=True, chunked_prefill=256), device="cpu", backend="ref")
+    runner = EngineLoop(eng)
+    try:
+        client = TestClient(create_app(runner, model_name="tiny"))
+        prompt = list(range(3, 3 + 140))
+        r = client.post("/v1/completions", json={"prompt": prompt, "max_tokens": 3, "ignore_eos": True,
+                                                 "n": 3}).json()
+        assert [c["index"] for c in r["choices"]] == [0, 1, 2]
+        assert all(c["token_ids"] == r["choices"][0]["token_ids"] for c in r["choices"])  # greedy: identical
+        assert r["usage"]["completion_tokens"] == 9
+        with client.stream("POST", "/v1/completions", json={"prompt": prompt, "max_tokens": 2, "stream": True,
+                                                            "ignore_eos": True, "n": 2}) as s:
+            events = [ln for ln in s.iter_lines() if ln.startswith("data: ")]
+        import json as _json
+        idx = sorted(_json.loads(e[6:])["choices"][0]["index"] for e in events[:-1])
+        assert events[-1] == "data: [DONE]" and idx == [0, 0, 1, 1]
+        assert eng.sched.prefix_hit_tokens >= 128  # the samples share the prompt's cached pages
+    finally:
+        runner.shutdown()
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 
