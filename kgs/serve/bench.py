@@ -45,7 +45,7 @@ def run_engine(a) -> dict:
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
-                      packed_decode=not a.no_packed_decode)
+                      packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -74,7 +74,8 @@ def run_engine(a) -> dict:
         "backend": "kgs", "requests": a.requests, "input_len": a.input_len, "output_len": a.output_len,
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
-        "kv_cache_dtype": a.kv_cache_dtype, "chunked_prefill": a.chunked_prefill,
+        "kv_cache_dtype": a.kv_cache_dtype, "prefill_weights": a.prefill_weights,
+        "chunked_prefill": a.chunked_prefill,
         "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
         "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
         "seconds": round(dt, 3), "output_tok_per_s": round(n_out / dt, 1),
@@ -210,6 +211,8 @@ def main(argv=None) -> int:
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")
+    ap.add_argument("--prefill-weights", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8 = W8A8 prompt pass (e4m3 weights, per-row activation scales); the headline is bf16")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = e4m3 KV pages (half the attention bytes); the headline is bf16")
     ap.add_argument("--chunked-prefill", type=int, default=0,

@@ -69,6 +69,7 @@ class EngineConfig:
     chunked_prefill: int = 0          # > 0: mixed steps of at most this many rows (prompt chunks + decodes)
     prefix_caching: bool = False      # reuse cached KV pages of shared prompt prefixes (runs on mixed steps)
     packed_decode: bool = True        # prepacked skinny-GEMM decode copies (False: one weight copy, e.g. 70B)
+    prefill_weights: str = "bf16"     # "fp8": W8A8 prompt pass (e4m3 weight copies, per-row activation scales)
     seed: int = 0
 
 
@@ -90,7 +91,7 @@ class LLMEngine:
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
                                   max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
                                   decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype,
-                                  packed_decode=cfg.packed_decode)
+                                  packed_decode=cfg.packed_decode, prefill_weights=cfg.prefill_weights)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
@@ -115,6 +116,7 @@ class LLMEngine:
         weights = 2 * (mc.layers * per_layer + 2 * mc.vocab * h)
         # the kgs backend keeps prefill-order and prepacked decode copies of every projection
         copies = (1.5 if self.cfg.decode_weights == "fp8" else 2) if self.cfg.packed_decode else 1
+        copies += 0.5 if self.cfg.prefill_weights == "fp8" else 0
         resident = weights * (copies if self.backend == "kgs" else 1)
         avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
         return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, self.cfg.kv_cache_dtype)))

@@ -48,7 +48,8 @@ from kgs.ops import decode as D
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 64,
-                 decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True):
+                 decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True,
+                 prefill_weights: str = "bf16"):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -84,6 +85,16 @@ class ServingModel:
                             "down": D.PackedWeight(lw["down"], fp8=f8)} for i, lw in enumerate(self.w)]
             self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm, fp8=f8)
             D.reserve_workspace(self.device)
+        if prefill_weights not in ("bf16", "fp8"):
+            raise ValueError(f"prefill_weights must be bf16 or fp8, got {prefill_weights!r}")
+        self.prefill_f8 = None
+        if prefill_weights == "fp8" and backend == "kgs":
+            # W8A8 prefill (e4m3 weights, per-tensor scale; activations quantised per
+            # row by the fused norm / SwiGLU producers): ~2x the bf16 GEMM rate on the
+            # compute-bound prompt pass; decode and the oracle keep the bf16 weights
+            from kgs.ops import Fp8Linear
+
+            self.prefill_f8 = [{n: Fp8Linear(lw[n]) for n in ("qkv", "o", "gate_up", "down")} for lw in self.w]
         self.cache = D.PagedKVCache(cfg.layers, num_pages, cfg.kv_heads, self.device, dtype=kv_cache_dtype)
         self.max_model_len = max_model_len
         from kgs.ops.transformer import rope_tables
@@ -159,6 +170,8 @@ class ServingModel:
         """Flattened padded prompts -> logits of each sequence's last real token [S, vocab]."""
         c = self.cfg
         h, hd = c.hidden, c.head_dim
+        if self.prefill_f8 is not None:
+            return self._prefill_fp8(tokens, positions, slots, seq_starts, seq_lens, padded_lens)
         x = self.embed[tokens.long()].reshape(-1, h).contiguous()
         y = self._norm(x, None, self.ln1[0])
         for i in range(c.layers):
@@ -172,6 +185,31 @@ class ServingModel:
         last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
         yl = y[last].contiguous()
         return self._proj(yl, None, "lm", True)
+
+    def _prefill_fp8(self, tokens, positions, slots, seq_starts, seq_lens, padded_lens) -> torch.Tensor:
+        """W8A8 prompt pass: every GEMM input is e4m3 rows with per-row scales from
+        its fused producer (add_rmsnorm_fp8, silu_mul_fp8, quantize_rows_fp8);
+        attention, RoPE/KV write, the residual stream and the LM head stay bf16."""
+        from kgs.ops.transformer import add_rmsnorm, add_rmsnorm_fp8, quantize_rows_fp8, silu_mul_fp8
+
+        c = self.cfg
+        x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
+        y8, ys = add_rmsnorm_fp8(x, None, self.ln1[0], c.eps)
+        y = None
+        for i in range(c.layers):
+            F = self.prefill_f8[i]
+            qkv = F["qkv"].forward_q(y8, ys)
+            self._rope_cache(qkv, i, positions, slots)
+            a8, as_ = quantize_rows_fp8(self._prefill_attention(qkv, seq_starts, seq_lens, padded_lens))
+            y8, ys = add_rmsnorm_fp8(x, F["o"].forward_q(a8, as_), self.ln2[i], c.eps)
+            m8, ms = silu_mul_fp8(F["gate_up"].forward_q(y8, ys))
+            d = F["down"].forward_q(m8, ms)
+            if i + 1 < c.layers:
+                y8, ys = add_rmsnorm_fp8(x, d, self.ln1[i + 1], c.eps)
+            else:
+                y = add_rmsnorm(x, d, self.norm, c.eps)
+        last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
+        return self._proj(y[last].contiguous(), None, "lm", True)
 
     def _prefill_attention(self, qkv, seq_starts, seq_lens, padded_lens):
         c = self.cfg

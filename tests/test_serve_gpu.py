@@ -237,3 +237,16 @@ def test_unpacked_decode_gqa8_engine_matches_oracle():
     prompts = [rng.integers(3, 1024, size=n).tolist() for n in (20, 150, 300)]
     outs = eng.generate(prompts, SamplingParams(max_tokens=5, ignore_eos=True))
     _oracle_check(eng, prompts, outs)
+
+
+def test_fp8_prefill_engine():
+    """W8A8 prompt pass (prefill_weights='fp8'): generations stay within fp8
+    rounding of the bf16 oracle (the decode and the KV writes stay bf16)."""
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(29)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (64, 200)]
+    eng = _engine(True, prefill_weights="fp8")
+    assert eng.model.prefill_f8 is not None
+    outs = eng.generate(prompts, SamplingParams(max_tokens=4, ignore_eos=True))
+    _oracle_check(eng, prompts, outs, tol=0.12)
