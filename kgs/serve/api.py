@@ -380,6 +380,8 @@ def main(argv=None) -> int:
     ap.add_argument("--prefix-caching", action="store_true", help="reuse cached pages of shared prompt prefixes")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16")
+    ap.add_argument("--prefill-weights", choices=("bf16", "fp8"), default="bf16",
+                    help="fp8: W8A8 whole-prompt prefill steps (chunked-prefill steps stay bf16)")
     ap.add_argument("--data-parallel", type=int, default=1,
                     help="replicas, one engine process per GPU (cuda:0 .. N-1) behind this front end")
     ap.add_argument("--engine-process", action=argparse.BooleanOptionalAction, default=True,
@@ -396,7 +398,8 @@ def main(argv=None) -> int:
     mc = LlamaConfig.llama3_8b(layers=a.layers)
     ec = EngineConfig(max_batch=a.max_batch, max_model_len=a.max_model_len, cuda_graphs=not a.no_graphs,
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
-                      kv_cache_dtype=a.kv_cache_dtype, decode_weights=a.decode_weights)
+                      kv_cache_dtype=a.kv_cache_dtype, decode_weights=a.decode_weights,
+                      prefill_weights=a.prefill_weights)
     if a.data_parallel > 1 or a.engine_process:
         import dataclasses
 
