@@ -381,7 +381,7 @@ def main(argv=None) -> int:
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--prefill-weights", choices=("bf16", "fp8"), default="bf16",
-                    help="fp8: W8A8 whole-prompt prefill steps (chunked-prefill steps stay bf16)")
+                    help="fp8: W8A8 projections in prefill and mixed (chunked-prefill) steps")
     ap.add_argument("--data-parallel", type=int, default=1,
                     help="replicas, one engine process per GPU (cuda:0 .. N-1) behind this front end")
     ap.add_argument("--engine-process", action=argparse.BooleanOptionalAction, default=True,

@@ -256,9 +256,15 @@ class ServingModel:
         x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
         n_pf = sum(ch[2] for ch in chunks)
         nd = x.shape[0] - n_pf
-        y = self._norm(x, None, self.ln1[0])
+        f8 = self.prefill_f8 is not None and n_pf > 0  # W8A8 projections for the whole mixed step
+        if f8:
+            from kgs.ops.transformer import add_rmsnorm_fp8, quantize_rows_fp8, silu_mul_fp8
+
+            y8, ys = add_rmsnorm_fp8(x, None, self.ln1[0], c.eps)
+        else:
+            y = self._norm(x, None, self.ln1[0])
         for i in range(c.layers):
-            qkv = self._proj(y, i, "qkv", False)
+            qkv = self.prefill_f8[i]["qkv"].forward_q(y8, ys) if f8 else self._proj(y, i, "qkv", False)
             self._rope_cache(qkv, i, positions, slots)
             a = torch.empty((x.shape[0], c.heads * hd), dtype=torch.bfloat16, device=x.device)
             for row0, n, p, ctx0, pages, _ in chunks:
@@ -271,9 +277,20 @@ class ServingModel:
                 else:
                     D.paged_decode_attention(qd, self.cache.layer(i), dec_block_tables, dec_ctx_lens, c.heads,
                                              c.kv_heads, out=a[n_pf:])
+            nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
+            if f8:
+                F = self.prefill_f8[i]
+                a8, as_ = quantize_rows_fp8(a)
+                y8, ys = add_rmsnorm_fp8(x, F["o"].forward_q(a8, as_), self.ln2[i], c.eps)
+                m8, ms = silu_mul_fp8(F["gate_up"].forward_q(y8, ys))
+                d = F["down"].forward_q(m8, ms)
+                if i + 1 < c.layers:
+                    y8, ys = add_rmsnorm_fp8(x, d, nxt, c.eps)
+                else:
+                    y = self._norm(x, d, nxt)
+                continue
             y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
             act = self._silu_mul(self._proj(y, i, "gate_up", False))
-            nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             y = self._norm(x, self._proj(act, i, "down", False), nxt)
         rows = [row0 + n - 1 for row0, n, _, _, _, last in chunks if last] + list(range(n_pf, n_pf + nd))
         if not rows:

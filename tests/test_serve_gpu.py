@@ -250,3 +250,15 @@ def test_fp8_prefill_engine():
     assert eng.model.prefill_f8 is not None
     outs = eng.generate(prompts, SamplingParams(max_tokens=4, ignore_eos=True))
     _oracle_check(eng, prompts, outs, tol=0.12)
+
+
+def test_fp8_prefill_with_chunked_prefill():
+    """W8A8 projections in mixed (chunk + decode) steps."""
+    from kgs.serve import SamplingParams
+
+    rng = np.random.default_rng(31)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (40, 600)]
+    eng = _engine(True, prefill_weights="fp8", chunked_prefill=256)
+    outs = eng.generate(prompts, SamplingParams(max_tokens=4, ignore_eos=True))
+    assert eng.stats["mixed_steps"] >= 3
+    _oracle_check(eng, prompts, outs, tol=0.12)
