@@ -40,6 +40,9 @@ class _SamplingFields(BaseModel):
     stream: bool = False
     ignore_eos: bool = False
     n: int = 1  # independent samples of the prompt (choices 0 .. n-1)
+    presence_penalty: float = 0.0
+    frequency_penalty: float = 0.0
+    repetition_penalty: float = 1.0
 
     def n_logprobs(self) -> int | None:
         return None
@@ -47,7 +50,9 @@ class _SamplingFields(BaseModel):
     def params(self) -> SamplingParams:
         return SamplingParams(max_tokens=self.max_tokens, temperature=self.temperature, top_k=self.top_k,
                               top_p=self.top_p, ignore_eos=self.ignore_eos,
-                              stop_token_ids=tuple(self.stop_token_ids or ()), logprobs=self.n_logprobs())
+                              stop_token_ids=tuple(self.stop_token_ids or ()), logprobs=self.n_logprobs(),
+                              presence_penalty=self.presence_penalty, frequency_penalty=self.frequency_penalty,
+                              repetition_penalty=self.repetition_penalty)
 
     def stops(self) -> list[str]:
         return [self.stop] if isinstance(self.stop, str) else [t for t in (self.stop or []) if t]

@@ -36,6 +36,9 @@ class SamplingParams:
     ignore_eos: bool = False
     stop_token_ids: tuple = ()
     logprobs: int | None = None  # None: off; k >= 0: the sampled token's logprob + the k most likely
+    presence_penalty: float = 0.0   # OpenAI: minus this once for every token already generated
+    frequency_penalty: float = 0.0  # OpenAI: minus this times the token's count in the output
+    repetition_penalty: float = 1.0  # CTRL/HF: logits of prompt+output tokens divided (>0) / multiplied (<0)
 
 
 @dataclass
@@ -304,7 +307,29 @@ class LLMEngine:
             out[j] = (chosen[n], list(zip(top_i[n][:kj], top_v[n][:kj])))
         return out
 
+    def _penalize(self, ids, logits: torch.Tensor) -> torch.Tensor:
+        """Presence / frequency / repetition penalties on the rows that ask for
+        them (a per-row token-count vector built from that request's tokens)."""
+        rows = [j for j, r in enumerate(ids) if (lambda p: p.presence_penalty or p.frequency_penalty
+                                                 or p.repetition_penalty != 1.0)(self.requests[int(r)].params)]
+        if not rows:
+            return logits
+        logits = logits.float().clone()
+        vocab = logits.shape[1]
+        for j in rows:
+            r = self.requests[int(ids[j])]
+            p = r.params
+            if r.output and (p.presence_penalty or p.frequency_penalty):
+                cnt = torch.bincount(torch.as_tensor(r.output, device=logits.device), minlength=vocab)[:vocab]
+                logits[j] -= p.frequency_penalty * cnt + p.presence_penalty * (cnt > 0)
+            if p.repetition_penalty != 1.0:
+                seen = torch.as_tensor(sorted(set(r.prompt) | set(r.output)), device=logits.device)
+                v = logits[j, seen]
+                logits[j, seen] = torch.where(v > 0, v / p.repetition_penalty, v * p.repetition_penalty)
+        return logits
+
     def _sample(self, ids, logits: torch.Tensor) -> torch.Tensor:
+        logits = self._penalize(ids, logits)
         ps = [self.requests[int(r)].params for r in ids]
         if all(p.temperature <= 0 for p in ps):
             return logits.argmax(dim=-1)

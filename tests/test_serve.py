@@ -552,6 +552,26 @@ def test_http_n_samples():
         runner.shutdown()
 
 
+def test_sampling_penalties():
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+    rid = eng.add_request([5, 6], SamplingParams(max_tokens=1, presence_penalty=1.0, frequency_penalty=0.5,
+                                                 repetition_penalty=2.0))
+    eng.abort(rid)
+    r = eng.requests[rid]
+    r.output = [7, 7, 9]
+    logits = torch.zeros(1, 16)
+    logits[0, 5], logits[0, 7], logits[0, 9], logits[0, 3] = 4.0, 4.0, -2.0, 1.0
+    out = eng._penalize([rid], logits)[0]
+    # 7: (4 - 0.5*2 - 1) / 2 = 1; 9: (-2 - 0.5 - 1) * 2 = -7; 5 (prompt): 4 / 2 = 2; 3 untouched
+    assert out[7].item() == 1.0 and out[9].item() == -7.0 and out[5].item() == 2.0 and out[3].item() == 1.0
+    # greedy with a strong presence penalty never repeats a generated token
+    g = eng.generate([[5, 6, 7]], SamplingParams(max_tokens=12, ignore_eos=True, presence_penalty=100.0))[0]
+    assert len(set(g.output)) == len(g.output)
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 
