@@ -43,6 +43,7 @@ class _SamplingFields(BaseModel):
     presence_penalty: float = 0.0
     frequency_penalty: float = 0.0
     repetition_penalty: float = 1.0
+    seed: int | None = None
 
     def n_logprobs(self) -> int | None:
         return None
@@ -52,7 +53,7 @@ class _SamplingFields(BaseModel):
                               top_p=self.top_p, ignore_eos=self.ignore_eos,
                               stop_token_ids=tuple(self.stop_token_ids or ()), logprobs=self.n_logprobs(),
                               presence_penalty=self.presence_penalty, frequency_penalty=self.frequency_penalty,
-                              repetition_penalty=self.repetition_penalty)
+                              repetition_penalty=self.repetition_penalty, seed=self.seed)
 
     def stops(self) -> list[str]:
         return [self.stop] if isinstance(self.stop, str) else [t for t in (self.stop or []) if t]

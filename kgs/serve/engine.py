@@ -39,6 +39,7 @@ class SamplingParams:
     presence_penalty: float = 0.0   # OpenAI: minus this once for every token already generated
     frequency_penalty: float = 0.0  # OpenAI: minus this times the token's count in the output
     repetition_penalty: float = 1.0  # CTRL/HF: logits of prompt+output tokens divided (>0) / multiplied (<0)
+    seed: int | None = None          # per-request sampling generator (reproducible regardless of batch mates)
 
 
 @dataclass
@@ -55,6 +56,7 @@ class Request:
     # per output token, when params.logprobs is set: (logprob, [(token, logprob)] top-k),
     # from the model's distribution before temperature / top-k / top-p
     logprobs: list = field(default_factory=list)
+    gen: object = None  # torch.Generator of a seeded request
 
 
 @dataclass
@@ -356,5 +358,11 @@ class LLMEngine:
             lf = torch.full_like(lf, float("-inf")).scatter(1, idx, srt)
         probs = torch.softmax(lf, dim=-1)
         sampled = torch.multinomial(probs, 1, generator=self._gen).squeeze(1)
+        for j, r in enumerate(ids):  # seeded requests draw from their own generator: reproducible per request
+            req = self.requests[int(r)]
+            if req.params.seed is not None and req.params.temperature > 0:
+                if req.gen is None:
+                    req.gen = torch.Generator(device=lf.device).manual_seed(int(req.params.seed))
+                sampled[j] = torch.multinomial(probs[j], 1, generator=req.gen)[0]
         greedy = torch.tensor([p.temperature <= 0 for p in ps], device=lf.device)
         return torch.where(greedy, logits.argmax(dim=-1), sampled)

@@ -572,6 +572,26 @@ def test_sampling_penalties():
     assert len(set(g.output)) == len(g.output)
 
 
+def test_seeded_sampling_is_reproducible():
+    """A seeded request draws from its own generator: its tokens do not depend on
+    the engine-wide generator the unseeded requests beside it consume."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    prompts = [[5, 6, 7], [9, 10], [11, 12, 13]]
+
+    def run(engine_seed, seed):
+        eng = LLMEngine(_tiny(), EngineConfig(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False),
+                        device="cpu", backend="ref")
+        eng._gen.manual_seed(engine_seed)  # the engine-wide sampling stream (the weights stay the same)
+        ps = [SamplingParams(max_tokens=6, temperature=1.0, seed=seed, ignore_eos=True)] + \
+             [SamplingParams(max_tokens=6, temperature=1.0, ignore_eos=True)] * 2
+        return [r.output for r in eng.generate(prompts, ps)]
+
+    a, b = run(1, 1234), run(2, 1234)
+    assert a[0] == b[0] and a[1:] != b[1:]  # the seeded row repeats, its unseeded mates do not
+    assert run(1, 99)[0] != a[0]
+
+
 def test_stop_text_truncates_and_holds_back():
     from kgs.serve.api import ByteTokenizer, StopText
 
