@@ -111,6 +111,8 @@ class LLMEngine:
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "mixed_steps": 0, "preemptions": 0, "graph_replays": 0, "graph_captures": 0}
         self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs"
+        self._want_lp: set = set()
+        self._want_pen: set = set()
 
     def _pages_from_memory(self, mc: LlamaConfig) -> int:
         if self.device.type != "cuda":
@@ -134,9 +136,17 @@ class LLMEngine:
             raise ValueError(f"request does not fit: prompt {len(prompt)} + max_tokens {params.max_tokens} "
                              f"(max_model_len {self.cfg.max_model_len}, {self.num_pages} pages)")
         self.requests[rid] = Request(rid, list(prompt), params, t_arrival=time.perf_counter())
+        # requests that need per-row work after the model step (the common greedy /
+        # plain-sampling batch skips those scans entirely)
+        if params.logprobs is not None:
+            self._want_lp.add(rid)
+        if params.presence_penalty or params.frequency_penalty or params.repetition_penalty != 1.0:
+            self._want_pen.add(rid)
         return rid
 
     def abort(self, rid: int) -> None:
+        self._want_lp.discard(rid)
+        self._want_pen.discard(rid)
         if self.sched.abort(rid):
             r = self.requests[rid]
             r.finished, r.finish_reason, r.t_done = True, "abort", time.perf_counter()
@@ -193,6 +203,8 @@ class LLMEngine:
             fin = rid in done
             if fin:
                 r.finished, r.t_done = True, now
+                self._want_lp.discard(rid)
+                self._want_pen.discard(rid)
                 r.finish_reason = "stop" if eos[j] else "length"
                 self.sched.release(rid)
             out.append((rid, int(toks[j]), fin))
@@ -294,7 +306,9 @@ class LLMEngine:
     def _logprobs(self, ids, logits: torch.Tensor, toks: torch.Tensor):
         """{row: (logprob of the sampled token, [(token, logprob)] top-k)} for the
         rows whose request asked for logprobs; None when none did."""
-        rows = [j for j, r in enumerate(ids) if self.requests[int(r)].params.logprobs is not None]
+        if not self._want_lp:
+            return None
+        rows = [j for j, r in enumerate(ids) if int(r) in self._want_lp]
         if not rows:
             return None
         sel = torch.as_tensor(rows, device=logits.device)
@@ -312,8 +326,9 @@ class LLMEngine:
     def _penalize(self, ids, logits: torch.Tensor) -> torch.Tensor:
         """Presence / frequency / repetition penalties on the rows that ask for
         them (a per-row token-count vector built from that request's tokens)."""
-        rows = [j for j, r in enumerate(ids) if (lambda p: p.presence_penalty or p.frequency_penalty
-                                                 or p.repetition_penalty != 1.0)(self.requests[int(r)].params)]
+        if not self._want_pen:
+            return logits
+        rows = [j for j, r in enumerate(ids) if int(r) in self._want_pen]
         if not rows:
             return logits
         logits = logits.float().clone()

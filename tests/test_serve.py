@@ -559,7 +559,8 @@ def test_sampling_penalties():
                     device="cpu", backend="ref")
     rid = eng.add_request([5, 6], SamplingParams(max_tokens=1, presence_penalty=1.0, frequency_penalty=0.5,
                                                  repetition_penalty=2.0))
-    eng.abort(rid)
+    eng.abort(rid)  # keep it out of the scheduler; drive the sampler by hand
+    eng._want_pen.add(rid)
     r = eng.requests[rid]
     r.output = [7, 7, 9]
     logits = torch.zeros(1, 16)
