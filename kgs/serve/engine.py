@@ -113,6 +113,7 @@ class LLMEngine:
         self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs"
         self._want_lp: set = set()
         self._want_pen: set = set()
+        self._seeded: set = set()
 
     def _pages_from_memory(self, mc: LlamaConfig) -> int:
         if self.device.type != "cuda":
@@ -142,11 +143,14 @@ class LLMEngine:
             self._want_lp.add(rid)
         if params.presence_penalty or params.frequency_penalty or params.repetition_penalty != 1.0:
             self._want_pen.add(rid)
+        if params.seed is not None:
+            self._seeded.add(rid)
         return rid
 
     def abort(self, rid: int) -> None:
         self._want_lp.discard(rid)
         self._want_pen.discard(rid)
+        self._seeded.discard(rid)
         if self.sched.abort(rid):
             r = self.requests[rid]
             r.finished, r.finish_reason, r.t_done = True, "abort", time.perf_counter()
@@ -205,6 +209,7 @@ class LLMEngine:
                 r.finished, r.t_done = True, now
                 self._want_lp.discard(rid)
                 self._want_pen.discard(rid)
+                self._seeded.discard(rid)
                 r.finish_reason = "stop" if eos[j] else "length"
                 self.sched.release(rid)
             out.append((rid, int(toks[j]), fin))
@@ -373,7 +378,7 @@ class LLMEngine:
             lf = torch.full_like(lf, float("-inf")).scatter(1, idx, srt)
         probs = torch.softmax(lf, dim=-1)
         sampled = torch.multinomial(probs, 1, generator=self._gen).squeeze(1)
-        for j, r in enumerate(ids):  # seeded requests draw from their own generator: reproducible per request
+        for j, r in enumerate(ids if self._seeded else ()):  # seeded requests: their own generator
             req = self.requests[int(r)]
             if req.params.seed is not None and req.params.temperature > 0:
                 if req.gen is None:
