@@ -267,8 +267,23 @@ class ServingModel:
             qkv = self.prefill_f8[i]["qkv"].forward_q(y8, ys) if f8 else self._proj(y, i, "qkv", False)
             self._rope_cache(qkv, i, positions, slots)
             a = torch.empty((x.shape[0], c.heads * hd), dtype=torch.bfloat16, device=x.device)
-            for row0, n, p, ctx0, pages, _ in chunks:
-                a[row0:row0 + p] = self._chunk_attention(qkv[row0:row0 + p], i, n, p, ctx0, pages)
+            j = 0
+            while j < len(chunks):
+                row0, n, p, ctx0, pages, _ = chunks[j]
+                # first chunks (no cached context) of equal padded length sit back to
+                # back: one batched flash-attention launch for the run
+                k = j + 1
+                if ctx0 == 0 and self.backend != "ref":
+                    while k < len(chunks) and chunks[k][3] == 0 and chunks[k][2] == p:
+                        k += 1
+                if k - j > 1:
+                    from kgs.ops.transformer import attention_qkv
+
+                    attention_qkv(qkv[row0:row0 + p * (k - j)], k - j, p, c.heads, c.kv_heads, head_dim=hd,
+                                  causal=True, out=a[row0:row0 + p * (k - j)])
+                else:
+                    a[row0:row0 + p] = self._chunk_attention(qkv[row0:row0 + p], i, n, p, ctx0, pages)
+                j = k
             if nd:
                 qd = qkv[n_pf:]
                 if self.backend == "ref":
