@@ -220,7 +220,9 @@ def build_all(jobs: int | None = None, verbose: bool = True, only: list[str] | N
 def clean() -> None:
     shutil.rmtree(REPO / "build" / "obj", ignore_errors=True)
     for p in OUT.glob("*"):
-        if p.name != "__init__.py":
+        if p.is_dir():
+            shutil.rmtree(p, ignore_errors=True)  # __pycache__
+        elif p.name != "__init__.py":
             p.unlink()
 
 
