@@ -20,6 +20,10 @@ fast, cdna_hip_programming.md rule 25).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         torchrun --nproc-per-node N bench.py --gpus N ...
+
+With ``--gpus N > 1`` and no WORLD_SIZE in the environment the script launches
+itself: the parent (which never touches the GPU) spawns N ranks with the
+torchrun env contract (kgs.parallel.launch) and exits with their status.
 """
 from __future__ import annotations
 
@@ -61,6 +65,12 @@ def parse(argv=None):
 
 def main(argv=None) -> int:
     args = parse(argv)
+    from kgs.parallel import launch
+
+    if launch.needs_self_launch(args.gpus):
+        raw = list(sys.argv[1:] if argv is None else argv)
+        return launch.spawn_local(args.gpus, [os.path.abspath(__file__), *raw], require_gpus=not args.cpu)
+
     import torch
     from kgs.models.gemm_workload import GemmWorkload
     from kgs.parallel import dist as kdist
@@ -98,6 +108,7 @@ def main(argv=None) -> int:
     sync()
     kdist.barrier(ctx)
     sync()
+    wl.reset_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
@@ -107,12 +118,19 @@ def main(argv=None) -> int:
     elapsed = time.perf_counter() - t0
 
     elapsed_max = kdist.max_over_ranks(ctx, elapsed)
+    per_rank_ms = [round(t / max(1, args.steps) * 1e3, 4) for t in kdist.all_gather_object(ctx, elapsed)]
+    ar_ms = wl.allreduce_ms()  # mean in-step all-reduce time over the timed steps (None at N=1)
     ms_per_step = elapsed_max / max(1, args.steps) * 1e3
     flops_per_step = wl.flops_per_step()
     per_gpu_tflops = flops_per_step / (ms_per_step * 1e-3) / 1e12
     total_tflops = per_gpu_tflops * world
 
     extra = {}
+    if ar_ms:
+        ar_bytes = wl.bucket.numel() * wl.bucket.element_size()
+        extra["allreduce_ms_in_step"] = round(ar_ms, 4)
+        # nccl-tests convention: busBW = algBW * 2 (N-1) / N
+        extra["allreduce_busbw_gbs"] = round(ar_bytes / (ar_ms * 1e-3) * 2 * (world - 1) / world / 1e9, 2)
     if args.compare_torch:
         extra["torch_matmul_tflops_per_gpu"] = round(wl.torch_reference_tflops(), 1)
 
@@ -145,6 +163,7 @@ def main(argv=None) -> int:
                 "allreduce_overlap": not args.no_overlap,
             },
             "per_gpu_tflops": round(per_gpu_tflops, 2),
+            "per_rank_ms_per_step": per_rank_ms,
             "gemm_path": wl.path_name(),
             "backend": args.backend,
             **extra,

@@ -41,6 +41,7 @@ class GemmWorkload:
             if self.cuda:
                 self.comm_stream = torch.cuda.Stream(device=self.device)
         self.dtype = dtype
+        self.reset_stats()
         if dtype == "fp8":
             # e4m3 operands (per-tensor scales), bf16 out: the scaled fp8 MFMA path
             from kgs.ops import quantize_fp8
@@ -77,9 +78,35 @@ class GemmWorkload:
             "kgs gemm_nt_generic"
 
     def _allreduce(self):
+        import time
+
         import torch.distributed as dist
 
-        dist.all_reduce(self.bucket, group=self.group)
+        if self.cuda:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+            dist.all_reduce(self.bucket, group=self.group)
+            ev[1].record()
+            self._ar_events.append(ev)
+        else:
+            t0 = time.perf_counter()
+            dist.all_reduce(self.bucket, group=self.group)
+            self._ar_wall.append((time.perf_counter() - t0) * 1e3)
+
+    def reset_stats(self) -> None:
+        self._ar_events, self._ar_wall = [], []
+
+    def allreduce_ms(self):
+        """Mean duration of the in-step all-reduce (stream time between its
+        start and end events: includes waiting for CUs the GEMM holds)."""
+        if self.bucket is None:
+            return None
+        if self.cuda:
+            torch.cuda.synchronize(self.device)
+            ts = [a.elapsed_time(b) for a, b in self._ar_events]
+        else:
+            ts = list(self._ar_wall)
+        return sum(ts) / len(ts) if ts else None
 
     def step(self) -> None:
         if not self.cuda:

@@ -1,6 +1,8 @@
 """Distributed paths on CPU: gloo, world_size 2 (the RCCL code paths are the
 same torch.distributed calls; the GPU box only has one GPU)."""
+import json
 import os
+import sys
 import socket
 
 import pytest
@@ -225,3 +227,55 @@ def test_tensor_parallel_mlp_gloo():
     ref = reference_mlp(x, w1, b1, w2, b2)
     for r in (0, 1):
         torch.testing.assert_close(res[r], ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_self_launches_n_ranks_cpu(world):
+    """`python bench.py --gpus N` without torchrun: the parent spawns N ranks
+    (torchrun env contract) and rank 0 prints exactly one valid JSON line."""
+    import subprocess
+
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(world), "--cpu",
+                        "--backend", "torch", "--gemm-m", "64", "--gemm-n", "64", "--gemm-k", "64",
+                        "--steps", "2", "--warmup", "1", "--allreduce-mb", "0.25"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == world and j["config"]["parallelism"] == f"dp{world}"
+    assert len(j["per_rank_ms_per_step"]) == world
+    assert j["ms_per_step"] == max(j["per_rank_ms_per_step"])
+    assert j["allreduce_busbw_gbs"] > 0 and j["allreduce_ms_in_step"] > 0
+
+
+def test_self_launch_propagates_rank_failure(tmp_path):
+    """One failing rank fails the whole launch (non-zero) and the surviving
+    ranks are stopped instead of hanging in a rendezvous."""
+    from kgs.parallel import launch
+
+    script = tmp_path / "w.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "if r == 1: sys.exit(7)\n"
+                      "time.sleep(60)\n")
+    import time
+
+    t0 = time.monotonic()
+    rc = launch.spawn_local(3, [str(script)], require_gpus=False)
+    assert rc == 7
+    assert time.monotonic() - t0 < 30
+
+
+def test_self_launch_refuses_missing_gpus():
+    from kgs.parallel import launch
+
+    assert launch.needs_self_launch(2, {}) and not launch.needs_self_launch(2, {"WORLD_SIZE": "2"})
+    assert not launch.needs_self_launch(1, {})
+    # this container has no GPU: asking for 2 real GPUs must fail fast, before spawning
+    if launch.visible_gpu_count() < 2:
+        assert launch.spawn_local(2, ["-c", "pass"], require_gpus=True) == 1
