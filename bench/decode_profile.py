@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Decode kernels under rocprofv3 counters: a fixed, HBM-streaming workload per
 kernel so per-dispatch counters (FETCH_SIZE, MFMA busy) can be set against the
-kernel-trace durations. Run it three times, once per pass (scripts/gpu_decode_pmc.sh):
+kernel-trace durations. Run it three times, once per pass (one rocprofv3 pass per run):
 
   rocprofv3 --kernel-trace --stats ... -- python3 bench/decode_profile.py
   rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE ... -- python3 bench/decode_profile.py

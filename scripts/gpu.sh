@@ -1,0 +1,74 @@
+# One GPU-box call, assembled from named steps:
+#
+#   gpurun --timeout 1200 -- 'bash scripts/gpu.sh OUT step [step ...]'
+#
+# Every step runs under its own `timeout -k 10`, logs to gpurun_out/OUT/<step>.log
+# and the chain stops at the first failure (no retries, nothing after a fault).
+# Counter passes (pmc_*) are separate rocprofv3 runs with --pmc only; they are
+# never combined with tracing.
+#
+# Steps:
+#   tests        full GPU pytest tier (per-test thread timeout)
+#   smoke        __graft_entry__.smoke()
+#   bench        python bench.py (driver defaults)
+#   bench_long   sustained >=10 s run of the bench config (steps=400)
+#   gemm_sweep   kgs vs hipBLASLt interleaved sweep of the headline shapes
+#   gemm_trace   rocprofv3 kernel trace + stats of the GEMM profile driver
+#   gemm_pmc     two counter passes over the GEMM (stall / MFMA busy)
+#   overlap      GEMM vs comm-kernel overlap measurement (bench/overlap.py)
+#   overlap_trace  kernel trace of the overlap run
+#   serve        kgs.serve batch-256 serving bench
+#   decode_trace kernel trace of batch-256 decode
+#   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
+#   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+OUT=${1:?usage: gpu.sh OUT step...}
+shift
+O=gpurun_out/$OUT
+mkdir -p "$O"
+
+run() {
+    local name=$1 t=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$t" "$@" > "$O/$name.log" 2>&1
+    local rc=$?
+    tail -3 "$O/$name.log" | cut -c1-900
+    echo "== $name rc=$rc"
+    return $rc
+}
+
+PMC_GEMM="python3 bench/gemm_profile.py --iters 5 --torch"
+
+step() {
+    case "$1" in
+        tests) run tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+        smoke) run smoke 300 python __graft_entry__.py smoke ;;
+        bench) run bench 300 python bench.py ;;
+        bench_long) run bench_long 300 python bench.py --steps 4000 --warmup 20 ;;
+        gemm_sweep) run gemm_sweep 600 python bench/gemm_sweep.py --shapes 4096,8192,16384x16384x8192 \
+            --variants fast --rounds 7 --out "$O/gemm_sweep.json" ;;
+        gemm_trace) run gemm_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o gemm \
+            -- python3 bench/gemm_profile.py --iters 20 --torch ;;
+        gemm_pmc) run pmc_stall 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+            SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc1" -o gemm -- $PMC_GEMM &&
+            run pmc_mfma 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU \
+            GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc2" -o gemm -- $PMC_GEMM ;;
+        overlap) run overlap 300 python bench/overlap.py --out "$O/overlap.json" ;;
+        overlap_trace) run overlap_trace 300 rocprofv3 --kernel-trace --output-format csv -d "$O/otrace" -o ov \
+            -- python3 bench/overlap.py --iters 3 ;;
+        serve) run serve 400 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
+            --max-batch 256 --max-model-len 2048 ;;
+        decode_trace) run decode_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace" -o d \
+            -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 --max-batch 256 \
+            --max-model-len 2048 ;;
+        e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
+        gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
+        *) echo "unknown step $1" >&2; return 2 ;;
+    esac
+}
+
+for s in "$@"; do
+    step "$s" || exit $?
+done
