@@ -1,12 +1,11 @@
 #!/usr/bin/env python3
 """Where does a phase's time go? Runs the production GEMM schedule built with
-s_memtime stamps (gemm_experiments.hip, S bit 16) at 8192^3 and reports, per
+s_memtime stamps (native/experiments/gemm_experiments.hip, S bit 16) at 8192^3 and reports, per
 wave group, the mean cycles of each section of a phase:
 
   read   reads + LDS-DMA issue + vmcnt wait      bar1   first barrier + lgkmcnt
   mfma   16 MFMAs issued                         bar2   second barrier
 (diagnostic build: the stamps themselves cost a few % of wave cycles)."""
-import ctypes
 import json
 import os
 import statistics
@@ -16,11 +15,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from kgs.ops import _lib, gemm_nt  # noqa: E402
+from kgs.ops import _lib, experiments, gemm_nt  # noqa: E402
 
-so = _lib.lib()
-so.kgs_gemm_bf16_nt_stamps.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 6 + [ctypes.c_void_p] * 2
-so.kgs_gemm_stamp_n.restype = ctypes.c_int
+so = experiments.lib()
 SN = so.kgs_gemm_stamp_n()
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 A = (torch.rand(n, n, device="cuda") * 2 - 1).bfloat16()

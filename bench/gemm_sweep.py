@@ -20,6 +20,26 @@ from kgs.ops import gemm_nt  # noqa: E402
 _rand = None
 
 
+def _gemm(v):
+    """Production variants through kgs.ops; measured alternatives (and, with a
+    wrong result, the timing probes) through the opt-in kgs.ops.experiments."""
+    from kgs.ops import experiments
+    from kgs.ops.gemm import VARIANTS
+
+    if v in VARIANTS:
+        return lambda A, B, out: gemm_nt(A, B, out=out, variant=v)
+    return lambda A, B, out: experiments.gemm_nt(A, B, v, out=out, allow_wrong=True)
+
+
+def _gemm_fp8(v):
+    from kgs.ops import experiments, gemm_fp8_nt
+    from kgs.ops.gemm import FP8_VARIANTS
+
+    if v in FP8_VARIANTS:
+        return lambda qa, qb, sa, sb, out: gemm_fp8_nt(qa, qb, sa, sb, out=out, variant=v)
+    return lambda qa, qb, sa, sb, out: experiments.gemm_fp8_nt(qa, qb, sa, sb, v, out=out)
+
+
 def time_fn(fn, iters):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
@@ -55,7 +75,7 @@ def main():
         B = _rand(N, K).bfloat16()
         C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         C2 = torch.empty_like(C)
-        fns = {f"kgs_{v}": (lambda v=v: gemm_nt(A, B, out=C, variant=v)) for v in a.variants.split(",")}
+        fns = {f"kgs_{v}": (lambda v=v: _gemm(v)(A, B, out=C)) for v in a.variants.split(",")}
         fns["hipblaslt"] = lambda: torch.matmul(A, B.T, out=C2)
         for f in fns.values():
             for _ in range(3):
@@ -67,7 +87,7 @@ def main():
                 times[k].append(time_fn(f, a.iters))
         errs = {}
         for v in a.variants.split(","):
-            gemm_nt(A, B, out=C, variant=v)
+            _gemm(v)(A, B, out=C)
             errs[v] = ((C.float() - C2.float()).abs().max() / C2.float().abs().max()).item()
         fl = 2.0 * M * N * K
         r = {"shape": [M, N, K]}
@@ -95,7 +115,7 @@ def sweep_fp8(a):
         C2 = torch.empty_like(C)
         ta = torch.tensor(sa, device="cuda")
         tb = torch.tensor(sb, device="cuda")
-        fns = {f"kgs_fp8_{v}": (lambda v=v: gemm_fp8_nt(qa, qb, sa, sb, out=C, variant=v))
+        fns = {f"kgs_fp8_{v}": (lambda v=v: _gemm_fp8(v)(qa, qb, sa, sb, out=C))
                for v in a.variants.split(",")}
         try:
             torch._scaled_mm(qa, qb.T, scale_a=ta, scale_b=tb, out_dtype=torch.bfloat16)
@@ -114,7 +134,7 @@ def sweep_fp8(a):
         ref = (qa.float() * sa) @ (qb.float() * sb).T
         errs = {}
         for v in a.variants.split(","):
-            gemm_fp8_nt(qa, qb, sa, sb, out=C, variant=v)
+            _gemm_fp8(v)(qa, qb, sa, sb, out=C)
             errs[v] = ((C.float() - ref).abs().max() / ref.abs().max()).item()
         if "hipblaslt_fp8" in fns:
             errs["hipblaslt_fp8"] = ((C2.float() - ref).abs().max() / ref.abs().max()).item()

@@ -1,0 +1,107 @@
+"""Opt-in access to the measured GEMM alternatives (``libkgs_experiments.so``).
+
+Production code never imports this module: ``kgs.ops.gemm_nt`` exposes only the
+correct production kernels (auto / fast / generic / bounded). The kernels here
+are the alternatives and timing probes behind ``profiles/gemm_tuning.md``
+(source: ``native/experiments/gemm_experiments.hip``). Entries with
+``probe=True`` compute a WRONG product by construction (they exist to time one
+cost in isolation) and are only callable with ``allow_wrong=True``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from functools import lru_cache
+from pathlib import Path
+
+import torch
+
+from . import _lib
+from .gemm import EPI, _check_operand
+
+LIB_PATH = Path(os.environ.get("KGS_EXPERIMENTS_LIB", _lib.NATIVE_DIR / "libkgs_experiments.so"))
+
+
+@dataclass(frozen=True)
+class Experiment:
+    id: int
+    what: str
+    probe: bool = False  # wrong result by construction (timing only)
+    epilogue: bool = True  # supports the bias/activation epilogues
+
+
+BF16 = {
+    "w4": Experiment(3, "4 waves x 128x128, AGPR-pinned asm MFMAs"),
+    "pp_prio": Experiment(4, "s_setprio around the MFMA blocks", epilogue=False),
+    "pp_gm8": Experiment(5, "GROUP_M 8", epilogue=False),
+    "pp_v0": Experiment(6, "first schedule (12/4/8/0 reads, look-ahead 5)", epilogue=False),
+    "pp_gm2": Experiment(7, "GROUP_M 2", epilogue=False),
+    "pp_gm16": Experiment(8, "GROUP_M 16", epilogue=False),
+    "probe_2xmfma": Experiment(9, "every MFMA block doubled", probe=True, epilogue=False),
+    "p32": Experiment(10, "32-MFMA phases, 160 KiB ring"),
+    "probe_l2": Experiment(11, "all blocks load tile (0,0)", probe=True, epilogue=False),
+    "lockstep": Experiment(12, "no ping-pong stagger", epilogue=False),
+    "lockstep_1bar": Experiment(13, "lockstep, one barrier per phase", epilogue=False),
+    "pl": Experiment(14, "lockstep with in-wave software pipelining"),
+    "narrow_store": Experiment(15, "2 x 8-B store tail", epilogue=False),
+    "persistent": Experiment(20, "persistent tile walk"),
+    "vgpr_stage": Experiment(21, "VGPR staging, 4 phases in flight"),
+    "vgpr_stage2": Experiment(22, "VGPR staging, 2 phases in flight"),
+}
+FP8 = {"gm8": 17, "gm16": 18, "gm2": 19}
+
+
+@lru_cache(maxsize=1)
+def lib() -> ctypes.CDLL:
+    _lib.lib()  # torch's HIP runtime first, then the production library (shared runtime)
+    if not LIB_PATH.exists():
+        raise _lib.NativeUnavailable(f"{LIB_PATH} is missing: `python -m kgs.utils.build --only experiments`")
+    so = ctypes.CDLL(str(LIB_PATH))
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    so.kgs_exp_gemm_bf16_nt.argtypes = [vp] * 4 + [i] * 8 + [vp]
+    so.kgs_exp_gemm_bf16_nt.restype = i
+    so.kgs_exp_gemm_fp8_nt.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
+    so.kgs_exp_gemm_fp8_nt.restype = i
+    so.kgs_gemm_bf16_nt_stamps.argtypes = [vp] * 3 + [i] * 6 + [vp] * 2
+    so.kgs_gemm_bf16_nt_stamps.restype = i
+    so.kgs_gemm_stamp_n.restype = i
+    return so
+
+
+def gemm_nt(a: torch.Tensor, b: torch.Tensor, variant: str, bias: torch.Tensor | None = None,
+            act: str | None = None, out: torch.Tensor | None = None, allow_wrong: bool = False) -> torch.Tensor:
+    """``act(a @ b.T + bias)`` on experimental kernel ``variant`` (aligned shapes only)."""
+    ex = BF16[variant]
+    if ex.probe and not allow_wrong:
+        raise ValueError(f"{variant} is a timing probe with a wrong result; pass allow_wrong=True")
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N = b.shape[0]
+    epi_name = act if act is not None else ("bias" if bias is not None else None)
+    epi = EPI[epi_name]
+    if epi and not ex.epilogue:
+        raise ValueError(f"{variant} has no epilogue variant")
+    if epi and bias is None:
+        bias = torch.zeros(N, dtype=torch.bfloat16, device=a.device)
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    rc = lib().kgs_exp_gemm_bf16_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(),
+                                    bias.data_ptr() if bias is not None else None, M, N, K, a.stride(0),
+                                    b.stride(0), out.stride(0), epi, ex.id, _lib.stream_handle(a.device))
+    _lib.check(rc, f"experiment {variant}[{M}x{N}x{K}]")
+    return out
+
+
+def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, scale_a: float, scale_b: float, variant: str,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    M, K = a.shape
+    N = b.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    rc = lib().kgs_exp_gemm_fp8_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                   out.stride(0), float(scale_a) * float(scale_b), FP8[variant],
+                                   _lib.stream_handle(a.device))
+    _lib.check(rc, f"fp8 experiment {variant}[{M}x{N}x{K}]")
+    return out

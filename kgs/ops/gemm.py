@@ -16,11 +16,9 @@ import torch
 from . import _lib
 
 EPI = {None: 0, "none": 0, "bias": 1, "gelu": 2, "relu": 3, "silu": 4}
-VARIANTS = {"auto": 0, "fast": 1, "pingpong": 1, "generic": 2, "w4": 3, "bounded": 16, "persistent": 20, "vgpr_stage": 21, "vgpr_stage2": 22,
-            # tuning experiments (no epilogue), see native/kernels/gemm_bf16.hip launch():
-            "pp_prio": 4, "pp_gm8": 5, "pp_v0": 6, "pp_gm2": 7, "pp_gm16": 8, "probe_2xmfma": 9,
-            "p32": 10, "probe_l2": 11, "lockstep": 12, "lockstep_1bar": 13, "pl": 14,
-            "narrow_store": 15}
+# Production kernels only; the measured alternatives and timing probes are in
+# kgs.ops.experiments (a separate, opt-in library).
+VARIANTS = {"auto": 0, "fast": 1, "pingpong": 1, "generic": 2, "bounded": 16}
 
 
 def _check_operand(t: torch.Tensor, name: str) -> None:
@@ -136,7 +134,7 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
 
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
-FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16, "gm8": 17, "gm16": 18, "gm2": 19}  # gm*: experiments
+FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}
 
 
 def quantize_fp8(x: torch.Tensor, scale: float | None = None) -> tuple[torch.Tensor, float]:

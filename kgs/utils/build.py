@@ -4,7 +4,11 @@ Builds, with the ROCm toolchain in ``/opt/rocm``:
 
 * ``kgs/_native/libkgs_kernels.so`` -- every ``native/kernels/*.hip`` (bf16 MFMA
   GEMM, vector add, transpose, checksum, P2P all-reduce) behind a C ABI that
-  ``kgs/ops/_lib.py`` loads with ctypes.
+  ``kgs/ops/_lib.py`` loads with ctypes. Built with ``-fvisibility=hidden``:
+  only the ``KGS_EXPORT`` production entry points are exported.
+* ``kgs/_native/libkgs_experiments.so`` -- ``native/experiments/*.hip``, the
+  measured GEMM alternatives and timing probes (some wrong by construction),
+  opt-in through ``kgs.ops.experiments`` and never loaded by production code.
 * ``kgs/_native/libkgs_gpuinfo.so`` + ``kgs/_native/kgs-gpuinfo`` -- the C++
   device-enumeration core (KFD sysfs topology + amd-smi) used by the device
   plugin, also as a standalone CLI.
@@ -108,7 +112,15 @@ def targets() -> list[Target]:
             OUT / "libkgs_kernels.so",
             sorted(kdir.glob("*.hip")),
             HIPCC,
-            flags=HIP_FLAGS + [f"-I{kdir}"],
+            flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
+            headers=k_headers,
+        ),
+        Target(
+            "experiments",
+            OUT / "libkgs_experiments.so",
+            sorted((NATIVE / "experiments").glob("*.hip")),
+            HIPCC,
+            flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
             headers=k_headers,
         ),
         Target(

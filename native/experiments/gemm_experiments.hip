@@ -1,6 +1,12 @@
-// Measured alternatives to the production GEMM (gemm_bf16.hip), kept so every
-// result in profiles/gemm_tuning.md can be re-run (variants 3-14 of the C ABI):
+// Measured alternatives to the production GEMM (native/kernels/gemm_bf16.hip),
+// kept so every result in profiles/gemm_tuning.md can be re-run. Built into
+// its own opt-in library, kgs/_native/libkgs_experiments.so (never loaded by
+// production code; Python: kgs.ops.experiments). Variant ids:
 //
+//  * 15 narrow_store -- production schedule with the 2 x 8-B store tail.
+//  * 20 persistent -- the production pipeline as a persistent tile walk.
+//  * 21/22 vgpr_stage(2) -- VGPR staging instead of LDS-DMA.
+//  * fp8 17-19 -- GROUP_M 8 / 16 / 2 of the fp8 pipeline.
 //  * gemm_nt_256pl (14) -- lockstep 8 waves with in-wave software pipelining.
 //  * gemm_nt_256p32 (10) -- 32-MFMA phases (half the barriers), 160 KiB ring.
 //  * gemm_nt_256w4 (3) -- 4 waves x 128x128 with AGPR-pinned asm MFMAs.
@@ -672,6 +678,23 @@ static hipError_t launch_experiment(int variant, const unsigned short* A, const 
   } else if (variant == 3) {
     dim3 grid((M / g4::BM) * (N / g4::BN));
     hipLaunchKernelGGL(g4::gemm_nt_256w4<EPI>, grid, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else if (variant == 15) {
+    // production schedule with the narrow (2 x 8-B per lane) store tail
+    if constexpr (EPI != EPI_NONE) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 256>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
+                       ldb, ldc, 1.0f, nullptr);
+  } else if (variant == 20) {
+    // persistent: one block per CU walking the tiles (measured slightly slower)
+    static int cus = 0;
+    if (!cus) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    }
+    const int nwg = (M / g256::BM) * (N / g256::BN);
+    const dim3 gridp(nwg < cus ? nwg : cus);
+    hipLaunchKernelGGL((g256::gemm_nt_256_persist<EPI, 7 + 32768>), gridp, dim3(512), 0, s, A, B, C, bias, M, N, K,
+                       lda, ldb, ldc, 1.0f, nullptr);
   } else {
     return hipErrorInvalidValue;
   }
@@ -680,28 +703,73 @@ static hipError_t launch_experiment(int variant, const unsigned short* A, const 
 
 }  // namespace kgs
 
-// Called by kgs_gemm_bf16_nt (gemm_bf16.hip) for variants 3-14 after the
-// shared eligibility checks.
-extern "C" hipError_t kgs_gemm_bf16_nt_experiment(int variant, int epi, const unsigned short* A,
-                                                  const unsigned short* B, unsigned short* C,
-                                                  const unsigned short* bias, int M, int N, int K, int lda, int ldb,
-                                                  int ldc, hipStream_t s) {
+// The same eligibility as the production fast path (M, N % 256, K % 128,
+// 16-B aligned operands and rows).
+static bool exp_fast_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda, int ldb,
+                        int ldc) {
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return false;
+  if (M % 256 || N % 256 || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return false;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return false;
+  return (long)lda * 256 < (1L << 31) && (long)ldb * 256 < (1L << 31);
+}
+
+// bf16 NT experiments: variants 3-15, 20-22. Returns 0 or a KGS_ERR_* / hipError_t.
+KGS_EXPORT int kgs_exp_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                                    int lda, int ldb, int ldc, int epi, int variant, hipStream_t s) {
+  if (!((variant >= 3 && variant <= 15) || (variant >= 20 && variant <= 22))) return KGS_ERR_ARG;
+  if (epi != kgs::EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
+  if (!exp_fast_ok(A, B, C, M, N, K, lda, ldb, ldc)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto bb = (const unsigned short*)bias;
+  hipError_t e;
   switch (epi) {
-    case kgs::EPI_NONE: return kgs::launch_experiment<kgs::EPI_NONE>(variant, A, B, C, bias, M, N, K, lda, ldb, ldc, s);
-    case kgs::EPI_BIAS: return kgs::launch_experiment<kgs::EPI_BIAS>(variant, A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+    case kgs::EPI_NONE: e = kgs::launch_experiment<kgs::EPI_NONE>(variant, a, b, c, bb, M, N, K, lda, ldb, ldc, s); break;
+    case kgs::EPI_BIAS: e = kgs::launch_experiment<kgs::EPI_BIAS>(variant, a, b, c, bb, M, N, K, lda, ldb, ldc, s); break;
     case kgs::EPI_BIAS_GELU:
-      return kgs::launch_experiment<kgs::EPI_BIAS_GELU>(variant, A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+      e = kgs::launch_experiment<kgs::EPI_BIAS_GELU>(variant, a, b, c, bb, M, N, K, lda, ldb, ldc, s);
+      break;
     case kgs::EPI_BIAS_RELU:
-      return kgs::launch_experiment<kgs::EPI_BIAS_RELU>(variant, A, B, C, bias, M, N, K, lda, ldb, ldc, s);
+      e = kgs::launch_experiment<kgs::EPI_BIAS_RELU>(variant, a, b, c, bb, M, N, K, lda, ldb, ldc, s);
+      break;
     case kgs::EPI_BIAS_SILU:
-      return kgs::launch_experiment<kgs::EPI_BIAS_SILU>(variant, A, B, C, bias, M, N, K, lda, ldb, ldc, s);
-    default: return hipErrorInvalidValue;
+      e = kgs::launch_experiment<kgs::EPI_BIAS_SILU>(variant, a, b, c, bb, M, N, K, lda, ldb, ldc, s);
+      break;
+    default: return KGS_ERR_ARG;
   }
+  return (int)e;
+}
+
+// fp8 e4m3 tile-group height experiments (aligned shapes, no epilogue):
+// 17 = GROUP_M 8, 18 = GROUP_M 16, 19 = GROUP_M 2. Lengths in fp8 elements.
+KGS_EXPORT int kgs_exp_gemm_fp8_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                   int ldc, float alpha, int variant, hipStream_t s) {
+  using namespace kgs;
+  if (variant < 17 || variant > 19) return KGS_ERR_ARG;
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (M % 256 || N % 256 || K % 256 || lda % 16 || ldb % 16 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  const int Kw = K / 2, ldaw = lda / 2, ldbw = ldb / 2;
+  const dim3 grid((M / g256::BM) * (N / g256::BN));
+  if (variant == 17)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 3 + 1024>), grid, dim3(512), 0, s, a, b, c, nullptr, M, N, Kw,
+                       ldaw, ldbw, ldc, alpha, nullptr);
+  if (variant == 18)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 11 + 1024>), grid, dim3(512), 0, s, a, b, c, nullptr, M, N, Kw,
+                       ldaw, ldbw, ldc, alpha, nullptr);
+  if (variant == 19)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 15 + 1024>), grid, dim3(512), 0, s, a, b, c, nullptr, M, N, Kw,
+                       ldaw, ldbw, ldc, alpha, nullptr);
+  return (int)hipGetLastError();
 }
 
 // Diagnostic build: the production schedule with s_memtime stamps (S bit 16).
 // stamps: 4 * STAMP_N u64 (blocks 0..3); layout in gemm_pipeline.h (stamp()).
-extern "C" int kgs_gemm_bf16_nt_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+KGS_EXPORT int kgs_gemm_bf16_nt_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                        int ldc, void* stamps, hipStream_t s) {
   if (M % 256 || N % 256 || K % 128 || (K / 128) < kgs::g256::STAMP_IT0 + kgs::g256::STAMP_ITS) return KGS_ERR_SHAPE;
   const dim3 grid((M / 256) * (N / 256));
@@ -711,4 +779,4 @@ extern "C" int kgs_gemm_bf16_nt_stamps(const void* A, const void* B, void* C, in
   return (int)hipGetLastError();
 }
 
-extern "C" int kgs_gemm_stamp_n() { return kgs::g256::STAMP_N; }
+KGS_EXPORT int kgs_gemm_stamp_n() { return kgs::g256::STAMP_N; }

@@ -31,14 +31,12 @@
 //      glds SOURCE address. Grid: one block per 256x256 tile, XCD-bijective
 //      remap, then GROUP_M=4 grouped order so the 32 co-resident tiles of an
 //      XCD form a 4x8 patch sharing A/B panels (L2 hit 81 % = 1 - 12/64).
-//      Template S selects schedule knobs; variants 3-14 are the measured
-//      alternatives and timing probes, in gemm_experiments.hip
-//      (profiles/gemm_tuning.md).
+//      Template S selects schedule knobs; the measured alternatives and timing
+//      probes live in native/experiments/gemm_experiments.hip, built into a
+//      separate opt-in libkgs_experiments.so (profiles/gemm_tuning.md).
 //
 //  * fp8 (kgs_gemm_fp8_nt) and the K-major layouts (kgs_gemm_bf16) are the same
 //      pipeline with the scaled fp8 MFMA / ds_read_b64_tr_b16 fragments.
-//
-//  * variant 20 -- the pipeline as a persistent tile walk (measured slower).
 //
 //  * gemm_nt_256<.., S|512> (variant 16, "bounded") -- the same pipeline for any
 //      M, N and K % 8 == 0: operands are read by `buffer_load_dwordx4 ... lds`
@@ -56,12 +54,6 @@
 // test pod only echoes (pods/rocm-gpu-test-pod.yaml:9, Readme.md:16-20). This is
 // the in-pod hot path required by BASELINE.json configs 3-4.
 #include "gemm_pipeline.h"
-
-// Measured alternatives (variants 3-14) live in gemm_experiments.hip.
-extern "C" hipError_t kgs_gemm_bf16_nt_experiment(int variant, int epi, const unsigned short* A,
-                                                  const unsigned short* B, unsigned short* C,
-                                                  const unsigned short* bias, int M, int N, int K, int lda, int ldb,
-                                                  int ldc, hipStream_t s);
 
 namespace kgs {
 
@@ -167,24 +159,6 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
     const dim3 gridb(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512>), gridb, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
                        ldc, 1.0f, nullptr);
-  } else if (variant == 15) {
-    // production schedule with the narrow (2 x 8-B per lane) store tail, for A/B
-    if constexpr (EPI != EPI_NONE) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 256>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda,
-                       ldb, ldc, 1.0f, nullptr);
-  } else if (variant == 20) {
-    // persistent: one block per CU walking the tiles (aligned shapes; measured
-    // slightly slower than the one-shot grid, kept for A/B)
-    static int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    }
-    const int nwg = (M / g256::BM) * (N / g256::BN);
-    const dim3 gridp(nwg < cus ? nwg : cus);
-    hipLaunchKernelGGL((g256::gemm_nt_256_persist<EPI, 7 + 32768>), gridp, dim3(512), 0, s, A, B, C, bias, M, N, K,
-                       lda, ldb, ldc, 1.0f, nullptr);
   } else {
     const int vec_ok = ((lda % 8) == 0 && (ldb % 8) == 0 && ((uintptr_t)A % 16) == 0 && ((uintptr_t)B % 16) == 0);
     dim3 grid((N + gen::BN - 1) / gen::BN, (M + gen::BM - 1) / gen::BM);
@@ -220,8 +194,8 @@ KGS_EXPORT int kgs_gemm_bf16_nt_bounded_ok(const void* A, const void* B, const v
   return 1;
 }
 
-// variant: 0 = auto, 1 = force 256x256 8-wave ping-pong, 2 = force generic,
-//          3 = force 256x256 4-wave (both pipelined variants need the same eligibility).
+// variant: 0 = auto, 1 = force the 256x256 8-wave ping-pong, 2 = force generic,
+//          16 = force the bounded 256x256 pipeline. Anything else is rejected.
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                 int ldb, int ldc, int epi, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
@@ -236,16 +210,11 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
-  else if ((variant >= 3 && variant <= 15) || variant == 20 || variant == 21 || variant == 22) {
-    if (!fast) return KGS_ERR_ALIGN;
-    v = variant;
-  }
   else return KGS_ERR_ARG;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
   auto bb = (const unsigned short*)bias;
-  if ((v >= 3 && v <= 14) || v == 21 || v == 22) return (int)kgs_gemm_bf16_nt_experiment(v, epi, a, b, c, bb, M, N, K, lda, ldb, ldc, stream);
   hipError_t e;
   switch (epi) {
     case kgs::EPI_NONE: e = kgs::launch<kgs::EPI_NONE>(v, a, b, c, bb, M, N, K, lda, ldb, ldc, stream); break;
@@ -277,19 +246,6 @@ hipError_t launch_fp8(int v, const unsigned short* A, const unsigned short* B, u
   if (v == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
                        ldbw, ldc, alpha, alpha_ptr);
-  } else if (v >= 17 && v <= 19) {
-    // tile-group height experiments for fp8 (aligned shapes): GROUP_M 8 / 16 / 2
-    if constexpr (EPI == EPI_NONE) {
-      if (v == 17)
-        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 3 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha, alpha_ptr);
-      if (v == 18)
-        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 11 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha, alpha_ptr);
-      if (v == 19)
-        hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 15 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
-                           ldaw, ldbw, ldc, alpha, alpha_ptr);
-    }
   } else {
     const dim3 grid(((M + g256::BM - 1) / g256::BM) * ((N + g256::BN - 1) / g256::BN));
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 512 + 1024>), grid, dim3(512), 0, s, A, B, C, bias, M, N, Kw,
@@ -322,7 +278,7 @@ KGS_EXPORT int kgs_gemm_fp8_nt_dev(const void* A, const void* B, void* C, const 
   const int bounded = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 1);
   int v;
   if (variant == 0) v = fast ? 1 : 16;
-  else if (variant == 1 || variant == 16 || (variant >= 17 && variant <= 19)) v = variant;
+  else if (variant == 1 || variant == 16) v = variant;
   else return KGS_ERR_ARG;
   if (!(v == 16 ? bounded : fast)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;

@@ -67,9 +67,19 @@ def test_checksum():
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-2)
 
 
+def _gemm_v(a, b, variant, **kw):
+    """Production variants via kgs.ops.gemm_nt; measured alternatives via the
+    opt-in experiments library (kept correct, so they stay tested)."""
+    from kgs.ops import experiments, gemm_nt
+    from kgs.ops.gemm import VARIANTS
+
+    if variant in VARIANTS:
+        return gemm_nt(a, b, variant=variant, **kw)
+    return experiments.gemm_nt(a, b, variant, **kw)
+
+
 @pytest.mark.parametrize("variant", ["generic", "fast", "w4", "p32"])
 def test_gemm_identity_asymmetric(variant):
-    from kgs.ops import gemm_nt
 
     n = 256
     a = torch.eye(n, device=DEV).bfloat16()
@@ -79,7 +89,7 @@ def test_gemm_identity_asymmetric(variant):
     k = 256
     a2 = torch.zeros(n, k, device=DEV).bfloat16()
     a2[:, :n] = a
-    c = gemm_nt(a2, b, variant=variant)
+    c = _gemm_v(a2, b, variant)
     torch.testing.assert_close(c.float(), b.float().T, rtol=0, atol=0)
 
 
@@ -94,7 +104,7 @@ def test_gemm_fast_random(M, N, K, variant):
     a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
     assert fast_path_ok(a, b)
-    c = gemm_nt(a, b, variant=variant)
+    c = _gemm_v(a, b, variant)
     ref = _ref_nt(a, b)
     assert _rel_err(c, ref) < 1e-2
     # the two variants agree (same fp32 accumulation, possibly different order)
@@ -120,7 +130,7 @@ def test_gemm_strided_operands(variant):
     big_b = torch.randn(512, 1024, device=DEV).bfloat16()
     a = big_a[:, 128:384]  # ld = 1024, K = 256
     b = big_b[:256, 256:512]
-    c = gemm_nt(a, b, variant=variant)
+    c = _gemm_v(a, b, variant)
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
 
 
@@ -133,7 +143,7 @@ def test_gemm_epilogues(act, variant):
     a = (torch.rand(M, K, device=DEV) - 0.5).bfloat16()
     b = (torch.rand(N, K, device=DEV) - 0.5).bfloat16()
     bias = torch.randn(N, device=DEV).bfloat16()
-    c = gemm_nt(a, b, bias=bias, act=act, variant=variant)
+    c = _gemm_v(a, b, variant, bias=bias, act=act)
     ref = _ref_nt(a, b, bias, None if act == "bias" else act)
     torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
 
@@ -147,10 +157,10 @@ def test_gemm_repeatable_large(variant):
     for M, N, K in ((2048, 2048, 2048), (1024, 3072, 4096), (4096, 512, 640)):
         a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
         b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
-        c0 = gemm_nt(a, b, variant=variant)
+        c0 = _gemm_v(a, b, variant)
         assert _rel_err(c0, _ref_nt(a, b)) < 1e-2
         for _ in range(10):
-            assert torch.equal(gemm_nt(a, b, variant=variant), c0)
+            assert torch.equal(_gemm_v(a, b, variant), c0)
         # same per-accumulator K order as production -> bitwise equal
         assert torch.equal(gemm_nt(a, b, variant="fast"), c0)
 
@@ -236,7 +246,7 @@ def test_gemm_wide_store_tail_matches_narrow():
     for M, N, K in ((512, 768, 256), (2048, 2048, 2048)):
         a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
         b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
-        assert torch.equal(gemm_nt(a, b, variant="fast"), gemm_nt(a, b, variant="narrow_store"))
+        assert torch.equal(gemm_nt(a, b, variant="fast"), _gemm_v(a, b, "narrow_store"))
 
 
 def test_gemm_misaligned_out_and_bias_fall_back():
@@ -449,3 +459,13 @@ def test_gemm_fp8_device_scale_and_fp8_linear():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(ys, f8(x))
+
+
+def test_timing_probes_refuse_without_opt_in():
+    from kgs.ops import experiments
+
+    a = (torch.rand(256, 256, device=DEV) * 2 - 1).bfloat16()
+    with pytest.raises(ValueError):
+        experiments.gemm_nt(a, a, "probe_l2")
+    experiments.gemm_nt(a, a, "probe_l2", allow_wrong=True)  # runs, result undefined
+    torch.cuda.synchronize()
