@@ -18,14 +18,23 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--mnk", default="8192")
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--torch", action="store_true")
+ap.add_argument("--variant", default="auto", help="kgs.ops.gemm variant or a kgs.ops.experiments name")
 a = ap.parse_args()
 d = [int(x) for x in a.mnk.split("x")]
 M, N, K = (d * 3)[:3] if len(d) == 1 else d
 A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
 B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
 C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+if a.variant == "auto":
+    run = lambda: gemm_nt(A, B, out=C)  # noqa: E731
+else:
+    from kgs.ops import experiments
+    from kgs.ops.gemm import VARIANTS
+
+    run = (lambda: gemm_nt(A, B, out=C, variant=a.variant)) if a.variant in VARIANTS else \
+        (lambda: experiments.gemm_nt(A, B, a.variant, out=C))
 for _ in range(a.iters):
-    gemm_nt(A, B, out=C)
+    run()
 if a.torch:
     for _ in range(a.iters):
         torch.matmul(A, B.T, out=C)

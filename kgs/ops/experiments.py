@@ -32,7 +32,7 @@ class Experiment:
 
 
 BF16 = {
-    "w4": Experiment(3, "4 waves x 128x128, AGPR-pinned asm MFMAs"),
+    "w4_bk32": Experiment(3, "round-1 4-wave try: BK=32 4-deep ring, one barrier per 64 MFMAs"),
     "pp_prio": Experiment(4, "s_setprio around the MFMA blocks", epilogue=False),
     "pp_gm8": Experiment(5, "GROUP_M 8", epilogue=False),
     "pp_v0": Experiment(6, "first schedule (12/4/8/0 reads, look-ahead 5)", epilogue=False),
@@ -50,6 +50,12 @@ BF16 = {
     "vgpr_stage2": Experiment(22, "VGPR staging, 2 phases in flight"),
 }
 FP8 = {"gm8": 17, "gm16": 18, "gm2": 19}
+# gemm_w4h (native/experiments/gemm_w4h.hip): 4 waves x 128x128, two barriers
+# per 128-MFMA K-step; name w4h_ORD_B1_R_P_X -> table id in gemm_w4h.hip (barrier 1 after MFMA B1, R
+# MFMAs after barrier 2, P reads per MFMA there)
+_W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (1, 24, 20, 1, 480000),
+            (1, 20, 20, 1, 160000), (1, 20, 24, 1, 320000))
+W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
 
 
 @lru_cache(maxsize=1)
@@ -66,12 +72,27 @@ def lib() -> ctypes.CDLL:
     so.kgs_gemm_bf16_nt_stamps.argtypes = [vp] * 3 + [i] * 6 + [vp] * 2
     so.kgs_gemm_bf16_nt_stamps.restype = i
     so.kgs_gemm_stamp_n.restype = i
+    so.kgs_exp_gemm_w4h.argtypes = [vp] * 3 + [i] * 7 + [vp]
+    so.kgs_exp_gemm_w4h.restype = i
     return so
 
 
 def gemm_nt(a: torch.Tensor, b: torch.Tensor, variant: str, bias: torch.Tensor | None = None,
             act: str | None = None, out: torch.Tensor | None = None, allow_wrong: bool = False) -> torch.Tensor:
     """``act(a @ b.T + bias)`` on experimental kernel ``variant`` (aligned shapes only)."""
+    if variant in W4H:
+        if bias is not None or act is not None:
+            raise ValueError("w4h variants have no epilogue")
+        _check_operand(a, "a")
+        _check_operand(b, "b")
+        M, K = a.shape
+        N = b.shape[0]
+        if out is None:
+            out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+        rc = lib().kgs_exp_gemm_w4h(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                    out.stride(0), W4H[variant], _lib.stream_handle(a.device))
+        _lib.check(rc, f"experiment {variant}[{M}x{N}x{K}]")
+        return out
     ex = BF16[variant]
     if ex.probe and not allow_wrong:
         raise ValueError(f"{variant} is a timing probe with a wrong result; pass allow_wrong=True")

@@ -112,11 +112,49 @@ def all_gather_object(ctx: DistContext, obj):
     return out
 
 
-def shutdown(ctx: DistContext) -> None:
-    if ctx.initialized_here:
-        import torch.distributed as dist
+def shutdown(ctx: DistContext, timeout_s: float = 60.0) -> None:
+    """Tear the process group down so that no rank exits while a peer still
+    holds live transport state towards it.
 
-        try:
-            dist.destroy_process_group()
-        except Exception:  # pragma: no cover
-            pass
+    A gloo rank whose peer process has already exited can abort in its
+    transport thread ("terminate called without an active exception", seen on
+    8-rank CPU runs). So: barrier (all collectives done), drop our references and
+    destroy the group, then a store-side exit barrier -- every rank counts itself
+    out and leaves only once all have destroyed theirs. Rank 0 hosts the store
+    and is therefore the last to go.
+    """
+    if not ctx.initialized_here:
+        return
+    import gc
+    import time
+
+    import torch.distributed as dist
+
+    store = None
+    try:
+        if ctx.world_size > 1:
+            store = dist.distributed_c10d._get_default_store()
+            barrier(ctx)
+    except Exception:  # pragma: no cover - best effort on a broken group
+        store = None
+    ctx.group = None
+    try:
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        pass
+    gc.collect()
+    if store is None:
+        return
+    try:
+        store.add("kgs/exit", 1)
+        deadline = time.monotonic() + timeout_s
+        while store.add("kgs/exit", 0) < ctx.world_size and time.monotonic() < deadline:
+            time.sleep(0.01)
+        if ctx.rank == 0:  # give the others a moment to read the final count
+            deadline = time.monotonic() + 2.0
+            while store.add("kgs/exit_ack", 0) < ctx.world_size - 1 and time.monotonic() < deadline:
+                time.sleep(0.01)
+        else:
+            store.add("kgs/exit_ack", 1)
+    except Exception:  # pragma: no cover - rank 0's store already gone: nothing left to protect
+        pass

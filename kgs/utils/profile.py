@@ -39,7 +39,9 @@ def trace_command(cmd: list, outdir: str, name: str = "run") -> list:
 def short(name: str) -> str:
     n = name.split("(")[0]
     if "gemm_nt_256w4" in n:
-        return "kgs gemm_nt_256w4 (4-wave)"
+        return "kgs gemm_nt_256w4 (round-1 4-wave experiment)"
+    if "gemm_nt_w4" in n:
+        return "kgs gemm_nt_w4 (4-wave, production) " + n.split("<")[-1].rstrip(">") if "<" in n else n
     if "gemm_nt_256" in n:
         return "kgs gemm_nt_256 (8-wave ping-pong) " + n.split("<")[-1].rstrip(">") if "<" in n else n
     if "Cijk" in n:

@@ -1,0 +1,37 @@
+// Measured alternatives of the four-wave GEMM (native/kernels/gemm_w4.h): the
+// K-step schedule knobs B1 / R / P / ORD / X of gemm_nt_w4. Built into the
+// opt-in libkgs_experiments.so; names and ids in kgs/ops/experiments.py (W4H),
+// numbers in profiles/gemm_tuning.md ("Four-wave kernel").
+#include "gemm_w4.h"
+
+// variant = table id below; template <B1, R, P, ORD, X>, X = 10000 W + 100 AUX + GROUP_M
+// (W = DMA window in MFMAs, AUX = DMA cache bits, 0 = default). Aligned shapes
+// only: M, N % 256, K % 128, lda/ldb/ldc % 8, 16-B aligned operands.
+KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb, int ldc,
+                                int variant, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (M % 256 || N % 256 || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  if ((long)lda * 256 * 2 >= (1L << 31) || (long)ldb * 256 * 2 >= (1L << 31)) return KGS_ERR_SHAPE;
+  const dim3 grid((M / 256) * (N / 256));
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+#define KGS_W4H(ID, B1, R, P, ORD, X)                                                                         \
+  case ID:                                                                                                    \
+    hipLaunchKernelGGL((kgs::w4::gemm_nt_w4<kgs::EPI_NONE, B1, R, P, ORD, X>), grid, dim3(256), 0, s, a, b, c, \
+                       nullptr, M, N, K, lda, ldb, ldc);                                                      \
+    break;
+  // ids: kgs/ops/experiments.py W4H (name = w4h_ORD_B1_R_P_X)
+  switch (variant) {
+    KGS_W4H(1, 24, 20, 1, 1, 0)
+    KGS_W4H(2, 24, 20, 1, 1, 160000)
+    KGS_W4H(3, 24, 20, 1, 1, 320000)
+    KGS_W4H(4, 24, 20, 1, 1, 480000)
+    KGS_W4H(5, 20, 20, 1, 1, 160000)
+    KGS_W4H(6, 20, 24, 1, 1, 320000)
+    default: return KGS_ERR_ARG;
+  }
+#undef KGS_W4H
+  return (int)hipGetLastError();
+}

@@ -7,7 +7,13 @@
 //
 // Kernels (variant numbers are the C ABI's `variant` argument):
 //
-//  * gemm_nt_256 -- the hot path (M%256 == N%256 == 0, K%128 == 0), variant 1.
+//  * gemm_nt_w4 -- the hot path since round 2 (aligned shapes, variant 3; see
+//      gemm_w4.h): the same 256x256x64 tile and LDS image with four waves of
+//      128x128, two barriers per 128-MFMA K-step. Interleaved against the
+//      8-wave kernel below: +2-3 % at 4096^3..16384^2x8192.
+//
+//  * gemm_nt_256 -- the 8-wave ping-pong (aligned shapes), variant 1; still the
+//      engine of the bounded / fp8 / K-major / split-K paths below.
 //      256x256x64 block tile, 512 threads = 8 waves as 2(M) x 4(N), each wave
 //      owns 128x64 of C as 2x2 quadrants of 64x32 (4x2 MFMA 16x16x32 tiles).
 //      A and B K-tiles are split into 128-row halves (A0 A1 B0 B1, 16 KiB each)
@@ -54,6 +60,7 @@
 // test pod only echoes (pods/rocm-gpu-test-pod.yaml:9, Readme.md:16-20). This is
 // the in-pod hot path required by BASELINE.json configs 3-4.
 #include "gemm_pipeline.h"
+#include "gemm_w4.h"
 
 namespace kgs {
 
@@ -150,7 +157,9 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   // Production S = 7: balanced schedule, no s_setprio, GROUP_M 4 (measured best
   // at 4096^3..16384^2x8192 in interleaved A/B, profiles/gemm_tuning.md).
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
-  if (variant == 1) {
+  if (variant == 3) {
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI>), grid256, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
                        ldc, 1.0f, nullptr);
   } else if (variant == 16) {
@@ -182,6 +191,14 @@ KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void
   return 1;
 }
 
+// Can the four-wave kernel (variant 3) take this problem? The fast-path shape
+// rules plus 32-bit buffer-resource byte offsets over a 256-row panel.
+KGS_EXPORT int kgs_gemm_bf16_nt_w4_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
+                                      int ldb, int ldc) {
+  if (!kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc)) return 0;
+  return (long)lda * 512 < (1L << 31) && (long)ldb * 512 < (1L << 31);
+}
+
 // Can the bounded 256x256 kernel (variant 16) take this problem? Any M, N;
 // K, the leading dimensions and the pointers in 16-B units.
 KGS_EXPORT int kgs_gemm_bf16_nt_bounded_ok(const void* A, const void* B, const void* C, int M, int N, int K,
@@ -195,7 +212,8 @@ KGS_EXPORT int kgs_gemm_bf16_nt_bounded_ok(const void* A, const void* B, const v
 }
 
 // variant: 0 = auto, 1 = force the 256x256 8-wave ping-pong, 2 = force generic,
-//          16 = force the bounded 256x256 pipeline. Anything else is rejected.
+//          3 = force the four-wave kernel, 16 = force the bounded 256x256
+//          pipeline. Anything else is rejected.
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                 int ldb, int ldc, int epi, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
@@ -204,9 +222,11 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   // the fast epilogue reads the bias 4 elements (8 B) at a time
   const int bias_ok = epi == kgs::EPI_NONE || (uintptr_t)bias % 8 == 0;
   const int fast = kgs_gemm_bf16_nt_fast_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
+  const int w4 = kgs_gemm_bf16_nt_w4_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
   const int bounded = kgs_gemm_bf16_nt_bounded_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
   int v;
-  if (variant == 0) v = fast ? 1 : bounded ? 16 : 2;
+  if (variant == 0) v = w4 ? 3 : fast ? 1 : bounded ? 16 : 2;
+  else if (variant == 3) { if (!w4) return KGS_ERR_ALIGN; v = 3; }
   else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;

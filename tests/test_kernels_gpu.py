@@ -78,7 +78,7 @@ def _gemm_v(a, b, variant, **kw):
     return experiments.gemm_nt(a, b, variant, **kw)
 
 
-@pytest.mark.parametrize("variant", ["generic", "fast", "w4", "p32"])
+@pytest.mark.parametrize("variant", ["generic", "fast", "pingpong", "w4_bk32", "p32", "w4h_1_20_24_1_320000"])
 def test_gemm_identity_asymmetric(variant):
 
     n = 256
@@ -97,7 +97,7 @@ def test_gemm_identity_asymmetric(variant):
     "M,N,K",
     [(256, 256, 128), (512, 768, 256), (256, 512, 1024), (1024, 1024, 1024), (768, 256, 384), (2048, 1280, 640)],
 )
-@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
+@pytest.mark.parametrize("variant", ["fast", "pingpong", "w4_bk32", "p32"])
 def test_gemm_fast_random(M, N, K, variant):
     from kgs.ops import fast_path_ok, gemm_nt
 
@@ -122,7 +122,7 @@ def test_gemm_generic_ragged(M, N, K):
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
 
 
-@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
+@pytest.mark.parametrize("variant", ["fast", "pingpong", "w4_bk32", "p32"])
 def test_gemm_strided_operands(variant):
     from kgs.ops import gemm_nt
 
@@ -135,7 +135,7 @@ def test_gemm_strided_operands(variant):
 
 
 @pytest.mark.parametrize("act", ["bias", "gelu", "relu", "silu"])
-@pytest.mark.parametrize("variant", ["fast", "generic", "w4", "p32"])
+@pytest.mark.parametrize("variant", ["fast", "pingpong", "generic", "w4_bk32", "p32"])
 def test_gemm_epilogues(act, variant):
     from kgs.ops import gemm_nt
 
@@ -148,7 +148,7 @@ def test_gemm_epilogues(act, variant):
     torch.testing.assert_close(c.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("variant", ["fast", "w4", "p32"])
+@pytest.mark.parametrize("variant", ["fast", "pingpong", "w4_bk32", "p32"])
 def test_gemm_repeatable_large(variant):
     """Race screen: the pipelined kernels must be bitwise deterministic, and the
     two pipelined variants must agree bitwise (same K order per accumulator)."""
@@ -220,6 +220,21 @@ def test_gemm_bounded_matches_fast_on_aligned():
     a = (torch.rand(1024, 2048, device=DEV) * 2 - 1).bfloat16()
     b = (torch.rand(768, 2048, device=DEV) * 2 - 1).bfloat16()
     assert torch.equal(gemm_nt(a, b, variant="bounded"), gemm_nt(a, b, variant="fast"))
+    assert torch.equal(gemm_nt(a, b, variant="pingpong"), gemm_nt(a, b, variant="fast"))
+
+
+def test_gemm_auto_routes_aligned_to_four_wave_kernel():
+    """auto == the four-wave kernel on aligned shapes; its knob variants (the
+    experiments library) compute the identical image."""
+    from kgs.ops import experiments, gemm_nt
+
+    a = (torch.rand(2048, 1024, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(1536, 1024, device=DEV) * 2 - 1).bfloat16()
+    c = gemm_nt(a, b, variant="w4")
+    assert _rel_err(c, _ref_nt(a, b)) < 1e-2
+    assert torch.equal(gemm_nt(a, b), c)
+    for name in experiments.W4H:
+        assert torch.equal(experiments.gemm_nt(a, b, name), c), name
 
 
 @pytest.mark.parametrize("act", ["bias", "gelu"])

@@ -32,7 +32,7 @@ def test_public_variants_are_production_only():
     from kgs.ops import experiments
     from kgs.ops.gemm import FP8_VARIANTS, VARIANTS
 
-    assert set(VARIANTS) == {"auto", "fast", "pingpong", "generic", "bounded"}
+    assert set(VARIANTS) == {"auto", "fast", "w4", "pingpong", "generic", "bounded"}
     assert set(FP8_VARIANTS) == {"auto", "fast", "bounded"}
     probes = {k for k, e in experiments.BF16.items() if e.probe}
     assert probes == {"probe_2xmfma", "probe_l2"}
