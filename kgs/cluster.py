@@ -326,6 +326,59 @@ class Provisioner:
             time.sleep(0.25)
         raise ProvisionError(f"ERROR: only {have} of {want} {C.RESOURCE_NAME} advertised after {timeout_s:.0f}s")
 
+    # ---------------------------------------------------------- reconcile ---
+    SHAPE_FILE = "cluster.json"
+
+    def desired_shape(self) -> dict:
+        """What this create would build: the parts of the kind config that an
+        existing cluster cannot be changed to in place (node list and the
+        /dev/kfd + renderD extraMounts are fixed at `kind create` time)."""
+        return {"fake": bool(self.fake), "workers": int(self.s.workers),
+                "partitions": [list(p) for p in (self.partitions or [])] if not self.fake else [],
+                "registry_port": int(self.s.registry_port)}
+
+    def write_shape(self) -> None:
+        if self.runner.dry_run:
+            return
+        self.state_dir.mkdir(parents=True, exist_ok=True)
+        (self.state_dir / self.SHAPE_FILE).write_text(json.dumps(self.desired_shape(), indent=1) + "\n")
+
+    def check_drift(self) -> None:
+        """Q15 reconcile, with drift detection: re-running create on an existing
+        cluster is fine only if it would build the same cluster. A cluster made
+        on the fake (CPU-only) path and re-created on a GPU host has workers
+        without /dev/kfd mounts; a changed partition or worker count likewise
+        cannot be applied in place -- fail now with a clear instruction instead
+        of timing out on capacity later."""
+        want = self.desired_shape()
+        path = self.state_dir / self.SHAPE_FILE
+        have = None
+        if path.exists():
+            try:
+                have = json.loads(path.read_text())
+            except ValueError:
+                have = None
+        diffs = []
+        if have is not None:
+            for key, label in (("fake", "GPU path (fake capacity vs real /dev/kfd passthrough)"),
+                               ("workers", "worker count"), ("partitions", "GPU partition (render minors per worker)"),
+                               ("registry_port", "registry port")):
+                if have.get(key) != want[key]:
+                    diffs.append(f"{label}: existing {have.get(key)!r}, requested {want[key]!r}")
+        else:
+            # created by another tool / an older kgs: the node list is still checkable
+            n = len(self.worker_names())
+            if n != want["workers"]:
+                diffs.append(f"worker count: existing {n}, requested {want['workers']}")
+        if diffs:
+            raise ProvisionError(
+                f"ERROR: kind cluster '{self.s.cluster_name}' exists with a different shape -- "
+                + "; ".join(diffs)
+                + f". These are fixed when kind creates the nodes: run `kgs delete --cluster-name={self.s.cluster_name}`"
+                  " first, then create again.")
+        if have is None:
+            self.write_shape()
+
     # --------------------------------------------------------------- verbs ---
     def create(self, gpu_type: str = "rocm") -> int:
         if gpu_type != "rocm":
@@ -350,12 +403,14 @@ class Provisioner:
         try:
             with t.phase("kind-create") as rec:
                 if not self.runner.dry_run and self.cluster_exists():
+                    self.check_drift()
                     self.out(f"Kind cluster '{self.s.cluster_name}' already exists; reconciling.")
                     rec["reused"] = True
                 else:
                     args = ["create", "cluster", "--name", self.s.cluster_name, "--config", str(cfg)]
                     self.kind(*args)
                     self.created_cluster = True
+                    self.write_shape()
             with t.phase("registry-network"):
                 self.ensure_runtime().network_connect(C.KIND_NETWORK, C.REGISTRY_NAME)
             with t.phase("nodes") as rec:

@@ -36,6 +36,18 @@ def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None
     return out
 
 
+def comm_standin(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32, passes: int = 1) -> torch.Tensor:
+    """``dst += src`` (f32) on a fixed number of workgroups, ``passes`` times: the
+    footprint of a ring collective's kernel (a few tens of long-lived,
+    memory-bound workgroups) on one GPU, for GEMM/comm overlap measurements."""
+    _dev_check(dst, src)
+    if dst.dtype != torch.float32 or src.dtype != torch.float32 or dst.shape != src.shape:
+        raise ValueError("comm_standin needs two f32 tensors of one shape")
+    _lib.check(_lib.lib().kgs_comm_standin_f32(dst.data_ptr(), src.data_ptr(), dst.numel(), int(blocks), int(passes),
+                                               _lib.stream_handle(dst.device)), "comm_standin")
+    return dst
+
+
 def transpose_bf16(x: torch.Tensor, variant: int = 0) -> torch.Tensor:
     """Materialised ``x.T`` (variant 0 = auto: 16-B path when shapes allow,
     1 = element-wise tile, 2 = force the 16-B path)."""

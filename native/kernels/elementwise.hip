@@ -171,6 +171,20 @@ __global__ __launch_bounds__(EW_THREADS) void checksum_bf16(const bf16x8* __rest
   }
 }
 
+// RCCL-shaped stand-in for a collective's kernel on ONE GPU (bench/overlap.py):
+// a fixed, small number of workgroups ("channels") each streams its slice of
+// dst += src, `passes` times. A ring all-reduce kernel has this footprint --
+// tens of long-lived workgroups, memory-bound -- so it measures whether such a
+// kernel gets CUs next to a GEMM that fills every CU, without needing peers.
+__global__ __launch_bounds__(EW_THREADS) void comm_standin_f32(f32x4* __restrict__ dst, const f32x4* __restrict__ src,
+                                                              long nvec, int passes) {
+  const long per = (nvec + gridDim.x - 1) / gridDim.x;
+  const long lo = per * blockIdx.x;
+  const long hi = lo + per < nvec ? lo + per : nvec;
+  for (int p = 0; p < passes; ++p)
+    for (long i = lo + threadIdx.x; i < hi; i += EW_THREADS) dst[i] += src[i];
+}
+
 static int blocks_for(long n) {
   long b = (n + EW_THREADS - 1) / EW_THREADS;
   if (b < 1) b = 1;
@@ -244,6 +258,15 @@ KGS_EXPORT int kgs_vector_add_bf16_v(const void* a, const void* b, void* c, long
   if (rest)
     hipLaunchKernelGGL(kgs::vadd_bf16_tail, dim3((rest + 255) / 256), dim3(256), 0, s,
                        (const unsigned short*)a, (const unsigned short*)b, (unsigned short*)c, n8 * 8, n);
+  return (int)hipGetLastError();
+}
+
+// dst += src (f32, n % 4 == 0, 16-B aligned) on `nblocks` workgroups, `passes` times.
+KGS_EXPORT int kgs_comm_standin_f32(void* dst, const void* src, long n, int nblocks, int passes, hipStream_t s) {
+  if (n <= 0 || n % 4 || nblocks <= 0 || passes <= 0) return KGS_ERR_SHAPE;
+  if ((uintptr_t)dst % 16 || (uintptr_t)src % 16) return KGS_ERR_ALIGN;
+  hipLaunchKernelGGL(kgs::comm_standin_f32, dim3(nblocks), dim3(kgs::EW_THREADS), 0, s, (f32x4*)dst,
+                     (const f32x4*)src, n / 4, passes);
   return (int)hipGetLastError();
 }
 
