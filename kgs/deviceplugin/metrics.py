@@ -7,6 +7,8 @@ Exposed gauges/counters are computed at scrape time from the plugin's state:
   kgs_deviceplugin_allocations_total                        Allocate container responses
   kgs_deviceplugin_registrations_total                      kubelet registrations
   kgs_deviceplugin_health_flips_total                       health transitions streamed
+  kgs_gpu_ecc_errors{id,kind=correctable|uncorrectable|deferred}   amd-smi totals (last health tick)
+  kgs_gpu_xgmi_links{id,state=up|down}                      amd-smi xGMI link status (last health tick)
 
 The reference has no observability beyond ``echo``.
 """
@@ -32,6 +34,22 @@ class PluginCollector:
         for d in devs:
             per.add_metric([d.id, str(d.render_minor), str(d.numa)], 1.0 if d.healthy else 0.0)
         yield per
+        samples = getattr(self.plugin.source, "last_sample", {}) or {}
+        ecc = GaugeMetricFamily("kgs_gpu_ecc_errors", "amd-smi accumulated ECC error counts", labels=["id", "kind"])
+        links = GaugeMetricFamily("kgs_gpu_xgmi_links", "amd-smi xGMI link status", labels=["id", "state"])
+        for dev_id, st in sorted(samples.items()):
+            if not st.get("amdsmi"):
+                continue
+            for kind in ("correctable", "uncorrectable", "deferred"):
+                v = st.get(f"ecc_{kind}", -1)
+                if v is not None and v >= 0:
+                    ecc.add_metric([dev_id, kind], float(v))
+            for state in ("up", "down"):
+                v = st.get(f"xgmi_links_{state}", -1)
+                if v is not None and v >= 0:
+                    links.add_metric([dev_id, state], float(v))
+        yield ecc
+        yield links
         for name, attr, doc in (("allocations", "allocations", "Allocate container responses"),
                                 ("registrations", "registrations", "kubelet registrations"),
                                 ("health_flips", "health_flips", "health transitions streamed")):

@@ -7,7 +7,8 @@ Lifecycle (kubelet device-plugin protocol v1beta1):
 2. serve ``v1beta1.DevicePlugin`` on ``<plugin-dir>/kgs-amdgpu.sock``;
 3. ``Register`` with the kubelet on ``<plugin-dir>/kubelet.sock``;
 4. stream the device list on ``ListAndWatch`` and re-send it whenever a GPU's
-   health flips (health = device nodes present + KFD node alive, polled);
+   health flips (device nodes present + KFD node alive, plus amd-smi
+   uncorrectable-ECC count and xGMI link status against a baseline; polled);
 5. on ``Allocate`` hand the container ``/dev/kfd`` and the allocated
    ``/dev/dri/renderD<minor>`` nodes (ROCr only enumerates GPUs whose render node
    it can open, so the pod sees exactly its GPUs);
@@ -61,10 +62,15 @@ class RealSource:
     """GPUs from the native gpuinfo core, filtered to this node's partition."""
 
     def __init__(self, root: str = "/", allowed_minors: set | None = None, use_amdsmi: bool = True):
+        from kgs import gpuinfo
+
         self.root = root
         self.allowed = allowed_minors
         self.use_amdsmi = use_amdsmi
         self._devs: list[PluginDevice] = []
+        # stateful: ECC / xGMI baselines are taken at the first health tick
+        self.monitor = gpuinfo.HealthMonitor(root, use_amdsmi=use_amdsmi)
+        self.last_sample: dict = {}
         self.rescan()
 
     def rescan(self) -> None:
@@ -90,12 +96,13 @@ class RealSource:
         return list(self._devs)
 
     def refresh(self) -> bool:
-        """Re-evaluate health; True if any device changed state."""
-        from kgs import gpuinfo
-
+        """Re-evaluate health (sysfs + amd-smi ECC / xGMI against the baseline);
+        True if any device changed state."""
         changed = False
         for d in self._devs:
-            ok, why = gpuinfo.health(self.root, d.node_id, d.render_minor)
+            st = self.monitor.check(d.node_id, d.render_minor, d.meta.get("bdf", ""))
+            self.last_sample[d.id] = st
+            ok, why = bool(st["healthy"]), st["reason"]
             if ok != d.healthy:
                 log.warning("device %s (renderD%d) health %s -> %s: %s", d.id, d.render_minor,
                             d.healthy, ok, why)

@@ -60,6 +60,14 @@ class Gpu:
     vram_bytes: int = 0
     numa_node: int = -1
     uuid: str = ""
+    # amd-smi health sample (-1 = not available)
+    ecc_correctable: int = -1
+    ecc_uncorrectable: int = -1
+    ecc_deferred: int = -1
+    xgmi_links_total: int = -1
+    xgmi_links_up: int = -1
+    xgmi_links_down: int = -1
+    smi_links: list = field(default_factory=list)  # [{to_index, type, hops, weight, p2p}] from amd-smi
     properties_readable: bool = True
     render_node_present: bool = False
     healthy: bool = False
@@ -88,6 +96,9 @@ class Topology:
     cpu_nodes: int
     gpus: list
     warnings: list
+    amdsmi_library: str = ""
+    smi_topology_checked: bool = False  # amd-smi's link matrix compared with the KFD io_links
+    smi_topology_agrees: bool = False
 
     def by_node(self) -> dict:
         return {g.node_id: g for g in self.gpus}
@@ -109,6 +120,8 @@ def _parse(js: str) -> Topology:
     return Topology(
         root=d["root"], kfd_present=d["kfd_present"], topology_present=d["topology_present"],
         amdsmi_used=d["amdsmi_used"], cpu_nodes=d["cpu_nodes"], gpus=gpus, warnings=d["warnings"],
+        amdsmi_library=d.get("amdsmi_library", ""), smi_topology_checked=d.get("smi_topology_checked", False),
+        smi_topology_agrees=d.get("smi_topology_agrees", False),
     )
 
 
@@ -156,3 +169,29 @@ def health(root: str, node_id: int, render_minor: int) -> tuple:
     t = discover(root, use_amdsmi=False)
     g = t.by_node().get(node_id)
     return (bool(g and g.healthy), g.health_reason if g else "KFD node gone")
+
+
+class HealthMonitor:
+    """Stateful per-GPU health (native ``HealthMonitor``, native/gpuinfo/gpuinfo.h):
+    the sysfs checks plus amd-smi's uncorrectable-ECC count and xGMI link
+    status against a baseline taken at the first check. ``check`` returns a dict
+    with ``healthy``, ``reason`` and the sample (``ecc_*``, ``xgmi_links_*``,
+    ``amdsmi``). Without the pybind core it degrades to the stateless sysfs check.
+    """
+
+    def __init__(self, root: str = "/", use_amdsmi: bool = True, ecc_tolerance: int | None = None):
+        if ecc_tolerance is None:
+            ecc_tolerance = int(os.environ.get("KGS_ECC_UNCORRECTABLE_TOLERANCE", "0"))
+        self.root = str(root)
+        kind, mod = _backend()
+        self._native = mod.HealthMonitor(self.root, use_amdsmi, int(ecc_tolerance)) if kind == "pybind" else None
+
+    @property
+    def amdsmi_used(self) -> bool:
+        return bool(self._native is not None and self._native.amdsmi_used)
+
+    def check(self, node_id: int, render_minor: int, bdf: str = "") -> dict:
+        if self._native is not None:
+            return dict(self._native.check(node_id, render_minor, bdf))
+        ok, why = health(self.root, node_id, render_minor)
+        return {"healthy": ok, "reason": why, "amdsmi": False}

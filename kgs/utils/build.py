@@ -12,6 +12,9 @@ Builds, with the ROCm toolchain in ``/opt/rocm``:
 * ``kgs/_native/libkgs_gpuinfo.so`` + ``kgs/_native/kgs-gpuinfo`` -- the C++
   device-enumeration core (KFD sysfs topology + amd-smi) used by the device
   plugin, also as a standalone CLI.
+* ``kgs/_native/libamd_smi_stub.so`` -- a test double of the amd-smi C API
+  (ECC counts and xGMI link states from a text file) for the CPU tests of the
+  plugin's health path; loaded only through ``KGS_AMDSMI_LIB``.
 * ``kgs/_native/_serve*.so`` -- the continuous-batching scheduler and paged-KV
   block allocator of ``kgs.serve`` (C++17, pybind11).
 * ``kgs/_native/kgs-rccl-bench`` -- single-process multi-GPU RCCL all-reduce
@@ -104,8 +107,9 @@ def targets() -> list[Target]:
     g_headers = sorted(gdir.glob("*.h"))
     amdsmi_ok = (ROCM / "include" / "amd_smi" / "amdsmi.h").exists()
     smi_flags = ["-DKGS_HAVE_AMDSMI=1", f"-I{ROCM / 'include'}"] if amdsmi_ok else []
-    smi_link = [f"-L{ROCM / 'lib'}", "-lamd_smi", f"-Wl,-rpath,{ROCM / 'lib'}"] if amdsmi_ok else []
-    core = [gdir / "gpuinfo.cpp"]
+    # amd-smi is dlopen'ed at run time (native/gpuinfo/smi.cpp): headers only, no link dependency
+    smi_link = ["-ldl"]
+    core = [gdir / "gpuinfo.cpp", gdir / "smi.cpp"]
     ts = [
         Target(
             "kernels",
@@ -150,6 +154,14 @@ def targets() -> list[Target]:
             link_flags=smi_link,
             shared=False,
             headers=g_headers,
+        ),
+        Target(
+            "amdsmi-stub",
+            OUT / "libamd_smi_stub.so",
+            [gdir / "testing" / "amdsmi_stub.cpp"],
+            CXX,
+            flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{ROCM / 'include'}"],
+            optional=True,
         ),
         Target(
             "serve-py",

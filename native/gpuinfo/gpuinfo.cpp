@@ -4,7 +4,6 @@
 #include "gpuinfo.h"
 
 #include <dirent.h>
-#include <dlfcn.h>
 #include <sys/stat.h>
 
 #include <algorithm>
@@ -14,9 +13,6 @@
 #include <map>
 #include <sstream>
 
-#ifdef KGS_HAVE_AMDSMI
-#include <amd_smi/amdsmi.h>
-#endif
 
 namespace kgs {
 namespace gpuinfo {
@@ -130,92 +126,67 @@ std::string json_escape(const std::string& s) {
   return o;
 }
 
-// ---- amd-smi (optional) ------------------------------------------------------
-#ifdef KGS_HAVE_AMDSMI
-struct Smi {
-  void* h = nullptr;
-  decltype(&amdsmi_init) init = nullptr;
-  decltype(&amdsmi_shut_down) shut_down = nullptr;
-  decltype(&amdsmi_get_socket_handles) sockets = nullptr;
-  decltype(&amdsmi_get_processor_handles) procs = nullptr;
-  decltype(&amdsmi_get_gpu_enumeration_info) enum_info = nullptr;
-  decltype(&amdsmi_get_gpu_device_bdf) bdf = nullptr;
-  decltype(&amdsmi_get_gpu_device_uuid) uuid = nullptr;
-
-  bool load() {
-    for (const char* name : {"libamd_smi.so", "libamd_smi.so.26", "/opt/rocm/lib/libamd_smi.so"}) {
-      h = ::dlopen(name, RTLD_NOW | RTLD_LOCAL);
-      if (h) break;
-    }
-    if (!h) return false;
-#define KGS_SYM(f, n) f = reinterpret_cast<decltype(f)>(::dlsym(h, n))
-    KGS_SYM(init, "amdsmi_init");
-    KGS_SYM(shut_down, "amdsmi_shut_down");
-    KGS_SYM(sockets, "amdsmi_get_socket_handles");
-    KGS_SYM(procs, "amdsmi_get_processor_handles");
-    KGS_SYM(enum_info, "amdsmi_get_gpu_enumeration_info");
-    KGS_SYM(bdf, "amdsmi_get_gpu_device_bdf");
-    KGS_SYM(uuid, "amdsmi_get_gpu_device_uuid");
-#undef KGS_SYM
-    return init && shut_down && sockets && procs;
-  }
-  ~Smi() {
-    if (h) ::dlclose(h);
-  }
-};
-
+// ---- amd-smi (optional, smi.cpp) -------------------------------------------
+// UUID, health sample and the GPU-to-GPU link view, cross-checked against the
+// KFD io_links: both must agree on which pairs are xGMI peers.
 bool enrich_with_amdsmi(Topology& t) {
-  if (std::getenv("KGS_NO_AMDSMI")) return false;
-  Smi s;
-  if (!s.load()) return false;
-  if (s.init(AMDSMI_INIT_AMD_GPUS) != AMDSMI_STATUS_SUCCESS) return false;
-  uint32_t nsock = 0;
-  if (s.sockets(&nsock, nullptr) != AMDSMI_STATUS_SUCCESS || nsock == 0) {
-    s.shut_down();
-    return false;
-  }
-  std::vector<amdsmi_socket_handle> socks(nsock);
-  s.sockets(&nsock, socks.data());
+  auto s = SmiSession::open();
+  if (!s) return false;
+  t.amdsmi_library = s->library();
+  std::vector<const SmiGpu*> sg(t.gpus.size(), nullptr);
   bool any = false;
-  for (auto sk : socks) {
-    uint32_t np = 0;
-    if (s.procs(sk, &np, nullptr) != AMDSMI_STATUS_SUCCESS || np == 0) continue;
-    std::vector<amdsmi_processor_handle> ps(np);
-    s.procs(sk, &np, ps.data());
-    for (auto p : ps) {
-      int minor = -1;
-      std::string bdf;
-      if (s.enum_info) {
-        amdsmi_enumeration_info_t ei{};
-        if (s.enum_info(p, &ei) == AMDSMI_STATUS_SUCCESS) minor = (int)ei.drm_render;
+  for (size_t i = 0; i < t.gpus.size(); ++i) {
+    Gpu& g = t.gpus[i];
+    const SmiGpu* x = s->by_minor(g.render_minor);
+    if (!x) x = s->by_bdf(g.bdf);
+    sg[i] = x;
+    if (!x) continue;
+    any = true;
+    if (!x->uuid.empty()) g.uuid = x->uuid;
+    SmiHealth h;
+    if (s->health(*x, h)) {
+      g.ecc_correctable = h.ecc_correctable;
+      g.ecc_uncorrectable = h.ecc_uncorrectable;
+      g.ecc_deferred = h.ecc_deferred;
+      g.xgmi_links_total = h.links_total;
+      g.xgmi_links_up = h.links_up;
+      g.xgmi_links_down = h.links_down;
+    }
+  }
+  std::map<int, size_t> idx;
+  for (size_t i = 0; i < t.gpus.size(); ++i) idx[t.gpus[i].node_id] = i;
+  bool checked = false, agrees = true;
+  for (size_t i = 0; i < t.gpus.size(); ++i) {
+    if (!sg[i]) continue;
+    for (size_t j = 0; j < t.gpus.size(); ++j) {
+      if (j == i || !sg[j]) continue;
+      SmiLink L = s->link(*sg[i], *sg[j]);
+      if (!L.ok) continue;
+      SmiPeer p;
+      p.to_index = (int)j;
+      p.type = L.type;
+      p.hops = L.hops;
+      p.weight = L.weight;
+      p.p2p = L.p2p;
+      t.gpus[i].smi_links.push_back(p);
+      int kfd = 0;
+      for (auto& kl : t.gpus[i].links) {
+        auto it = idx.find(kl.to_node);
+        if (it != idx.end() && it->second == j) kfd = std::max(kfd, kl.type);
       }
-      if (s.bdf) {
-        amdsmi_bdf_t b{};
-        if (s.bdf(p, &b) == AMDSMI_STATUS_SUCCESS) {
-          char buf[32];
-          std::snprintf(buf, sizeof buf, "%04x:%02x:%02x.%x", (unsigned)b.domain_number, (unsigned)b.bus_number,
-                        (unsigned)b.device_number, (unsigned)b.function_number);
-          bdf = buf;
-        }
-      }
-      char uuid[AMDSMI_MAX_STRING_LENGTH] = {0};
-      unsigned len = sizeof uuid;
-      std::string u;
-      if (s.uuid && s.uuid(p, &len, uuid) == AMDSMI_STATUS_SUCCESS) u = uuid;
-      for (auto& g : t.gpus) {
-        if ((minor >= 0 && g.render_minor == minor) || (!bdf.empty() && g.bdf == bdf)) {
-          if (!u.empty()) g.uuid = u;
-          any = true;
-        }
+      checked = true;
+      if ((L.type == 11) != (kfd == 11)) {
+        agrees = false;
+        t.warnings.push_back("amd-smi and KFD disagree on GPU " + std::to_string(i) + " -> " + std::to_string(j) +
+                             ": amd-smi link type " + std::to_string(L.type) + ", KFD io_link type " +
+                             std::to_string(kfd));
       }
     }
   }
-  s.shut_down();
+  t.smi_topology_checked = checked;
+  t.smi_topology_agrees = checked && agrees;
   return any;
 }
-#else
-bool enrich_with_amdsmi(Topology&) { return false; }
-#endif
 
 }  // namespace
 
@@ -253,6 +224,61 @@ bool refresh_health(const std::string& root, Gpu& g) {
     g.health_reason = "ok";
   }
   return g.healthy;
+}
+
+bool amdsmi_allowed(const std::string& root, bool use_amdsmi) {
+  if (!use_amdsmi) return false;
+  if (root.empty() || root == "/") return true;
+  const char* stub = std::getenv("KGS_AMDSMI_LIB");
+  return stub && *stub;
+}
+
+HealthMonitor::HealthMonitor(const std::string& root, bool use_amdsmi, int64_t ecc_tolerance)
+    : root_(root.empty() ? "/" : root), tol_(ecc_tolerance < 0 ? 0 : ecc_tolerance) {
+  if (amdsmi_allowed(root_, use_amdsmi)) smi_ = SmiSession::open();
+}
+
+HealthState HealthMonitor::check(int node_id, int render_minor, const std::string& bdf) {
+  HealthState st;
+  Gpu g;
+  g.node_id = node_id;
+  g.render_minor = render_minor;
+  st.healthy = refresh_health(root_, g);
+  st.reason = g.health_reason;
+  if (!smi_) return st;
+  const SmiGpu* x = smi_->by_minor(render_minor);
+  if (!x) x = smi_->by_bdf(bdf);
+  if (!x || !smi_->health(*x, st.sample)) return st;
+  st.smi = true;
+  auto it = base_.find(render_minor);
+  if (it == base_.end()) {
+    Base b;
+    b.uncorr = st.sample.ecc_uncorrectable;
+    b.links = st.sample.link_state;
+    it = base_.emplace(render_minor, b).first;
+  }
+  Base& b = it->second;
+  const int64_t u = st.sample.ecc_uncorrectable;
+  if (st.sample.ecc_ok && b.uncorr >= 0 && u >= 0 && u < b.uncorr) b.uncorr = u;  // counters reset: re-baseline
+  if (b.uncorr < 0 && st.sample.ecc_ok) b.uncorr = u;
+  if (!st.healthy) return st;  // the sysfs verdict (device gone) stands
+  if (st.sample.ecc_ok && b.uncorr >= 0 && u - b.uncorr > tol_) {
+    st.healthy = false;
+    st.reason = "uncorrectable ECC errors rose from " + std::to_string(b.uncorr) + " to " + std::to_string(u);
+    return st;
+  }
+  if (st.sample.links_ok) {
+    for (size_t i = 0; i < b.links.size() && i < st.sample.link_state.size(); ++i) {
+      if (b.links[i] == 1 && st.sample.link_state[i] == 0) {
+        st.healthy = false;
+        st.reason = "xGMI link " + std::to_string(i) + " down (up at start)";
+        return st;
+      }
+    }
+  }
+  st.reason = "ok (amd-smi: ECC uncorrectable " + std::to_string(u) + ", xGMI links up " +
+              std::to_string(st.sample.links_up) + "/" + std::to_string(st.sample.links_total) + ")";
+  return st;
 }
 
 Topology discover(const std::string& root, bool use_amdsmi) {
@@ -344,7 +370,7 @@ Topology discover(const std::string& root, bool use_amdsmi) {
                   g.links.end());
     refresh_health(root, g);
   }
-  if (use_amdsmi && (root.empty() || root == "/")) t.amdsmi_used = enrich_with_amdsmi(t);
+  if (amdsmi_allowed(root, use_amdsmi)) t.amdsmi_used = enrich_with_amdsmi(t);
   if (!t.kfd_present) t.warnings.push_back("/dev/kfd not present: no usable AMD GPU (fake capacity path)");
   (void)render_nodes;
   return t;
@@ -369,7 +395,9 @@ std::string to_json(const Topology& t) {
   std::ostringstream o;
   o << "{\"root\":\"" << json_escape(t.root) << "\",\"kfd_present\":" << (t.kfd_present ? "true" : "false")
     << ",\"topology_present\":" << (t.topology_present ? "true" : "false")
-    << ",\"amdsmi_used\":" << (t.amdsmi_used ? "true" : "false") << ",\"cpu_nodes\":" << t.cpu_nodes
+    << ",\"amdsmi_used\":" << (t.amdsmi_used ? "true" : "false") << ",\"amdsmi_library\":\""
+    << json_escape(t.amdsmi_library) << "\",\"smi_topology_checked\":" << (t.smi_topology_checked ? "true" : "false")
+    << ",\"smi_topology_agrees\":" << (t.smi_topology_agrees ? "true" : "false") << ",\"cpu_nodes\":" << t.cpu_nodes
     << ",\"warnings\":[";
   for (size_t i = 0; i < t.warnings.size(); ++i) o << (i ? "," : "") << "\"" << json_escape(t.warnings[i]) << "\"";
   o << "],\"gpus\":[";
@@ -385,7 +413,16 @@ std::string to_json(const Topology& t) {
       << json_escape(g.uuid) << "\",\"properties_readable\":" << (g.properties_readable ? "true" : "false")
       << ",\"render_node_present\":" << (g.render_node_present ? "true" : "false")
       << ",\"healthy\":" << (g.healthy ? "true" : "false") << ",\"health_reason\":\""
-      << json_escape(g.health_reason) << "\",\"links\":[";
+      << json_escape(g.health_reason) << "\",\"ecc_correctable\":" << g.ecc_correctable
+      << ",\"ecc_uncorrectable\":" << g.ecc_uncorrectable << ",\"ecc_deferred\":" << g.ecc_deferred
+      << ",\"xgmi_links_total\":" << g.xgmi_links_total << ",\"xgmi_links_up\":" << g.xgmi_links_up
+      << ",\"xgmi_links_down\":" << g.xgmi_links_down << ",\"smi_links\":[";
+    for (size_t j = 0; j < g.smi_links.size(); ++j) {
+      const SmiPeer& p = g.smi_links[j];
+      o << (j ? "," : "") << "{\"to_index\":" << p.to_index << ",\"type\":" << p.type << ",\"hops\":" << p.hops
+        << ",\"weight\":" << p.weight << ",\"p2p\":" << p.p2p << "}";
+    }
+    o << "],\"links\":[";
     for (size_t j = 0; j < g.links.size(); ++j) {
       const Link& L = g.links[j];
       o << (j ? "," : "") << "{\"to_node\":" << L.to_node << ",\"type\":" << L.type << ",\"weight\":" << L.weight

@@ -4,8 +4,11 @@
 // which every ROCm host exposes without any library: one node per CPU socket and
 // per GPU (or GPU partition), with the DRM render minor, PCI location, XCC
 // count, HBM size, hive id and the io_links (type 11 = xGMI, 2 = PCIe) that
-// form the xGMI mesh. amd-smi (libamd_smi.so, dlopen'ed, optional) enriches
-// the records with the HIP UUID.
+// form the xGMI mesh. amd-smi (libamd_smi.so, dlopen'ed, optional; smi.h)
+// adds the HIP UUID, ECC/RAS error counts, xGMI link status and its own
+// GPU-to-GPU link matrix, which is cross-checked against the KFD io_links;
+// HealthMonitor turns the error counts and link status into the plugin's
+// Healthy/Unhealthy signal.
 //
 // Everything is parameterised by a filesystem `root` so tests run against a
 // fake tree (tests/fixtures/) and the plugin can read the host's /sys mounted
@@ -17,8 +20,12 @@
 #pragma once
 
 #include <cstdint>
+#include <map>
+#include <memory>
 #include <string>
 #include <vector>
+
+#include "smi.h"
 
 namespace kgs {
 namespace gpuinfo {
@@ -34,6 +41,14 @@ struct Link {
   int type = 0;         // KFD io_link type (11 = xGMI)
   int weight = 0;       // KFD link weight (lower = closer)
   uint64_t max_bandwidth_mbs = 0;
+};
+
+// amd-smi's view of the link from this GPU to GPU `to_index`.
+struct SmiPeer {
+  int to_index = -1;
+  int type = 0;  // KFD numbering: 11 xGMI, 2 PCIe, 0 other / unknown
+  uint64_t hops = 0, weight = 0;
+  int p2p = -1;  // 1 accessible, 0 not, -1 unknown
 };
 
 struct Gpu {
@@ -53,6 +68,10 @@ struct Gpu {
   uint64_t vram_bytes = 0;
   int numa_node = -1;
   std::string uuid;           // from amd-smi when available
+  // amd-smi health sample (-1 = not available)
+  int64_t ecc_correctable = -1, ecc_uncorrectable = -1, ecc_deferred = -1;
+  int xgmi_links_total = -1, xgmi_links_up = -1, xgmi_links_down = -1;
+  std::vector<SmiPeer> smi_links;  // amd-smi link type / hops / weight / P2P to the other GPUs
   bool properties_readable = false;
   bool render_node_present = false;
   bool healthy = false;
@@ -65,6 +84,10 @@ struct Topology {
   bool kfd_present = false;       // <root>/dev/kfd exists
   bool topology_present = false;  // KFD topology directory exists
   bool amdsmi_used = false;
+  std::string amdsmi_library;
+  // amd-smi's link matrix checked against the KFD io_links (xGMI both ways)
+  bool smi_topology_checked = false;
+  bool smi_topology_agrees = false;
   std::vector<Gpu> gpus;
   int cpu_nodes = 0;
   std::vector<std::string> warnings;
@@ -76,6 +99,42 @@ Topology discover(const std::string& root, bool use_amdsmi = true);
 // Re-evaluate one GPU's health against the filesystem (device nodes present,
 // KFD node still readable). Cheap; the plugin calls it on every health tick.
 bool refresh_health(const std::string& root, Gpu& g);
+
+// Stateful health for the device plugin's tick: the sysfs checks of
+// refresh_health plus, when amd-smi is available, two hardware signals against a
+// per-GPU baseline taken at the first check:
+//   * uncorrectable ECC errors rising by more than `ecc_tolerance` -> Unhealthy
+//     (a counter that drops -- GPU reset / driver reload -- re-baselines, so a
+//     recovered GPU turns Healthy again);
+//   * an xGMI link that was up at baseline reported down -> Unhealthy (Healthy
+//     again once it is back up).
+struct HealthState {
+  bool healthy = false;
+  std::string reason;
+  bool smi = false;  // amd-smi sampled this GPU
+  SmiHealth sample;
+};
+
+class HealthMonitor {
+ public:
+  HealthMonitor(const std::string& root, bool use_amdsmi, int64_t ecc_tolerance = 0);
+  HealthState check(int node_id, int render_minor, const std::string& bdf = "");
+  bool amdsmi_used() const { return smi_ != nullptr; }
+
+ private:
+  struct Base {
+    int64_t uncorr = -1;
+    std::vector<int> links;
+  };
+  std::string root_;
+  std::unique_ptr<SmiSession> smi_;
+  std::map<int, Base> base_;  // by render minor
+  int64_t tol_;
+};
+
+// amd-smi is consulted for the live system ("/") and, for tests, whenever
+// KGS_AMDSMI_LIB names a (stub) library.
+bool amdsmi_allowed(const std::string& root, bool use_amdsmi);
 
 // "gfx950" from 90500.
 std::string gfx_name(uint32_t target_version);

@@ -30,4 +30,29 @@ PYBIND11_MODULE(_gpuinfo, m) {
         return py::make_tuple(ok, g.health_reason);
       },
       py::arg("root"), py::arg("node_id"), py::arg("render_minor"));
+  py::class_<HealthMonitor>(m, "HealthMonitor")
+      .def(py::init<const std::string&, bool, int64_t>(), py::arg("root") = "/", py::arg("use_amdsmi") = true,
+           py::arg("ecc_tolerance") = 0)
+      .def_property_readonly("amdsmi_used", &HealthMonitor::amdsmi_used)
+      .def(
+          "check",
+          [](HealthMonitor& hm, int node_id, int render_minor, const std::string& bdf) {
+            HealthState st;
+            {
+              py::gil_scoped_release nogil;
+              st = hm.check(node_id, render_minor, bdf);
+            }
+            py::dict d;
+            d["healthy"] = st.healthy;
+            d["reason"] = st.reason;
+            d["amdsmi"] = st.smi;
+            d["ecc_correctable"] = st.sample.ecc_correctable;
+            d["ecc_uncorrectable"] = st.sample.ecc_uncorrectable;
+            d["ecc_deferred"] = st.sample.ecc_deferred;
+            d["xgmi_links_total"] = st.sample.links_total;
+            d["xgmi_links_up"] = st.sample.links_up;
+            d["xgmi_links_down"] = st.sample.links_down;
+            return d;
+          },
+          py::arg("node_id"), py::arg("render_minor"), py::arg("bdf") = "");
 }

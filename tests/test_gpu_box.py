@@ -40,6 +40,34 @@ def test_gpuinfo_live_box():
         assert ok, why
 
 
+def test_gpuinfo_amdsmi_health_and_topology_on_the_box():
+    """amd-smi is live on the box: it identifies the visible GPUs (UUID, BDF),
+    answers the ECC and xGMI-status queries the plugin's health tick uses, and
+    its GPU-to-GPU link view agrees with the KFD io_links."""
+    from kgs import gpuinfo
+
+    topo = gpuinfo.discover("/")
+    assert topo.amdsmi_used, topo.warnings
+    seen = [g for g in topo.gpus if g.render_minor >= 0 and g.uuid]
+    assert seen, "amd-smi matched none of the KFD GPUs"
+    for g in seen:
+        assert g.bdf and g.bdf != "0000:00:00.0"
+        assert g.ecc_uncorrectable >= 0 and g.ecc_correctable >= 0, g
+    assert not [w for w in topo.warnings if "disagree" in w], topo.warnings
+    if topo.smi_topology_checked:
+        assert topo.smi_topology_agrees
+    hm = gpuinfo.HealthMonitor("/")
+    assert hm.amdsmi_used
+    for g in seen:
+        st = hm.check(g.node_id, g.render_minor, g.bdf)
+        assert st["healthy"] and st["amdsmi"], st
+    print(json.dumps({"gpus": [{"minor": g.render_minor, "bdf": g.bdf, "uuid": g.uuid,
+                                "ecc": [g.ecc_correctable, g.ecc_uncorrectable, g.ecc_deferred],
+                                "xgmi_links": [g.xgmi_links_up, g.xgmi_links_total],
+                                "smi_links": g.smi_links, "kfd_links": [lk.type for lk in g.links]} for g in seen],
+                      "smi_topology_checked": topo.smi_topology_checked}))
+
+
 def test_device_plugin_self_test_allocates_real_paths():
     r = subprocess.run([sys.executable, "-m", "kgs.deviceplugin", "--self-test",
                         "--partition-file", "/nonexistent/gpus.json"],
