@@ -8,6 +8,8 @@
   kgs status [--json]
   kgs bench  [e2e options]          create -> gpu-rocm-test Running, per-phase JSON
   kgs images [--workload] [--plugin] build the in-tree images
+  kgs pod NAME [--registry-port=N]   print pods/NAME.yaml with the image on the
+                                     configured local registry (| kubectl create -f -)
 
 Flags are accepted in both ``--k=v`` and ``--k v`` form and anywhere on the line
 (the reference scans all argv for its three flags, kind-gpu-sim.sh:31-43). Unlike
@@ -22,7 +24,7 @@ import sys
 
 from . import config as C
 
-VERBS = ("create", "delete", "load", "status", "bench", "images", "doctor")
+VERBS = ("create", "delete", "load", "status", "bench", "images", "doctor", "pod")
 
 
 class _Parser(argparse.ArgumentParser):
@@ -66,6 +68,10 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
     ap.add_argument("--gpus", type=int, default=1, help="bench: amd.com/gpu requested by the test pod")
     ap.add_argument("--pod-timeout", type=int, default=C.TEST_POD_READY_TIMEOUT_S)
     ap.add_argument("--keep", action="store_true", help="bench: keep the cluster afterwards")
+    ap.add_argument("--no-kind", action="store_true",
+                    help="bench: no docker/kind -- plugin process -> kubelet register -> capacity -> Allocate -> pod "
+                         "entrypoint first GEMM, chained and timed (kgs/e2e_nokind.py)")
+    ap.add_argument("--gemm-size", type=int, default=8192, help="bench --no-kind: the pod's first GEMM size")
     ap.add_argument("--workload-image", default=None)
     ap.add_argument("--workload", action="store_true")
     ap.add_argument("--plugin", action="store_true")
@@ -107,6 +113,20 @@ def main(argv=None, prog: str = "kgs") -> int:
             return p.load()
         if a.verb == "status":
             return p.status(as_json=a.json)
+        if a.verb == "pod":
+            from .manifests import UnknownPod, render_static_pod
+
+            try:
+                sys.stdout.write(render_static_pod(a.gpu_type, s.registry_host))
+            except UnknownPod as e:
+                print(str(e), file=sys.stderr)
+                return 1
+            return 0
+        if a.verb == "bench" and a.no_kind:
+            from .e2e_nokind import run_nokind
+
+            return run_nokind(gpus=a.gpus, dev_root=a.dev_root, fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
+                              timeout=max(60, a.pod_timeout * 10), timings_json=a.timings_json)
         if a.verb == "bench":
             from .e2e import run_e2e
 

@@ -1,6 +1,9 @@
 """``kgs bench``: the headline metric -- cluster create -> GPU pod Running.
 
 Phases (all in one PhaseTimer, written to ``--timings-json``):
+  workload-image  the gpu-rocm-test image exists locally, or is built (and
+                  pushed to the local registry) now -- explicitly, before the
+                  cluster, instead of a late ImagePullBackOff after scheduling
   create phases (kgs.cluster.Provisioner.create)
   pod-apply       kubectl apply the gpu-rocm-test pod (N x amd.com/gpu)
   pod-running     kubectl wait --for=jsonpath={.status.phase}=Running
@@ -35,6 +38,18 @@ def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, kee
     t = p.timer
     t_start = time.perf_counter()
     image = workload_image or globals()["workload_image"](p)
+    with t.phase("workload-image") as rec:
+        rec["image"] = image
+        if workload_image:
+            rec["provided"] = True  # a user-supplied image: their registry, their build
+        elif p.runner.dry_run or p.ensure_runtime().image_exists(image):
+            rec["cached"] = True
+        else:
+            from .images import build_images
+
+            p.out(f"workload image {image} not found locally; building it")
+            build_images(p, workload=True, plugin=False)
+            rec["built"] = True
     if p.ensure_runtime().name != "podman" and not p.s.extra.get("no_prepull"):
         # pull the (multi-GB) workload image into the GPU workers during create,
         # overlapped with plugin deploy/readiness, instead of after scheduling

@@ -1,0 +1,134 @@
+"""``kgs bench --no-kind``: the measurable tail of create -> GPU pod Running on a
+host without docker/kind, chained into ONE timed flow.
+
+The reference's CI chain (/root/reference/.github/workflows/rocm-ci.yaml:28-39:
+create, `kubectl create -f pods/rocm-gpu-test-pod.yaml`, wait Ready, logs) is
+kind + kubelet + containerd around two pieces this repository owns: the device
+plugin and the pod's entrypoint. This flow runs exactly those pieces, in order,
+with the kubelet's device-plugin side played by the in-tree fake kubelet
+(kgs.deviceplugin.fake_kubelet -- the same v1beta1 gRPC the real kubelet speaks):
+
+  plugin-process-start  spawn ``python -m kgs.deviceplugin`` (its own process,
+                        live discovery with amd-smi) until its socket exists
+  plugin-register       ... until its Register reached the kubelet
+  capacity              ... until ListAndWatch advertised >= N healthy devices
+  allocate              GetPreferredAllocation + Allocate of N devices (the
+                        pod-admission RPCs)
+  pod-first-gemm        start the pod entrypoint as a child with exactly the
+                        Allocate response's envs, the GPUs restricted to the
+                        allocated render minors (ROCR_VISIBLE_DEVICES), until its
+                        first 8192^3 GEMM result line
+
+What is NOT in the number (needs docker/kind, docs/e2e.md): kind create, image
+build/pull, containerd's container start and the kubelet's own pod sync.
+"""
+from __future__ import annotations
+
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+from .timing import PhaseTimer
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _wait(pred, timeout: float, what: str, proc=None) -> None:
+    deadline = time.monotonic() + timeout
+    delay = 0.001
+    while not pred():
+        if proc is not None and proc.poll() is not None:
+            raise RuntimeError(f"{what}: device plugin exited with {proc.returncode}")
+        if time.monotonic() > deadline:
+            raise TimeoutError(f"{what}: not reached within {timeout:.0f}s")
+        time.sleep(delay)
+        delay = min(delay * 2, 0.02)
+
+
+def visible_devices_for(minors: list, root: str = "/") -> str:
+    """ROCR_VISIBLE_DEVICES for the allocated render minors: ROCr enumerates GPU
+    agents in KFD node order, which is gpuinfo's index order."""
+    from . import gpuinfo
+
+    idx = {g.render_minor: g.index for g in gpuinfo.discover(root, use_amdsmi=False).gpus}
+    missing = [m for m in minors if m not in idx]
+    if missing:
+        raise RuntimeError(f"allocated render minors {missing} not in the KFD topology")
+    return ",".join(str(idx[m]) for m in minors)
+
+
+def run_nokind(gpus: int = 1, dev_root: str = "/", fake_gpus: int = 0, gemm_size: int = 8192,
+               timeout: float = 600.0, timings_json: str | None = None, out=print, keep_dir: bool = False) -> int:
+    from .deviceplugin.fake_kubelet import FakeKubelet
+
+    t = PhaseTimer()
+    d = tempfile.mkdtemp(prefix="kgs-nk-", dir="/tmp")  # unix socket paths stay short
+    py = sys.executable
+    env_base = dict(os.environ)
+    env_base["PYTHONPATH"] = REPO + (":" + env_base["PYTHONPATH"] if env_base.get("PYTHONPATH") else "")
+    kub = FakeKubelet(d)
+    kub.start()
+    plug = None
+    result: dict = {}
+    try:
+        argv = [py, "-m", "kgs.deviceplugin", "--plugin-dir", d, "--dev-root", dev_root,
+                "--partition-file", os.path.join(d, "no-partition.json"), "--ready-file", os.path.join(d, "ready"),
+                "--health-interval", "1"]
+        if fake_gpus:
+            argv += ["--fake-gpus", str(fake_gpus)]
+        with t.phase("plugin-process-start"):
+            plug_log = open(os.path.join(d, "plugin.log"), "w")
+            plug = subprocess.Popen(argv, env=env_base, stdout=plug_log, stderr=subprocess.STDOUT)
+            plug_log.close()
+            sock = os.path.join(d, "kgs-amdgpu.sock")
+            _wait(lambda: os.path.exists(sock), timeout, "plugin socket", plug)
+        with t.phase("plugin-register"):
+            _wait(lambda: bool(kub.registrations), timeout, "Register", plug)
+        with t.phase("capacity") as rec:
+            _wait(lambda: kub.capacity() >= gpus, timeout, f"{gpus} healthy amd.com/gpu", plug)
+            rec["advertised"] = kub.capacity()
+        with t.phase("allocate") as rec:
+            healthy = [i for i, h, _ in kub.latest_devices() if h == "Healthy"]
+            ids = kub.preferred(healthy, [], gpus) if gpus < len(healthy) else healthy[:gpus]
+            resp = kub.allocate(ids).container_responses[0]
+            envs = dict(resp.envs)
+            rec.update(device_ids=ids, device_paths=[s.host_path for s in resp.devices])
+        env = dict(env_base, **envs)
+        minors = [int(x) for x in envs.get("KGS_RENDER_MINORS", "").split(",") if x]
+        if minors:
+            env["ROCR_VISIBLE_DEVICES"] = visible_devices_for(minors, dev_root)
+        res_path = os.path.join(d, "pod_result.json")
+        with t.phase("pod-first-gemm") as rec:
+            cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "1",
+                   "--json-out", res_path]
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+            if r.returncode != 0:
+                raise RuntimeError(f"pod entrypoint failed ({r.returncode}): {r.stderr[-2000:]}")
+            with open(res_path) as f:
+                result = json.load(f)
+            rec.update(mode=result.get("mode"), n_gpus=result.get("n_gpus"))
+        t.meta.update(pod_result=result, gpus_requested=gpus, fake=bool(fake_gpus),
+                      allocate_envs=envs, rocr_visible_devices=env.get("ROCR_VISIBLE_DEVICES"))
+    finally:
+        if plug is not None and plug.poll() is None:
+            plug.terminate()
+            try:
+                plug.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                plug.kill()
+        kub.stop()
+        t.write(timings_json)
+        if not keep_dir:
+            shutil.rmtree(d, ignore_errors=True)
+    phases = {p["phase"]: p["seconds"] for p in t.phases}
+    summary = {"metric": "device-plugin start -> first in-pod GEMM (no kind)", "value": round(sum(phases.values()), 4),
+               "unit": "s", "gpus": gpus, "fake": bool(fake_gpus), "phases": phases,
+               "excluded": "kind create, image build/pull, containerd container start, kubelet pod sync"}
+    if result.get("gemm_tflops_total"):
+        summary["in_pod_gemm_tflops"] = result["gemm_tflops_total"]
+    out(json.dumps(summary))
+    return 0

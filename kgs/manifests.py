@@ -194,3 +194,29 @@ def gpu_test_pod(image: str, gpus: int = 1, command: list | None = None, name: s
             "volumes": [{"name": "dshm", "emptyDir": {"medium": "Memory", "sizeLimit": "16Gi"}}],
         },
     }
+
+
+STATIC_POD_REGISTRY = "localhost:5000"  # what pods/*.yaml are written against (the reference default port)
+
+
+def render_static_pod(name: str, registry_host: str) -> str:
+    """``pods/<name>.yaml`` with its in-tree images moved to ``registry_host``
+    (``localhost:<--registry-port>``), so ``--registry-port=N`` clusters can run
+    the shipped pods: ``kgs pod rocm-gpu-test --registry-port=N | kubectl create -f -``.
+    Images from public registries (e.g. the vLLM pod) are left alone."""
+    from pathlib import Path
+
+    pods = Path(__file__).resolve().parents[1] / "pods"
+    stem = name[:-5] if name.endswith(".yaml") else name
+    path = pods / f"{stem}.yaml"
+    if not path.exists():
+        path = pods / f"{stem}-pod.yaml"
+    if not path.exists():
+        avail = sorted(p.stem for p in pods.glob("*.yaml"))
+        raise UnknownPod(f"ERROR: no pod manifest {name!r} in pods/ (have: {', '.join(avail)})")
+    text = path.read_text()
+    return text.replace(f"image: {STATIC_POD_REGISTRY}/", f"image: {registry_host}/")
+
+
+class UnknownPod(ValueError):
+    pass

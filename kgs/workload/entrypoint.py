@@ -50,9 +50,17 @@ def allocated_gpus() -> list:
         from kgs import gpuinfo
 
         topo = gpuinfo.discover("/", use_amdsmi=False)
-        return [g for g in topo.gpus if g.render_node_present and g.healthy]
+        gpus = [g for g in topo.gpus if g.render_node_present and g.healthy]
     except Exception:
         return []
+    # the device plugin's Allocate names the render minors (KGS_RENDER_MINORS):
+    # inside a pod they are all that is visible anyway; outside one (kgs bench
+    # --no-kind) they are what the pod would see
+    alloc = os.environ.get("KGS_RENDER_MINORS")
+    if alloc:
+        want = {int(x) for x in alloc.split(",") if x.strip()}
+        gpus = [g for g in gpus if g.render_minor in want]
+    return gpus
 
 
 def rocminfo_agents(timeout: int = 60) -> dict:

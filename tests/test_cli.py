@@ -323,6 +323,10 @@ def test_bench_e2e(world, tmp_path, capsys):
     assert summary["metric"] == "cluster-create->GPU-pod-Running" and summary["value"] > 0
     t = json.loads((tmp_path / "e2e.json").read_text())
     assert [p["phase"] for p in t["phases"]][-4:] == ["pod-apply", "pod-running", "pod-ready", "pod-logs"]
+    # a fresh host: the workload image is built (and pushed) first, as its own phase
+    assert t["phases"][0]["phase"] == "workload-image" and t["phases"][0].get("built")
+    builds = [a for a in world.calls("docker", "build") if "localhost:5000/kgs-rocm-test:dev" in a]
+    assert builds and any(a[:2] == ["push", "localhost:5000/kgs-rocm-test:dev"] for a in world.calls("docker"))
     assert t["pod_result"]["mode"] == "fake"
     pod = [o for o in world.log() if o["tool"] == "kubectl" and "apply" in o["argv"] and o["stdin"]
            and "kind: Pod" in o["stdin"]]
@@ -336,6 +340,47 @@ def test_bench_e2e(world, tmp_path, capsys):
              and "crictl" in e["argv"]]
     assert pulls and all(a[-1] == "localhost:5000/kgs-rocm-test:dev" for a in pulls)
     assert any(p["phase"] == "prepull-wait" for p in t["phases"])
+
+
+def test_bench_uses_cached_workload_image_and_registry_port(world, tmp_path, capsys):
+    """An image already present is not rebuilt; --registry-port flows into the
+    pod's image reference (VERDICT r1 weak #8, #9)."""
+    rc = run("bench", "--dev-root", world.nogpu, "--registry-port=5123", "--timings-json", str(tmp_path / "a.json"))
+    assert rc == 0
+    t = json.loads((tmp_path / "a.json").read_text())
+    assert t["phases"][0].get("built")
+    rc = run("bench", "--dev-root", world.nogpu, "--registry-port=5123", "--timings-json", str(tmp_path / "b.json"))
+    assert rc == 0
+    t = json.loads((tmp_path / "b.json").read_text())
+    assert t["phases"][0].get("cached") and not t["phases"][0].get("built")
+    pods = [yaml.safe_load(o["stdin"]) for o in world.log() if o["tool"] == "kubectl" and o["stdin"]
+            and "kind: Pod" in o["stdin"]]
+    assert pods and all(p["spec"]["containers"][0]["image"] == "localhost:5123/kgs-rocm-test:dev" for p in pods)
+
+
+def test_bench_no_kind_fake_chain(world, tmp_path, capsys):
+    """`kgs bench --no-kind`: the real plugin process, kubelet Register,
+    ListAndWatch capacity, Allocate and the pod entrypoint, chained and timed."""
+    rc = run("bench", "--no-kind", "--fake-gpus", "2", "--gpus", "2", "--timings-json", str(tmp_path / "nk.json"))
+    assert rc == 0
+    line = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith('{"metric"')][-1]
+    s = json.loads(line)
+    assert s["metric"].startswith("device-plugin start -> first in-pod GEMM") and s["value"] > 0
+    assert list(s["phases"]) == ["plugin-process-start", "plugin-register", "capacity", "allocate", "pod-first-gemm"]
+    t = json.loads((tmp_path / "nk.json").read_text())
+    assert t["pod_result"]["mode"] == "fake" and t["allocate_envs"]["KGS_FAKE_GPUS"].count(",") == 1
+    alloc = [p for p in t["phases"] if p["phase"] == "allocate"][0]
+    assert len(alloc["device_ids"]) == 2
+
+
+def test_pod_verb_renders_static_pods_on_the_configured_registry(world, capsys):
+    assert run("pod", "rocm-gpu-test", "--registry-port=5123") == 0
+    doc = yaml.safe_load(capsys.readouterr().out)
+    assert doc["metadata"]["name"] == "gpu-rocm-test"
+    assert doc["spec"]["containers"][0]["image"] == "localhost:5123/kgs-rocm-test:dev"
+    assert run("pod", "vllm-rocm-pod", "--registry-port=5123") == 0
+    assert "docker.io/rocm/vllm" in capsys.readouterr().out  # public images untouched
+    assert run("pod", "no-such-pod") == 1
 
 
 def test_shell_wrapper_is_executable():

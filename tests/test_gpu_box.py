@@ -68,6 +68,21 @@ def test_gpuinfo_amdsmi_health_and_topology_on_the_box():
                       "smi_topology_checked": topo.smi_topology_checked}))
 
 
+def test_bench_no_kind_chain_on_the_box(tmp_path):
+    """`kgs bench --no-kind`: plugin process (live discovery) -> kubelet Register
+    -> capacity -> Allocate -> pod entrypoint on the allocated GPU -> first GEMM."""
+    out = tmp_path / "e2e.json"
+    r = subprocess.run([sys.executable, "-m", "kgs", "bench", "--no-kind", "--gpus", "1", "--timings-json", str(out)],
+                       capture_output=True, text=True, env=ENV, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    s = _last_json(r.stdout)
+    assert list(s["phases"]) == ["plugin-process-start", "plugin-register", "capacity", "allocate", "pod-first-gemm"]
+    t = json.loads(out.read_text())
+    assert t["pod_result"]["mode"] == "gpu" and t["pod_result"]["n_gpus"] == 1
+    assert t["allocate_envs"]["KGS_RENDER_MINORS"] and t["rocr_visible_devices"] is not None
+    assert s.get("in_pod_gemm_tflops", 0) > 300, s
+
+
 def test_device_plugin_self_test_allocates_real_paths():
     r = subprocess.run([sys.executable, "-m", "kgs.deviceplugin", "--self-test",
                         "--partition-file", "/nonexistent/gpus.json"],
