@@ -40,6 +40,7 @@ _SIGS = {
     "kgs_gemm_bf16_nt_bounded_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_splitk": ([_c_void_p] * 4 + [_c_int] * 7 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_w4x": ([_c_void_p] * 4 + [_c_int] * 8 + [_c_void_p], _c_int),
     "kgs_gemm_fp8_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [ctypes.c_float, _c_int, _c_int,
                                                                                      _c_void_p], _c_int),
     "kgs_gemm_fp8_nt_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 7, _c_int),

@@ -163,6 +163,29 @@ SPLITK_TUNED: dict = {
 }
 SPLITK_WS_FLOATS = 8 * 256 * 8192  # the largest entry above (M x N x slices)
 
+# Decode batches 128-512 on the four-wave kernel (kgs.ops.gemm.gemm_nt_w4x):
+# (tile width, K slices) per (batch bucket, N, K) where it beat hipBLASLt and
+# the 8-wave split-K, weights streamed from HBM (bench/decode_w4x_sweep.py,
+# profiles/r2/decode_w4x_sweep.jsonl; speed-up vs hipBLASLt in the comments).
+# Buckets not listed stay on the routes below.
+_W4X_BUCKETS = (128, 192, 256, 384, 512)
+W4X_TUNED: dict = {
+    (128, *_QKV): (128, 4), (192, *_QKV): (128, 4), (256, *_QKV): (128, 4), (384, *_QKV): (128, 2),  # 1.27/1.39/1.49/1.06
+    (128, *_O): (128, 8), (192, *_O): (128, 8), (256, *_O): (128, 8), (384, *_O): (128, 4),  # 1.37/1.62/1.05/1.02
+    (512, *_O): (128, 4),  # 1.10
+    (192, *_GU): (128, 1), (256, *_GU): (128, 1), (512, *_GU): (256, 1),  # 1.07/1.06/1.06
+    (128, *_DOWN): (128, 8), (192, *_DOWN): (128, 8), (256, *_DOWN): (128, 8), (384, *_DOWN): (128, 4),  # 2.2/2.7/1.5/1.4
+    (512, *_DOWN): (128, 4),  # 1.45
+}
+
+
+def w4x_route(m: int, n: int, k: int):
+    """(tile width, K slices) of the four-wave decode GEMM for batch m, or None."""
+    if m < 96 or m > 512:
+        return None
+    b = next(x for x in _W4X_BUCKETS if m <= x)
+    return W4X_TUNED.get((b, n, k))
+
 
 def splitk_slices(m: int, n: int, k: int) -> int | None:
     """K slices for a decode GEMM of batch m (bucketed to a power of two), or

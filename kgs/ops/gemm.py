@@ -134,6 +134,38 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
     return out
 
 
+def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1,
+                out: torch.Tensor | None = None) -> torch.Tensor:
+    """``a @ b.T`` on the four-wave kernel with a tile width of ``bn`` (256 or
+    128) columns, any M (rows past M read as zeros), over ``nslice`` K-slices
+    (fp32 partials + reduce when > 1): the decode-batch GEMM path.
+    ``N % bn == 0`` and ``(K / nslice) % 128 == 0``."""
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    ws_ptr = None
+    if nslice > 1:
+        from .decode import device_key
+
+        need = nslice * M * N
+        ws = _SPLITK_WS.get(device_key(a.device))
+        if ws is None or ws.numel() < need:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("gemm_nt_w4x: reserve_splitk_workspace() before hipGraph capture")
+            ws = reserve_splitk_workspace(a.device, need)
+        ws_ptr = ws.data_ptr()
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws_ptr, M, N, K, a.stride(0),
+                                         b.stride(0), out.stride(0), int(bn), int(nslice),
+                                         _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} bn{bn}/{nslice}]")
+    return out
+
+
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
 FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}

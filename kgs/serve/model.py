@@ -111,6 +111,12 @@ class ServingModel:
         if self.backend == "ref":
             return (x.float() @ w.float().T).to(torch.bfloat16)
         m = x.shape[0]
+        if decode and layer is not None:
+            route = D.w4x_route(m, w.shape[0], w.shape[1])
+            if route is not None:
+                from kgs.ops.gemm import gemm_nt_w4x
+
+                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1])
         if decode:
             ns = D.splitk_slices(m, w.shape[0], w.shape[1])
             if ns == 1:

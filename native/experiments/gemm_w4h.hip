@@ -19,7 +19,7 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
   auto c = (unsigned short*)C;
 #define KGS_W4H(ID, B1, R, P, ORD, X)                                                                         \
   case ID:                                                                                                    \
-    hipLaunchKernelGGL((kgs::w4::gemm_nt_w4<kgs::EPI_NONE, B1, R, P, ORD, X>), grid, dim3(256), 0, s, a, b, c, \
+    hipLaunchKernelGGL((kgs::w4::gemm_nt_w4<kgs::EPI_NONE, 256, 0, B1, R, P, ORD, X>), grid, dim3(256), 0, s, a, b, c, \
                        nullptr, M, N, K, lda, ldb, ldc);                                                      \
     break;
   // ids: kgs/ops/experiments.py W4H (name = w4h_ORD_B1_R_P_X)

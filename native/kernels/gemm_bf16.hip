@@ -440,6 +440,56 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ P
 }
 }  // namespace kgs
 
+// Four-wave kernel for short-M (decode-batch) GEMMs: tile width bn (256 or 128),
+// any M (rows past M read as zeros, stores predicated), and nslice K-slices
+// (nslice > 1: fp32 partial tiles into ws, then splitk_reduce). Requirements:
+// N % bn == 0, (K / nslice) % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
+                                    int ldb, int ldc, int bn, int nslice, hipStream_t stream) {
+  using namespace kgs;
+  if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
+  if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (bn != 128 && bn != 256) return KGS_ERR_ARG;
+  const int ks = K / nslice;
+  if (N % bn || ks % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  if ((long)lda * 512 >= (1L << 31) || (long)ldb * 512 >= (1L << 31)) return KGS_ERR_SHAPE;
+  if (nslice > 1 && (ws == nullptr || (uintptr_t)ws % 16)) return KGS_ERR_ARG;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  const int ntm = (M + 255) / 256;
+  const dim3 grid(ntm * (N / bn) * nslice);
+  const bool aligned_m = M % 256 == 0;
+#define KGS_W4X(BN, MODE, OUT, LDC)                                                                                \
+  hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, MODE>), grid, dim3(256), 0, stream, a, b, OUT, nullptr, M, N, ks, \
+                     lda, ldb, LDC)
+  unsigned short* out = nslice > 1 ? (unsigned short*)ws : c;
+  const int ld = nslice > 1 ? N : ldc;
+  const int mode = (aligned_m ? 0 : 1) | (nslice > 1 ? 2 : 0);
+  if (bn == 256) {
+    switch (mode) {
+      case 0: KGS_W4X(256, 0, out, ld); break;
+      case 1: KGS_W4X(256, 1, out, ld); break;
+      case 2: KGS_W4X(256, 2, out, ld); break;
+      default: KGS_W4X(256, 3, out, ld); break;
+    }
+  } else {
+    switch (mode) {
+      case 0: KGS_W4X(128, 0, out, ld); break;
+      case 1: KGS_W4X(128, 1, out, ld); break;
+      case 2: KGS_W4X(128, 2, out, ld); break;
+      default: KGS_W4X(128, 3, out, ld); break;
+    }
+  }
+#undef KGS_W4X
+  if (nslice > 1) {
+    const long groups = ((long)M * N / 8 + 255) / 256;
+    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)groups), dim3(256), 0, stream, ws, c, M, N, ldc, nslice);
+  }
+  return (int)hipGetLastError();
+}
+
 // C[M, N] (bf16) = A[M, K] . B[N, K]^T over nslice K-slices; ws holds nslice *
 // M * N floats. K / nslice must be a multiple of 128 (aligned M % 256 == 0,
 // N % 256 == 0) or of 8 (any M, N % 8 == 0: the bounded pipeline).

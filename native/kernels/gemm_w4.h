@@ -37,14 +37,39 @@
 
 #include "kgs_common.h"
 
+
+// Generalisations (round 2, for the serving decode GEMMs):
+//   BN   256 (production square tile) or 128 (256x128: twice the tiles for the
+//        short-M / narrow-N decode projections); a wave owns 128 x BN/2.
+//   MODE bit 0  bounded M: A rows past M read as zeros (buffer resource ends at
+//               the last valid row), stores predicated -- any M, e.g. a decode
+//               batch of 200.
+//   MODE bit 1  split-K: gridDim.x = tiles x slices; slice s computes K columns
+//               [s K, (s + 1) K) and stores an fp32 partial tile to
+//               ((float*)C)[s][M][N] for kgs::splitk_reduce.
+
 namespace kgs {
 namespace w4 {
 
-constexpr int BM = 256, BN = 256, BK = 64;
-constexpr int OPB = 256 * BK * 2;    // one operand of one stage: 32 KiB
-constexpr int STAGE = 2 * OPB;       // A + B: 64 KiB
-constexpr int LDS_BYTES = 2 * STAGE;  // 128 KiB
-constexpr int GM = 4;                // tile-group height (production choice)
+constexpr int BM = 256, BK = 64;
+constexpr int GM = 4;  // tile-group height (production choice)
+
+template <int BN>
+struct Shape {
+  static_assert(BN == 256 || BN == 128, "BN must be 256 or 128");
+  static constexpr int NB = BN / 32;         // B fragments per wave per k-sub (8 or 4)
+  static constexpr int OPA = BM * BK * 2;    // A operand of one stage: 32 KiB
+  static constexpr int OPB = BN * BK * 2;    // B operand of one stage: 32 or 16 KiB
+  static constexpr int STAGE = OPA + OPB;
+  static constexpr int LDS_BYTES = 2 * STAGE;
+  static constexpr int HM = 8 * NB;          // MFMAs per k-sub
+  static constexpr int KM = 2 * HM;          // MFMAs per K-step
+  static constexpr int NR = 8 + NB;          // fragment reads per k-sub
+};
+
+// DMA instructions per wave per stage: A 256 rows / (8 rows x 4 waves) = 8, B BN / 32
+template <int BN>
+constexpr int dma_per_stage() { return 8 + BN / 32; }
 
 struct Ctx {
   char* smem;
@@ -56,9 +81,10 @@ struct Ctx {
   int nt;
 };
 
+template <int NB>
 struct Frag {
   bf16x8 a[8];
-  bf16x8 b[8];
+  bf16x8 b[NB];
 };
 
 __device__ __forceinline__ void bar() {
@@ -67,105 +93,129 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// DMA instruction j (0..7) of operand OP for K-tile starting at k0 into stage st:
-// rows j*32 + w*8 + lane/8 of the tile, 1 KiB = 8 rows of 128 B.
+// DMA instruction j of operand OP (0 = A: j < 8, 1 = B: j < BN/32) for the K-tile
+// starting at k0 into stage st: rows j*32 + w*8 + lane/8, 1 KiB = 8 rows of 128 B.
 // AUX: cache-policy bits of the load (0 = default; 16 = sc1)
-template <int OP, int AUX = 0>
+template <int BN, int OP, int AUX = 0>
 __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
-  char* dst = c.smem + st * STAGE + OP * OPB + (j * 4 + c.w) * 1024;
+  using S = Shape<BN>;
+  char* dst = c.smem + st * S::STAGE + OP * S::OPA + (j * 4 + c.w) * 1024;
   const int so = j * (OP ? c.sb32 : c.sa32) + k0 * 2;
   __builtin_amdgcn_raw_ptr_buffer_load_lds(OP ? c.rb : c.ra, (KGS_LDS void*)dst, 16, OP ? c.vob : c.voa, so, 0, AUX);
 }
 
+template <int BN, int AUX>
+__device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
+  if (j < 8) dma<BN, 0, AUX>(c, st, j, k0); else dma<BN, 1, AUX>(c, st, j - 8, k0);
+}
+
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *(const bf16x8*)p; }
 
-template <int SUB>
+template <int BN, int SUB>
 __device__ __forceinline__ const char* abase(const Ctx& c, int st) {
-  return c.smem + st * STAGE + c.wr * 128 * 128 + (SUB ? c.ro1 : c.ro0);
+  return c.smem + st * Shape<BN>::STAGE + c.wr * 128 * 128 + (SUB ? c.ro1 : c.ro0);
 }
-template <int SUB>
+template <int BN, int SUB>
 __device__ __forceinline__ const char* bbase(const Ctx& c, int st) {
-  return c.smem + st * STAGE + OPB + c.wc * 128 * 128 + (SUB ? c.ro1 : c.ro0);
+  return c.smem + st * Shape<BN>::STAGE + Shape<BN>::OPA + c.wc * (BN / 2) * 128 + (SUB ? c.ro1 : c.ro0);
 }
 
 // One MFMA on an accumulator pinned to AGPRs: the tied "+a" operand keeps each
-// of the 64 accumulators in one place across the K-loop (the builtin form lets
-// the register allocator rename accumulators and then repair the loop with
+// accumulator in one place across the K-loop (the builtin form lets the
+// register allocator rename accumulators and then repair the loop with
 // hundreds of v_accvgpr moves per K-step). Operands swapped (B first) so a lane
 // holds C[m = lane&15][n = 4*(lane>>4)+e]. asm MFMAs are invisible to the
 // hazard recognizer: the only hazard left (AGPR results read by VALU) is padded
 // before the epilogue.
-__device__ __forceinline__ void mma(f32x4 (&acc)[8][8], const Frag& f, int i, int n) {
+template <int NB>
+__device__ __forceinline__ void mma(f32x4 (&acc)[8][NB], const Frag<NB>& f, int i, int n) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][n]) : "v"(f.b[n]), "v"(f.a[i]));
 }
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 
-// One K-step as a single pinned sequence of 128 MFMAs (k < 64 on f0 = k-sub 0,
-// k >= 64 on f1 = k-sub 1) with its other instructions placed after MFMA k:
-//   k in [0, 16)          ds_read f1 fragment k (B frags first: MFMA k-sub order is i-major)
-//   k == B1 - 1           lgkmcnt(0) + barrier 1 (stage ST free)
-//   k in [B1, 128 - R)    the 16 LDS-DMA issues of K-tile t+2, evenly spread
-//   k == 128 - R - 1      vmcnt(16) + barrier 2 (K-tile t+1 visible)
-//   k in [128 - R, ...)   P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
-// MFMA order inside a k-sub. ORD 0: i-major (a[i] over all n), reads b0..b7 then
-// a0..a7. ORD 1: "growing square": reads alternate b0 a0 b1 a1 ..., and MFMA
-// (i, n) runs as soon as both of its fragments have been read, so the first
-// MFMA of a k-sub needs 2 reads instead of 9.
+// MFMA order inside a k-sub. ORD 0: i-major (a[i] over all n), reads b0..b(NB-1)
+// then a0..a7. ORD 1: "growing square": reads alternate b0 a0 b1 a1 ... (the
+// remaining a's after the last b), and each MFMA (i, n) runs right after the
+// read that completes its pair, so the first MFMA of a k-sub waits for 2 reads.
 struct MOrder {
   unsigned char i[64], n[64];
 };
-constexpr MOrder make_order(int ord) {
+
+// read r of a k-sub: which fragment (0 = b, 1 = a) and its index
+constexpr int rd_isa(int ord, int nb, int r) {
+  return ord == 0 ? (r >= nb) : (r < 2 * nb ? (r & 1) : 1);
+}
+constexpr int rd_idx(int ord, int nb, int r) {
+  return ord == 0 ? (r < nb ? r : r - nb) : (r < 2 * nb ? (r >> 1) : r - nb);
+}
+
+constexpr MOrder make_order(int ord, int nb) {
   MOrder o{};
   int k = 0;
   if (ord == 0) {
     for (int i = 0; i < 8; ++i)
-      for (int n = 0; n < 8; ++n) { o.i[k] = i; o.n[k] = n; ++k; }
-  } else {
-    for (int m = 0; m < 8; ++m) {
-      for (int j = 0; j < m; ++j) { o.i[k] = j; o.n[k] = m; ++k; }  // after b[m]
-      for (int j = 0; j <= m; ++j) { o.i[k] = m; o.n[k] = j; ++k; }  // after a[m]
+      for (int n = 0; n < nb; ++n) { o.i[k] = i; o.n[k] = n; ++k; }
+    return o;
+  }
+  bool ha[8] = {}, hb[8] = {};
+  for (int r = 0; r < 8 + nb; ++r) {
+    const int x = rd_idx(ord, nb, r);
+    if (rd_isa(ord, nb, r)) {
+      ha[x] = true;
+      for (int n = 0; n < nb; ++n)
+        if (hb[n]) { o.i[k] = x; o.n[k] = n; ++k; }
+    } else {
+      hb[x] = true;
+      for (int i = 0; i < 8; ++i)
+        if (ha[i]) { o.i[k] = i; o.n[k] = x; ++k; }
     }
   }
   return o;
 }
-constexpr MOrder ORDERS[2] = {make_order(0), make_order(1)};
 
-// read r of a k-sub: which fragment (0 = b, 1 = a) and its index
-constexpr int rd_isa(int ord, int r) { return ord == 0 ? (r >= 8) : (r & 1); }
-constexpr int rd_idx(int ord, int r) { return ord == 0 ? (r & 7) : (r >> 1); }
+template <int ORD, int NB>
+struct Order {
+  static constexpr MOrder o = make_order(ORD, NB);
+};
 
 struct StepPtrs {
   const char *pa1, *pb1, *pa0, *pb0;
   int k0;
 };
 
-// MFMA k of the K-step and what follows it, all decided at compile time.
-template <int ST, int B1, int R, int P, int ORD, int X, int K>
-__device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag& f0, Frag& f1, f32x4 (&acc)[8][8]) {
-  if constexpr (K < 128) {
-    constexpr int mi = ORDERS[ORD].i[K & 63], mn = ORDERS[ORD].n[K & 63];
-    if constexpr (K < 64) mma(acc, f0, mi, mn); else mma(acc, f1, mi, mn);
-    if constexpr (K < 16) {
-      constexpr int x = rd_idx(ORD, K);
-      if constexpr (rd_isa(ORD, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
+// MFMA k of the K-step and what follows it, all decided at compile time:
+//   k < NR              ds_read f1 (k-sub 1 of this K-tile) read k
+//   k == B1 - 1         lgkmcnt(0) + barrier 1 (stage ST free)
+//   k in [B1, KM - R)   the ND LDS-DMA issues of K-tile t+2, evenly spread
+//   k == KM - R - 1     vmcnt(ND) + barrier 2 (K-tile t+1 visible)
+//   k >= KM - R         P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
+template <int BN, int ST, int B1, int R, int P, int ORD, int X, int K>
+__device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BN / 32>& f0, Frag<BN / 32>& f1,
+                                      f32x4 (&acc)[8][BN / 32]) {
+  using S = Shape<BN>;
+  constexpr int NB = S::NB, KM = S::KM, HM = S::HM, NR = S::NR, ND = dma_per_stage<BN>();
+  if constexpr (K < KM) {
+    constexpr int mi = Order<ORD, NB>::o.i[K % HM], mn = Order<ORD, NB>::o.n[K % HM];
+    if constexpr (K < HM) mma<NB>(acc, f0, mi, mn); else mma<NB>(acc, f1, mi, mn);
+    if constexpr (K < NR) {
+      constexpr int x = rd_idx(ORD, NB, K);
+      if constexpr (rd_isa(ORD, NB, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
     }
-    if constexpr (K >= B1 && K < 128 - R) {
+    if constexpr (K >= B1 && K < KM - R) {
       // MFMAs that carry the DMA issues: the whole window, or the first W (X / 10000) of it
-      constexpr int ND = (X / 10000) ? X / 10000 : 128 - R - B1;
+      constexpr int NW = (X / 10000) ? X / 10000 : KM - R - B1;
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        if (B1 + (j * ND) / 16 == K) {
-          if (j < 8) dma<0, (X / 100) % 100>(c, ST, j, sp.k0); else dma<1, (X / 100) % 100>(c, ST, j - 8, sp.k0);
-        }
+      for (int j = 0; j < ND; ++j) {
+        if (B1 + (j * NW) / ND == K) dma_any<BN, (X / 100) % 100>(c, ST, j, sp.k0);
       }
     }
-    if constexpr (K >= 128 - R) {
-      constexpr int q = K - (128 - R);
+    if constexpr (K >= KM - R) {
+      constexpr int q = K - (KM - R);
 #pragma unroll
-      for (int e = q * P; e < (q + 1) * P && e < 16; ++e) {
-        const int x = rd_idx(ORD, e);
-        if (rd_isa(ORD, e)) f0.a[x] = frag(sp.pa0 + x * 2048); else f0.b[x] = frag(sp.pb0 + x * 2048);
+      for (int e = q * P; e < (q + 1) * P && e < NR; ++e) {
+        const int x = rd_idx(ORD, NB, e);
+        if (rd_isa(ORD, NB, e)) f0.a[x] = frag(sp.pa0 + x * 2048); else f0.b[x] = frag(sp.pb0 + x * 2048);
       }
     }
     fence();
@@ -173,48 +223,65 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag& f0
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage ST retired
       bar();
     }
-    if constexpr (K == 128 - R - 1) {
-      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // own DMA of K-tile t+1 landed
+    if constexpr (K == KM - R - 1) {
+      // own DMA of K-tile t+1 landed (the ND issued after it belong to t+2)
+      if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
       bar();
     }
-    kbody<ST, B1, R, P, ORD, X, K + 1>(c, sp, f0, f1, acc);
+    kbody<BN, ST, B1, R, P, ORD, X, K + 1>(c, sp, f0, f1, acc);
   }
 }
 
-// One K-step as a single pinned sequence of 128 MFMAs (k < 64 on f0 = k-sub 0,
-// k >= 64 on f1 = k-sub 1) with its other instructions placed after MFMA k:
-//   k in [0, 16)          ds_read f1 fragment k (B frags first: MFMA k-sub order is i-major)
-//   k == B1 - 1           lgkmcnt(0) + barrier 1 (stage ST free)
-//   k in [B1, 128 - R)    the 16 LDS-DMA issues of K-tile t+2, evenly spread
-//   k == 128 - R - 1      vmcnt(16) + barrier 2 (K-tile t+1 visible)
-//   k in [128 - R, ...)   P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
-template <int ST, int B1, int R, int P, int ORD, int X>
-__device__ __forceinline__ void kstep(const Ctx& c, Frag& f0, Frag& f1, f32x4 (&acc)[8][8], int t) {
-  static_assert(B1 >= 16 && B1 + 16 <= 128 - R && 16 <= R * P, "bad K-step schedule");
+// One K-step: a single pinned sequence of KM MFMAs (the first half on f0 = k-sub 0,
+// the second on f1 = k-sub 1) with the reads, DMA issues and the two barriers
+// placed between them (kbody).
+template <int BN, int ST, int B1, int R, int P, int ORD, int X>
+__device__ __forceinline__ void kstep(const Ctx& c, Frag<BN / 32>& f0, Frag<BN / 32>& f1, f32x4 (&acc)[8][BN / 32],
+                                      int t) {
+  using S = Shape<BN>;
+  static_assert(B1 >= S::NR && B1 + dma_per_stage<BN>() <= S::KM - R && S::NR <= R * P, "bad K-step schedule");
   StepPtrs sp;
-  sp.pa1 = abase<1>(c, ST);
-  sp.pb1 = bbase<1>(c, ST);
-  sp.pa0 = abase<0>(c, ST ^ 1);
-  sp.pb0 = bbase<0>(c, ST ^ 1);
+  sp.pa1 = abase<BN, 1>(c, ST);
+  sp.pb1 = bbase<BN, 1>(c, ST);
+  sp.pa0 = abase<BN, 0>(c, ST ^ 1);
+  sp.pb0 = bbase<BN, 0>(c, ST ^ 1);
   int tl = t + 2;
   tl = tl < c.nt ? tl : c.nt - 1;  // past the end: harmless re-load into the free stage
   sp.k0 = tl * BK;
-  kbody<ST, B1, R, P, ORD, X, 0>(c, sp, f0, f1, acc);
+  kbody<BN, ST, B1, R, P, ORD, X, 0>(c, sp, f0, f1, acc);
 }
 
-// Production knobs: barrier 1 after MFMA 24, 20 MFMAs after barrier 2, one
-// read per MFMA there, growing-square order, GROUP_M 4, default cache policy.
-constexpr int PB1 = 24, PR = 20, PP = 1, PORD = 1, PX = 0;
+// Production knobs per tile width: barrier 1 after MFMA B1, R MFMAs after
+// barrier 2, P reads per MFMA there, growing-square order, GROUP_M 4.
+template <int BN>
+struct Knobs;
+template <>
+struct Knobs<256> {
+  static constexpr int B1 = 24, R = 20, P = 1, ORD = 1, X = 0;
+};
+template <>
+struct Knobs<128> {
+  static constexpr int B1 = 18, R = 16, P = 1, ORD = 1, X = 0;
+};
 
-template <int EPI, int B1 = PB1, int R = PR, int P = PP, int ORD = PORD, int X = PX>
+template <int EPI, int BN = 256, int MODE = 0, int B1 = Knobs<BN>::B1, int R = Knobs<BN>::R, int P = Knobs<BN>::P,
+          int ORD = Knobs<BN>::ORD, int X = Knobs<BN>::X>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  using S = Shape<BN>;
+  constexpr int NB = S::NB, ND = dma_per_stage<BN>(), AUX = (X / 100) % 100;
+  constexpr bool BNDM = (MODE & 1) != 0, SPLITK = (MODE & 2) != 0;
+  __shared__ __attribute__((aligned(1024))) char smem[S::LDS_BYTES];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntm = M / BM, ntn = N / BN, nwg = ntm * ntn;
-  const int wg = xcd_remap(blockIdx.x, nwg);
+  const int ntm = BNDM ? (M + BM - 1) / BM : M / BM, ntn = N / BN, nwg = ntm * ntn;
+  // split-K: remap over the whole grid, so the blocks of one XCD share a slice
+  const int nslice = SPLITK ? gridDim.x / nwg : 1;
+  const int wga = SPLITK ? xcd_remap(blockIdx.x, nwg * nslice) : xcd_remap(blockIdx.x, nwg);
+  const int slice = SPLITK ? wga / nwg : 0;
+  const int wg = SPLITK ? wga - slice * nwg : wga;
   constexpr int G = (X % 100) ? X % 100 : GM;
   const int per_group = G * ntn;
   const int group = wg / per_group;
@@ -222,6 +289,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int gsz = min(ntm - first_m, G);
   const int tm = first_m + (wg % per_group) % gsz;
   const int tn = (wg % per_group) / gsz;
+  const int rows_a = BNDM ? min(M - tm * BM, BM) : BM;
 
   Ctx c;
   c.smem = smem;
@@ -229,8 +297,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   c.wr = w >> 1;
   c.wc = w & 1;
   c.nt = K / BK;
-  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda), 0, BM * lda * 2, 0x00020000);
-  c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb), 0, BN * ldb * 2, 0x00020000);
+  const long koff = SPLITK ? (long)slice * K : 0;  // split-K: K is the slice length
+  c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda + koff), 0, rows_a * lda * 2, 0x00020000);
+  c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb + koff), 0, BN * ldb * 2, 0x00020000);
   c.sa32 = 32 * lda * 2;
   c.sb32 = 32 * ldb * 2;
   {
@@ -243,32 +312,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
   }
 
-  f32x4 acc[8][8];
+  f32x4 acc[8][NB];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int n = 0; n < 8; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int n = 0; n < NB; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: K-tiles 0 and 1 into stages 0 and 1, k-sub 0 of K-tile 0 into f0
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dma<0, (X / 100) % 100>(c, 0, j, 0);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dma<1, (X / 100) % 100>(c, 0, j, 0);
+  for (int j = 0; j < ND; ++j) dma_any<BN, AUX>(c, 0, j, 0);
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) dma<0, (X / 100) % 100>(c, 1, j, k1);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dma<1, (X / 100) % 100>(c, 1, j, k1);
-  asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  for (int j = 0; j < ND; ++j) dma_any<BN, AUX>(c, 1, j, k1);
+  if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   bar();
-  Frag f0, f1;
+  Frag<NB> f0, f1;
   {
-    const char* pa = abase<0>(c, 0);
-    const char* pb = bbase<0>(c, 0);
+    const char* pa = abase<BN, 0>(c, 0);
+    const char* pb = bbase<BN, 0>(c, 0);
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {  // same order as the loop's reads
-      const int x = rd_idx(ORD, e);
-      if (rd_isa(ORD, e)) f0.a[x] = frag(pa + x * 2048); else f0.b[x] = frag(pb + x * 2048);
+    for (int e = 0; e < S::NR; ++e) {  // same order as the loop's reads
+      const int x = rd_idx(ORD, NB, e);
+      if (rd_isa(ORD, NB, e)) f0.a[x] = frag(pa + x * 2048); else f0.b[x] = frag(pb + x * 2048);
     }
   }
   // nothing outstanding on lgkm at loop entry: otherwise the waitcnt pass merges
@@ -276,22 +342,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __builtin_amdgcn_s_waitcnt(0xc07f);
 
   for (int t = 0; t < c.nt; t += 2) {
-    kstep<0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
-    kstep<1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
+    kstep<BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
+    kstep<BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read hazard
 
+  const int fr = lane & 15, fq = lane >> 4;
+  if constexpr (SPLITK) {
+    // fp32 partial tile, row-major [M][N]: one 16-B store per lane per fragment
+    float* part = (float*)C + (long)slice * M * N;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+      if (BNDM && row >= M) continue;
+#pragma unroll
+      for (int n = 0; n < NB; ++n)
+        *(f32x4*)(part + (long)row * N + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4) = acc[i][n];
+    }
+    return;
+  }
   // epilogue: bias + activation, then pair n-tiles (n, n+1) with
   // v_permlane16_swap -> one 16-B store per lane (guide T21)
-  const int fr = lane & 15, fq = lane >> 4;
-  float bv[8][4];
+  float bv[NB][4];
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
+  for (int n = 0; n < NB; ++n) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[n][e] = 0.f;
     if constexpr (EPI != EPI_NONE) {
-      const bf16x4 bb = *(const bf16x4*)(bias + tn * BN + c.wc * 128 + n * 16 + fq * 4);
+      const bf16x4 bb = *(const bf16x4*)(bias + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[n][e] = bf2f((unsigned short)bb[e]);
     }
@@ -300,8 +379,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int i = 0; i < 8; ++i) {
     const int row = tm * BM + c.wr * 128 + i * 16 + fr;
     unsigned short* crow = C + (long)row * ldc;
+    const bool row_ok = !BNDM || row < M;
 #pragma unroll
-    for (int n = 0; n < 8; n += 2) {
+    for (int n = 0; n < NB; n += 2) {
       uint2 o[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
@@ -312,8 +392,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
       auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
       const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-      const int col0 = tn * BN + c.wc * 128 + n * 16;
-      *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
+      const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
+      if (row_ok) *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
     }
   }
 }
