@@ -19,11 +19,40 @@ def _port():
     return p
 
 
+class _T:
+    """A tensor sent by value: torch's queue pickling shares tensor storage by
+    file descriptor, which the parent cannot open once the worker has exited."""
+
+    def __init__(self, t):
+        self.dtype = t.dtype
+        self.a = t.detach().cpu().float().numpy().copy() if t.is_floating_point() else t.detach().cpu().numpy().copy()
+
+
+def _pack(v):
+    if isinstance(v, torch.Tensor):
+        return _T(v)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_pack(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _pack(x) for k, x in v.items()}
+    return v
+
+
+def _unpack(v):
+    if isinstance(v, _T):
+        return torch.from_numpy(v.a).to(v.dtype)
+    if isinstance(v, (list, tuple)):
+        return type(v)(_unpack(x) for x in v)
+    if isinstance(v, dict):
+        return {k: _unpack(x) for k, x in v.items()}
+    return v
+
+
 def _worker(rank, world, port, fn, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     try:
-        q.put((rank, fn(rank, world)))
+        q.put((rank, _pack(fn(rank, world))))
     except Exception:  # pragma: no cover
         import traceback
 
@@ -44,7 +73,7 @@ def _spawn(fn, world=2, attempts=3):
         ps = [ctx.Process(target=_worker, args=(r, world, port, fn, q)) for r in range(world)]
         for p in ps:
             p.start()
-        res = dict(q.get(timeout=120) for _ in ps)
+        res = {r: _unpack(v) for r, v in (q.get(timeout=120) for _ in ps)}
         for p in ps:
             p.join(timeout=60)
         errs = [v for v in res.values() if isinstance(v, str)]
