@@ -21,6 +21,8 @@
 #   decode_trace kernel trace of batch-256 decode
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
+#   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
+#   kt           GPU tests matching $KT (pytest -k)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${1:?usage: gpu.sh OUT step...}
@@ -65,6 +67,9 @@ step() {
             --max-model-len 2048 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
+        w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
+            --out "$O/w4x_sweep.jsonl" ;;
+        kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac
 }

@@ -197,6 +197,22 @@ def test_gemm_splitk(M, N, K, nslice):
     assert torch.equal(gemm_nt_splitk(a, b, nslice), c)
 
 
+@pytest.mark.parametrize("M,N,K,bn,nslice", [(256, 1024, 4096, 128, 1), (200, 768, 4096, 128, 4),
+                                             (256, 512, 14336, 128, 8), (96, 1024, 1024, 256, 2),
+                                             (384, 256, 2048, 256, 1), (130, 384, 640, 128, 5)])
+def test_gemm_w4x_decode_shapes(M, N, K, bn, nslice):
+    """The four-wave decode GEMM (any M, 256x128 / 256x256 tiles, K slices)
+    against fp32 torch; slices are summed in a fixed order (repeatable bits)."""
+    from kgs.ops.gemm import gemm_nt_w4x
+
+    a_full = (torch.rand(M, K + 64, device=DEV) * 2 - 1).bfloat16()
+    a = a_full[:, 32:32 + K]
+    b = ((torch.rand(N, K, device=DEV) * 2 - 1) * torch.linspace(0.5, 1.5, K, device=DEV)).bfloat16()
+    c = gemm_nt_w4x(a, b, bn=bn, nslice=nslice)
+    assert _rel_err(c, _ref_nt(a, b)) < 1e-2
+    assert torch.equal(gemm_nt_w4x(a, b, bn=bn, nslice=nslice), c)
+
+
 def test_splitk_workspace_is_stable_for_graphs():
     """The partial-tile buffer reserved under torch.device("cuda") is the one
     calls on "cuda:0" use (no silent second allocation), and a growth retires the
