@@ -79,7 +79,10 @@ _SIGS = {
     "kgs_skinny_gemm_bf16_fused": ([_c_void_p] * 5 + [_c_int] * 3 + [_c_long, _c_long] + [_c_int] * 3 +
                                    [_c_void_p] * 3 + [ctypes.c_float, ctypes.c_float, _c_void_p, _c_void_p], _c_int),
     "kgs_skinny_variant_geometry": ([_c_int, _c_int] + [ctypes.POINTER(_c_int)] * 3, _c_int),
-    "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p], _c_int),
+    "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p, _c_int,
+                                                  _c_void_p], _c_int),
+    "kgs_splitk_add_rmsnorm_bf16": ([_c_void_p, _c_int] + [_c_void_p] * 3 + [_c_int, _c_int, _c_long, _c_long,
+                                                                              ctypes.c_float, _c_void_p], _c_int),
     "kgs_paged_decode_bf16": ([_c_void_p] * 8 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_int, _c_void_p],
                               _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)

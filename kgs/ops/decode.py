@@ -388,13 +388,25 @@ class PagedKVCache:
 
 
 def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positions: torch.Tensor,
-                slots: torch.Tensor, cache_layer: torch.Tensor, heads: int, kv_heads: int) -> torch.Tensor:
+                slots: torch.Tensor, cache_layer: torch.Tensor, heads: int, kv_heads: int,
+                partials: torch.Tensor | None = None) -> torch.Tensor:
     """In place: rotate the q and k heads of every row of the fused ``qkv``
     ``[T, (H + 2 HKV) * 128]`` at ``positions[t]``, and write k, v into cache slot
-    ``slots[t]`` (``page * 32 + offset``; < 0 skips the write)."""
+    ``slots[t]`` (``page * 32 + offset``; < 0 skips the write).
+
+    ``partials`` (fp32 ``[nslice, T, (H + 2 HKV) * 128]``, from
+    ``kgs.ops.gemm.gemm_nt_w4x_partials``): the projection arrives as split-K
+    partial products; they are reduced (bf16-rounded like the unfused reduce)
+    in the same launch and ``qkv`` is output only."""
     t = qkv.shape[0]
     if qkv.dtype != torch.bfloat16 or not qkv.is_cuda or qkv.stride(1) != 1:
         raise ValueError("qkv must be a row-major bf16 GPU matrix")
+    nslice = 0
+    if partials is not None:
+        if partials.dtype != torch.float32 or partials.dim() != 3 or not partials.is_contiguous() or \
+                tuple(partials.shape[1:]) != (t, (heads + 2 * kv_heads) * HEAD_DIM):
+            raise ValueError("partials must be contiguous fp32 [nslice, T, (H + 2 HKV) * 128]")
+        nslice = partials.shape[0]
     for v, name in ((positions, "positions"), (slots, "slots")):
         if v.dtype != torch.int32 or not v.is_contiguous() or v.numel() != t:
             raise ValueError(f"{name} must be a contiguous int32 vector of length {t}")
@@ -406,6 +418,7 @@ def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positio
     rc = _lib.lib().kgs_rope_cache_bf16(qkv.data_ptr(), cos.data_ptr(), sin.data_ptr(), positions.data_ptr(),
                                         slots.data_ptr(), cache_layer.data_ptr(), t, heads, kv_heads, HEAD_DIM,
                                         qkv.stride(0), 1 if cache_layer.dtype == FP8 else 0,
+                                        None if partials is None else partials.data_ptr(), nslice,
                                         _lib.stream_handle(qkv.device))
     _lib.check(rc, "rope_cache")
     return qkv

@@ -166,6 +166,33 @@ def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1
     return out
 
 
+def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int) -> torch.Tensor:
+    """The split-K four-wave GEMM WITHOUT its reduce: returns the fp32 partial
+    products ``[nslice, M, N]`` (a view of the per-GPU split-K workspace, valid
+    until the next split-K call on the stream) for a fused consumer --
+    ``kgs.ops.transformer.splitk_add_rmsnorm`` or ``kgs.ops.decode.rope_cache_``."""
+    if nslice < 2:
+        raise ValueError("partials need nslice >= 2")
+    _check_operand(a, "a")
+    _check_operand(b, "b")
+    M, K = a.shape
+    N, K2 = b.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+    from .decode import device_key
+
+    need = nslice * M * N
+    ws = _SPLITK_WS.get(device_key(a.device))
+    if ws is None or ws.numel() < need:
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("gemm_nt_w4x_partials: reserve_splitk_workspace() before hipGraph capture")
+        ws = reserve_splitk_workspace(a.device, need)
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), None, ws.data_ptr(), M, N, K, a.stride(0),
+                                         b.stride(0), N, int(bn), int(nslice), _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_w4x_partials[{M}x{N}x{K} bn{bn}/{nslice}]")
+    return ws[:need].view(nslice, M, N)
+
+
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
 FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}

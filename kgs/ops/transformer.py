@@ -56,6 +56,29 @@ def add_rmsnorm(x: torch.Tensor, d: torch.Tensor | None, w: torch.Tensor, eps: f
     return y
 
 
+def splitk_add_rmsnorm(partials: torch.Tensor, x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """``x += bf16(sum(partials))`` (in place) and return ``rmsnorm(x) * w``:
+    the split-K reduce of a decode projection fused with the residual add and
+    norm after it. ``partials``: contiguous fp32 ``[nslice, rows, cols]``
+    (``kgs.ops.gemm.gemm_nt_w4x_partials``); cols a multiple of 2048 up to 8192.
+    The delta is rounded to bf16 as the unfused reduce would round it."""
+    _need(x, "x")
+    rows, cols = x.shape
+    if partials.dtype != torch.float32 or partials.dim() != 3 or tuple(partials.shape[1:]) != (rows, cols) or \
+            not partials.is_contiguous():
+        raise ValueError("partials must be a contiguous fp32 [nslice, rows, cols] tensor")
+    if w.shape != (cols,) or w.dtype != torch.bfloat16 or not w.is_contiguous():
+        raise ValueError("w must be a contiguous bf16 vector of length cols")
+    y = torch.empty((rows, cols), dtype=torch.bfloat16, device=x.device) if out is None else out
+    _need(y, "out")
+    rc = _lib.lib().kgs_splitk_add_rmsnorm_bf16(partials.data_ptr(), partials.shape[0], x.data_ptr(), w.data_ptr(),
+                                                y.data_ptr(), rows, cols, x.stride(0), y.stride(0), float(eps),
+                                                _lib.stream_handle(x.device))
+    _lib.check(rc, "splitk_add_rmsnorm")
+    return y
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     return add_rmsnorm(x, None, w, eps)
 

@@ -45,7 +45,8 @@ def run_engine(a) -> dict:
                       max_prefill_tokens=a.max_prefill_tokens, fused_max_batch=a.fused_max_batch,
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
-                      packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights)
+                      packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights,
+                      fuse_splitk=not a.no_fuse_splitk)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -75,6 +76,7 @@ def run_engine(a) -> dict:
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "kv_cache_dtype": a.kv_cache_dtype, "prefill_weights": a.prefill_weights,
+        "fuse_splitk": not a.no_fuse_splitk,
         "chunked_prefill": a.chunked_prefill,
         "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
         "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
@@ -207,6 +209,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-packed-decode", action="store_true",
                     help="one weight copy: decode on hipBLASLt / split-K (needed for llama3-70b on one GPU)")
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-fuse-splitk", action="store_true",
+                    help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
     ap.add_argument("--fused-max-batch", type=int, default=64,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",

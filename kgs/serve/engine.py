@@ -75,6 +75,7 @@ class EngineConfig:
     prefix_caching: bool = False      # reuse cached KV pages of shared prompt prefixes (runs on mixed steps)
     packed_decode: bool = True        # prepacked skinny-GEMM decode copies (False: one weight copy, e.g. 70B)
     prefill_weights: str = "bf16"     # "fp8": W8A8 prompt pass (e4m3 weight copies, per-row activation scales)
+    fuse_splitk: bool = True          # split-K decode partials reduced inside RoPE/KV-write and add+RMSNorm
     seed: int = 0
 
 
@@ -96,7 +97,8 @@ class LLMEngine:
         self.model = ServingModel(model_cfg, device=device, backend=backend, seed=cfg.seed, num_pages=num_pages,
                                   max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
                                   decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype,
-                                  packed_decode=cfg.packed_decode, prefill_weights=cfg.prefill_weights)
+                                  packed_decode=cfg.packed_decode, prefill_weights=cfg.prefill_weights,
+                                  fuse_splitk=cfg.fuse_splitk)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128

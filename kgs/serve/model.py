@@ -49,10 +49,14 @@ class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 64,
                  decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True,
-                 prefill_weights: str = "bf16"):
+                 prefill_weights: str = "bf16", fuse_splitk: bool = True):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
+        # split-K decode projections hand their fp32 partials straight to the
+        # next op (RoPE + KV write after qkv, residual add + RMSNorm after o and
+        # down) instead of reducing them in a launch of their own
+        self.fuse_splitk = fuse_splitk and backend == "kgs"
         base = LlamaModel(cfg, device=device, backend="torch" if backend == "ref" else "kgs", seed=seed)
         self.oracle = base  # same weights, full-recompute forward (tests)
         self.embed, self.norm = base.embed, base.norm
@@ -138,6 +142,19 @@ class ServingModel:
         from kgs.ops import gemm_nt
 
         return gemm_nt(x, w)
+
+    def _splitk_route(self, m: int, layer: int, name: str):
+        """(bn, nslice) when this decode projection runs split-K on the
+        four-wave kernel and its reduce can be fused into the consumer."""
+        if not self.fuse_splitk:
+            return None
+        w = self.w[layer][name]
+        r = D.w4x_route(m, w.shape[0], w.shape[1])
+        if r is None or r[1] < 2:
+            return None
+        if name in ("o", "down") and self.cfg.hidden % 2048:
+            return None
+        return r
 
     def _norm(self, x, d, w):
         """x += d (in place, bf16) and return rmsnorm(x) * w."""
@@ -354,19 +371,36 @@ class ServingModel:
             return self._decode_fused(tokens, positions, slots, block_tables, ctx_lens, pages_per_split)
         x = self.embed[tokens.long()].reshape(-1, c.hidden).contiguous()
         y = self._norm(x, None, self.ln1[0])
+        m = x.shape[0]
+        rq, ro, rd = (self._splitk_route(m, 0, n) for n in ("qkv", "o", "down"))  # same shapes in every layer
+        if rq or ro or rd:
+            from kgs.ops.gemm import gemm_nt_w4x_partials
+            from kgs.ops.transformer import splitk_add_rmsnorm
         for i in range(c.layers):
-            qkv = self._proj(y, i, "qkv", True)
-            self._rope_cache(qkv, i, positions, slots)
+            if rq:
+                part = gemm_nt_w4x_partials(y, self.w[i]["qkv"], *rq)
+                qkv = torch.empty((m, part.shape[2]), dtype=torch.bfloat16, device=x.device)
+                D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(i), c.heads, c.kv_heads,
+                              partials=part)
+            else:
+                qkv = self._proj(y, i, "qkv", True)
+                self._rope_cache(qkv, i, positions, slots)
             if self.backend == "ref":
                 a = D.ref_paged_decode(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads,
                                        c.kv_heads).to(torch.bfloat16)
             else:
                 a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                              pages_per_split=pages_per_split)
-            y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
+            if ro:
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self.w[i]["o"], *ro), x, self.ln2[i], c.eps)
+            else:
+                y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
             act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
-            y = self._norm(x, self._proj(act, i, "down", True), nxt)
+            if rd:
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self.w[i]["down"], *rd), x, nxt, c.eps)
+            else:
+                y = self._norm(x, self._proj(act, i, "down", True), nxt)
         return self._proj(y, None, "lm", True)
 
     def _decode_fused(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split):

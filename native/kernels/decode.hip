@@ -366,11 +366,17 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 // place; k and v heads are also written into page slot[t] (skipped when < 0).
 // KV8: the cache holds OCP e4m3 bytes (scale 1, saturating) in the same
 // element order -- a page region is 4 KB instead of 8 KB.
-template <bool KV8>
+// SK: the projection arrives as nslice fp32 split-K partials P[s][t][nh * 128]
+// (gemm_nt_w4x without its reduce); they are summed in slice order and rounded
+// to bf16 exactly as kgs::splitk_reduce would, then rotated and stored to qkv
+// and the cache -- one launch instead of reduce + rope_cache. NSL > 0: the
+// slice count at compile time (all partial loads issued before the first add).
+template <bool KV8, bool SK = false, int NSL = 0>
 __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ qkv, const float* __restrict__ cosv,
                                                   const float* __restrict__ sinv, const int* __restrict__ pos,
                                                   const int* __restrict__ slot, void* __restrict__ cache,
-                                                  long tokens, int H, int HKV, long ld) {
+                                                  long tokens, int H, int HKV, long ld,
+                                                  const float* __restrict__ P = nullptr, int nslice = 0) {
   const int nh = H + 2 * HKV;
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= tokens * nh * 8) return;
@@ -380,7 +386,42 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
   unsigned short* base = qkv + t * ld + (long)h * HD + 8 * c;
   bf16x8* p1 = (bf16x8*)base;
   bf16x8* p2 = (bf16x8*)(base + HD / 2);
-  bf16x8 a = *p1, b = *p2;
+  bf16x8 a, b;
+  if constexpr (SK) {
+    const long MN = tokens * nh * HD, e = t * nh * HD + (long)h * HD + 8 * c;
+    f32x4 s[4];
+    if constexpr (NSL > 0) {
+      f32x4 ps[NSL][4];
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ps[sl][q] = *(const f32x4*)(P + sl * MN + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s[q] = ps[0][q];
+#pragma unroll
+        for (int sl = 1; sl < NSL; ++sl) s[q] += ps[sl][q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s[q] = *(const f32x4*)(P + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+      for (int sl = 1; sl < nslice; ++sl)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s[q] += *(const f32x4*)(P + sl * MN + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a[k] = (short)f2bf(s[k >> 2][k & 3]);
+      b[k] = (short)f2bf(s[2 + (k >> 2)][k & 3]);
+    }
+    if (h >= H + HKV) {  // v heads are not rotated: store them here
+      *p1 = a;
+      *p2 = b;
+    }
+  } else {
+    a = *p1;
+    b = *p2;
+  }
   if (h < H + HKV) {
     const int p = pos[t];
     const f32x4* cp = (const f32x4*)(cosv + (long)p * (HD / 2) + 8 * c);
@@ -769,20 +810,45 @@ KGS_EXPORT int kgs_skinny_gemm_bf16(const void* wp, const void* x, void* y, floa
 // of 128); pos/slot: int32 [tokens]; cache: this layer's pages
 // [pages][HKV][2][4096] bf16. q and k are rotated in place; k, v land in the cache.
 // kv8: the cache holds e4m3 bytes ([pages][HKV][2][4096] B) instead of bf16.
+// P != nullptr: the projection is given as nslice fp32 split-K partials
+// [nslice][tokens][(H + 2 HKV) * hd] instead of in qkv; the reduced, rotated
+// rows are written to qkv (which is then output only).
 KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* sinv, const int* pos, const int* slot,
-                                  void* cache, long tokens, int H, int HKV, int hd, long ld, int kv8, hipStream_t s) {
+                                  void* cache, long tokens, int H, int HKV, int hd, long ld, int kv8, const float* P,
+                                  int nslice, hipStream_t s) {
   if (tokens < 0 || H <= 0 || HKV <= 0 || H % HKV || hd != kgs::dec::HD) return KGS_ERR_SHAPE;
   if (ld < (long)(H + 2 * HKV) * hd) return KGS_ERR_SHAPE;
   if (!al16(qkv) || !al16(cosv) || !al16(sinv) || !al16(cache) || ld % 8) return KGS_ERR_ALIGN;
+  if (P != nullptr && (nslice <= 0 || !al16(P))) return KGS_ERR_ARG;
   const long n = tokens * (H + 2 * HKV) * 8;
   if (n == 0) return 0;
   const dim3 g((unsigned)((n + 255) / 256)), b(256);
-  if (kv8)
-    hipLaunchKernelGGL(kgs::dec::rope_cache<true>, g, b, 0, s, (unsigned short*)qkv, cosv, sinv, pos, slot, cache,
-                       tokens, H, HKV, ld);
-  else
-    hipLaunchKernelGGL(kgs::dec::rope_cache<false>, g, b, 0, s, (unsigned short*)qkv, cosv, sinv, pos, slot, cache,
-                       tokens, H, HKV, ld);
+  auto q = (unsigned short*)qkv;
+  if (P != nullptr) {
+#define KGS_RCS(KV, NSL)                                                                                           \
+  hipLaunchKernelGGL((kgs::dec::rope_cache<KV, true, NSL>), g, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, \
+                     HKV, ld, P, nslice)
+#define KGS_RCS_KV(KV)                \
+  switch (nslice) {                   \
+    case 2: KGS_RCS(KV, 2); break;    \
+    case 4: KGS_RCS(KV, 4); break;    \
+    case 8: KGS_RCS(KV, 8); break;    \
+    default: KGS_RCS(KV, 0); break;   \
+  }
+    if (kv8) {
+      KGS_RCS_KV(true);
+    } else {
+      KGS_RCS_KV(false);
+    }
+#undef KGS_RCS_KV
+#undef KGS_RCS
+  } else if (kv8) {
+    hipLaunchKernelGGL(kgs::dec::rope_cache<true>, g, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, HKV, ld,
+                       nullptr, 0);
+  } else {
+    hipLaunchKernelGGL(kgs::dec::rope_cache<false>, g, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, HKV, ld,
+                       nullptr, 0);
+  }
   return (int)hipGetLastError();
 }
 

@@ -420,16 +420,37 @@ hipError_t launch_layout(int ta, int tb, const unsigned short* A, const unsigned
 // tiles); the slices fill the rest.
 // ---------------------------------------------------------------------------
 namespace kgs {
+// NSL > 0: slice count at compile time -- a thread issues all its partial loads
+// before the first add instead of waiting out one cache latency per slice.
+template <int NSL>
 __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ P, unsigned short* __restrict__ C,
                                                      int M, int N, int ldc, int nslice) {
   const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 8;  // 8 consecutive columns of one row
   const long MN = (long)M * N;
   if (e >= MN) return;
   const int row = (int)(e / N), col = (int)(e - (long)row * N);
-  f32x4 a = *(const f32x4*)(P + e), b = *(const f32x4*)(P + e + 4);
-  for (int s = 1; s < nslice; ++s) {
-    a += *(const f32x4*)(P + s * MN + e);
-    b += *(const f32x4*)(P + s * MN + e + 4);
+  f32x4 a, b;
+  if constexpr (NSL > 0) {
+    f32x4 pa[NSL], pb[NSL];
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      pa[s] = *(const f32x4*)(P + s * MN + e);
+      pb[s] = *(const f32x4*)(P + s * MN + e + 4);
+    }
+    a = pa[0];
+    b = pb[0];
+#pragma unroll
+    for (int s = 1; s < NSL; ++s) {
+      a += pa[s];
+      b += pb[s];
+    }
+  } else {
+    a = *(const f32x4*)(P + e);
+    b = *(const f32x4*)(P + e + 4);
+    for (int s = 1; s < nslice; ++s) {
+      a += *(const f32x4*)(P + s * MN + e);
+      b += *(const f32x4*)(P + s * MN + e + 4);
+    }
   }
   uint4 o;
   o.x = pack_bf16x2(a[0], a[1]);
@@ -438,11 +459,24 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ P
   o.w = pack_bf16x2(b[2], b[3]);
   *(uint4*)(C + (long)row * ldc + col) = o;
 }
+
+inline void launch_splitk_reduce(const float* P, unsigned short* C, int M, int N, int ldc, int nslice,
+                                 hipStream_t s) {
+  const dim3 g((unsigned)(((long)M * N / 8 + 255) / 256)), b(256);
+  switch (nslice) {
+    case 2: hipLaunchKernelGGL(splitk_reduce<2>, g, b, 0, s, P, C, M, N, ldc, nslice); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce<4>, g, b, 0, s, P, C, M, N, ldc, nslice); break;
+    case 8: hipLaunchKernelGGL(splitk_reduce<8>, g, b, 0, s, P, C, M, N, ldc, nslice); break;
+    default: hipLaunchKernelGGL(splitk_reduce<0>, g, b, 0, s, P, C, M, N, ldc, nslice); break;
+  }
+}
 }  // namespace kgs
 
 // Four-wave kernel for short-M (decode-batch) GEMMs: tile width bn (256 or 128),
 // any M (rows past M read as zeros, stores predicated), and nslice K-slices
-// (nslice > 1: fp32 partial tiles into ws, then splitk_reduce). Requirements:
+// (nslice > 1: fp32 partial tiles into ws, then splitk_reduce; with C == nullptr
+// the reduce is left to a fused consumer such as kgs_splitk_add_rmsnorm_bf16 or
+// kgs_rope_cache_bf16, which read ws directly). Requirements:
 // N % bn == 0, (K / nslice) % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
                                     int ldb, int ldc, int bn, int nslice, hipStream_t stream) {
@@ -455,6 +489,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
   if ((long)lda * 512 >= (1L << 31) || (long)ldb * 512 >= (1L << 31)) return KGS_ERR_SHAPE;
   if (nslice > 1 && (ws == nullptr || (uintptr_t)ws % 16)) return KGS_ERR_ARG;
+  if (nslice == 1 && C == nullptr) return KGS_ERR_ARG;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
@@ -483,10 +518,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
     }
   }
 #undef KGS_W4X
-  if (nslice > 1) {
-    const long groups = ((long)M * N / 8 + 255) / 256;
-    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)groups), dim3(256), 0, stream, ws, c, M, N, ldc, nslice);
-  }
+  if (nslice > 1 && c != nullptr) launch_splitk_reduce(ws, c, M, N, ldc, nslice, stream);
   return (int)hipGetLastError();
 }
 
@@ -514,9 +546,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt_splitk(const void* A, const void* B, void* C, fl
   else
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 7 + 512 + 1048576>), grid, dim3(512), 0, stream, a, b,
                        (unsigned short*)ws, nullptr, M, N, ks, lda, ldb, N, 1.0f, nullptr);
-  const long groups = ((long)M * N / 8 + 255) / 256;
-  hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)groups), dim3(256), 0, stream, ws, (unsigned short*)C, M, N, ldc,
-                     nslice);
+  launch_splitk_reduce(ws, (unsigned short*)C, M, N, ldc, nslice, stream);
   return (int)hipGetLastError();
 }
 

@@ -252,10 +252,123 @@ __global__ __launch_bounds__(256) void silu_mul(const unsigned short* __restrict
   ((bf16x8*)(out + r * ld_out))[c] = o;
 }
 
+// Split-K reduce fused with the residual add and the RMSNorm that follow a
+// decode projection (o, down): d = bf16(sum_s P[s][row]) with the slice order
+// and rounding of kgs::splitk_reduce, x' = bf16(x + d) written back, y =
+// rmsnorm(x') * w. One 256-thread workgroup per row (a decode batch of 256
+// rows fills the 256 CUs; add_rmsnorm's wave-per-row grid would use 64 of
+// them); thread t owns the 8-column chunks t + 256 j, cols == 2048 * NJ. The
+// partial tiles never round-trip through a bf16 delta in HBM and the separate
+// add_rmsnorm launch disappears.
+// NSL > 0: the slice count at compile time, so every partial load of a thread
+// is issued before the first add (a run-time slice loop waits out one cache
+// latency per slice); 0 = run-time count.
+template <int NJ, int NSL>
+__global__ __launch_bounds__(256) void splitk_add_rmsnorm(const float* __restrict__ P, int nslice, long MN,
+                                                          unsigned short* __restrict__ x,
+                                                          const unsigned short* __restrict__ w,
+                                                          unsigned short* __restrict__ y, int cols, long ldx,
+                                                          long ldy, float eps) {
+  __shared__ float red[4];
+  const int row = blockIdx.x, t = threadIdx.x;
+  bf16x8* xr = (bf16x8*)(x + row * ldx);
+  float v[NJ][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const long e = (long)row * cols + 8 * (t + 256 * j);
+    f32x4 a, b;
+    if constexpr (NSL > 0) {
+      f32x4 pa[NSL], pb[NSL];
+#pragma unroll
+      for (int sl = 0; sl < NSL; ++sl) {
+        pa[sl] = *(const f32x4*)(P + sl * MN + e);
+        pb[sl] = *(const f32x4*)(P + sl * MN + e + 4);
+      }
+      a = pa[0];
+      b = pb[0];
+#pragma unroll
+      for (int sl = 1; sl < NSL; ++sl) {
+        a += pa[sl];
+        b += pb[sl];
+      }
+    } else {
+      a = *(const f32x4*)(P + e);
+      b = *(const f32x4*)(P + e + 4);
+      for (int sl = 1; sl < nslice; ++sl) {
+        a += *(const f32x4*)(P + sl * MN + e);
+        b += *(const f32x4*)(P + sl * MN + e + 4);
+      }
+    }
+    const bf16x8 xv = xr[t + 256 * j];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float d = bf2f(f2bf(k < 4 ? a[k] : b[k - 4]));
+      o[k] = (short)f2bf(bf2f((unsigned short)xv[k]) + d);
+      v[j][k] = bf2f((unsigned short)o[k]);
+      ss += v[j][k] * v[j][k];
+    }
+    xr[t + 256 * j] = o;
+  }
+  ss = wave_sum(ss);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  ss = (red[0] + red[1]) + (red[2] + red[3]);
+  const float r = rsqrtf(ss / (float)cols + eps);
+  const bf16x8* wr = (const bf16x8*)w;
+  bf16x8* yr = (bf16x8*)(y + row * ldy);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const bf16x8 wv = wr[t + 256 * j];
+    bf16x8 o;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = (short)f2bf(v[j][k] * r * bf2f((unsigned short)wv[k]));
+    yr[t + 256 * j] = o;
+  }
+}
+
 }  // namespace tfm
 }  // namespace kgs
 
 static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+// P: nslice fp32 partial products [nslice][rows][cols] (gemm_nt_w4x without its
+// reduce); x: [rows, ldx] residual stream, updated in place; w: [cols]; y: out.
+// cols a multiple of 2048 up to 8192.
+KGS_EXPORT int kgs_splitk_add_rmsnorm_bf16(const float* P, int nslice, void* x, const void* w, void* y, int rows,
+                                          int cols, long ldx, long ldy, float eps, hipStream_t s) {
+  if (rows < 0 || cols <= 0 || nslice <= 0) return KGS_ERR_SHAPE;
+  if (cols % 2048 || cols > 8192 || ldx < cols || ldy < cols) return KGS_ERR_SHAPE;
+  if (!al16(P) || !al16(x) || !al16(w) || !al16(y) || ldx % 8 || ldy % 8) return KGS_ERR_ALIGN;
+  if (rows == 0) return 0;
+  using namespace kgs::tfm;
+  const long MN = (long)rows * cols;
+  auto X = (unsigned short*)x;
+  auto W = (const unsigned short*)w;
+  auto Y = (unsigned short*)y;
+  const int nj = cols / 2048;
+  if (nj < 1 || nj > 4) return KGS_ERR_SHAPE;
+#define KGS_SARN(NJ, NSL)                                                                                           \
+  hipLaunchKernelGGL((splitk_add_rmsnorm<NJ, NSL>), dim3(rows), dim3(256), 0, s, P, nslice, MN, X, W, Y, cols, ldx, \
+                     ldy, eps)
+#define KGS_SARN_NJ(NJ)                                           \
+  switch (nslice) {                                               \
+    case 2: KGS_SARN(NJ, 2); break;                               \
+    case 4: KGS_SARN(NJ, 4); break;                               \
+    case 8: KGS_SARN(NJ, 8); break;                               \
+    default: KGS_SARN(NJ, 0); break;                              \
+  }
+  switch (nj) {
+    case 1: KGS_SARN_NJ(1); break;
+    case 2: KGS_SARN_NJ(2); break;
+    case 3: KGS_SARN_NJ(3); break;
+    default: KGS_SARN_NJ(4); break;
+  }
+#undef KGS_SARN_NJ
+#undef KGS_SARN
+  return (int)hipGetLastError();
+}
 
 // x: [rows, cols] residual stream; d: optional delta (same ld) -- when given,
 // xo = x + d is written (xo may alias x) and normalised; w: [cols]; y: out.

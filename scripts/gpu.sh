@@ -17,7 +17,7 @@
 #   gemm_pmc     two counter passes over the GEMM (stall / MFMA busy)
 #   overlap      GEMM vs comm-kernel overlap measurement (bench/overlap.py)
 #   overlap_trace  kernel trace of the overlap run
-#   serve        kgs.serve batch-256 serving bench
+#   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
@@ -62,6 +62,8 @@ step() {
             -- python3 bench/overlap.py --iters 3 ;;
         serve) run serve 400 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
             --max-batch 256 --max-model-len 2048 ;;
+        serve_nofuse) run serve_nofuse 400 python -u -m kgs.serve bench --requests 256 --input-len 512 \
+            --output-len 256 --max-batch 256 --max-model-len 2048 --no-fuse-splitk ;;
         decode_trace) run decode_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace" -o d \
             -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 --max-batch 256 \
             --max-model-len 2048 ;;

@@ -308,3 +308,57 @@ def test_fp8_kv_cache(pps):
     o = paged_decode_attention(q, cache.layer(0), bt, ctx_t, heads, hkv, pages_per_split=pps)
     torch.cuda.synchronize()
     assert (o.float() - ref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("kv_dtype", ["bf16", "fp8"])
+def test_rope_cache_from_splitk_partials(kv_dtype):
+    """qkv projection handed over as split-K partials: one launch reduces,
+    rotates and writes the cache -- bit-identical to reduce + rope_cache_."""
+    from kgs.ops.decode import PAGE, PagedKVCache, rope_cache_
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_partials
+    from kgs.ops.transformer import rope_tables
+
+    heads, hkv, hd, m, k = 32, 8, 128, 200, 4096
+    width = (heads + 2 * hkv) * hd
+    x = _bf(m, k)
+    w = _bf(width, k, scale=k ** -0.5)
+    cos, sin = rope_tables(4096, hd, 500000.0, DEV)
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(64 * PAGE, device=DEV)[:m].int()
+    slots[3] = -1  # no cache write for this row
+    caches = [PagedKVCache(1, 64, hkv, DEV, dtype=kv_dtype) for _ in range(2)]
+    q1 = gemm_nt_w4x(x, w, bn=128, nslice=4)
+    rope_cache_(q1, cos, sin, pos, slots, caches[0].layer(0), heads, hkv)
+    q2 = torch.empty_like(q1)
+    rope_cache_(q2, cos, sin, pos, slots, caches[1].layer(0), heads, hkv,
+                partials=gemm_nt_w4x_partials(x, w, 128, 4))
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2)
+    assert torch.equal(caches[0].layer(0).view(torch.uint8), caches[1].layer(0).view(torch.uint8))
+
+
+@pytest.mark.parametrize("m,cols,nslice", [(256, 4096, 8), (200, 4096, 4), (130, 8192, 2)])
+def test_splitk_add_rmsnorm_matches_unfused(m, cols, nslice):
+    """o / down projection partials reduced inside the residual add + RMSNorm:
+    the residual stream is bit-identical to reduce + add_rmsnorm, the normed
+    output agrees to bf16 rounding (the row sum of squares is added in another
+    order) and with fp32 torch."""
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_partials
+    from kgs.ops.transformer import add_rmsnorm, splitk_add_rmsnorm
+
+    k = 4096
+    a = _bf(m, k)
+    wt = _bf(cols, k, scale=k ** -0.5)
+    lnw = (1 + 0.1 * torch.randn(cols, device=DEV)).bfloat16()
+    x0 = _bf(m, cols)
+    x1, x2 = x0.clone(), x0.clone()
+    d = gemm_nt_w4x(a, wt, bn=128, nslice=nslice)
+    y1 = add_rmsnorm(x1, d, lnw, 1e-5)
+    y2 = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, wt, 128, nslice), x2, lnw, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(x1, x2)
+    diff = (y1.float() - y2.float()).abs()
+    assert diff.max().item() <= 2 ** -6 * y1.float().abs().max().item()
+    xr = x0.float() + (a.float() @ wt.float().T)
+    yr = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-5) * lnw.float()
+    assert ((y2.float() - yr).abs().max() / yr.abs().max()).item() < 2e-2

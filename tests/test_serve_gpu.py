@@ -262,3 +262,37 @@ def test_fp8_prefill_with_chunked_prefill():
     outs = eng.generate(prompts, SamplingParams(max_tokens=4, ignore_eos=True))
     assert eng.stats["mixed_steps"] >= 3
     _oracle_check(eng, prompts, outs, tol=0.12)
+
+
+def test_splitk_fused_decode_llama8b_layer():
+    """Batch-128 decode through one Llama-3-8B-shaped layer, where qkv / o /
+    down run split-K on the four-wave kernel: with their partials reduced
+    inside RoPE/KV-write and add+RMSNorm the KV cache is bit-identical and the
+    logits agree with the unfused launches."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.ops.decode import PAGE
+    from kgs.serve.model import ServingModel
+
+    cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=1, vocab=2048)
+    b, ctx = 128, 40
+    outs, caches = [], []
+    for fuse in (False, True):
+        torch.manual_seed(0)
+        m = ServingModel(cfg, device="cuda", num_pages=b * 2 + 8, max_model_len=256, fuse_splitk=fuse,
+                         packed_decode=False)
+        assert (m._splitk_route(b, 0, "qkv") is not None) == fuse
+        bt = torch.arange(b * 2, dtype=torch.int32, device="cuda").view(b, 2)
+        g = torch.Generator(device="cuda").manual_seed(1)
+        lay = m.cache.layer(0)
+        lay.copy_((torch.randn(lay.shape, generator=g, device="cuda") * 0.5).to(lay.dtype))
+        tokens = torch.randint(0, cfg.vocab, (b,), generator=g, device="cuda")
+        pos = torch.full((b,), ctx - 1, dtype=torch.int32, device="cuda")
+        slots = (bt[:, (ctx - 1) // PAGE] * PAGE + (ctx - 1) % PAGE).contiguous()
+        ctx_lens = torch.full((b,), ctx, dtype=torch.int32, device="cuda")
+        outs.append(m.decode(tokens, pos, slots, bt, ctx_lens).float())
+        caches.append(lay.clone())
+        torch.cuda.synchronize()
+        del m
+    assert torch.equal(caches[0], caches[1])
+    err = ((outs[0] - outs[1]).abs().max() / outs[0].abs().max()).item()
+    assert err < 2e-2, err
