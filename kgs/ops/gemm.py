@@ -193,6 +193,28 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int)
     return ws[:need].view(nslice, M, N)
 
 
+def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
+                       out: torch.Tensor | None = None) -> torch.Tensor:
+    """``silu(a @ gate.T) * (a @ up.T)`` for a fused gate|up weight ``[2I, K]``
+    (gate rows first) on the four-wave kernel, the SwiGLU applied in the GEMM
+    epilogue: returns ``[M, I]`` (both products rounded to bf16 first, as
+    ``gemm_nt`` + ``kgs.ops.transformer.silu_mul`` round them). Any M;
+    ``2I % bn == 0``, ``K % 128 == 0``."""
+    _check_operand(a, "a")
+    _check_operand(w_gate_up, "w_gate_up")
+    M, K = a.shape
+    N, K2 = w_gate_up.shape
+    if K != K2:
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} w {tuple(w_gate_up.shape)}")
+    if out is None:
+        out = torch.empty((M, N // 2), dtype=torch.bfloat16, device=a.device)
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x_swiglu(a.data_ptr(), w_gate_up.data_ptr(), out.data_ptr(), M, N, K,
+                                                a.stride(0), w_gate_up.stride(0), out.stride(0), int(bn),
+                                                _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_w4x_swiglu[{M}x{N}x{K} bn{bn}]")
+    return out
+
+
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
 FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}

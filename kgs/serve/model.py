@@ -53,9 +53,10 @@ class ServingModel:
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
-        # split-K decode projections hand their fp32 partials straight to the
-        # next op (RoPE + KV write after qkv, residual add + RMSNorm after o and
-        # down) instead of reducing them in a launch of their own
+        # decode projections on the four-wave kernel fuse into their neighbours:
+        # split-K partials go straight to the next op (RoPE + KV write after
+        # qkv, residual add + RMSNorm after o and down) instead of a reduce
+        # launch, and an unsplit gate|up applies SwiGLU in its epilogue
         self.fuse_splitk = fuse_splitk and backend == "kgs"
         base = LlamaModel(cfg, device=device, backend="torch" if backend == "ref" else "kgs", seed=seed)
         self.oracle = base  # same weights, full-recompute forward (tests)
@@ -155,6 +156,15 @@ class ServingModel:
         if name in ("o", "down") and self.cfg.hidden % 2048:
             return None
         return r
+
+    def _swiglu_route(self, m: int):
+        """(bn, 1) when the decode gate|up projection runs unsplit on the
+        four-wave kernel: SwiGLU then goes into its epilogue."""
+        if not self.fuse_splitk:
+            return None
+        w = self.w[0]["gate_up"]
+        r = D.w4x_route(m, w.shape[0], w.shape[1])
+        return r if r is not None and r[1] == 1 else None
 
     def _norm(self, x, d, w):
         """x += d (in place, bf16) and return rmsnorm(x) * w."""
@@ -373,8 +383,9 @@ class ServingModel:
         y = self._norm(x, None, self.ln1[0])
         m = x.shape[0]
         rq, ro, rd = (self._splitk_route(m, 0, n) for n in ("qkv", "o", "down"))  # same shapes in every layer
-        if rq or ro or rd:
-            from kgs.ops.gemm import gemm_nt_w4x_partials
+        rg = self._swiglu_route(m)
+        if rq or ro or rd or rg:
+            from kgs.ops.gemm import gemm_nt_w4x_partials, gemm_nt_w4x_swiglu
             from kgs.ops.transformer import splitk_add_rmsnorm
         for i in range(c.layers):
             if rq:
@@ -395,7 +406,10 @@ class ServingModel:
                 y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self.w[i]["o"], *ro), x, self.ln2[i], c.eps)
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
-            act = self._silu_mul(self._proj(y, i, "gate_up", True))
+            if rg:
+                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], rg[0])
+            else:
+                act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             if rd:
                 y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self.w[i]["down"], *rd), x, nxt, c.eps)

@@ -522,6 +522,36 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
   return (int)hipGetLastError();
 }
 
+// SwiGLU decode GEMM on the four-wave kernel: B is a fused gate|up weight
+// [N = 2I, K] (gate rows first); C[M, I] = silu(A . gate^T) * (A . up^T) with
+// both products rounded to bf16 first (the roundings of gemm + silu_mul). Any
+// M; N % bn == 0, K % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                                           int ldb, int ldc, int bn, hipStream_t stream) {
+  using namespace kgs;
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N / 2) return KGS_ERR_SHAPE;
+  if (bn != 128 && bn != 256) return KGS_ERR_ARG;
+  if (N % bn || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  if ((long)lda * 512 >= (1L << 31) || (long)ldb * 512 >= (1L << 31)) return KGS_ERR_SHAPE;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  const dim3 grid(((M + 255) / 256) * (N / bn));
+  const bool aligned_m = M % 256 == 0;
+#define KGS_W4SW(BN, MODE)                                                                                      \
+  hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, MODE, w4::Knobs<BN>::B1, w4::Knobs<BN>::R, w4::Knobs<BN>::P, \
+                                     w4::Knobs<BN>::ORD, 1000000>),                                             \
+                     grid, dim3(256), 0, stream, a, b, c, nullptr, M, N, K, lda, ldb, ldc)
+  if (bn == 256) {
+    if (aligned_m) KGS_W4SW(256, 0); else KGS_W4SW(256, 1);
+  } else {
+    if (aligned_m) KGS_W4SW(128, 0); else KGS_W4SW(128, 1);
+  }
+#undef KGS_W4SW
+  return (int)hipGetLastError();
+}
+
 // C[M, N] (bf16) = A[M, K] . B[N, K]^T over nslice K-slices; ws holds nslice *
 // M * N floats. K / nslice must be a multiple of 128 (aligned M % 256 == 0,
 // N % 256 == 0) or of 8 (any M, N % 8 == 0: the bounded pipeline).

@@ -47,6 +47,13 @@
 //   MODE bit 1  split-K: gridDim.x = tiles x slices; slice s computes K columns
 //               [s K, (s + 1) K) and stores an fp32 partial tile to
 //               ((float*)C)[s][M][N] for kgs::splitk_reduce.
+//   X digit 10^6  SwiGLU: B is a fused gate|up weight of N = 2I rows (gate rows
+//               [0, I), up rows [I, 2I)). A tile stages gate and up rows in
+//               alternating 32-row DMA groups (gate block tn BN/2 .., up block
+//               I + tn BN/2 ..), so every wave holds the gate and up columns of
+//               the same outputs, and the epilogue stores silu(g) * u: a
+//               [M, I] activation with no [M, 2I] round trip and no silu_mul
+//               launch. Same roundings as gate|up GEMM + silu_mul.
 
 namespace kgs {
 namespace w4 {
@@ -74,6 +81,7 @@ constexpr int dma_per_stage() { return 8 + BN / 32; }
 struct Ctx {
   char* smem;
   __amdgpu_buffer_rsrc_t ra, rb;
+  __amdgpu_buffer_rsrc_t rb2;  // SwiGLU: the up block (rb holds the gate block)
   int voa, vob;     // per-lane DMA byte offsets (row, swizzled chunk)
   int sa32, sb32;   // bytes between DMA row groups (32 rows)
   int w, wr, wc;
@@ -95,18 +103,28 @@ __device__ __forceinline__ void bar() {
 
 // DMA instruction j of operand OP (0 = A: j < 8, 1 = B: j < BN/32) for the K-tile
 // starting at k0 into stage st: rows j*32 + w*8 + lane/8, 1 KiB = 8 rows of 128 B.
-// AUX: cache-policy bits of the load (0 = default; 16 = sc1)
-template <int BN, int OP, int AUX = 0>
+// AUX: cache-policy bits of the load (0 = default; 16 = sc1). SW: SwiGLU
+// staging of B (groups alternate gate / up, see the MODE notes above).
+template <int BN, int OP, int AUX = 0, bool SW = false>
 __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
   using S = Shape<BN>;
   char* dst = c.smem + st * S::STAGE + OP * S::OPA + (j * 4 + c.w) * 1024;
-  const int so = j * (OP ? c.sb32 : c.sa32) + k0 * 2;
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(OP ? c.rb : c.ra, (KGS_LDS void*)dst, 16, OP ? c.vob : c.voa, so, 0, AUX);
+  if constexpr (OP == 1 && SW) {
+    const int so = (j >> 1) * c.sb32 + k0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds((j & 1) ? c.rb2 : c.rb, (KGS_LDS void*)dst, 16, c.vob, so, 0, AUX);
+  } else {
+    const int so = j * (OP ? c.sb32 : c.sa32) + k0 * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(OP ? c.rb : c.ra, (KGS_LDS void*)dst, 16, OP ? c.vob : c.voa, so, 0,
+                                             AUX);
+  }
 }
 
-template <int BN, int AUX>
+// X: the knob bag of the kernel template (AUX = X / 100 % 100, SW = X / 10^6 % 10)
+template <int BN, int X>
 __device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
-  if (j < 8) dma<BN, 0, AUX>(c, st, j, k0); else dma<BN, 1, AUX>(c, st, j - 8, k0);
+  constexpr int AUX = (X / 100) % 100;
+  constexpr bool SW = (X / 1000000) % 10 != 0;
+  if (j < 8) dma<BN, 0, AUX>(c, st, j, k0); else dma<BN, 1, AUX, SW>(c, st, j - 8, k0);
 }
 
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *(const bf16x8*)p; }
@@ -203,11 +221,11 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BN 
       if constexpr (rd_isa(ORD, NB, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
     }
     if constexpr (K >= B1 && K < KM - R) {
-      // MFMAs that carry the DMA issues: the whole window, or the first W (X / 10000) of it
-      constexpr int NW = (X / 10000) ? X / 10000 : KM - R - B1;
+      // MFMAs that carry the DMA issues: the whole window, or the first W (X / 10000 % 100) of it
+      constexpr int NW = ((X / 10000) % 100) ? (X / 10000) % 100 : KM - R - B1;
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        if (B1 + (j * NW) / ND == K) dma_any<BN, (X / 100) % 100>(c, ST, j, sp.k0);
+        if (B1 + (j * NW) / ND == K) dma_any<BN, X>(c, ST, j, sp.k0);
       }
     }
     if constexpr (K >= KM - R) {
@@ -271,7 +289,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
   using S = Shape<BN>;
-  constexpr int NB = S::NB, ND = dma_per_stage<BN>(), AUX = (X / 100) % 100;
+  constexpr int NB = S::NB, ND = dma_per_stage<BN>();
+  constexpr bool SW = (X / 1000000) % 10 != 0;
+  static_assert(!SW || (EPI == EPI_NONE && (MODE & 2) == 0), "SwiGLU: no bias epilogue, no split-K");
   constexpr bool BNDM = (MODE & 1) != 0, SPLITK = (MODE & 2) != 0;
   __shared__ __attribute__((aligned(1024))) char smem[S::LDS_BYTES];
   const int lane = threadIdx.x & 63;
@@ -299,7 +319,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   c.nt = K / BK;
   const long koff = SPLITK ? (long)slice * K : 0;  // split-K: K is the slice length
   c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda + koff), 0, rows_a * lda * 2, 0x00020000);
-  c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb + koff), 0, BN * ldb * 2, 0x00020000);
+  if constexpr (SW) {
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * (BN / 2) * ldb + koff), 0, (BN / 2) * ldb * 2,
+                                             0x00020000);
+    c.rb2 = __builtin_amdgcn_make_buffer_rsrc((void*)(B + ((long)N / 2 + (long)tn * (BN / 2)) * ldb + koff), 0,
+                                              (BN / 2) * ldb * 2, 0x00020000);
+  } else {
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb + koff), 0, BN * ldb * 2, 0x00020000);
+  }
   c.sa32 = 32 * lda * 2;
   c.sb32 = 32 * ldb * 2;
   {
@@ -320,10 +347,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // prologue: K-tiles 0 and 1 into stages 0 and 1, k-sub 0 of K-tile 0 into f0
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BN, AUX>(c, 0, j, 0);
+  for (int j = 0; j < ND; ++j) dma_any<BN, X>(c, 0, j, 0);
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BN, AUX>(c, 1, j, k1);
+  for (int j = 0; j < ND; ++j) dma_any<BN, X>(c, 1, j, k1);
   if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
   bar();
@@ -359,6 +386,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int n = 0; n < NB; ++n)
         *(f32x4*)(part + (long)row * N + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4) = acc[i][n];
+    }
+    return;
+  }
+  if constexpr (SW) {
+    // out fragment q (16 columns) = silu(gate fragment ng) * up fragment ng + 2,
+    // ng = 4 (q / 2) + q % 2; pairs (q, q + 1) share one 16-B store per lane
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+      unsigned short* crow = C + (long)row * ldc;
+      const bool row_ok = !BNDM || row < M;
+#pragma unroll
+      for (int q = 0; q < NB / 2; q += 2) {
+        uint2 o[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ng = 4 * ((q + h) / 2) + (q + h) % 2;
+          const f32x4 g = acc[i][ng], u = acc[i][ng + 2];
+          float r[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float gf = bf2f(f2bf(g[e]));
+            r[e] = gf / (1.0f + __expf(-gf)) * bf2f(f2bf(u[e]));
+          }
+          o[h].x = pack_bf16x2(r[0], r[1]);
+          o[h].y = pack_bf16x2(r[2], r[3]);
+        }
+        auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+        auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+        const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+        const int col0 = tn * (BN / 2) + c.wc * (BN / 4) + q * 16;
+        if (row_ok) *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
+      }
     }
     return;
   }

@@ -500,3 +500,23 @@ def test_timing_probes_refuse_without_opt_in():
         experiments.gemm_nt(a, a, "probe_l2")
     experiments.gemm_nt(a, a, "probe_l2", allow_wrong=True)  # runs, result undefined
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("M,I,K,bn", [(256, 1024, 4096, 128), (200, 768, 1024, 128), (512, 1024, 2048, 256),
+                                      (130, 512, 640, 256)])
+def test_gemm_w4x_swiglu_epilogue(M, I, K, bn):
+    """SwiGLU in the four-wave kernel's epilogue == the gate|up GEMM followed by
+    silu_mul, bit for bit (same roundings), and close to fp32 torch."""
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu
+    from kgs.ops.transformer import silu_mul
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * K ** -0.5 *
+         torch.linspace(0.5, 1.5, K, device=DEV)).bfloat16()
+    fused = gemm_nt_w4x_swiglu(a, w, bn=bn)
+    assert fused.shape == (M, I)
+    ref = silu_mul(gemm_nt_w4x(a, w, bn=bn, nslice=1))
+    assert torch.equal(fused, ref)
+    gu = a.float() @ w.float().T
+    r32 = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    assert ((fused.float() - r32).abs().max() / r32.abs().max()).item() < 2e-2
