@@ -23,6 +23,7 @@
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
+#   serve_sweep  offline serving at batch 128 / 512, fp8 KV, fp8 prefill + fp8 KV (batch 256 and 512)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${1:?usage: gpu.sh OUT step...}
@@ -71,6 +72,13 @@ step() {
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
             --out "$O/w4x_sweep.jsonl" ;;
+        serve_sweep)
+            local SB="python -u -m kgs.serve bench --input-len 512 --output-len 256 --max-model-len 2048"
+            run serve_b128 300 $SB --requests 128 --max-batch 128 &&
+                run serve_b512 300 $SB --requests 512 --max-batch 512 &&
+                run serve_b256_kv8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 &&
+                run serve_b256_f8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 --prefill-weights fp8 &&
+                run serve_b512_f8 300 $SB --requests 512 --max-batch 512 --kv-cache-dtype fp8 --prefill-weights fp8 ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac
