@@ -375,7 +375,8 @@ class AmdGpuDevicePlugin:
                 if self._server is not None:
                     self._server.stop(0).wait()
                     self._server = None
-                self._stop.clear()
+                if self._stop.is_set():  # stop() raced the restart: do not come back up
+                    break
                 self.start()
                 self._wait_kubelet_and_register()
                 kubelet_id = self._kubelet_id()
