@@ -515,7 +515,10 @@ __device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, f
 // One wave per (sequence, KV head, context split). With nsplit > 1 the partial (m, l, O)
 // go to a workspace and the split that arrives last (agent-scope ticket per
 // (sequence, KV head)) merges them -- no separate reduction launch.
-template <bool KV8>
+// PIPE (small grids, e.g. batch 1-16): the next page's loads are issued before
+// the current page is computed. With a few dozen waves on the chip no other wave
+// hides a page's HBM latency, so a split otherwise pays it once per page.
+template <bool KV8, bool PIPE = false>
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int lane = threadIdx.x;
   const int G = a.H / a.HKV;
@@ -603,13 +606,27 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, acc[dt], 0, 0, 0);
       }
     };
-    // one page at a time: the loads of other waves on the SIMD hide this one's
-    // latency (a two-register-set pipeline measured slower: 208 VGPRs cost a
-    // wave of occupancy, 47 -> 59 us at batch 64 x 1024)
-    for (int pi = p0; pi < p1; ++pi) {
-      bf16x8 kf[8], vf[8];
-      load_page(kf, vf, pi);
-      page(kf, vf, pi);
+    if constexpr (PIPE) {
+      // two register sets: page pi + 1 is in flight while page pi is computed
+      bf16x8 ka[8], va[8], kb[8], vb[8];
+      load_page(ka, va, p0);
+      for (int pi = p0; pi < p1; pi += 2) {
+        if (pi + 1 < p1) load_page(kb, vb, pi + 1);
+        page(ka, va, pi);
+        if (pi + 1 < p1) {
+          if (pi + 2 < p1) load_page(ka, va, pi + 2);
+          page(kb, vb, pi + 1);
+        }
+      }
+    } else {
+      // one page at a time: the loads of other waves on the SIMD hide this one's
+      // latency (a two-register-set pipeline measured slower here: 208 VGPRs cost
+      // a wave of occupancy, 47 -> 59 us at batch 64 x 1024)
+      for (int pi = p0; pi < p1; ++pi) {
+        bf16x8 kf[8], vf[8];
+        load_page(kf, vf, pi);
+        page(kf, vf, pi);
+      }
     }
   }
   lsum = wsum16(lsum);
@@ -646,7 +663,47 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
     }
   }
   last = __shfl(last, 0, 64);
-  if (!last || n >= G) return;
+  if (!last) return;
+  if constexpr (PIPE) {
+    // one pass with an online rescale (as over pages), the (m, l, O) loads of
+    // four splits in flight together: the serial two-pass loop below pays an
+    // L2 round trip per split (it stays for the large-grid variant, whose
+    // occupancy the 128 extra VGPRs would cost)
+    if (n >= G) return;
+    float M = -INFINITY, L = 0.f;
+    f32x4v o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int s0 = 0; s0 < a.nsplit; s0 += 4) {
+      float mv[4], lv[4];
+      f32x4v part[4][8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mv[j] = -INFINITY;
+        lv[j] = 0.f;
+        if (s0 + j < a.nsplit) {
+          mv[j] = ld1_sc1(mlr, (unsigned)((row + s0 + j) * 8));
+          lv[j] = ld1_sc1(mlr, (unsigned)((row + s0 + j) * 8 + 4));
+#pragma unroll
+          for (int dt = 0; dt < 8; ++dt)
+            part[j][dt] = ld_sc1(por, (unsigned)(((row + s0 + j) * HD + 16 * dt + 4 * g) * 4));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (lv[j] <= 0.f) continue;
+        const float mn = fmaxf(M, mv[j]);
+        const float sc = __builtin_amdgcn_exp2f(M - mn), f = __builtin_amdgcn_exp2f(mv[j] - mn);
+        L = L * sc + f * lv[j];
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[dt] = o[dt] * sc + f * part[j][dt];
+        M = mn;
+      }
+    }
+    store_o(op, o, L > 0.f ? 1.f / L : 0.f);
+    return;
+  }
+  if (n >= G) return;
   float M = -INFINITY;
   for (int s2 = 0; s2 < a.nsplit; ++s2) M = fmaxf(M, ld1_sc1(mlr, (unsigned)((row + s2) * 8)));
   float L = 0.f;
@@ -875,10 +932,16 @@ KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int
   const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
              pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
-  if (kv8)
-    hipLaunchKernelGGL(paged_decode<true>, dim3((unsigned)nwg), dim3(64), 0, s, a);
-  else
-    hipLaunchKernelGGL(paged_decode<false>, dim3((unsigned)nwg), dim3(64), 0, s, a);
+  // a grid of at most 2 waves per CU cannot hide page latency across waves:
+  // pipeline inside the wave there
+  const bool pipe = nwg <= 512;
+  if (kv8) {
+    if (pipe) hipLaunchKernelGGL((paged_decode<true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((paged_decode<true, false>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+  } else {
+    if (pipe) hipLaunchKernelGGL((paged_decode<false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((paged_decode<false, false>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+  }
   if (nsplit > 1 && !merge)
     hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
                        ldo);

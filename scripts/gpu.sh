@@ -18,7 +18,7 @@
 #   overlap      GEMM vs comm-kernel overlap measurement (bench/overlap.py)
 #   overlap_trace  kernel trace of the overlap run
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
-#   decode_trace kernel trace of batch-256 decode
+#   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
@@ -68,6 +68,11 @@ step() {
         decode_trace) run decode_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace" -o d \
             -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 --max-batch 256 \
             --max-model-len 2048 ;;
+        decode_trace_b1) run decode_trace_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace1" \
+            -o d -- python3 -m kgs.serve bench --requests 2 --input-len 512 --output-len 64 --max-batch 1 \
+            --max-model-len 2048 ;;
+        serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
+            --max-batch 1 --max-model-len 2048 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
