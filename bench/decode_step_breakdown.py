@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel breakdown of one decode step from a rocprofv3 kernel trace of
-``python -m kgs.serve bench`` (steps are delimited by the sampler's argmax).
+``python -m kgs.serve bench`` (steps are delimited by the sampler's argmax:
+torch's reduce or ``kgs::tfm::argmax_rows``).
 
   python bench/decode_step_breakdown.py gpurun_out/prof_decode/b1/d_kernel_trace.csv [--step -3]
 """
@@ -15,7 +16,7 @@ def main(argv=None) -> int:
     ap.add_argument("--step", type=int, default=-3, help="which argmax-delimited step (python index)")
     a = ap.parse_args(argv)
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "ArgMax" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "ArgMax" in r["Kernel_Name"] or "argmax_rows" in r["Kernel_Name"]]
     s0, s1 = idx[a.step - 1], idx[a.step]
     seg = rows[s0 + 1:s1 + 1]
     agg = collections.defaultdict(lambda: [0, 0])

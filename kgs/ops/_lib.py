@@ -82,6 +82,7 @@ _SIGS = {
     "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p, _c_int,
                                                   _c_void_p], _c_int),
     "kgs_gemm_bf16_nt_w4x_swiglu": ([_c_void_p] * 3 + [_c_int] * 7 + [_c_void_p], _c_int),
+    "kgs_argmax_rows_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_long, _c_void_p], _c_int),
     "kgs_splitk_add_rmsnorm_bf16": ([_c_void_p, _c_int] + [_c_void_p] * 3 + [_c_int, _c_int, _c_long, _c_long,
                                                                               ctypes.c_float, _c_void_p], _c_int),
     "kgs_paged_decode_bf16": ([_c_void_p] * 8 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_int, _c_void_p],

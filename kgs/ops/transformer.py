@@ -79,6 +79,18 @@ def splitk_add_rmsnorm(partials: torch.Tensor, x: torch.Tensor, w: torch.Tensor,
     return y
 
 
+def argmax_rows(x: torch.Tensor) -> torch.Tensor:
+    """``x.argmax(dim=-1)`` for bf16 GPU logits ``[rows, cols]`` (cols % 8 == 0):
+    int64, the first index of each row's maximum (NaN counts as the maximum)."""
+    _need(x, "x")
+    rows, cols = x.shape
+    out = torch.empty(rows, dtype=torch.int64, device=x.device)
+    rc = _lib.lib().kgs_argmax_rows_bf16(x.data_ptr(), out.data_ptr(), rows, cols, x.stride(0),
+                                         _lib.stream_handle(x.device))
+    _lib.check(rc, "argmax_rows")
+    return out
+
+
 def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
     return add_rmsnorm(x, None, w, eps)
 

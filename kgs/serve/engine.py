@@ -356,7 +356,7 @@ class LLMEngine:
         logits = self._penalize(ids, logits)
         ps = [self.requests[int(r)].params for r in ids]
         if all(p.temperature <= 0 for p in ps):
-            return logits.argmax(dim=-1)
+            return self._argmax(logits)
         lf = logits.float()
         temp = torch.tensor([max(p.temperature, 1e-5) for p in ps], device=lf.device)[:, None]
         lf = lf / temp
@@ -387,4 +387,15 @@ class LLMEngine:
                     req.gen = torch.Generator(device=lf.device).manual_seed(int(req.params.seed))
                 sampled[j] = torch.multinomial(probs[j], 1, generator=req.gen)[0]
         greedy = torch.tensor([p.temperature <= 0 for p in ps], device=lf.device)
-        return torch.where(greedy, logits.argmax(dim=-1), sampled)
+        return torch.where(greedy, self._argmax(logits), sampled)
+
+    def _argmax(self, logits: torch.Tensor) -> torch.Tensor:
+        """Greedy pick: the native row argmax for bf16 GPU logits of the kgs
+        backend (torch's generic reduce takes ~40 us for one 128k-vocab row)."""
+        if self.backend == "kgs" and logits.is_cuda and logits.dtype == torch.bfloat16 and \
+                logits.dim() == 2 and logits.shape[-1] % 8 == 0 and logits.stride(-1) == 1 and \
+                logits.stride(0) % 8 == 0 and logits.data_ptr() % 16 == 0:
+            from kgs.ops.transformer import argmax_rows
+
+            return argmax_rows(logits)
+        return logits.argmax(dim=-1)

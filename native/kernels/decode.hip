@@ -169,7 +169,9 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   using C = SkinnyCfg<MT, KC_>;
   constexpr int KC = C::KC;
   // W ring depth in k-steps (divides KC); fp8 fragments are half the bytes, so
-  // twice the depth keeps the same bytes in flight
+  // twice the depth keeps the same bytes in flight (a 16-deep bf16 ring at
+  // batch 1 measured the same per launch: the fixed launch / split-K costs, not
+  // the bytes in flight, set a batch-1 launch's time)
   constexpr int PF = KC < (W8 ? 16 : 8) ? KC : (W8 ? 16 : 8);
   // the only __shared__ object (a second one can make hipcc drain vmcnt before
   // every ds_read, cdna_hip_programming.md s5 trap 4a); the split-K "last
@@ -352,7 +354,17 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     for (int r = 0; r < R; ++r) {
       const int n = 16 * (nt0 + r) + 4 * g;
       f32x4v t = f32x4v{0.f, 0.f, 0.f, 0.f};
-      for (int sp = 0; sp < ksplit; ++sp) t += ld_sc1(wr, (unsigned)((sp * sstride + ms * mstride + n) * 4));
+      // four slabs' loads in flight at a time (a load-add chain pays one L2
+      // round trip per slab); summed in slab order as before
+      for (int sp0 = 0; sp0 < ksplit; sp0 += 4) {
+        f32x4v pv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (sp0 + j < ksplit) pv[j] = ld_sc1(wr, (unsigned)(((sp0 + j) * sstride + ms * mstride + n) * 4));
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (sp0 + j < ksplit) t += pv[j];
+      }
       emit(t, m, r);
     }
   }

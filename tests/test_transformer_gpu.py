@@ -223,3 +223,20 @@ def test_gemm_fp8_rows(m, n, k):
     ref = (a8.float() * sa[:, None]) @ (b8.float() * sb).T + bias.float()
     rel = ((got.float() - ref).abs().max() / ref.abs().max()).item()
     assert rel < 1e-2, rel
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 128256), (7, 1024), (256, 128256), (3, 8)])
+def test_argmax_rows_matches_torch(rows, cols):
+    """Native greedy pick == torch.argmax: first index of the maximum (ties are
+    planted), NaN counts as the maximum."""
+    from kgs.ops.transformer import argmax_rows
+
+    x = torch.randn(rows, cols, device="cuda").bfloat16()
+    x[0, cols // 3] = x[0, cols - 1] = 40.0  # tie: the first index wins
+    if rows > 2:
+        x[2, cols // 2] = float("nan")
+        x[2, cols // 4] = 50.0
+    got = argmax_rows(x)
+    assert got.dtype == torch.int64
+    assert torch.equal(got, x.argmax(dim=-1))
+    assert int(got[0]) == cols // 3
