@@ -128,7 +128,8 @@ class LlamaModel:
     def forward(self, tokens: torch.Tensor) -> torch.Tensor:
         if self.backend == "torch":
             return self._forward_torch(tokens)
-        from kgs.ops.transformer import add_rmsnorm, attention_qkv, rope_qkv_, rope_tables, silu_mul
+        from kgs.ops.gemm import gemm_swiglu
+        from kgs.ops.transformer import add_rmsnorm, attention_qkv, rope_qkv_, rope_tables
 
         cfg = self.cfg
         b, s = tokens.shape
@@ -143,7 +144,7 @@ class LlamaModel:
             rope_qkv_(qkv, cos, sin, nh + nkv, hd, s)
             a = attention_qkv(qkv, b, s, nh, nkv, head_dim=hd, causal=True)
             y = add_rmsnorm(x, L["o"](a), L["ln2"], cfg.eps)  # x += o-proj
-            act = silu_mul(L["gate_up"](y))
+            act = gemm_swiglu(y, L["gate_up"].w)  # SwiGLU in the GEMM epilogue
             nxt = self.layers[i + 1]["ln1"] if i + 1 < len(self.layers) else self.norm
             y = add_rmsnorm(x, L["down"](act), nxt, cfg.eps)  # x += down-proj
         return self.lm_head(y).reshape(b, s, cfg.vocab)

@@ -215,6 +215,23 @@ def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
     return out
 
 
+def gemm_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
+    """SwiGLU MLP input projection ``silu(a @ gate.T) * (a @ up.T)`` -> ``[M, I]``:
+    fused into the four-wave GEMM's epilogue (256x256 tiles; 256x128 when
+    ``2I % 256 != 0``) when the shape allows, else GEMM + ``silu_mul``. Same
+    bits either way."""
+    N, K = w_gate_up.shape
+    ok = (a.dim() == 2 and a.dtype == torch.bfloat16 and w_gate_up.dtype == torch.bfloat16 and a.is_cuda
+          and a.stride(1) == 1 and w_gate_up.stride(1) == 1 and K % 128 == 0 and N % 128 == 0
+          and a.stride(0) % 8 == 0 and w_gate_up.stride(0) % 8 == 0 and (N // 2) % 8 == 0
+          and a.data_ptr() % 16 == 0 and w_gate_up.data_ptr() % 16 == 0 and a.shape[1] == K)
+    if ok:
+        return gemm_nt_w4x_swiglu(a, w_gate_up, bn=256 if N % 256 == 0 else 128)
+    from .transformer import silu_mul
+
+    return silu_mul(gemm_nt(a, w_gate_up))
+
+
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
 FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}

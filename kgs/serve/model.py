@@ -176,6 +176,14 @@ class ServingModel:
 
         return add_rmsnorm(x, d, w, self.cfg.eps)
 
+    def _gate_up_act(self, y, layer):
+        """Prompt-pass SwiGLU MLP input: fused into the GEMM epilogue on kgs."""
+        if self.backend == "kgs" and self.fuse_splitk:
+            from kgs.ops.gemm import gemm_swiglu
+
+            return gemm_swiglu(y, self.w[layer]["gate_up"])
+        return self._silu_mul(self._proj(y, layer, "gate_up", False))
+
     def _silu_mul(self, gu):
         if self.backend == "ref":
             i = gu.shape[1] // 2
@@ -212,7 +220,7 @@ class ServingModel:
             self._rope_cache(qkv, i, positions, slots)
             a = self._prefill_attention(qkv, seq_starts, seq_lens, padded_lens)
             y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
-            act = self._silu_mul(self._proj(y, i, "gate_up", False))
+            act = self._gate_up_act(y, i)
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             y = self._norm(x, self._proj(act, i, "down", False), nxt)
         last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
@@ -338,7 +346,7 @@ class ServingModel:
                     y = self._norm(x, d, nxt)
                 continue
             y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
-            act = self._silu_mul(self._proj(y, i, "gate_up", False))
+            act = self._gate_up_act(y, i)
             y = self._norm(x, self._proj(act, i, "down", False), nxt)
         rows = [row0 + n - 1 for row0, n, _, _, _, last in chunks if last] + list(range(n_pf, n_pf + nd))
         if not rows:

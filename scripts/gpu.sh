@@ -20,6 +20,7 @@
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
+#   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
@@ -73,6 +74,9 @@ step() {
             --max-model-len 2048 ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
             --max-batch 1 --max-model-len 2048 ;;
+        prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
+        prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
+            -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
