@@ -174,6 +174,7 @@ W4X_TUNED: dict = {
     (128, *_O): (128, 8), (192, *_O): (128, 8), (256, *_O): (128, 8), (384, *_O): (128, 4),  # 1.37/1.62/1.05/1.02
     (512, *_O): (128, 4),  # 1.10
     (192, *_GU): (128, 1), (256, *_GU): (128, 1), (512, *_GU): (256, 1),  # 1.07/1.06/1.06
+    (128, *_GU): (128, 1),  # 1.00 alone; with SwiGLU in its epilogue it also drops the silu_mul launch
     (128, *_DOWN): (128, 8), (192, *_DOWN): (128, 8), (256, *_DOWN): (128, 8), (384, *_DOWN): (128, 4),  # 2.2/2.7/1.5/1.4
     (512, *_DOWN): (128, 4),  # 1.45
 }
@@ -425,12 +426,23 @@ def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positio
 
 
 def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS, min_pages: int = 4) -> tuple[int, int]:
-    """(pages_per_split, nsplit): split each sequence's context so the grid has
-    about 8 waves per CU, but give every split at least ``min_pages`` pages (a
+    """(pages_per_split, nsplit) for a block-table width of ``max_pages``.
+
+    Fewer (sequence, KV head) groups than CUs: split each context so the grid
+    has about 8 waves per CU, every split at least ``min_pages`` pages (a
     one-page split is all launch and merge overhead: 52 us for batch 1 x 4096
-    tokens with 1-page splits, profiles/decode_kernels.md)."""
-    want = max(1, math.ceil(8 * cus / max(1, batch * kv_heads)))
-    nsplit = max(1, min(math.ceil(max_pages / min_pages), want))
+    tokens with 1-page splits, profiles/decode_kernels.md). From one group per
+    CU up, a split costs more (partial writes + the merge pass) than the extra
+    waves give back unless it keeps >= 32 pages and the grid stays <= 8 waves
+    per CU: at 528 cached tokens one split is fastest for batch 32-256
+    (batch 64: 32.7 vs 44.0 us with the old 8-waves-per-CU rule), at 2000
+    tokens two splits win at batch 32 and 128 (profiles/r2/paged_split_sweep.md)."""
+    groups = max(1, batch * kv_heads)
+    if groups < cus:
+        want = max(1, math.ceil(8 * cus / groups))
+        nsplit = max(1, min(math.ceil(max_pages / min_pages), want))
+    else:
+        nsplit = max(1, min(max_pages // 32, (8 * cus) // groups))
     pps = math.ceil(max_pages / nsplit)
     return pps, math.ceil(max_pages / pps)
 

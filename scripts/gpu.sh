@@ -72,6 +72,13 @@ step() {
         decode_trace_b1) run decode_trace_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace1" \
             -o d -- python3 -m kgs.serve bench --requests 2 --input-len 512 --output-len 64 --max-batch 1 \
             --max-model-len 2048 ;;
+        decode_trace_b64) run decode_trace_b64 300 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$O/dtrace64" -o d -- python3 -m kgs.serve bench --requests 64 --input-len 512 --output-len 32 \
+            --max-batch 64 --max-model-len 2048 ;;
+        decode_trace_b128) run decode_trace_b128 300 rocprofv3 --kernel-trace --stats --output-format csv \
+            -d "$O/dtrace128" -o d -- python3 -m kgs.serve bench --requests 128 --input-len 512 --output-len 32 \
+            --max-batch 128 --max-model-len 2048 ;;
+        paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
             --max-batch 1 --max-model-len 2048 ;;
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;

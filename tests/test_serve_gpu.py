@@ -267,7 +267,7 @@ def test_fp8_prefill_with_chunked_prefill():
 @pytest.mark.parametrize("b", [128, 256])
 def test_splitk_fused_decode_llama8b_layer(b):
     """Decode through one Llama-3-8B-shaped layer, where qkv / o / down run
-    split-K on the four-wave kernel (and, at batch 256, gate|up unsplit): with
+    split-K on the four-wave kernel (and gate|up unsplit): with
     their partials reduced inside RoPE/KV-write and add+RMSNorm and SwiGLU in
     the gate|up epilogue, the KV cache is bit-identical and the logits agree
     with the unfused launches."""
@@ -283,7 +283,7 @@ def test_splitk_fused_decode_llama8b_layer(b):
         m = ServingModel(cfg, device="cuda", num_pages=b * 2 + 8, max_model_len=256, fuse_splitk=fuse,
                          packed_decode=False)
         assert (m._splitk_route(b, 0, "qkv") is not None) == fuse
-        assert (m._swiglu_route(b) is not None) == (fuse and b == 256)
+        assert (m._swiglu_route(b) is not None) == fuse  # gate|up unsplit on the four-wave kernel at 128 / 256
         bt = torch.arange(b * 2, dtype=torch.int32, device="cuda").view(b, 2)
         g = torch.Generator(device="cuda").manual_seed(1)
         lay = m.cache.layer(0)
