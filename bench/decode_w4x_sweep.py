@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Decode-batch GEMMs on one MI355X: the four-wave kernel at tile widths 256 /
-128 with 1-8 K-slices (kgs.ops.gemm.gemm_nt_w4x) against hipBLASLt
+128 (and 128-row tiles for batches <= 128) with 1-8 K-slices (kgs.ops.gemm.gemm_nt_w4x) against hipBLASLt
 (torch.matmul) and the 8-wave split-K kernel, on the Llama-3-8B projection
 shapes at serving batches. Weights stream from HBM (a fresh weight copy per
 call rotates through a pool larger than the 256 MiB Infinity Cache), as in
@@ -40,13 +40,16 @@ def main():
             out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             ref = (x.float() @ Ws[0].float().T)
             cands = {"hipblaslt": lambda w: torch.matmul(x, w.T, out=out)}
-            for bn in (256, 128):
-                if N % bn:
-                    continue
-                for ns in (1, 2, 4, 8):
-                    if (K // ns) % 128 or K % ns:
+            for bm in ((256, 128) if M <= 128 else (256,)):
+                for bn in (256, 128):
+                    if N % bn:
                         continue
-                    cands[f"w4_bn{bn}_s{ns}"] = (lambda w, bn=bn, ns=ns: gemm_nt_w4x(x, w, bn=bn, nslice=ns, out=out))
+                    for ns in (1, 2, 4, 8):
+                        if (K // ns) % 128 or K % ns:
+                            continue
+                        tag = f"w4_bn{bn}_s{ns}" if bm == 256 else f"w4_bm128_bn{bn}_s{ns}"
+                        cands[tag] = (lambda w, bn=bn, ns=ns, bm=bm: gemm_nt_w4x(x, w, bn=bn, nslice=ns, out=out,
+                                                                                 bm=bm))
             for ns in (4, 8):
                 if (K // ns) % 8 == 0:
                     cands[f"pp_splitk{ns}"] = (lambda w, ns=ns: gemm_nt_splitk(x, w, ns, out=out))

@@ -40,7 +40,7 @@ _SIGS = {
     "kgs_gemm_bf16_nt_bounded_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_splitk": ([_c_void_p] * 4 + [_c_int] * 7 + [_c_void_p], _c_int),
-    "kgs_gemm_bf16_nt_w4x": ([_c_void_p] * 4 + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_w4x": ([_c_void_p] * 4 + [_c_int] * 9 + [_c_void_p], _c_int),
     "kgs_gemm_fp8_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [ctypes.c_float, _c_int, _c_int,
                                                                                      _c_void_p], _c_int),
     "kgs_gemm_fp8_nt_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 7, _c_int),
@@ -81,7 +81,7 @@ _SIGS = {
     "kgs_skinny_variant_geometry": ([_c_int, _c_int] + [ctypes.POINTER(_c_int)] * 3, _c_int),
     "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p, _c_int,
                                                   _c_void_p], _c_int),
-    "kgs_gemm_bf16_nt_w4x_swiglu": ([_c_void_p] * 3 + [_c_int] * 7 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_w4x_swiglu": ([_c_void_p] * 3 + [_c_int] * 8 + [_c_void_p], _c_int),
     "kgs_argmax_rows_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_long, _c_void_p], _c_int),
     "kgs_splitk_add_rmsnorm_bf16": ([_c_void_p, _c_int] + [_c_void_p] * 3 + [_c_int, _c_int, _c_long, _c_long,
                                                                               ctypes.c_float, _c_void_p], _c_int),

@@ -163,26 +163,34 @@ SPLITK_TUNED: dict = {
 }
 SPLITK_WS_FLOATS = 8 * 256 * 8192  # the largest entry above (M x N x slices)
 
-# Decode batches 128-512 on the four-wave kernel (kgs.ops.gemm.gemm_nt_w4x):
-# (tile width, K slices) per (batch bucket, N, K) where it beat hipBLASLt and
-# the 8-wave split-K, weights streamed from HBM (bench/decode_w4x_sweep.py,
-# profiles/r2/decode_w4x_sweep.jsonl; speed-up vs hipBLASLt in the comments).
-# Buckets not listed stay on the routes below.
-_W4X_BUCKETS = (128, 192, 256, 384, 512)
+# Decode batches 49-512 on the four-wave kernel (kgs.ops.gemm.gemm_nt_w4x):
+# (tile width, K slices, tile height) per (batch bucket, N, K) where it beat
+# hipBLASLt and the 8-wave split-K, weights streamed from HBM
+# (bench/decode_w4x_sweep.py, profiles/r2/decode_w4x_sweep.jsonl and
+# decode_w4x_bm128.jsonl; speed-up vs hipBLASLt in the comments). Batches up to
+# 128 take 128-row tiles (no MFMAs on padding rows: qkv / o / down 3-20 %
+# faster than 256-row tiles at 64-128 rows, and ahead of the fused skinny
+# GEMMs from 49 rows up). Buckets not listed stay on the routes below.
+_W4X_BUCKETS = (64, 96, 128, 192, 256, 384, 512)
+W4X_MIN_BATCH = 49
 W4X_TUNED: dict = {
-    (128, *_QKV): (128, 4), (192, *_QKV): (128, 4), (256, *_QKV): (128, 4), (384, *_QKV): (128, 2),  # 1.27/1.39/1.49/1.06
-    (128, *_O): (128, 8), (192, *_O): (128, 8), (256, *_O): (128, 8), (384, *_O): (128, 4),  # 1.37/1.62/1.05/1.02
-    (512, *_O): (128, 4),  # 1.10
-    (192, *_GU): (128, 1), (256, *_GU): (128, 1), (512, *_GU): (256, 1),  # 1.07/1.06/1.06
-    (128, *_GU): (128, 1),  # 1.00 alone; with SwiGLU in its epilogue it also drops the silu_mul launch
-    (128, *_DOWN): (128, 8), (192, *_DOWN): (128, 8), (256, *_DOWN): (128, 8), (384, *_DOWN): (128, 4),  # 2.2/2.7/1.5/1.4
-    (512, *_DOWN): (128, 4),  # 1.45
+    (64, *_QKV): (128, 4, 128), (96, *_QKV): (128, 8, 128), (128, *_QKV): (128, 4, 128),  # 1.99/4.39/3.31
+    (64, *_O): (128, 8, 128), (96, *_O): (128, 8, 128), (128, *_O): (128, 8, 128),  # 4.95/2.27/2.22
+    (64, *_GU): (128, 1, 128), (96, *_GU): (128, 1, 128), (128, *_GU): (128, 1, 128),  # 1.16/1.15/1.14
+    (64, *_DOWN): (128, 8, 128), (96, *_DOWN): (128, 8, 128), (128, *_DOWN): (128, 8, 128),  # 1.75/2.07/2.29
+    (192, *_QKV): (128, 4, 256), (256, *_QKV): (128, 4, 256), (384, *_QKV): (128, 2, 256),  # 1.39/1.49/1.06
+    (192, *_O): (128, 8, 256), (256, *_O): (128, 8, 256), (384, *_O): (128, 4, 256),  # 1.62/1.05/1.02
+    (512, *_O): (128, 4, 256),  # 1.10
+    (192, *_GU): (128, 1, 256), (256, *_GU): (128, 1, 256), (512, *_GU): (256, 1, 256),  # 1.07/1.06/1.06
+    (192, *_DOWN): (128, 8, 256), (256, *_DOWN): (128, 8, 256), (384, *_DOWN): (128, 4, 256),  # 2.7/1.5/1.4
+    (512, *_DOWN): (128, 4, 256),  # 1.45
 }
 
 
 def w4x_route(m: int, n: int, k: int):
-    """(tile width, K slices) of the four-wave decode GEMM for batch m, or None."""
-    if m < 96 or m > 512:
+    """(tile width, K slices, tile height) of the four-wave decode GEMM for
+    batch m, or None."""
+    if m < W4X_MIN_BATCH or m > 512:
         return None
     b = next(x for x in _W4X_BUCKETS if m <= x)
     return W4X_TUNED.get((b, n, k))

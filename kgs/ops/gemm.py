@@ -135,10 +135,10 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
 
 
 def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1,
-                out: torch.Tensor | None = None) -> torch.Tensor:
-    """``a @ b.T`` on the four-wave kernel with a tile width of ``bn`` (256 or
-    128) columns, any M (rows past M read as zeros), over ``nslice`` K-slices
-    (fp32 partials + reduce when > 1): the decode-batch GEMM path.
+                out: torch.Tensor | None = None, bm: int = 256) -> torch.Tensor:
+    """``a @ b.T`` on the four-wave kernel with ``bm`` x ``bn`` tiles (256 or 128
+    each), any M (rows past M read as zeros), over ``nslice`` K-slices (fp32
+    partials + reduce when > 1): the decode-batch GEMM path.
     ``N % bn == 0`` and ``(K / nslice) % 128 == 0``."""
     _check_operand(a, "a")
     _check_operand(b, "b")
@@ -160,13 +160,13 @@ def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1
             ws = reserve_splitk_workspace(a.device, need)
         ws_ptr = ws.data_ptr()
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws_ptr, M, N, K, a.stride(0),
-                                         b.stride(0), out.stride(0), int(bn), int(nslice),
+                                         b.stride(0), out.stride(0), int(bn), int(nslice), int(bm),
                                          _lib.stream_handle(a.device))
-    _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} bn{bn}/{nslice}]")
+    _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return out
 
 
-def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int) -> torch.Tensor:
+def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int, bm: int = 256) -> torch.Tensor:
     """The split-K four-wave GEMM WITHOUT its reduce: returns the fp32 partial
     products ``[nslice, M, N]`` (a view of the per-GPU split-K workspace, valid
     until the next split-K call on the stream) for a fused consumer --
@@ -188,13 +188,13 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int)
             raise RuntimeError("gemm_nt_w4x_partials: reserve_splitk_workspace() before hipGraph capture")
         ws = reserve_splitk_workspace(a.device, need)
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), None, ws.data_ptr(), M, N, K, a.stride(0),
-                                         b.stride(0), N, int(bn), int(nslice), _lib.stream_handle(a.device))
-    _lib.check(rc, f"gemm_nt_w4x_partials[{M}x{N}x{K} bn{bn}/{nslice}]")
+                                         b.stride(0), N, int(bn), int(nslice), int(bm), _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_w4x_partials[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return ws[:need].view(nslice, M, N)
 
 
 def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
-                       out: torch.Tensor | None = None) -> torch.Tensor:
+                       out: torch.Tensor | None = None, bm: int = 256) -> torch.Tensor:
     """``silu(a @ gate.T) * (a @ up.T)`` for a fused gate|up weight ``[2I, K]``
     (gate rows first) on the four-wave kernel, the SwiGLU applied in the GEMM
     epilogue: returns ``[M, I]`` (both products rounded to bf16 first, as
@@ -209,9 +209,9 @@ def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
     if out is None:
         out = torch.empty((M, N // 2), dtype=torch.bfloat16, device=a.device)
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x_swiglu(a.data_ptr(), w_gate_up.data_ptr(), out.data_ptr(), M, N, K,
-                                                a.stride(0), w_gate_up.stride(0), out.stride(0), int(bn),
+                                                a.stride(0), w_gate_up.stride(0), out.stride(0), int(bn), int(bm),
                                                 _lib.stream_handle(a.device))
-    _lib.check(rc, f"gemm_nt_w4x_swiglu[{M}x{N}x{K} bn{bn}]")
+    _lib.check(rc, f"gemm_nt_w4x_swiglu[{M}x{N}x{K} {bm}x{bn}]")
     return out
 
 

@@ -211,7 +211,7 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-fuse-splitk", action="store_true",
                     help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
-    ap.add_argument("--fused-max-batch", type=int, default=64,
+    ap.add_argument("--fused-max-batch", type=int, default=48,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",
                     help="fp8 = weight-only fp8 decode GEMMs (W8A16); the headline is bf16")

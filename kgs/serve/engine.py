@@ -68,7 +68,7 @@ class EngineConfig:
     max_model_len: int = 8192
     eos_token_id: int = 2
     cuda_graphs: bool = True
-    fused_max_batch: int = 64         # decode batches up to this use the fused skinny-GEMM layer (measured crossover)
+    fused_max_batch: int = 48         # decode batches up to this use the fused skinny-GEMM layer; above: four-wave GEMMs (measured crossover)
     decode_weights: str = "bf16"      # "fp8": weight-only fp8 decode copies (W8A16)
     kv_cache_dtype: str = "bf16"      # "fp8": e4m3 KV pages
     chunked_prefill: int = 0          # > 0: mixed steps of at most this many rows (prompt chunks + decodes)

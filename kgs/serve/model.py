@@ -47,7 +47,7 @@ from kgs.ops import decode as D
 
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
-                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 64,
+                 num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 48,
                  decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True,
                  prefill_weights: str = "bf16", fuse_splitk: bool = True):
         if cfg.head_dim != D.HEAD_DIM:
@@ -121,7 +121,7 @@ class ServingModel:
             if route is not None:
                 from kgs.ops.gemm import gemm_nt_w4x
 
-                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1])
+                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1], bm=route[2])
         if decode:
             ns = D.splitk_slices(m, w.shape[0], w.shape[1])
             if ns == 1:
@@ -415,7 +415,7 @@ class ServingModel:
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
             if rg:
-                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], rg[0])
+                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], bn=rg[0], bm=rg[2])
             else:
                 act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm

@@ -473,17 +473,50 @@ inline void launch_splitk_reduce(const float* P, unsigned short* C, int M, int N
 }  // namespace kgs
 
 // Four-wave kernel for short-M (decode-batch) GEMMs: tile width bn (256 or 128),
+// tile height bm (256 or 128: 65-128-row batches waste no MFMAs on padding rows),
 // any M (rows past M read as zeros, stores predicated), and nslice K-slices
 // (nslice > 1: fp32 partial tiles into ws, then splitk_reduce; with C == nullptr
 // the reduce is left to a fused consumer such as kgs_splitk_add_rmsnorm_bf16 or
 // kgs_rope_cache_bf16, which read ws directly). Requirements:
 // N % bn == 0, (K / nslice) % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
+namespace {
+template <int BN, int TM>
+void launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
+                int M, int N, int ks, int lda, int ldb, int ld, int mode) {
+  using namespace kgs;
+  switch (mode) {
+    case 0: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 0>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
+                               ks, lda, ldb, ld); break;
+    case 1: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 1>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
+                               ks, lda, ldb, ld); break;
+    case 2: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 2>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
+                               ks, lda, ldb, ld); break;
+    default: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 3>), grid, dim3(256), 0, s, a, b, out, nullptr, M,
+                                N, ks, lda, ldb, ld); break;
+  }
+}
+
+template <int BN, int TM>
+void launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c, int M,
+                 int N, int K, int lda, int ldb, int ldc, bool aligned_m) {
+  using namespace kgs;
+  constexpr int BM = w4::tile_m<TM>();
+  using Kn = w4::Knobs<BM, BN>;
+  if (aligned_m)
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM, Kn::B1, Kn::R, Kn::P, Kn::ORD, 1000000>), grid, dim3(256), 0,
+                       s, a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 1, Kn::B1, Kn::R, Kn::P, Kn::ORD, 1000000>), grid, dim3(256),
+                       0, s, a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+}
+}  // namespace
+
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
-                                    int ldb, int ldc, int bn, int nslice, hipStream_t stream) {
+                                    int ldb, int ldc, int bn, int nslice, int bm, hipStream_t stream) {
   using namespace kgs;
   if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
-  if (bn != 128 && bn != 256) return KGS_ERR_ARG;
+  if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
   const int ks = K / nslice;
   if (N % bn || ks % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
@@ -493,31 +526,18 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
-  const int ntm = (M + 255) / 256;
+  const int ntm = (M + bm - 1) / bm;
   const dim3 grid(ntm * (N / bn) * nslice);
-  const bool aligned_m = M % 256 == 0;
-#define KGS_W4X(BN, MODE, OUT, LDC)                                                                                \
-  hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, MODE>), grid, dim3(256), 0, stream, a, b, OUT, nullptr, M, N, ks, \
-                     lda, ldb, LDC)
   unsigned short* out = nslice > 1 ? (unsigned short*)ws : c;
   const int ld = nslice > 1 ? N : ldc;
-  const int mode = (aligned_m ? 0 : 1) | (nslice > 1 ? 2 : 0);
-  if (bn == 256) {
-    switch (mode) {
-      case 0: KGS_W4X(256, 0, out, ld); break;
-      case 1: KGS_W4X(256, 1, out, ld); break;
-      case 2: KGS_W4X(256, 2, out, ld); break;
-      default: KGS_W4X(256, 3, out, ld); break;
-    }
+  const int mode = (M % bm == 0 ? 0 : 1) | (nslice > 1 ? 2 : 0);
+  if (bm == 256) {
+    if (bn == 256) launch_w4x<256, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    else launch_w4x<128, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
   } else {
-    switch (mode) {
-      case 0: KGS_W4X(128, 0, out, ld); break;
-      case 1: KGS_W4X(128, 1, out, ld); break;
-      case 2: KGS_W4X(128, 2, out, ld); break;
-      default: KGS_W4X(128, 3, out, ld); break;
-    }
+    if (bn == 256) launch_w4x<256, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    else launch_w4x<128, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
   }
-#undef KGS_W4X
   if (nslice > 1 && c != nullptr) launch_splitk_reduce(ws, c, M, N, ldc, nslice, stream);
   return (int)hipGetLastError();
 }
@@ -525,30 +545,28 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
 // SwiGLU decode GEMM on the four-wave kernel: B is a fused gate|up weight
 // [N = 2I, K] (gate rows first); C[M, I] = silu(A . gate^T) * (A . up^T) with
 // both products rounded to bf16 first (the roundings of gemm + silu_mul). Any
-// M; N % bn == 0, K % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
+// M; tiles bm x bn (256 / 128 each); N % bn == 0, K % 128 == 0, lda/ldb/ldc % 8,
+// 16-B aligned pointers.
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C, int M, int N, int K, int lda,
-                                           int ldb, int ldc, int bn, hipStream_t stream) {
+                                           int ldb, int ldc, int bn, int bm, hipStream_t stream) {
   using namespace kgs;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N / 2) return KGS_ERR_SHAPE;
-  if (bn != 128 && bn != 256) return KGS_ERR_ARG;
+  if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
   if (N % bn || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
   if ((long)lda * 512 >= (1L << 31) || (long)ldb * 512 >= (1L << 31)) return KGS_ERR_SHAPE;
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
-  const dim3 grid(((M + 255) / 256) * (N / bn));
-  const bool aligned_m = M % 256 == 0;
-#define KGS_W4SW(BN, MODE)                                                                                      \
-  hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, MODE, w4::Knobs<BN>::B1, w4::Knobs<BN>::R, w4::Knobs<BN>::P, \
-                                     w4::Knobs<BN>::ORD, 1000000>),                                             \
-                     grid, dim3(256), 0, stream, a, b, c, nullptr, M, N, K, lda, ldb, ldc)
-  if (bn == 256) {
-    if (aligned_m) KGS_W4SW(256, 0); else KGS_W4SW(256, 1);
+  const dim3 grid(((M + bm - 1) / bm) * (N / bn));
+  const bool aligned_m = M % bm == 0;
+  if (bm == 256) {
+    if (bn == 256) launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    else launch_w4sw<128, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
   } else {
-    if (aligned_m) KGS_W4SW(128, 0); else KGS_W4SW(128, 1);
+    if (bn == 256) launch_w4sw<256, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    else launch_w4sw<128, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
   }
-#undef KGS_W4SW
   return (int)hipGetLastError();
 }
 

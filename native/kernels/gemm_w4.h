@@ -47,6 +47,9 @@
 //   MODE bit 1  split-K: gridDim.x = tiles x slices; slice s computes K columns
 //               [s K, (s + 1) K) and stores an fp32 partial tile to
 //               ((float*)C)[s][M][N] for kgs::splitk_reduce.
+//   MODE bit 3  128-row tiles (BM 128): each wave owns 64 x BN/2 (4 A fragments
+//               per k-sub). For decode batches of 65-128 rows a 256-row tile
+//               spends half its MFMAs on rows past M; this one does not.
 //   X digit 10^6  SwiGLU: B is a fused gate|up weight of N = 2I rows (gate rows
 //               [0, I), up rows [I, 2I)). A tile stages gate and up rows in
 //               alternating 32-row DMA groups (gate block tn BN/2 .., up block
@@ -58,25 +61,27 @@
 namespace kgs {
 namespace w4 {
 
-constexpr int BM = 256, BK = 64;
+constexpr int BK = 64;
 constexpr int GM = 4;  // tile-group height (production choice)
 
-template <int BN>
+template <int BM, int BN>
 struct Shape {
   static_assert(BN == 256 || BN == 128, "BN must be 256 or 128");
+  static_assert(BM == 256 || BM == 128, "BM must be 256 or 128");
+  static constexpr int MA = BM / 32;         // A fragments per wave per k-sub (8 or 4)
   static constexpr int NB = BN / 32;         // B fragments per wave per k-sub (8 or 4)
-  static constexpr int OPA = BM * BK * 2;    // A operand of one stage: 32 KiB
+  static constexpr int OPA = BM * BK * 2;    // A operand of one stage: 32 or 16 KiB
   static constexpr int OPB = BN * BK * 2;    // B operand of one stage: 32 or 16 KiB
   static constexpr int STAGE = OPA + OPB;
   static constexpr int LDS_BYTES = 2 * STAGE;
-  static constexpr int HM = 8 * NB;          // MFMAs per k-sub
+  static constexpr int HM = MA * NB;         // MFMAs per k-sub
   static constexpr int KM = 2 * HM;          // MFMAs per K-step
-  static constexpr int NR = 8 + NB;          // fragment reads per k-sub
+  static constexpr int NR = MA + NB;         // fragment reads per k-sub
 };
 
-// DMA instructions per wave per stage: A 256 rows / (8 rows x 4 waves) = 8, B BN / 32
-template <int BN>
-constexpr int dma_per_stage() { return 8 + BN / 32; }
+// DMA instructions per wave per stage: A BM rows / (8 rows x 4 waves), B BN / 32
+template <int BM, int BN>
+constexpr int dma_per_stage() { return BM / 32 + BN / 32; }
 
 struct Ctx {
   char* smem;
@@ -89,9 +94,9 @@ struct Ctx {
   int nt;
 };
 
-template <int NB>
+template <int MA, int NB>
 struct Frag {
-  bf16x8 a[8];
+  bf16x8 a[MA];
   bf16x8 b[NB];
 };
 
@@ -101,13 +106,13 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// DMA instruction j of operand OP (0 = A: j < 8, 1 = B: j < BN/32) for the K-tile
-// starting at k0 into stage st: rows j*32 + w*8 + lane/8, 1 KiB = 8 rows of 128 B.
-// AUX: cache-policy bits of the load (0 = default; 16 = sc1). SW: SwiGLU
-// staging of B (groups alternate gate / up, see the MODE notes above).
-template <int BN, int OP, int AUX = 0, bool SW = false>
+// DMA instruction j of operand OP (0 = A: j < BM/32, 1 = B: j < BN/32) for the
+// K-tile starting at k0 into stage st: rows j*32 + w*8 + lane/8, 1 KiB = 8 rows
+// of 128 B. AUX: cache-policy bits of the load (0 = default; 16 = sc1). SW:
+// SwiGLU staging of B (groups alternate gate / up, see the MODE notes above).
+template <int BM, int BN, int OP, int AUX = 0, bool SW = false>
 __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
-  using S = Shape<BN>;
+  using S = Shape<BM, BN>;
   char* dst = c.smem + st * S::STAGE + OP * S::OPA + (j * 4 + c.w) * 1024;
   if constexpr (OP == 1 && SW) {
     const int so = (j >> 1) * c.sb32 + k0 * 2;
@@ -120,22 +125,23 @@ __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
 }
 
 // X: the knob bag of the kernel template (AUX = X / 100 % 100, SW = X / 10^6 % 10)
-template <int BN, int X>
+template <int BM, int BN, int X>
 __device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
   constexpr int AUX = (X / 100) % 100;
   constexpr bool SW = (X / 1000000) % 10 != 0;
-  if (j < 8) dma<BN, 0, AUX>(c, st, j, k0); else dma<BN, 1, AUX, SW>(c, st, j - 8, k0);
+  constexpr int JA = BM / 32;
+  if (j < JA) dma<BM, BN, 0, AUX>(c, st, j, k0); else dma<BM, BN, 1, AUX, SW>(c, st, j - JA, k0);
 }
 
 __device__ __forceinline__ bf16x8 frag(const char* p) { return *(const bf16x8*)p; }
 
-template <int BN, int SUB>
+template <int BM, int BN, int SUB>
 __device__ __forceinline__ const char* abase(const Ctx& c, int st) {
-  return c.smem + st * Shape<BN>::STAGE + c.wr * 128 * 128 + (SUB ? c.ro1 : c.ro0);
+  return c.smem + st * Shape<BM, BN>::STAGE + c.wr * (BM / 2) * 128 + (SUB ? c.ro1 : c.ro0);
 }
-template <int BN, int SUB>
+template <int BM, int BN, int SUB>
 __device__ __forceinline__ const char* bbase(const Ctx& c, int st) {
-  return c.smem + st * Shape<BN>::STAGE + Shape<BN>::OPA + c.wc * (BN / 2) * 128 + (SUB ? c.ro1 : c.ro0);
+  return c.smem + st * Shape<BM, BN>::STAGE + Shape<BM, BN>::OPA + c.wc * (BN / 2) * 128 + (SUB ? c.ro1 : c.ro0);
 }
 
 // One MFMA on an accumulator pinned to AGPRs: the tied "+a" operand keeps each
@@ -145,56 +151,57 @@ __device__ __forceinline__ const char* bbase(const Ctx& c, int st) {
 // holds C[m = lane&15][n = 4*(lane>>4)+e]. asm MFMAs are invisible to the
 // hazard recognizer: the only hazard left (AGPR results read by VALU) is padded
 // before the epilogue.
-template <int NB>
-__device__ __forceinline__ void mma(f32x4 (&acc)[8][NB], const Frag<NB>& f, int i, int n) {
+template <int MA, int NB>
+__device__ __forceinline__ void mma(f32x4 (&acc)[MA][NB], const Frag<MA, NB>& f, int i, int n) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][n]) : "v"(f.b[n]), "v"(f.a[i]));
 }
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 
 // MFMA order inside a k-sub. ORD 0: i-major (a[i] over all n), reads b0..b(NB-1)
-// then a0..a7. ORD 1: "growing square": reads alternate b0 a0 b1 a1 ... (the
-// remaining a's after the last b), and each MFMA (i, n) runs right after the
-// read that completes its pair, so the first MFMA of a k-sub waits for 2 reads.
+// then a0..a(MA-1). ORD 1: "growing square": reads alternate b0 a0 b1 a1 ...
+// (then the remaining fragments of the larger side), and each MFMA (i, n) runs
+// right after the read that completes its pair, so the first MFMA of a k-sub
+// waits for 2 reads.
 struct MOrder {
   unsigned char i[64], n[64];
 };
 
 // read r of a k-sub: which fragment (0 = b, 1 = a) and its index
-constexpr int rd_isa(int ord, int nb, int r) {
-  return ord == 0 ? (r >= nb) : (r < 2 * nb ? (r & 1) : 1);
+constexpr int rd_isa(int ord, int ma, int nb, int r) {
+  return ord == 0 ? (r >= nb) : (r < 2 * (ma < nb ? ma : nb) ? (r & 1) : (ma > nb ? 1 : 0));
 }
-constexpr int rd_idx(int ord, int nb, int r) {
-  return ord == 0 ? (r < nb ? r : r - nb) : (r < 2 * nb ? (r >> 1) : r - nb);
+constexpr int rd_idx(int ord, int ma, int nb, int r) {
+  return ord == 0 ? (r < nb ? r : r - nb) : (r < 2 * (ma < nb ? ma : nb) ? (r >> 1) : r - (ma < nb ? ma : nb));
 }
 
-constexpr MOrder make_order(int ord, int nb) {
+constexpr MOrder make_order(int ord, int ma, int nb) {
   MOrder o{};
   int k = 0;
   if (ord == 0) {
-    for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < ma; ++i)
       for (int n = 0; n < nb; ++n) { o.i[k] = i; o.n[k] = n; ++k; }
     return o;
   }
   bool ha[8] = {}, hb[8] = {};
-  for (int r = 0; r < 8 + nb; ++r) {
-    const int x = rd_idx(ord, nb, r);
-    if (rd_isa(ord, nb, r)) {
+  for (int r = 0; r < ma + nb; ++r) {
+    const int x = rd_idx(ord, ma, nb, r);
+    if (rd_isa(ord, ma, nb, r)) {
       ha[x] = true;
       for (int n = 0; n < nb; ++n)
         if (hb[n]) { o.i[k] = x; o.n[k] = n; ++k; }
     } else {
       hb[x] = true;
-      for (int i = 0; i < 8; ++i)
+      for (int i = 0; i < ma; ++i)
         if (ha[i]) { o.i[k] = i; o.n[k] = x; ++k; }
     }
   }
   return o;
 }
 
-template <int ORD, int NB>
+template <int ORD, int MA, int NB>
 struct Order {
-  static constexpr MOrder o = make_order(ORD, NB);
+  static constexpr MOrder o = make_order(ORD, MA, NB);
 };
 
 struct StepPtrs {
@@ -202,38 +209,49 @@ struct StepPtrs {
   int k0;
 };
 
+// s_waitcnt vmcnt(N) for the per-stage DMA counts of the tile shapes
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else {
+    static_assert(N == 8, "unsupported vmcnt");
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  }
+}
+
 // MFMA k of the K-step and what follows it, all decided at compile time:
 //   k < NR              ds_read f1 (k-sub 1 of this K-tile) read k
 //   k == B1 - 1         lgkmcnt(0) + barrier 1 (stage ST free)
 //   k in [B1, KM - R)   the ND LDS-DMA issues of K-tile t+2, evenly spread
 //   k == KM - R - 1     vmcnt(ND) + barrier 2 (K-tile t+1 visible)
 //   k >= KM - R         P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
-template <int BN, int ST, int B1, int R, int P, int ORD, int X, int K>
-__device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BN / 32>& f0, Frag<BN / 32>& f1,
-                                      f32x4 (&acc)[8][BN / 32]) {
-  using S = Shape<BN>;
-  constexpr int NB = S::NB, KM = S::KM, HM = S::HM, NR = S::NR, ND = dma_per_stage<BN>();
+template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int K>
+__device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM / 32, BN / 32>& f0,
+                                      Frag<BM / 32, BN / 32>& f1, f32x4 (&acc)[BM / 32][BN / 32]) {
+  using S = Shape<BM, BN>;
+  constexpr int MA = S::MA, NB = S::NB, KM = S::KM, HM = S::HM, NR = S::NR, ND = dma_per_stage<BM, BN>();
   if constexpr (K < KM) {
-    constexpr int mi = Order<ORD, NB>::o.i[K % HM], mn = Order<ORD, NB>::o.n[K % HM];
-    if constexpr (K < HM) mma<NB>(acc, f0, mi, mn); else mma<NB>(acc, f1, mi, mn);
+    constexpr int mi = Order<ORD, MA, NB>::o.i[K % HM], mn = Order<ORD, MA, NB>::o.n[K % HM];
+    if constexpr (K < HM) mma<MA, NB>(acc, f0, mi, mn); else mma<MA, NB>(acc, f1, mi, mn);
     if constexpr (K < NR) {
-      constexpr int x = rd_idx(ORD, NB, K);
-      if constexpr (rd_isa(ORD, NB, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
+      constexpr int x = rd_idx(ORD, MA, NB, K);
+      if constexpr (rd_isa(ORD, MA, NB, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
     }
     if constexpr (K >= B1 && K < KM - R) {
       // MFMAs that carry the DMA issues: the whole window, or the first W (X / 10000 % 100) of it
       constexpr int NW = ((X / 10000) % 100) ? (X / 10000) % 100 : KM - R - B1;
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        if (B1 + (j * NW) / ND == K) dma_any<BN, X>(c, ST, j, sp.k0);
+        if (B1 + (j * NW) / ND == K) dma_any<BM, BN, X>(c, ST, j, sp.k0);
       }
     }
     if constexpr (K >= KM - R) {
       constexpr int q = K - (KM - R);
 #pragma unroll
       for (int e = q * P; e < (q + 1) * P && e < NR; ++e) {
-        const int x = rd_idx(ORD, NB, e);
-        if (rd_isa(ORD, NB, e)) f0.a[x] = frag(sp.pa0 + x * 2048); else f0.b[x] = frag(sp.pb0 + x * 2048);
+        const int x = rd_idx(ORD, MA, NB, e);
+        if (rd_isa(ORD, MA, NB, e)) f0.a[x] = frag(sp.pa0 + x * 2048); else f0.b[x] = frag(sp.pb0 + x * 2048);
       }
     }
     fence();
@@ -243,53 +261,65 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BN 
     }
     if constexpr (K == KM - R - 1) {
       // own DMA of K-tile t+1 landed (the ND issued after it belong to t+2)
-      if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      wait_vm<ND>();
       bar();
     }
-    kbody<BN, ST, B1, R, P, ORD, X, K + 1>(c, sp, f0, f1, acc);
+    kbody<BM, BN, ST, B1, R, P, ORD, X, K + 1>(c, sp, f0, f1, acc);
   }
 }
 
 // One K-step: a single pinned sequence of KM MFMAs (the first half on f0 = k-sub 0,
 // the second on f1 = k-sub 1) with the reads, DMA issues and the two barriers
 // placed between them (kbody).
-template <int BN, int ST, int B1, int R, int P, int ORD, int X>
-__device__ __forceinline__ void kstep(const Ctx& c, Frag<BN / 32>& f0, Frag<BN / 32>& f1, f32x4 (&acc)[8][BN / 32],
-                                      int t) {
-  using S = Shape<BN>;
-  static_assert(B1 >= S::NR && B1 + dma_per_stage<BN>() <= S::KM - R && S::NR <= R * P, "bad K-step schedule");
+template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X>
+__device__ __forceinline__ void kstep(const Ctx& c, Frag<BM / 32, BN / 32>& f0, Frag<BM / 32, BN / 32>& f1,
+                                      f32x4 (&acc)[BM / 32][BN / 32], int t) {
+  using S = Shape<BM, BN>;
+  static_assert(B1 >= S::NR && B1 + dma_per_stage<BM, BN>() <= S::KM - R && S::NR <= R * P, "bad K-step schedule");
   StepPtrs sp;
-  sp.pa1 = abase<BN, 1>(c, ST);
-  sp.pb1 = bbase<BN, 1>(c, ST);
-  sp.pa0 = abase<BN, 0>(c, ST ^ 1);
-  sp.pb0 = bbase<BN, 0>(c, ST ^ 1);
+  sp.pa1 = abase<BM, BN, 1>(c, ST);
+  sp.pb1 = bbase<BM, BN, 1>(c, ST);
+  sp.pa0 = abase<BM, BN, 0>(c, ST ^ 1);
+  sp.pb0 = bbase<BM, BN, 0>(c, ST ^ 1);
   int tl = t + 2;
   tl = tl < c.nt ? tl : c.nt - 1;  // past the end: harmless re-load into the free stage
   sp.k0 = tl * BK;
-  kbody<BN, ST, B1, R, P, ORD, X, 0>(c, sp, f0, f1, acc);
+  kbody<BM, BN, ST, B1, R, P, ORD, X, 0>(c, sp, f0, f1, acc);
 }
 
-// Production knobs per tile width: barrier 1 after MFMA B1, R MFMAs after
+// Production knobs per tile shape: barrier 1 after MFMA B1, R MFMAs after
 // barrier 2, P reads per MFMA there, growing-square order, GROUP_M 4.
-template <int BN>
+template <int BM, int BN>
 struct Knobs;
 template <>
-struct Knobs<256> {
+struct Knobs<256, 256> {
   static constexpr int B1 = 24, R = 20, P = 1, ORD = 1, X = 0;
 };
 template <>
-struct Knobs<128> {
+struct Knobs<256, 128> {
   static constexpr int B1 = 18, R = 16, P = 1, ORD = 1, X = 0;
 };
+template <>
+struct Knobs<128, 256> {
+  static constexpr int B1 = 18, R = 16, P = 1, ORD = 1, X = 0;
+};
+template <>
+struct Knobs<128, 128> {
+  static constexpr int B1 = 10, R = 10, P = 1, ORD = 1, X = 0;
+};
 
-template <int EPI, int BN = 256, int MODE = 0, int B1 = Knobs<BN>::B1, int R = Knobs<BN>::R, int P = Knobs<BN>::P,
-          int ORD = Knobs<BN>::ORD, int X = Knobs<BN>::X>
+template <int MODE>
+constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
+
+template <int EPI, int BN = 256, int MODE = 0, int B1 = Knobs<tile_m<MODE>(), BN>::B1,
+          int R = Knobs<tile_m<MODE>(), BN>::R, int P = Knobs<tile_m<MODE>(), BN>::P,
+          int ORD = Knobs<tile_m<MODE>(), BN>::ORD, int X = Knobs<tile_m<MODE>(), BN>::X>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
-  using S = Shape<BN>;
-  constexpr int NB = S::NB, ND = dma_per_stage<BN>();
+  constexpr int BM = tile_m<MODE>();
+  using S = Shape<BM, BN>;
+  constexpr int MA = S::MA, NB = S::NB, ND = dma_per_stage<BM, BN>();
   constexpr bool SW = (X / 1000000) % 10 != 0;
   static_assert(!SW || (EPI == EPI_NONE && (MODE & 2) == 0), "SwiGLU: no bias epilogue, no split-K");
   constexpr bool BNDM = (MODE & 1) != 0, SPLITK = (MODE & 2) != 0;
@@ -339,29 +369,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
   }
 
-  f32x4 acc[8][NB];
+  f32x4 acc[MA][NB];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < MA; ++i)
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // prologue: K-tiles 0 and 1 into stages 0 and 1, k-sub 0 of K-tile 0 into f0
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BN, X>(c, 0, j, 0);
+  for (int j = 0; j < ND; ++j) dma_any<BM, BN, X>(c, 0, j, 0);
   const int k1 = (c.nt > 1 ? 1 : 0) * BK;
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BN, X>(c, 1, j, k1);
-  if constexpr (ND == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  for (int j = 0; j < ND; ++j) dma_any<BM, BN, X>(c, 1, j, k1);
+  wait_vm<ND>();
   bar();
-  Frag<NB> f0, f1;
+  Frag<MA, NB> f0, f1;
   {
-    const char* pa = abase<BN, 0>(c, 0);
-    const char* pb = bbase<BN, 0>(c, 0);
+    const char* pa = abase<BM, BN, 0>(c, 0);
+    const char* pb = bbase<BM, BN, 0>(c, 0);
 #pragma unroll
     for (int e = 0; e < S::NR; ++e) {  // same order as the loop's reads
-      const int x = rd_idx(ORD, NB, e);
-      if (rd_isa(ORD, NB, e)) f0.a[x] = frag(pa + x * 2048); else f0.b[x] = frag(pb + x * 2048);
+      const int x = rd_idx(ORD, MA, NB, e);
+      if (rd_isa(ORD, MA, NB, e)) f0.a[x] = frag(pa + x * 2048); else f0.b[x] = frag(pb + x * 2048);
     }
   }
   // nothing outstanding on lgkm at loop entry: otherwise the waitcnt pass merges
@@ -369,8 +398,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __builtin_amdgcn_s_waitcnt(0xc07f);
 
   for (int t = 0; t < c.nt; t += 2) {
-    kstep<BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
-    kstep<BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
+    kstep<BM, BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
+    kstep<BM, BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read hazard
@@ -380,8 +409,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // fp32 partial tile, row-major [M][N]: one 16-B store per lane per fragment
     float* part = (float*)C + (long)slice * M * N;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+    for (int i = 0; i < MA; ++i) {
+      const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
       if (BNDM && row >= M) continue;
 #pragma unroll
       for (int n = 0; n < NB; ++n)
@@ -393,8 +422,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     // out fragment q (16 columns) = silu(gate fragment ng) * up fragment ng + 2,
     // ng = 4 (q / 2) + q % 2; pairs (q, q + 1) share one 16-B store per lane
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+    for (int i = 0; i < MA; ++i) {
+      const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
       unsigned short* crow = C + (long)row * ldc;
       const bool row_ok = !BNDM || row < M;
 #pragma unroll
@@ -436,8 +465,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int row = tm * BM + c.wr * 128 + i * 16 + fr;
+  for (int i = 0; i < MA; ++i) {
+    const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
     unsigned short* crow = C + (long)row * ldc;
     const bool row_ok = !BNDM || row < M;
 #pragma unroll

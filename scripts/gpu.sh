@@ -24,7 +24,7 @@
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
-#   serve_sweep  offline serving at batch 128 / 512, fp8 KV, fp8 prefill + fp8 KV (batch 256 and 512)
+#   serve_sweep  offline serving at batch 1 / 64 / 128 / 256 / 512, fp8 KV, fp8 prefill + fp8 KV (256 and 512)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${1:?usage: gpu.sh OUT step...}
@@ -90,7 +90,10 @@ step() {
             --out "$O/w4x_sweep.jsonl" ;;
         serve_sweep)
             local SB="python -u -m kgs.serve bench --input-len 512 --output-len 256 --max-model-len 2048"
-            run serve_b128 300 $SB --requests 128 --max-batch 128 &&
+            run serve_b1 300 $SB --requests 2 --max-batch 1 &&
+                run serve_b64 300 $SB --requests 64 --max-batch 64 &&
+                run serve_b128 300 $SB --requests 128 --max-batch 128 &&
+                run serve_b256 300 $SB --requests 256 --max-batch 256 &&
                 run serve_b512 300 $SB --requests 512 --max-batch 512 &&
                 run serve_b256_kv8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 &&
                 run serve_b256_f8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 --prefill-weights fp8 &&

@@ -197,10 +197,12 @@ def test_gemm_splitk(M, N, K, nslice):
     assert torch.equal(gemm_nt_splitk(a, b, nslice), c)
 
 
-@pytest.mark.parametrize("M,N,K,bn,nslice", [(256, 1024, 4096, 128, 1), (200, 768, 4096, 128, 4),
-                                             (256, 512, 14336, 128, 8), (96, 1024, 1024, 256, 2),
-                                             (384, 256, 2048, 256, 1), (130, 384, 640, 128, 5)])
-def test_gemm_w4x_decode_shapes(M, N, K, bn, nslice):
+@pytest.mark.parametrize("M,N,K,bn,nslice,bm", [(256, 1024, 4096, 128, 1, 256), (200, 768, 4096, 128, 4, 256),
+                                                (256, 512, 14336, 128, 8, 256), (96, 1024, 1024, 256, 2, 256),
+                                                (384, 256, 2048, 256, 1, 256), (130, 384, 640, 128, 5, 256),
+                                                (128, 1024, 4096, 256, 2, 128), (64, 512, 2048, 128, 4, 128),
+                                                (100, 768, 1024, 256, 1, 128), (200, 256, 640, 128, 5, 128)])
+def test_gemm_w4x_decode_shapes(M, N, K, bn, nslice, bm):
     """The four-wave decode GEMM (any M, 256x128 / 256x256 tiles, K slices)
     against fp32 torch; slices are summed in a fixed order (repeatable bits)."""
     from kgs.ops.gemm import gemm_nt_w4x
@@ -208,9 +210,11 @@ def test_gemm_w4x_decode_shapes(M, N, K, bn, nslice):
     a_full = (torch.rand(M, K + 64, device=DEV) * 2 - 1).bfloat16()
     a = a_full[:, 32:32 + K]
     b = ((torch.rand(N, K, device=DEV) * 2 - 1) * torch.linspace(0.5, 1.5, K, device=DEV)).bfloat16()
-    c = gemm_nt_w4x(a, b, bn=bn, nslice=nslice)
+    c = gemm_nt_w4x(a, b, bn=bn, nslice=nslice, bm=bm)
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
-    assert torch.equal(gemm_nt_w4x(a, b, bn=bn, nslice=nslice), c)
+    assert torch.equal(gemm_nt_w4x(a, b, bn=bn, nslice=nslice, bm=bm), c)
+    if bm == 128:  # same MFMA order along K as the 256-row tile: same bits
+        assert torch.equal(gemm_nt_w4x(a, b, bn=bn, nslice=nslice), c)
 
 
 def test_splitk_workspace_is_stable_for_graphs():
@@ -502,9 +506,10 @@ def test_timing_probes_refuse_without_opt_in():
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("M,I,K,bn", [(256, 1024, 4096, 128), (200, 768, 1024, 128), (512, 1024, 2048, 256),
-                                      (130, 512, 640, 256)])
-def test_gemm_w4x_swiglu_epilogue(M, I, K, bn):
+@pytest.mark.parametrize("M,I,K,bn,bm", [(256, 1024, 4096, 128, 256), (200, 768, 1024, 128, 256),
+                                         (512, 1024, 2048, 256, 256), (130, 512, 640, 256, 256),
+                                         (128, 1024, 2048, 256, 128), (72, 512, 1024, 128, 128)])
+def test_gemm_w4x_swiglu_epilogue(M, I, K, bn, bm):
     """SwiGLU in the four-wave kernel's epilogue == the gate|up GEMM followed by
     silu_mul, bit for bit (same roundings), and close to fp32 torch."""
     from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu
@@ -513,7 +518,7 @@ def test_gemm_w4x_swiglu_epilogue(M, I, K, bn):
     a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * K ** -0.5 *
          torch.linspace(0.5, 1.5, K, device=DEV)).bfloat16()
-    fused = gemm_nt_w4x_swiglu(a, w, bn=bn)
+    fused = gemm_nt_w4x_swiglu(a, w, bn=bn, bm=bm)
     assert fused.shape == (M, I)
     ref = silu_mul(gemm_nt_w4x(a, w, bn=bn, nslice=1))
     assert torch.equal(fused, ref)
