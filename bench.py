@@ -58,6 +58,11 @@ def parse(argv=None):
     ap.add_argument("--backend", choices=("kgs", "torch"), default="kgs",
                     help="kgs = hand-written gfx950 kernel (the benchmark); torch = reference / CPU test path")
     ap.add_argument("--cpu", action="store_true", help="CPU + gloo (tests of the distributed plumbing only)")
+    ap.add_argument("--dist-backend", choices=("auto", "nccl", "gloo"), default="auto",
+                    help="collective backend: auto = RCCL on GPUs (the benchmark), gloo on CPU")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="allow more ranks than GPUs (rank r on GPU r %% n): tests the multi-rank GPU path on a "
+                         "1-GPU box, with --dist-backend gloo; not a benchmark configuration")
     ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
                     help="bf16 = the headline (BASELINE.json); fp8 = e4m3 operands on the scaled MFMA (extra)")
     return ap.parse_args(argv)
@@ -69,13 +74,15 @@ def main(argv=None) -> int:
 
     if launch.needs_self_launch(args.gpus):
         raw = list(sys.argv[1:] if argv is None else argv)
-        return launch.spawn_local(args.gpus, [os.path.abspath(__file__), *raw], require_gpus=not args.cpu)
+        return launch.spawn_local(args.gpus, [os.path.abspath(__file__), *raw],
+                                  require_gpus=not (args.cpu or args.oversubscribe))
 
     import torch
     from kgs.models.gemm_workload import GemmWorkload
     from kgs.parallel import dist as kdist
 
-    ctx = kdist.init_from_env(expected_world=args.gpus, device_type="cpu" if args.cpu else None)
+    ctx = kdist.init_from_env(expected_world=args.gpus, device_type="cpu" if args.cpu else None,
+                              backend=None if args.dist_backend == "auto" else args.dist_backend)
     rank, world = ctx.rank, ctx.world_size
     dev = ctx.device
 

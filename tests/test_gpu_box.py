@@ -156,3 +156,19 @@ def test_doctor_device_checks_on_the_box():
     rep = json.loads(r.stdout)
     st = {c["name"]: c["status"] for c in rep["checks"]}
     assert st["/dev/kfd"] == "OK" and st["GPUs"] == "OK" and st["render nodes"] == "OK" and st["health"] == "OK"
+
+
+def test_bench_two_ranks_on_one_gpu():
+    """bench.py's multi-rank GPU path end to end on a 1-GPU box: the parent
+    self-launches 2 ranks (never touching the GPU itself), each rank runs the
+    kgs GEMM on the GPU and all-reduces its CUDA gradient bucket on a side
+    stream over gloo (RCCL refuses two ranks on one device), then max-over-ranks
+    timing and one JSON line from rank 0."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "3", "--warmup", "1", "--gemm-m", "2048",
+                        "--gemm-n", "2048", "--gemm-k", "2048", "--allreduce-mb", "4", "--dist-backend", "gloo",
+                        "--oversubscribe"], capture_output=True, text=True, env=ENV, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    s = _last_json(r.stdout)
+    assert s["n_gpus"] == 2 and s["config"]["parallelism"] == "dp2" and s["value"] > 0
+    assert len(s["per_rank_ms_per_step"]) == 2 and s["allreduce_busbw_gbs"] > 0
+    assert s["gemm_path"].startswith("kgs gemm_nt_w4")
