@@ -167,7 +167,7 @@ SPLITK_WS_FLOATS = 8 * 256 * 8192  # the largest entry above (M x N x slices)
 # (tile width, K slices, tile height) per (batch bucket, N, K) where it beat
 # hipBLASLt and the 8-wave split-K, weights streamed from HBM
 # (bench/decode_w4x_sweep.py, profiles/r2/decode_w4x_sweep.jsonl and
-# decode_w4x_bm128.jsonl; speed-up vs hipBLASLt in the comments). Batches up to
+# decode_w4x_bm128.jsonl, decode_w4x_lm_head.jsonl; speed-up vs hipBLASLt in the comments). Batches up to
 # 128 take 128-row tiles (no MFMAs on padding rows: qkv / o / down 3-20 %
 # faster than 256-row tiles at 64-128 rows, and ahead of the fused skinny
 # GEMMs from 49 rows up). Buckets not listed stay on the routes below.
@@ -178,6 +178,7 @@ W4X_TUNED: dict = {
     (64, *_O): (128, 8, 128), (96, *_O): (128, 8, 128), (128, *_O): (128, 8, 128),  # 4.95/2.27/2.22
     (64, *_GU): (128, 1, 128), (96, *_GU): (128, 1, 128), (128, *_GU): (128, 1, 128),  # 1.16/1.15/1.14
     (64, *_DOWN): (128, 8, 128), (96, *_DOWN): (128, 8, 128), (128, *_DOWN): (128, 8, 128),  # 1.75/2.07/2.29
+    (64, *_LM): (256, 1, 128), (96, *_LM): (256, 1, 128), (128, *_LM): (256, 1, 128),  # 1.18/1.22/1.24
     (192, *_QKV): (128, 4, 256), (256, *_QKV): (128, 4, 256), (384, *_QKV): (128, 2, 256),  # 1.39/1.49/1.06
     (192, *_O): (128, 8, 256), (256, *_O): (128, 8, 256), (384, *_O): (128, 4, 256),  # 1.62/1.05/1.02
     (512, *_O): (128, 4, 256),  # 1.10

@@ -116,7 +116,7 @@ class ServingModel:
         if self.backend == "ref":
             return (x.float() @ w.float().T).to(torch.bfloat16)
         m = x.shape[0]
-        if decode and layer is not None:
+        if decode:
             route = D.w4x_route(m, w.shape[0], w.shape[1])
             if route is not None:
                 from kgs.ops.gemm import gemm_nt_w4x

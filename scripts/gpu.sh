@@ -87,7 +87,7 @@ step() {
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
-            --out "$O/w4x_sweep.jsonl" ;;
+            --shapes ${SHAPES:-qkv,o,gate_up,down} --out "$O/w4x_sweep.jsonl" ;;
         serve_sweep)
             local SB="python -u -m kgs.serve bench --input-len 512 --output-len 256 --max-model-len 2048"
             run serve_b1 300 $SB --requests 2 --max-batch 1 &&
