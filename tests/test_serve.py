@@ -695,3 +695,18 @@ def test_fp8_routing_table_cpu():
         _, kpc, _ = D.skinny_geometry(16 * key[0], v)
         assert (key[2] // kpc) % ks == 0
     assert D.skinny_config(1, 28672, 4096, fp8=True) == D.TUNED_FP8[(1, 28672, 4096)]
+
+
+def test_w4x_routing_table_cpu():
+    """Every four-wave decode route is launchable (tile divides N, K slices of
+    whole 128-deep K-tiles, a known tile height) and its fp32 partials fit the
+    split-K workspace reserved before graph capture."""
+    from kgs.ops import decode as D
+
+    for (m, n, k), (bn, ns, bm) in D.W4X_TUNED.items():
+        assert m in D._W4X_BUCKETS and bn in (128, 256) and bm in (128, 256), (m, n, k)
+        assert n % bn == 0 and k % ns == 0 and (k // ns) % 128 == 0, (m, n, k, ns)
+        assert ns == 1 or ns * m * n <= D.SPLITK_WS_FLOATS, (m, n, k, ns)
+        assert bm == 256 or m <= 128, (m, bm)  # 128-row tiles only where they pad less
+    assert D.w4x_route(D.W4X_MIN_BATCH - 1, 4096, 4096) is None
+    assert D.w4x_route(64, 4096, 4096) == D.W4X_TUNED[(64, 4096, 4096)]
