@@ -82,6 +82,9 @@ _SIGS = {
     "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p, _c_int,
                                                   _c_void_p], _c_int),
     "kgs_gemm_bf16_nt_w4x_swiglu": ([_c_void_p] * 3 + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_skinny_gemm_bf16_rope": ([_c_void_p] * 5 + [_c_int] * 3 + [_c_long, _c_long] + [_c_int] * 3 +
+                                  [_c_void_p, ctypes.c_float, ctypes.c_float] + [_c_void_p] * 5 + [_c_int, _c_int,
+                                                                                                  _c_void_p], _c_int),
     "kgs_argmax_rows_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_long, _c_void_p], _c_int),
     "kgs_splitk_add_rmsnorm_bf16": ([_c_void_p, _c_int] + [_c_void_p] * 3 + [_c_int, _c_int, _c_long, _c_long,
                                                                               ctypes.c_float, _c_void_p], _c_int),

@@ -58,6 +58,19 @@ def swiglu_rows(n2: int) -> torch.Tensor:
     return torch.arange(n2).reshape(2, inter // 8, 8).permute(1, 0, 2).reshape(n2)
 
 
+def rope_rows(n: int, heads: int, kv_heads: int) -> torch.Tensor:
+    """Row order of a fused qkv weight ``[(H + 2 HKV) * 128, K]`` in which every
+    q / k head's 16-row tile ``t`` holds dims ``8t..8t+7`` then ``64+8t..64+8t+7``
+    (v heads unchanged): the skinny GEMM's RoPE epilogue pairs each rotate-half
+    partner lane-to-lane (``lane ^ 32``)."""
+    if n != (heads + 2 * kv_heads) * HEAD_DIM:
+        raise ValueError(f"qkv weight of {n} rows does not match {heads} + 2 x {kv_heads} heads of {HEAD_DIM}")
+    head = torch.arange(HEAD_DIM).reshape(2, 8, 8).permute(1, 0, 2).reshape(HEAD_DIM)
+    rot = heads + kv_heads
+    q_k = (torch.arange(rot)[:, None] * HEAD_DIM + head[None, :]).reshape(-1)
+    return torch.cat([q_k, torch.arange(rot * HEAD_DIM, n)])
+
+
 def pack_swiglu(w: torch.Tensor) -> torch.Tensor:
     return pack_weight(w[swiglu_rows(w.shape[0]).to(w.device)])
 
@@ -73,14 +86,21 @@ class PackedWeight:
     * ``fold``: an RMSNorm weight ``[K]`` folded into the columns (``W * fold``),
       for GEMMs that apply the norm in their epilogue (``rms=``);
     * ``fp8=True``: weight-only fp8 (W8A16): OCP e4m3 with one scale per output
-      row, dequantised to bf16 in registers (half the HBM bytes per step)."""
+      row, dequantised to bf16 in registers (half the HBM bytes per step);
+    * ``rope=(H, HKV)``: a fused qkv weight in :func:`rope_rows` order, for the
+      GEMM whose epilogue applies RoPE and writes the KV cache (``rope=`` of
+      :func:`skinny_gemm`); its output is in the original order."""
 
-    __slots__ = ("data", "n", "k", "swiglu", "fp8", "wscale")
+    __slots__ = ("data", "n", "k", "swiglu", "fp8", "wscale", "rope")
 
-    def __init__(self, w: torch.Tensor, swiglu: bool = False, fold: torch.Tensor | None = None, fp8: bool = False):
+    def __init__(self, w: torch.Tensor, swiglu: bool = False, fold: torch.Tensor | None = None, fp8: bool = False,
+                 rope: tuple | None = None):
         self.n, self.k = w.shape
-        self.swiglu, self.fp8 = swiglu, fp8
-        rows = swiglu_rows(self.n).to(w.device) if swiglu else None
+        self.swiglu, self.fp8, self.rope = swiglu, fp8, rope
+        if swiglu and rope:
+            raise ValueError("a weight is either SwiGLU- or RoPE-packed")
+        rows = swiglu_rows(self.n).to(w.device) if swiglu else \
+            rope_rows(self.n, *rope).to(w.device) if rope else None
         if fold is not None:
             w = w.float() * fold.float()[None, :]
         if fp8:
@@ -105,9 +125,10 @@ class PackedWeight:
         p = unpack_weight(self.data)
         if self.fp8:
             p = (p.view(FP8).float() * self.wscale[:, None]).to(torch.bfloat16)
-        if self.swiglu:
+        if self.swiglu or self.rope:
+            rows = swiglu_rows(self.n) if self.swiglu else rope_rows(self.n, *self.rope)
             inv = torch.empty(self.n, dtype=torch.long, device=p.device)
-            inv[swiglu_rows(self.n).to(p.device)] = torch.arange(self.n, device=p.device)
+            inv[rows.to(p.device)] = torch.arange(self.n, device=p.device)
             p = p[inv]
         return p
 
@@ -303,7 +324,7 @@ EPI_SWIGLU, EPI_RMS, EPI_RESID = 1, 2, 4
 def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = None,
                 ksplit: int | None = None, variant: int = 0, rms: torch.Tensor | None = None,
                 resid_ss: torch.Tensor | None = None, zero: torch.Tensor | None = None,
-                eps: float = 1e-5) -> torch.Tensor:
+                eps: float = 1e-5, rope: dict | None = None) -> torch.Tensor:
     """``x @ W^T`` (bf16, fp32 accumulate) for ``x: [M <= 256, K]`` row-major;
     ``silu(x @ Wg^T) * (x @ Wu^T)`` for a ``swiglu`` weight. Fused epilogues:
 
@@ -313,7 +334,11 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
     * ``resid_ss`` (fp32 ``[M]``): ``out`` is the residual stream, updated in
       place (``out += x @ W^T``), and the new rows' sums of squares are added
       into ``resid_ss`` (for the next ``rms`` consumer);
-    * ``zero`` (fp32 ``[M]``): cleared at kernel start (a consumed statistic)."""
+    * ``zero`` (fp32 ``[M]``): cleared at kernel start (a consumed statistic);
+    * ``rope`` (a ``rope=(H, HKV)``-packed qkv weight): dict of ``cos``, ``sin``
+      (fp32 ``[max_pos, 64]``), ``positions`` and ``slots`` (int32 ``[M]``) and
+      ``cache`` (the layer's bf16 pages): q / k rotated at their positions, k / v
+      written into their cache slots -- :func:`rope_cache_` in the epilogue."""
     if x.dtype != torch.bfloat16 or not x.is_cuda or x.dim() != 2 or x.stride(1) != 1:
         raise ValueError("x must be a row-major bf16 GPU matrix")
     m, k = x.shape
@@ -323,6 +348,10 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
         raise ValueError("fp8 (W8A16) skinny GEMM covers batches <= 64")
     if variant == 0 and ksplit is None:
         variant, ks = skinny_config(m, w.n, k, fp8=w.fp8)
+        if rope is not None and SKINNY_VARIANTS[variant][0] != 1:
+            # the RoPE epilogue is built for one-tile waves (R 1): the batch's default variant
+            variant = _DEFAULT_VARIANT[_mt(m)]
+            ks = choose_ksplit(m, w.n, k, variant=variant)
     else:
         ks = ksplit if ksplit is not None else choose_ksplit(m, w.n, k, variant=variant)
     rps, kpc, mpad = skinny_geometry(m, variant)
@@ -339,6 +368,26 @@ def skinny_gemm(x: torch.Tensor, w: PackedWeight, out: torch.Tensor | None = Non
     if out is None:
         out = torch.empty((m, w.n_out), dtype=torch.bfloat16, device=x.device)
     ws, cnt = _workspace(x.device, ks * mpad * w.n if ks > 1 else 0, w.n // rps)
+    if (rope is not None) != bool(w.rope):
+        raise ValueError("rope= needs a rope-packed qkv weight (PackedWeight(..., rope=(H, HKV))) and vice versa")
+    if rope is not None:
+        if w.fp8 or resid_ss is not None:
+            raise ValueError("the RoPE epilogue is bf16-weight only and writes a fresh qkv output")
+        cache = rope["cache"]
+        if cache.dtype != torch.bfloat16 or not cache.is_contiguous():
+            raise ValueError("the RoPE epilogue writes a bf16 KV cache")
+        for key in ("positions", "slots"):
+            v = rope[key]
+            if v.dtype != torch.int32 or not v.is_contiguous() or v.numel() < m:
+                raise ValueError(f"{key} must be a contiguous int32 vector of >= M elements")
+        rc = _lib.lib().kgs_skinny_gemm_bf16_rope(
+            w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(), cnt.data_ptr(), m, w.n, k, x.stride(0),
+            out.stride(0), ks, variant, EPI_RMS if rms is not None else 0,
+            rms.data_ptr() if rms is not None else None, 1.0 / k, float(eps), rope["cos"].data_ptr(),
+            rope["sin"].data_ptr(), rope["positions"].data_ptr(), rope["slots"].data_ptr(), cache.data_ptr(),
+            w.rope[0], w.rope[1], _lib.stream_handle(x.device))
+        _lib.check(rc, f"skinny_gemm_rope[{m}x{w.n}x{k}, variant={variant}, ksplit={ks}]")
+        return out
     rc = _lib.lib().kgs_skinny_gemm_bf16_fused(
         w.data.data_ptr(), x.data_ptr(), out.data_ptr(), ws.data_ptr(), cnt.data_ptr(), m, w.n, k, x.stride(0),
         out.stride(0), ks, variant, epi, rms.data_ptr() if rms is not None else None,

@@ -83,8 +83,11 @@ class ServingModel:
             f8 = self.decode_fp8
             # decode copies in skinny-GEMM fragment order; the RMSNorm weights
             # in front of qkv / gate|up / lm_head are folded into them (their
-            # GEMMs apply the norm in the epilogue), gate|up is SwiGLU-packed
-            self.packed = [{"qkv": D.PackedWeight(lw["qkv"], fold=self.ln1[i], fp8=f8),
+            # GEMMs apply the norm in the epilogue), gate|up is SwiGLU-packed,
+            # and with bf16 weights and a bf16 cache qkv is RoPE-packed (its
+            # epilogue rotates q / k and writes the KV cache)
+            rope = None if f8 or kv_cache_dtype != "bf16" else (cfg.heads, cfg.kv_heads)
+            self.packed = [{"qkv": D.PackedWeight(lw["qkv"], fold=self.ln1[i], fp8=f8, rope=rope),
                             "o": D.PackedWeight(lw["o"], fp8=f8),
                             "gate_up": D.PackedWeight(lw["gate_up"], swiglu=True, fold=self.ln2[i], fp8=f8),
                             "down": D.PackedWeight(lw["down"], fp8=f8)} for i, lw in enumerate(self.w)]
@@ -437,8 +440,13 @@ class ServingModel:
         ss_a = torch.zeros_like(ss_b)
         for i in range(c.layers):
             P = self.packed[i]
-            qkv = D.skinny_gemm(x, P["qkv"], rms=ss_b, eps=eps)
-            self._rope_cache(qkv, i, positions, slots)
+            if P["qkv"].rope:
+                qkv = D.skinny_gemm(x, P["qkv"], rms=ss_b, eps=eps,
+                                    rope={"cos": self.cos, "sin": self.sin, "positions": positions, "slots": slots,
+                                          "cache": self.cache.layer(i)})
+            else:
+                qkv = D.skinny_gemm(x, P["qkv"], rms=ss_b, eps=eps)
+                self._rope_cache(qkv, i, positions, slots)
             a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                          pages_per_split=pages_per_split)
             D.skinny_gemm(a, P["o"], out=x, resid_ss=ss_a, zero=ss_b)

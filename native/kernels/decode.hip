@@ -115,9 +115,15 @@ struct SkinnyCfg {
 //               atomics), the statistic the next EPI_RMS consumer needs.
 //   ss_zero     zeroed by workgroup 0 at kernel start (the sum-of-squares
 //               buffer of the previous layer boundary, already consumed).
-// Together they remove both add_rmsnorm launches and the SwiGLU launch from a
-// decode layer (kgs/serve/model.py fused decode path).
-enum { EPI_SWIGLU = 1, EPI_RMS = 2, EPI_RESID = 4 };
+//   EPI_ROPE    W is the fused qkv weight packed so that in every q / k head
+//               16-row tile t holds dims 8t..8t+7 then 64+8t..64+8t+7
+//               (kgs/ops/decode.py rope_rows): lane l pairs with lane l ^ 32,
+//               rotates (rotate-half RoPE at pos[m], fp32 cos/sin tables), stores
+//               the row in the original order, and writes k / v into the bf16
+//               paged cache slot slot[m] -- the rope_cache launch, folded in.
+// Together they remove both add_rmsnorm launches, the SwiGLU launch and the
+// RoPE / KV-write launch from a decode layer (kgs/serve/model.py fused path).
+enum { EPI_SWIGLU = 1, EPI_RMS = 2, EPI_RESID = 4, EPI_ROPE = 8 };
 struct SkinnyEpi {
   int mode;
   const float* ss_in;
@@ -125,6 +131,13 @@ struct SkinnyEpi {
   float* ss_zero;
   float inv_k, eps;
   const float* wscale;  // W8: per packed row dequant scale
+  // EPI_ROPE
+  const float* cosv;
+  const float* sinv;
+  const int* pos;
+  const int* slot;
+  unsigned short* cache;  // this layer's bf16 pages [pages][HKV][2][4096]
+  int H, HKV;
 };
 
 // W8 (weight-only fp8, "W8A16"): W is OCP e4m3 in the same fragment order, 8 B
@@ -161,7 +174,10 @@ __device__ __forceinline__ bf16x8 dequant8(u32x2 v, float s) {
   return o;
 }
 
-template <int R, int MT, int KC_, bool W8 = false>
+// EROPE: the EPI_ROPE instantiation (qkv of the fused decode layer only, so
+// the other projections keep the lean epilogue's registers); its RoPE tables,
+// positions and cache slots are loaded at kernel start, under the main loop.
+template <int R, int MT, int KC_, bool W8 = false, bool EROPE = false>
 __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void skinny(const void* __restrict__ wpv, const unsigned short* __restrict__ x,
                                                  unsigned short* __restrict__ y, float* __restrict__ ws,
                                                  int* __restrict__ cnt, int M, int N, int K, long ldx, long ldy,
@@ -193,6 +209,29 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   for (int r = 0; r < R; ++r) {
     wrow[r] = wp + ((long)(nt0 + r) * nkk + kk0) * 64 + lane;
     wsc[r] = W8 ? ep.wscale[16 * (nt0 + r) + (lane & 15)] : 1.f;
+  }
+  // EROPE: per (column tile c, row tile r) the lane's 4 cos / sin values and its
+  // row's cache slot, fetched now so their latency hides under the main loop
+  float rcs[EROPE ? MT : 1][EROPE ? R : 1][4], rsn[EROPE ? MT : 1][EROPE ? R : 1][4];
+  int rslot[EROPE ? MT : 1];
+  if constexpr (EROPE) {
+    const int gq = lane >> 4;
+#pragma unroll
+    for (int c = 0; c < MT; ++c) {
+      const int mr = min(16 * c + (lane & 15), M - 1);
+      const int p = ep.pos[mr];
+      rslot[c] = 16 * c + (lane & 15) < M ? ep.slot[mr] : -1;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int T = nt0 + r, t = T & 7;
+        const int dd = gq < 2 ? 8 * t + 4 * gq : 8 * t + 4 * (gq - 2);  // dim within the rotated half
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          rcs[c][r][i] = ep.cosv[(long)p * (HD / 2) + dd + i];
+          rsn[c][r][i] = ep.sinv[(long)p * (HD / 2) + dd + i];
+        }
+      }
+    }
   }
 
   // x chunk staging: element e = tid + 256 i of the chunk, row-major over
@@ -301,6 +340,46 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
       }
       sq = wsum16(sq);  // lanes of one column m (g = 0..3)
       if (m < M && g == 0) atomicAdd(ep.ss_out + m, sq);
+    } else if (EROPE) {
+      const int c = m >> 4;
+      const int T = nt0 + r, hh = T >> 3, t = T & 7;  // head and 16-row tile within it
+      const bool rot = hh < ep.H + ep.HKV;
+      f32x4v vb, pb;  // this lane's and its partner's (lane ^ 32) values, bf16-rounded
+#pragma unroll
+      for (int i = 0; i < 4; ++i) vb[i] = bf2f(f2bf(v[i]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pb[i] = __shfl_xor(vb[i], 32, 64);
+      // original dim of element 0: rotated heads hold (d, d + 64) pairs in a tile
+      const int d0 = rot ? (g < 2 ? 8 * t + 4 * g : 64 + 8 * t + 4 * (g - 2)) : 16 * t + 4 * g;
+      if (m < M) {
+        f32x4v o = vb;
+        if (rot) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float cs = rcs[c][r][i], sn = rsn[c][r][i];
+            o[i] = g < 2 ? vb[i] * cs - pb[i] * sn : vb[i] * cs + pb[i] * sn;
+          }
+        }
+        uint2 pk;
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
+        *(uint2*)(y + (long)m * ldy + hh * HD + d0) = pk;
+        const int sl = hh >= ep.H ? rslot[c] : -1;
+        if (sl >= 0) {
+          const int page = sl / PAGE, tau = sl - page * PAGE;
+          const bool isv = hh >= ep.H + ep.HKV;
+          const int kvh = isv ? hh - ep.H - ep.HKV : hh - ep.H;
+          unsigned short* pg = ep.cache + (((long)page * ep.HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
+          if (!isv) {
+            *(uint2*)(pg + kv_k_index(tau, d0)) = pk;  // 4 consecutive dims: one 8-B run of the K fragment
+          } else {
+            pg[kv_v_index(tau, d0 + 0)] = (unsigned short)(pk.x & 0xffff);
+            pg[kv_v_index(tau, d0 + 1)] = (unsigned short)(pk.x >> 16);
+            pg[kv_v_index(tau, d0 + 2)] = (unsigned short)(pk.y & 0xffff);
+            pg[kv_v_index(tau, d0 + 3)] = (unsigned short)(pk.y >> 16);
+          }
+        }
+      }
     } else if (m < M) {
       uint2 pk;
       pk.x = pack_bf16x2(v[0], v[1]);
@@ -790,6 +869,14 @@ template <int R, int MT, int KC, bool W8>
 hipError_t launch_skinny(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx,
                          long ldy, int ksplit, int cps, const kgs::dec::SkinnyEpi& ep, hipStream_t s) {
   const int nstrip = N / (64 * R);
+  if constexpr (!W8 && MT <= 4 && R == 1) {  // the fused layer's qkv variants (kgs/ops/decode.py rope_variant)
+    if (ep.mode & kgs::dec::EPI_ROPE) {
+      hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, false, true>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
+                         (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
+      return hipGetLastError();
+    }
+  }
+  if (ep.mode & kgs::dec::EPI_ROPE) return hipErrorInvalidValue;  // no RoPE instantiation for this variant
   hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, W8>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
                      (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
   return hipGetLastError();
@@ -821,16 +908,60 @@ KGS_EXPORT int kgs_skinny_geometry(int M, int* rows_per_strip, int* k_per_chunk,
 // zero-initialised ints (left zeroed on return). epi: EPI_* flags (SWIGLU: y is
 // [M, N/2]; RMS needs ss_in[M]; RESID accumulates into y and ss_out[M]);
 // ss_zero (optional, [M] floats) is cleared at kernel start.
+namespace {
+int skinny_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx, long ldy,
+                 int ksplit, int variant, int epi, const float* ss_in, float* ss_out, float* ss_zero, float inv_k,
+                 float eps, const float* wscale, const kgs::dec::SkinnyEpi* rope, hipStream_t s);
+}
+
 KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
                                          int K, long ldx, long ldy, int ksplit, int variant, int epi,
                                          const float* ss_in, float* ss_out, float* ss_zero, float inv_k, float eps,
                                          const float* wscale, hipStream_t s) {
+  if (epi & kgs::dec::EPI_ROPE) return KGS_ERR_ARG;  // kgs_skinny_gemm_bf16_rope
+  return skinny_fused(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, variant, epi, ss_in, ss_out, ss_zero, inv_k, eps,
+                      wscale, nullptr, s);
+}
+
+// The fused qkv projection with RoPE + the KV-cache write in its epilogue
+// (EPI_ROPE; W packed with kgs/ops/decode.py rope_rows): y [M, (H + 2 HKV) 128]
+// gets the rotated q, k and the v rows in the original order, and k / v land
+// in the bf16 cache slot slot[m] (< 0: no write). cos / sin: fp32 [max_pos, 64].
+// epi may add EPI_RMS (ss_in, inv_k, eps as in kgs_skinny_gemm_bf16_fused).
+KGS_EXPORT int kgs_skinny_gemm_bf16_rope(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
+                                        int K, long ldx, long ldy, int ksplit, int variant, int epi,
+                                        const float* ss_in, float inv_k, float eps, const float* cosv,
+                                        const float* sinv, const int* pos, const int* slot, void* cache, int H,
+                                        int HKV, hipStream_t s) {
+  using namespace kgs::dec;
+  if (epi & ~EPI_RMS) return KGS_ERR_ARG;
+  if (H <= 0 || HKV <= 0 || H % HKV || N != (H + 2 * HKV) * HD) return KGS_ERR_SHAPE;
+  if (!cosv || !sinv || !pos || !slot || !al16(cache)) return KGS_ERR_ARG;
+  SkinnyEpi r{};
+  r.cosv = cosv;
+  r.sinv = sinv;
+  r.pos = pos;
+  r.slot = slot;
+  r.cache = (unsigned short*)cache;
+  r.H = H;
+  r.HKV = HKV;
+  return skinny_fused(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, variant, epi | EPI_ROPE, ss_in, nullptr, nullptr,
+                      inv_k, eps, nullptr, &r, s);
+}
+
+namespace {
+int skinny_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx, long ldy,
+                 int ksplit, int variant, int epi, const float* ss_in, float* ss_out, float* ss_zero, float inv_k,
+                 float eps, const float* wscale, const kgs::dec::SkinnyEpi* rope, hipStream_t s) {
   using namespace kgs::dec;
   int rps, kpc, mpad;
   const int rc = kgs_skinny_variant_geometry(variant, M, &rps, &kpc, &mpad);
   if (rc) return rc;
   if (variant == 0) variant = default_variant(mt_for(M));
-  if (epi & ~(EPI_SWIGLU | EPI_RMS | EPI_RESID) || ((epi & EPI_SWIGLU) && (epi & EPI_RESID))) return KGS_ERR_ARG;
+  if (epi & ~(EPI_SWIGLU | EPI_RMS | EPI_RESID | EPI_ROPE) || ((epi & EPI_SWIGLU) && (epi & EPI_RESID)))
+    return KGS_ERR_ARG;
+  if ((epi & EPI_ROPE) && (rope == nullptr || (epi & (EPI_SWIGLU | EPI_RESID)) || wscale != nullptr))
+    return KGS_ERR_ARG;
   if (((epi & EPI_RMS) && ss_in == nullptr) || ((epi & EPI_RESID) && ss_out == nullptr)) return KGS_ERR_ARG;
   if (N <= 0 || K <= 0 || N % rps || K % kpc || ldx < K || ldy < ((epi & EPI_SWIGLU) ? N / 2 : N))
     return KGS_ERR_SHAPE;
@@ -839,7 +970,14 @@ KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y
   if (ksplit > 1 && (ws == nullptr || cnt == nullptr)) return KGS_ERR_ARG;
   if (!al16(wp) || !al16(x) || ((uintptr_t)y & 7) || ((uintptr_t)ws & 15) || ldx % 8 || ldy % 4) return KGS_ERR_ALIGN;
   const int cps = nchunks / ksplit;
-  const SkinnyEpi ep{epi, ss_in, ss_out, ss_zero, inv_k, eps, wscale};
+  SkinnyEpi ep = rope ? *rope : SkinnyEpi{};
+  ep.mode = epi;
+  ep.ss_in = ss_in;
+  ep.ss_out = ss_out;
+  ep.ss_zero = ss_zero;
+  ep.inv_k = inv_k;
+  ep.eps = eps;
+  ep.wscale = wscale;
   const bool w8 = wscale != nullptr;
   if (w8 && variant > 12) return KGS_ERR_ARG;  // fp8 weights: batch buckets <= 64 (variants 1-12)
   switch (variant * 2 + (w8 ? 1 : 0)) {
@@ -858,6 +996,7 @@ KGS_EXPORT int kgs_skinny_gemm_bf16_fused(const void* wp, const void* x, void* y
     default: return KGS_ERR_ARG;
   }
 }
+}  // namespace
 
 KGS_EXPORT int kgs_skinny_gemm_bf16_ex(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N,
                                       int K, long ldx, long ldy, int ksplit, int variant, int epi, hipStream_t s) {

@@ -389,3 +389,35 @@ def test_paged_decode_small_and_large_grids(b, pps, kv_dtype):
     torch.cuda.synchronize()
     assert (o.float() - ref).abs().max().item() < 2e-2
     assert torch.equal(o, o2)  # the merge re-arms its tickets: a second call is identical
+
+
+@pytest.mark.parametrize("m,heads,hkv", [(1, 32, 8), (16, 32, 8), (40, 8, 8), (7, 16, 1)])
+def test_skinny_rope_epilogue_matches_rope_cache(m, heads, hkv):
+    """The fused qkv skinny GEMM with RoPE + KV-cache write in its epilogue
+    (rope-packed weight) == skinny GEMM + rope_cache_, bit for bit (qkv rows and
+    cache pages), with the RMSNorm folded in and a skipped slot."""
+    from kgs.ops.decode import PAGE, PackedWeight, PagedKVCache, rope_cache_, skinny_gemm
+    from kgs.ops.transformer import rope_tables
+
+    k = 1024
+    n = (heads + 2 * hkv) * 128
+    w = _bf(n, k, scale=k ** -0.5)
+    lnw = (1 + 0.1 * torch.randn(k, device=DEV)).bfloat16()
+    x = _bf(m, k)
+    ss = x.float().pow(2).sum(-1).contiguous()
+    cos, sin = rope_tables(4096, 128, 500000.0, DEV)
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(16 * PAGE, device=DEV)[:m].int()
+    if m > 3:
+        slots[3] = -1
+    caches = [PagedKVCache(1, 16, hkv, DEV) for _ in range(2)]
+    plain = PackedWeight(w, fold=lnw)
+    roped = PackedWeight(w, fold=lnw, rope=(heads, hkv))
+    assert torch.equal(roped.unpacked(), plain.unpacked())
+    q1 = skinny_gemm(x, plain, rms=ss, eps=1e-5)
+    rope_cache_(q1, cos, sin, pos, slots, caches[0].layer(0), heads, hkv)
+    q2 = skinny_gemm(x, roped, rms=ss, eps=1e-5,
+                     rope={"cos": cos, "sin": sin, "positions": pos, "slots": slots, "cache": caches[1].layer(0)})
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2)
+    assert torch.equal(caches[0].layer(0), caches[1].layer(0))
