@@ -24,6 +24,7 @@
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
+#   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
 #   serve_sweep  offline serving at batch 1 / 64 / 128 / 256 / 512, fp8 KV, fp8 prefill + fp8 KV (256 and 512)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -98,6 +99,12 @@ step() {
                 run serve_b256_kv8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 &&
                 run serve_b256_f8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 --prefill-weights fp8 &&
                 run serve_b512_f8 300 $SB --requests 512 --max-batch 512 --kv-cache-dtype fp8 --prefill-weights fp8 ;;
+        online_sweep)
+            local OB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 --max-batch 256"
+            OB="$OB --max-model-len 2048 --chunked-prefill 2048"
+            run online_r8 300 $OB --request-rate 8 && run online_r16 300 $OB --request-rate 16 &&
+                run online_r32 300 $OB --request-rate 32 && run online_r64 300 $OB --request-rate 64 &&
+                run online_r96 300 $OB --request-rate 96 ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac
