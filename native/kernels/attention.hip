@@ -40,6 +40,7 @@ constexpr int QB = 128;  // query rows per workgroup (4 waves x 32)
 constexpr int KB = 64;   // keys per tile
 constexpr int TILE_BYTES = KB * HD * 2;  // 16 KB
 constexpr float NEG = -1.0e30f;
+constexpr float RESCALE = 8.0f;  // deferred-max threshold, log2 units: P <= 256
 
 struct Args {
   const unsigned short* q;
@@ -177,12 +178,21 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float alpha = __builtin_amdgcn_exp2f((m - mx) * sl2);
-      m = mx;
-      const float msl = mx * sl2;
-      l *= alpha;
+      // deferred rescale (guide T13): the running max m only moves when a row's
+      // new max exceeds it by more than RESCALE (log2 units after sl2), so most
+      // tiles skip the 64-multiply O rescale; p = exp2(s sl2 - m sl2) then stays
+      // <= 2^RESCALE (fp32 sums and bf16 P are scale-free). Both l and O see the
+      // same alpha, and the decision is wave-uniform, so no pending P.V is split.
+      const bool grow = (mx - m) * sl2 > RESCALE;
+      if (__any(grow)) {
+        const float mn = grow ? mx : m;
+        const float alpha = __builtin_amdgcn_exp2f((m - mn) * sl2);
+        m = mn;
+        l *= alpha;
 #pragma unroll
-      for (int d = 0; d < 4; ++d) o[d] *= alpha;
+        for (int d = 0; d < 4; ++d) o[d] *= alpha;
+      }
+      const float msl = m * sl2;
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
