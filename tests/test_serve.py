@@ -710,3 +710,28 @@ def test_w4x_routing_table_cpu():
         assert bm == 256 or m <= 128, (m, bm)  # 128-row tiles only where they pad less
     assert D.w4x_route(D.W4X_MIN_BATCH - 1, 4096, 4096) is None
     assert D.w4x_route(64, 4096, 4096) == D.W4X_TUNED[(64, 4096, 4096)]
+
+
+def test_rope_packing_cpu():
+    """The RoPE-packed qkv order: every q / k head's 16-row tile t holds dims
+    8t..8t+7 then 64+8t..64+8t+7 (lane g < 2 and its partner g ^ 2 hold a
+    rotate-half pair), v heads untouched; packing round-trips."""
+    import torch
+
+    from kgs.ops import decode as D
+
+    heads, hkv = 4, 2
+    n = (heads + 2 * hkv) * 128
+    rows = D.rope_rows(n, heads, hkv)
+    assert sorted(rows.tolist()) == list(range(n))
+    for hh in range(heads + hkv):
+        for t in range(8):
+            tile = rows[hh * 128 + 16 * t: hh * 128 + 16 * t + 16].tolist()
+            assert tile[:8] == [hh * 128 + 8 * t + j for j in range(8)]
+            assert tile[8:] == [hh * 128 + 64 + 8 * t + j for j in range(8)]
+    assert rows[(heads + hkv) * 128:].tolist() == list(range((heads + hkv) * 128, n))
+    w = torch.randn(n, 64).bfloat16()
+    p = D.PackedWeight(w, rope=(heads, hkv))
+    assert torch.equal(p.unpacked(), w)
+    with pytest.raises(ValueError):
+        D.rope_rows(n + 128, heads, hkv)
