@@ -141,7 +141,11 @@ SKINNY_VARIANTS = {
     8: (1, 4, 16), 9: (1, 4, 4), 10: (1, 4, 8), 11: (2, 4, 4), 12: (2, 4, 8),
     13: (2, 8, 2), 14: (2, 8, 4), 15: (4, 8, 2), 16: (1, 8, 4),
     17: (2, 16, 2), 18: (1, 16, 4), 19: (1, 16, 2),
+    20: (1, 1, 8), 21: (2, 1, 8),
 }
+# variants whose four waves split one strip's K range (decode.hip skinny KIN):
+# strips of 16 R rows, chunks of 4 x KC k-steps, no cross-workgroup split-K
+KIN_VARIANTS = frozenset({20, 21})
 _DEFAULT_VARIANT = {1: 1, 2: 4, 4: 8, 8: 13, 16: 17}
 
 # Measured routing per (MT, N, K) on MI355X with weights streamed from HBM
@@ -151,12 +155,16 @@ _DEFAULT_VARIANT = {1: 1, 2: 4, 4: 8, 8: 13, 16: 17}
 # lm_head 128256x4096.
 _QKV, _O, _GU, _DOWN, _LM = (6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336), (128256, 4096)
 TUNED: dict = {
-    (1, *_QKV): (1, 2), (1, *_O): (1, 4), (1, *_GU): (3, 1), (1, *_DOWN): (1, 4), (1, *_LM): (1, 1),
+    (1, *_QKV): (1, 2), (1, *_O): (20, 1), (1, *_GU): (3, 1), (1, *_DOWN): (1, 4), (1, *_LM): (1, 1),
     (2, *_QKV): (4, 2), (2, *_O): (4, 4), (2, *_GU): (6, 1), (2, *_DOWN): (4, 4), (2, *_LM): (6, 1),
     (4, *_QKV): None, (4, *_O): (9, 4), (4, *_GU): (11, 1), (4, *_DOWN): (10, 4), (4, *_LM): (11, 1),
     (8, *_QKV): None, (8, *_O): None, (8, *_GU): None, (8, *_DOWN): (16, 4), (8, *_LM): None,
     (16, *_QKV): None, (16, *_O): None, (16, *_GU): None, (16, *_DOWN): None, (16, *_LM): None,
 }
+# few-row batches: (variant, ksplit, up to M) -- the in-workgroup K split
+# (variant 20) wins while x is a few rows (each wave reads its B fragments
+# straight from L2, so x traffic grows with M); profiles/r2/skinny_kin_tune.jsonl
+TUNED_TINY: dict = {_QKV: (20, 1, 8), _GU: (20, 1, 4), _DOWN: (20, 1, 2)}
 # the same sweep for weight-only fp8 (--tune --fp8): (variant, ksplit) per (MT, N, K)
 TUNED_FP8: dict = {
     (1, *_QKV): (1, 4), (2, *_QKV): (5, 4), (4, *_QKV): (9, 4),
@@ -247,6 +255,8 @@ def skinny_geometry(m: int, variant: int = 0) -> tuple[int, int, int]:
     r, vmt, kc = SKINNY_VARIANTS[v]
     if vmt != mt:
         raise ValueError(f"variant {variant} is for {16 * vmt}-column batches, not M={m}")
+    if v in KIN_VARIANTS:
+        return 16 * r, 128 * kc, 16 * mt
     return 64 * r, 32 * kc, 16 * mt
 
 
@@ -268,6 +278,9 @@ def choose_ksplit(m: int, n: int, k: int, cus: int = CUS, variant: int = 0) -> i
 
 def skinny_config(m: int, n: int, k: int, fp8: bool = False) -> tuple[int, int]:
     """(variant, ksplit) for a skinny-GEMM call: the tuned entry, else the defaults."""
+    tiny = None if fp8 else TUNED_TINY.get((n, k))
+    if tiny is not None and m <= tiny[2]:
+        return tiny[:2]
     hit = (TUNED_FP8 if fp8 else TUNED).get((_mt(m), n, k))
     if hit is not None:
         return hit

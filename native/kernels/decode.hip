@@ -177,7 +177,14 @@ __device__ __forceinline__ bf16x8 dequant8(u32x2 v, float s) {
 // EROPE: the EPI_ROPE instantiation (qkv of the fused decode layer only, so
 // the other projections keep the lean epilogue's registers); its RoPE tables,
 // positions and cache slots are loaded at kernel start, under the main loop.
-template <int R, int MT, int KC_, bool W8 = false, bool EROPE = false>
+// KIN (batch <= 16, MT 1): the four waves share one strip of 16 R rows and
+// split its K range four ways instead of each taking its own rows, so a
+// 4096-row projection fills 256 CUs with no cross-workgroup split-K (the slab
+// stores, the ticket and the last arriver's reduce are ~3-4 us of a 12-14 us
+// batch-1 launch); the waves' partial tiles are summed through LDS. x comes
+// straight from global/L2 through the W ring (no LDS staging): chunk = KC
+// k-steps per wave, k_per_chunk = 4 * 32 * KC.
+template <int R, int MT, int KC_, bool W8 = false, bool EROPE = false, bool KIN = false>
 __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void skinny(const void* __restrict__ wpv, const unsigned short* __restrict__ x,
                                                  unsigned short* __restrict__ y, float* __restrict__ ws,
                                                  int* __restrict__ cnt, int M, int N, int K, long ldx, long ldy,
@@ -192,16 +199,18 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
   // the only __shared__ object (a second one can make hipcc drain vmcnt before
   // every ds_read, cdna_hip_programming.md s5 trap 4a); the split-K "last
   // arriver" flag reuses its first word after the main loop
-  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][C::CHUNK_SLOTS];
+  static_assert(!KIN || (MT == 1 && PF == KC), "KIN: batch <= 16, one ring round per chunk");
+  __shared__ __attribute__((aligned(16))) bf16x8 xs[2][KIN ? 2 * R * 64 : C::CHUNK_SLOTS];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int nstrip = N / (64 * R);
+  const int nstrip = N / ((KIN ? 16 : 64) * R);
   const int strip = blockIdx.x % nstrip, split = blockIdx.x / nstrip;
   if (ep.ss_zero != nullptr && blockIdx.x == 0 && tid < M) ep.ss_zero[tid] = 0.f;
   const int nkk = K / 32;
-  const int kk0 = split * chunks_per_split * KC;
-  const int nsteps = chunks_per_split * KC;  // k-steps (of 32) for this workgroup
-  const int nt0 = (strip * 4 + w) * R;       // first 16-row tile of this wave
+  // k-steps (of 32) of this wave and where they start
+  const int nsteps = chunks_per_split * KC;
+  const int kk0 = KIN ? (split * 4 + w) * nsteps : split * nsteps;
+  const int nt0 = KIN ? strip * R : (strip * 4 + w) * R;  // first 16-row tile of this wave
   const WFrag<W8>* wp = (const WFrag<W8>*)wpv;
   const WFrag<W8>* wrow[R];
   float wsc[R];
@@ -272,6 +281,46 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
     for (int r = 0; r < R; ++r) wf[p][r] = __builtin_nontemporal_load(wrow[r] + (long)min(p, nsteps - 1) * 64);
 
+  if constexpr (KIN) {
+    // B fragment of k-step s: lane (column m = lane & 15, k = 8 (lane >> 4) ..)
+    const unsigned short* xr = x + (long)min(lane & 15, M - 1) * ldx + (long)kk0 * 32 + 8 * (lane >> 4);
+    bf16x8 xf[PF];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) xf[p] = *(const bf16x8*)(xr + p * 32);
+    for (int s0 = 0; s0 < nsteps; s0 += PF) {
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          bf16x8 wdq;
+          if constexpr (W8) wdq = dequant8(wf[p][r], wsc[r]);
+          else wdq = wf[p][r];
+          acc[r][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wdq, xf[p], acc[r][0], 0, 0, 0);
+        }
+        const int sn = min(s0 + p + PF, nsteps - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) wf[p][r] = __builtin_nontemporal_load(wrow[r] + (long)sn * 64);
+        xf[p] = *(const bf16x8*)(xr + sn * 32);
+      }
+    }
+    // the four K quarters of the strip: waves 1-3 hand theirs to wave 0 (slot 0
+    // of xs stays free for the split-K flag); summed in wave order
+    f32x4v* red = (f32x4v*)&xs[0][1];
+    if (w > 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) red[((w - 1) * R + r) * 64 + lane] = acc[r][0];
+    }
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        f32x4v t = acc[r][0];
+#pragma unroll
+        for (int v = 0; v < 3; ++v) t += red[(v * R + r) * 64 + lane];
+        acc[r][0] = t;
+      }
+    }
+  } else {
   load_x(0);
   store_x(0);
   __syncthreads();
@@ -302,6 +351,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     store_x((chunk + 1) & 1);
     __syncthreads();
   }
+  }  // !KIN
 
   // C^T tile (r, c): lane holds column m = 16c + (lane & 15), rows n = 16*(nt0+r) + 4*(lane>>4) + i
   const int g = lane >> 4, mc = lane & 15;
@@ -388,6 +438,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     }
   };
   if (ksplit == 1) {
+    if (KIN && w != 0) return;
 #pragma unroll
     for (int c = 0; c < MT; ++c)
 #pragma unroll
@@ -402,7 +453,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
   for (int c = 0; c < MT; ++c) {
     const int m = 16 * c + mc;
-    if (m < M) {
+    if (m < M && (!KIN || w == 0)) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int n = 16 * (nt0 + r) + 4 * g;
@@ -424,7 +475,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     *flag = last;
   }
   __syncthreads();
-  if (!*flag) return;
+  if (!*flag || (KIN && w != 0)) return;
 #pragma unroll
   for (int c = 0; c < MT; ++c) {
     const int m = 16 * c + mc;
@@ -850,7 +901,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 // Tile variants (R = 16-row W tiles per wave, MT = 16-column x tiles, KC =
 // k-steps per x chunk). 0 = the measured default for the batch size.
 struct SkinnyVariant {
-  int r, mt, kc;
+  int r, mt, kc, kin;
 };
 constexpr SkinnyVariant kVariants[] = {
     {0, 0, 0},                                      // 0: auto
@@ -859,25 +910,26 @@ constexpr SkinnyVariant kVariants[] = {
     {1, 4, 16}, {1, 4, 4}, {1, 4, 8}, {2, 4, 4}, {2, 4, 8},  // 8-12: M <= 64
     {2, 8, 2}, {2, 8, 4}, {4, 8, 2}, {1, 8, 4},     // 13-16: M <= 128
     {2, 16, 2}, {1, 16, 4}, {1, 16, 2},             // 17-19: M <= 256
+    {1, 1, 8, 1}, {2, 1, 8, 1},                     // 20-21: M <= 16, K split inside the workgroup
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 int mt_for(int M) { return M <= 16 ? 1 : M <= 32 ? 2 : M <= 64 ? 4 : M <= 128 ? 8 : 16; }
 int default_variant(int mt) { return mt == 1 ? 1 : mt == 2 ? 4 : mt == 4 ? 8 : mt == 8 ? 13 : 17; }
 
-template <int R, int MT, int KC, bool W8>
+template <int R, int MT, int KC, bool W8, bool KIN = false>
 hipError_t launch_skinny(const void* wp, const void* x, void* y, float* ws, int* cnt, int M, int N, int K, long ldx,
                          long ldy, int ksplit, int cps, const kgs::dec::SkinnyEpi& ep, hipStream_t s) {
-  const int nstrip = N / (64 * R);
+  const int nstrip = N / ((KIN ? 16 : 64) * R);
   if constexpr (!W8 && MT <= 4 && R == 1) {  // the fused layer's qkv variants (kgs/ops/decode.py rope_variant)
     if (ep.mode & kgs::dec::EPI_ROPE) {
-      hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, false, true>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
+      hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, false, true, KIN>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
                          (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
       return hipGetLastError();
     }
   }
   if (ep.mode & kgs::dec::EPI_ROPE) return hipErrorInvalidValue;  // no RoPE instantiation for this variant
-  hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, W8>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
+  hipLaunchKernelGGL((kgs::dec::skinny<R, MT, KC, W8, false, KIN>), dim3(nstrip * ksplit), dim3(256), 0, s, wp,
                      (const unsigned short*)x, (unsigned short*)y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep);
   return hipGetLastError();
 }
@@ -893,8 +945,9 @@ KGS_EXPORT int kgs_skinny_variant_geometry(int variant, int M, int* rows_per_str
   if (variant == 0) variant = default_variant(mt);
   if (variant < 0 || variant >= kNumVariants || kVariants[variant].mt != mt) return KGS_ERR_ARG;
   *mpad = 16 * mt;
-  *rows_per_strip = 64 * kVariants[variant].r;
-  *k_per_chunk = 32 * kVariants[variant].kc;
+  const int kin = kVariants[variant].kin;
+  *rows_per_strip = (kin ? 16 : 64) * kVariants[variant].r;
+  *k_per_chunk = (kin ? 4 : 1) * 32 * kVariants[variant].kc;
   return 0;
 }
 
@@ -979,7 +1032,7 @@ int skinny_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, in
   ep.eps = eps;
   ep.wscale = wscale;
   const bool w8 = wscale != nullptr;
-  if (w8 && variant > 12) return KGS_ERR_ARG;  // fp8 weights: batch buckets <= 64 (variants 1-12)
+  if (w8 && variant > 12 && variant < 20) return KGS_ERR_ARG;  // fp8 weights: batch buckets <= 64
   switch (variant * 2 + (w8 ? 1 : 0)) {
 #define KGS_SKV(id, R, MT, KC)                                                                                       \
   case 2 * id: return (int)launch_skinny<R, MT, KC, false>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s); \
@@ -993,6 +1046,10 @@ int skinny_fused(const void* wp, const void* x, void* y, float* ws, int* cnt, in
     KGS_SKV(13, 2, 8, 2) KGS_SKV(14, 2, 8, 4) KGS_SKV(15, 4, 8, 2) KGS_SKV(16, 1, 8, 4)
     KGS_SKV(17, 2, 16, 2) KGS_SKV(18, 1, 16, 4) KGS_SKV(19, 1, 16, 2)
 #undef KGS_SKV
+    case 2 * 20: return (int)launch_skinny<1, 1, 8, false, true>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
+    case 2 * 20 + 1: return (int)launch_skinny<1, 1, 8, true, true>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
+    case 2 * 21: return (int)launch_skinny<2, 1, 8, false, true>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
+    case 2 * 21 + 1: return (int)launch_skinny<2, 1, 8, true, true>(wp, x, y, ws, cnt, M, N, K, ldx, ldy, ksplit, cps, ep, s);
     default: return KGS_ERR_ARG;
   }
 }

@@ -24,6 +24,7 @@
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
+#   serve_b16    batch-16 serving; skinny_tune: skinny GEMM variant x split-K tune at batches $MS
 #   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
 #   serve_sweep  offline serving at batch 1 / 64 / 128 / 256 / 512, fp8 KV, fp8 prefill + fp8 KV (256 and 512)
 set -o pipefail
@@ -82,6 +83,9 @@ step() {
         paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
             --max-batch 1 --max-model-len 2048 ;;
+        serve_b16) run serve_b16 300 python -u -m kgs.serve bench --requests 16 --input-len 512 --output-len 256 \
+            --max-batch 16 --max-model-len 2048 ;;
+        skinny_tune) run skinny_tune 400 python bench/decode_bench.py --tune --ms "${MS:-1,16}" --iters 20 ;;
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;

@@ -421,3 +421,67 @@ def test_skinny_rope_epilogue_matches_rope_cache(m, heads, hkv):
     torch.cuda.synchronize()
     assert torch.equal(q1, q2)
     assert torch.equal(caches[0].layer(0), caches[1].layer(0))
+
+
+@pytest.mark.parametrize("m", [1, 5, 16])
+@pytest.mark.parametrize("v", [20, 21])
+def test_skinny_kin_variants(m, v):
+    """In-workgroup K split (variants 20 / 21): every split-K factor, fp8
+    weights, and the fused decode epilogues (RMS, SwiGLU, residual + sum of
+    squares, RoPE + KV write) against fp32 references / the default variant."""
+    from kgs.ops.decode import (PAGE, PackedWeight, PagedKVCache, rope_cache_, skinny_gemm,
+                                skinny_geometry)
+    from kgs.ops.transformer import rope_tables
+
+    n, k = 1024, 4096
+    rps, kpc, _ = skinny_geometry(m, v)
+    assert (rps, kpc) == ((16, 1024) if v == 20 else (32, 1024))
+    x = _bf(m, k)
+    w = _bf(n, k, scale=k ** -0.5)
+    ref = x.float() @ w.float().T
+    tol = 2e-2 * ref.abs().max().item() + 1e-3
+    pw = PackedWeight(w)
+    for ks in (1, 2, 4):
+        y = skinny_gemm(x, pw, ksplit=ks, variant=v)
+        torch.cuda.synchronize()
+        assert (y.float() - ref).abs().max().item() <= tol, ks
+    y8 = skinny_gemm(x, PackedWeight(w, fp8=True), ksplit=2, variant=v)
+    torch.cuda.synchronize()
+    assert (y8.float() - ref).abs().max().item() <= 8 * tol
+    # rms + swiglu
+    lnw = (_bf(k, scale=0.2) + 1).contiguous()
+    ss = x.float().pow(2).sum(-1).contiguous()
+    xn = (x.float() * torch.rsqrt(ss / k + 1e-5)[:, None]).bfloat16().float() * lnw.float()
+    wgu = _bf(2 * n, k, scale=k ** -0.5)
+    g, u = xn @ wgu[:n].float().T, xn @ wgu[n:].float().T
+    ref2 = g * torch.sigmoid(g) * u
+    got2 = skinny_gemm(x, PackedWeight(wgu, swiglu=True, fold=lnw), rms=ss, eps=1e-5, variant=v, ksplit=2)
+    torch.cuda.synchronize()
+    assert (got2.float() - ref2).abs().max().item() <= 3e-2 * ref2.abs().max().item()
+    # residual update + sums of squares
+    for ks in (1, 4):
+        res = _bf(m, n)
+        res0 = res.clone()
+        ss_out = torch.zeros(m, device=DEV)
+        skinny_gemm(x, pw, out=res, resid_ss=ss_out, ksplit=ks, variant=v)
+        torch.cuda.synchronize()
+        new_ref = res0.float() + ref
+        assert (res.float() - new_ref).abs().max().item() <= 2e-2 * new_ref.abs().max().item()
+        assert torch.allclose(ss_out, res.float().pow(2).sum(-1), rtol=1e-4, atol=1e-3)
+    if v != 20:
+        return
+    # RoPE + KV-cache write: same bits as the variant's plain output + rope_cache_
+    heads, hkv = 32, 8
+    nq = (heads + 2 * hkv) * 128
+    wq = _bf(nq, k, scale=k ** -0.5)
+    cos, sin = rope_tables(4096, 128, 500000.0, DEV)
+    pos = torch.randint(0, 4000, (m,), dtype=torch.int32, device=DEV)
+    slots = torch.randperm(16 * PAGE, device=DEV)[:m].int()
+    caches = [PagedKVCache(1, 16, hkv, DEV) for _ in range(2)]
+    q1 = skinny_gemm(x, PackedWeight(wq, fold=lnw), rms=ss, eps=1e-5, variant=v, ksplit=2)
+    rope_cache_(q1, cos, sin, pos, slots, caches[0].layer(0), heads, hkv)
+    q2 = skinny_gemm(x, PackedWeight(wq, fold=lnw, rope=(heads, hkv)), rms=ss, eps=1e-5, variant=v, ksplit=2,
+                     rope={"cos": cos, "sin": sin, "positions": pos, "slots": slots, "cache": caches[1].layer(0)})
+    torch.cuda.synchronize()
+    assert torch.equal(q1, q2)
+    assert torch.equal(caches[0].layer(0), caches[1].layer(0))

@@ -660,7 +660,7 @@ def test_decode_routing_tables_cpu():
         assert vs and all(D.SKINNY_VARIANTS[v][1] == D._mt(m) for v in vs)
         for v in vs:
             rps, kpc, mpad = D.skinny_geometry(m, v)
-            assert rps % 64 == 0 and kpc % 32 == 0 and mpad >= m
+            assert rps % (16 if v in D.KIN_VARIANTS else 64) == 0 and kpc % 32 == 0 and mpad >= m
     for key, val in D.TUNED.items():
         if val is not None:
             v, ks = val
@@ -670,6 +670,12 @@ def test_decode_routing_tables_cpu():
     assert D.use_skinny(1, 6144, 4096) and not D.use_skinny(256, 6144, 4096)
     assert D.use_skinny(20, 512, 1024) and not D.use_skinny(40, 512, 1024)
     assert D.skinny_config(16, 4096, 4096) == D.TUNED[(1, 4096, 4096)]
+    for (n, k), (v, ks, top) in D.TUNED_TINY.items():
+        assert D.skinny_config(1, n, k) == (v, ks) and D.skinny_config(top, n, k) == (v, ks)
+        if top < 16:
+            assert D.skinny_config(top + 1, n, k) == D.TUNED[(1, n, k)]
+        _, kpc, _ = D.skinny_geometry(1, v)
+        assert (k // kpc) % ks == 0 and n % D.skinny_geometry(1, v)[0] == 0
     pps, ns = D.decode_splits(1, 8, 128)
     assert pps >= 4 and pps * ns >= 128
 
