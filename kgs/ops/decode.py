@@ -165,10 +165,11 @@ TUNED: dict = {
 # (variant 20) wins while x is a few rows (each wave reads its B fragments
 # straight from L2, so x traffic grows with M); profiles/r2/skinny_kin_tune.jsonl
 TUNED_TINY: dict = {_QKV: (20, 1, 8), _GU: (20, 1, 4), _DOWN: (20, 1, 2)}
+TUNED_TINY_FP8: dict = {_GU: (21, 1, 4), _DOWN: (21, 7, 4)}
 # the same sweep for weight-only fp8 (--tune --fp8): (variant, ksplit) per (MT, N, K)
 TUNED_FP8: dict = {
-    (1, *_QKV): (1, 4), (2, *_QKV): (5, 4), (4, *_QKV): (9, 4),
-    (1, *_O): (1, 4), (2, *_O): (5, 4), (4, *_O): (10, 4),
+    (1, *_QKV): (20, 1), (2, *_QKV): (5, 4), (4, *_QKV): (9, 4),
+    (1, *_O): (20, 1), (2, *_O): (5, 4), (4, *_O): (10, 4),
     (1, *_GU): (1, 1), (2, *_GU): (7, 1), (4, *_GU): (12, 2),
     (1, *_DOWN): (1, 7), (2, *_DOWN): (5, 8), (4, *_DOWN): (9, 8),
     (1, *_LM): (1, 1), (2, *_LM): (6, 1), (4, *_LM): (11, 1),
@@ -278,7 +279,7 @@ def choose_ksplit(m: int, n: int, k: int, cus: int = CUS, variant: int = 0) -> i
 
 def skinny_config(m: int, n: int, k: int, fp8: bool = False) -> tuple[int, int]:
     """(variant, ksplit) for a skinny-GEMM call: the tuned entry, else the defaults."""
-    tiny = None if fp8 else TUNED_TINY.get((n, k))
+    tiny = (TUNED_TINY_FP8 if fp8 else TUNED_TINY).get((n, k))
     if tiny is not None and m <= tiny[2]:
         return tiny[:2]
     hit = (TUNED_FP8 if fp8 else TUNED).get((_mt(m), n, k))

@@ -83,9 +83,12 @@ step() {
         paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
             --max-batch 1 --max-model-len 2048 ;;
+        serve_b1_f8) run serve_b1_f8 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
+            --max-batch 1 --max-model-len 2048 --decode-weights fp8 ;;
         serve_b16) run serve_b16 300 python -u -m kgs.serve bench --requests 16 --input-len 512 --output-len 256 \
             --max-batch 16 --max-model-len 2048 ;;
         skinny_tune) run skinny_tune 400 python bench/decode_bench.py --tune --ms "${MS:-1,16}" --iters 20 ;;
+        skinny_tune_fp8) run skinny_tune_fp8 400 python bench/decode_bench.py --tune --fp8 --ms "${MS:-1,16}" --iters 20 ;;
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;

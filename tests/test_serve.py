@@ -670,12 +670,13 @@ def test_decode_routing_tables_cpu():
     assert D.use_skinny(1, 6144, 4096) and not D.use_skinny(256, 6144, 4096)
     assert D.use_skinny(20, 512, 1024) and not D.use_skinny(40, 512, 1024)
     assert D.skinny_config(16, 4096, 4096) == D.TUNED[(1, 4096, 4096)]
-    for (n, k), (v, ks, top) in D.TUNED_TINY.items():
-        assert D.skinny_config(1, n, k) == (v, ks) and D.skinny_config(top, n, k) == (v, ks)
-        if top < 16:
-            assert D.skinny_config(top + 1, n, k) == D.TUNED[(1, n, k)]
-        _, kpc, _ = D.skinny_geometry(1, v)
-        assert (k // kpc) % ks == 0 and n % D.skinny_geometry(1, v)[0] == 0
+    for fp8, tiny, table in ((False, D.TUNED_TINY, D.TUNED), (True, D.TUNED_TINY_FP8, D.TUNED_FP8)):
+        for (n, k), (v, ks, top) in tiny.items():
+            assert D.skinny_config(1, n, k, fp8) == (v, ks) and D.skinny_config(top, n, k, fp8) == (v, ks)
+            if top < 16:
+                assert D.skinny_config(top + 1, n, k, fp8) == table[(1, n, k)]
+            _, kpc, _ = D.skinny_geometry(1, v)
+            assert (k // kpc) % ks == 0 and n % D.skinny_geometry(1, v)[0] == 0
     pps, ns = D.decode_splits(1, 8, 128)
     assert pps >= 4 and pps * ns >= 128
 
@@ -697,10 +698,10 @@ def test_fp8_routing_table_cpu():
     from kgs.ops import decode as D
 
     for key, (v, ks) in D.TUNED_FP8.items():
-        assert v <= 12 and D.SKINNY_VARIANTS[v][1] == key[0]  # fp8 kernels exist for variants 1-12
+        assert (v <= 12 or v in D.KIN_VARIANTS) and D.SKINNY_VARIANTS[v][1] == key[0]  # fp8: 1-12, 20-21
         _, kpc, _ = D.skinny_geometry(16 * key[0], v)
         assert (key[2] // kpc) % ks == 0
-    assert D.skinny_config(1, 28672, 4096, fp8=True) == D.TUNED_FP8[(1, 28672, 4096)]
+    assert D.skinny_config(16, 28672, 4096, fp8=True) == D.TUNED_FP8[(1, 28672, 4096)]
 
 
 def test_w4x_routing_table_cpu():
