@@ -88,6 +88,7 @@ step() {
         serve_b16) run serve_b16 300 python -u -m kgs.serve bench --requests 16 --input-len 512 --output-len 256 \
             --max-batch 16 --max-model-len 2048 ;;
         skinny_tune) run skinny_tune 400 python bench/decode_bench.py --tune --ms "${MS:-1,16}" --iters 20 ;;
+        skinny_tune_70b) run skinny_tune_70b 500 python bench/decode_bench.py --tune --model llama3-70b --ms "${MS:-1,16}" --iters 10 ;;
         skinny_tune_fp8) run skinny_tune_fp8 400 python bench/decode_bench.py --tune --fp8 --ms "${MS:-1,16}" --iters 20 ;;
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
