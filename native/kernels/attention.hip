@@ -133,6 +133,10 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
     KGS_ATT_STORE()
   }
   __syncthreads();
+  // Q fragments complete before the loop: otherwise the waitcnt pass merges
+  // their pending loads into the loop header and makes every tile's QK^T
+  // MFMAs wait (vmcnt) for the NEXT tile's prefetch, exposing its latency
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
 
   f32x16 o[4];
 #pragma unroll

@@ -24,6 +24,7 @@
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
+#   attn_bench   flash-attention forward vs SDPA
 #   serve_b16    batch-16 serving; skinny_tune: skinny GEMM variant x split-K tune at batches $MS
 #   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
 #   serve_sweep  offline serving at batch 1 / 64 / 128 / 256 / 512, fp8 KV, fp8 prefill + fp8 KV (256 and 512)
@@ -88,6 +89,13 @@ step() {
         serve_b16) run serve_b16 300 python -u -m kgs.serve bench --requests 16 --input-len 512 --output-len 256 \
             --max-batch 16 --max-model-len 2048 ;;
         skinny_tune) run skinny_tune 400 python bench/decode_bench.py --tune --ms "${MS:-1,16}" --iters 20 ;;
+        attn_bench) run attn_bench 300 python bench/attention_bench.py ;;
+        attn_pmc) run attn_pmc1 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+            SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$O/apmc1" -o attn \
+            -- python3 bench/attention_bench.py --only attn --iters 5 &&
+            run attn_pmc2 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU \
+            SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$O/apmc2" -o attn \
+            -- python3 bench/attention_bench.py --only attn --iters 5 ;;
         skinny_tune_70b) run skinny_tune_70b 500 python bench/decode_bench.py --tune --model llama3-70b --ms "${MS:-1,16}" --iters 10 ;;
         skinny_tune_fp8) run skinny_tune_fp8 400 python bench/decode_bench.py --tune --fp8 --ms "${MS:-1,16}" --iters 20 ;;
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
