@@ -20,9 +20,9 @@
 //     256-B-row XOR image off(r, c) = 256 r + 16 (c ^ ((r&3)<<2 | (r>>2)&3)),
 //     conflict-free for the 16-lane groups of ds_read_b128 and the 32-lane
 //     halves of the transposed read;
-//   * register-staged double buffer: the next K/V tile's global loads are
-//     issued before the current tile's MFMAs and written to the other LDS
-//     buffer after them (cdna_hip_programming.md T14), one barrier per tile;
+//   * double buffer filled by LDS-DMA: the next K/V tile's global_load_lds
+//     are issued before the current tile's MFMAs (no staging registers),
+//     vmcnt(0) + one barrier per tile;
 //   * causal: fully-masked tiles are skipped per wave, the diagonal tiles are
 //     masked in registers; q-blocks are dispatched heaviest first, and the four
 //     query heads sharing a KV head are dealt to the same XCD back to back so
@@ -71,7 +71,7 @@ __device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
   return r;
 }
 
-__global__ __launch_bounds__(256, 2) void fwd(Args a) {
+__global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void fwd(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -108,35 +108,27 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
 
   const unsigned short* kbase = a.k + ktok0 * a.ldk + (long)kvh * HD;
   const unsigned short* vbase = a.v + ktok0 * a.ldv + (long)kvh * HD;
-  // staging: thread moves 16-B chunks id = tid + 256 i (i < 4) of each tile
-  uint4 sk0, sk1, sk2, sk3, sv0, sv1, sv2, sv3;
-#define KGS_ATT_LD(i, SK, SV)                                              \
-  {                                                                        \
-    const int id = tid + 256 * (i), r = id >> 4, c = id & 15;              \
-    const long row = (long)jn * KB + r;                                    \
-    SK = *(const uint4*)(kbase + row * a.ldk + 8 * c);                     \
-    SV = *(const uint4*)(vbase + row * a.ldv + 8 * c);                     \
-  }
-#define KGS_ATT_ST(i, SK, SV)                                              \
-  {                                                                        \
-    const int id = tid + 256 * (i), r = id >> 4, c = id & 15;              \
-    *(uint4*)(smem[sb][0] + off(r, c)) = SK;                               \
-    *(uint4*)(smem[sb][1] + off(r, c)) = SV;                               \
-  }
-#define KGS_ATT_LOAD() KGS_ATT_LD(0, sk0, sv0) KGS_ATT_LD(1, sk1, sv1) KGS_ATT_LD(2, sk2, sv2) KGS_ATT_LD(3, sk3, sv3)
-#define KGS_ATT_STORE() KGS_ATT_ST(0, sk0, sv0) KGS_ATT_ST(1, sk1, sv1) KGS_ATT_ST(2, sk2, sv2) KGS_ATT_ST(3, sk3, sv3)
+  // K/V tile jn -> LDS buffer sb by LDS-DMA (global_load_lds, no staging
+  // registers): a 16 KB tile is 16 chunks of 1 KB = 4 rows of 256 B; wave w
+  // issues chunks 4w .. 4w+3 of K and of V. Lane l lands at chunk + 16 l, i.e.
+  // at slot (r, c') of the XOR image, so it fetches column c = c' ^ swz(r).
+  auto dma_tiles = [&](int jn, int sb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ch = 4 * w + i;
+      const int r = 4 * ch + (lane >> 4), c = (lane & 15) ^ swz(r);
+      const long row = (long)jn * KB + r;
+      glds16(kbase + row * a.ldk + 8 * c, smem[sb][0] + 1024 * ch);
+      glds16(vbase + row * a.ldv + 8 * c, smem[sb][1] + 1024 * ch);
+    }
+  };
 
   const int ntile = a.causal ? (qoff + q0 + QB) / KB : a.Sk / KB;
-  {
-    const int jn = 0, sb = 0;
-    KGS_ATT_LOAD()
-    KGS_ATT_STORE()
-  }
-  __syncthreads();
-  // Q fragments complete before the loop: otherwise the waitcnt pass merges
-  // their pending loads into the loop header and makes every tile's QK^T
-  // MFMAs wait (vmcnt) for the NEXT tile's prefetch, exposing its latency
+  dma_tiles(0, 0);
+  // Q fragments and tile 0 complete before the loop (a vmcnt the waitcnt pass
+  // sees, so it does not carry the Q loads into the loop header)
   __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  __syncthreads();
 
   f32x16 o[4];
 #pragma unroll
@@ -149,24 +141,44 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
 
   for (int j = 0; j < ntile; ++j) {
     const int buf = j & 1;
-    if (j + 1 < ntile) {
-      const int jn = j + 1;
-      KGS_ATT_LOAD()
-    }
+    // the other buffer was released by the previous tile's barrier
+    if (j + 1 < ntile) dma_tiles(j + 1, buf ^ 1);
     const int kv0 = j * KB;
     if (!a.causal || kv0 <= qoff + qw + 31) {
       const char* Ks = smem[buf][0];
       const char* Vs = smem[buf][1];
+      // all 16 K fragments of the tile are read up front (the registers the
+      // LDS-DMA staging freed), so the QK^T MFMAs never wait on one LDS read
+      bf16x8 kf[2][8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) kf[t][ks] = *(const bf16x8*)(Ks + off(32 * t + l32, 2 * ks + hh));
+      __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler sinks them otherwise)
       f32x16 s[2];
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         s[t] = f32x16{};
 #pragma unroll
-        for (int ks = 0; ks < 8; ++ks) {
-          const bf16x8 kf = *(const bf16x8*)(Ks + off(32 * t + l32, 2 * ks + hh));
-          s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[t], 0, 0, 0);
-        }
+        for (int ks = 0; ks < 8; ++ks) s[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[t][ks], qf[ks], s[t], 0, 0, 0);
       }
+      // the first half of the tile's V fragments is read now, so its LDS
+      // latency hides under the softmax below (all 16 would spill at 2 waves
+      // per SIMD); the second half is read under the first half's P.V MFMAs
+      bf16x8 vfr[4][2][2];
+      auto read_v = [&](int d) {
+        const int c0 = 4 * d + 2 * (g & 1) + (tp >> 1);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int sp = 0; sp < 2; ++sp) {
+            const int kvb = 32 * t + 16 * sp + 4 * hh + tq;
+            vfr[d][t][sp] = tr_frag(Vs + off(kvb, c0) + 8 * (tp & 1), Vs + off(kvb + 8, c0) + 8 * (tp & 1));
+          }
+      };
+      read_v(0);
+      read_v(1);
+      __builtin_amdgcn_sched_barrier(0);
       if (a.causal && kv0 + KB - 1 > qoff + qw) {
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -211,23 +223,17 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
         pf[t][0] = pack8(s[t], 0);
         pf[t][1] = pack8(s[t], 8);
       }
+      read_v(2);
+      read_v(3);
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        const int c0 = 4 * d + 2 * (g & 1) + (tp >> 1);
+      for (int d = 0; d < 4; ++d)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-          for (int sp = 0; sp < 2; ++sp) {
-            const int kvb = 32 * t + 16 * sp + 4 * hh + tq;
-            const bf16x8 vf = tr_frag(Vs + off(kvb, c0) + 8 * (tp & 1), Vs + off(kvb + 8, c0) + 8 * (tp & 1));
-            o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[t][sp], o[d], 0, 0, 0);
-          }
-      }
+          for (int sp = 0; sp < 2; ++sp)
+            o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vfr[d][t][sp], pf[t][sp], o[d], 0, 0, 0);
     }
-    if (j + 1 < ntile) {
-      const int sb = buf ^ 1;
-      KGS_ATT_STORE()
-    }
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the next tile has landed
     __syncthreads();
   }
 
@@ -246,10 +252,6 @@ __global__ __launch_bounds__(256, 2) void fwd(Args a) {
     }
 }
 
-#undef KGS_ATT_LD
-#undef KGS_ATT_ST
-#undef KGS_ATT_LOAD
-#undef KGS_ATT_STORE
 }  // namespace attn
 }  // namespace kgs
 
