@@ -528,6 +528,10 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
   unsigned short* base = qkv + t * ld + (long)h * HD + 8 * c;
   bf16x8* p1 = (bf16x8*)base;
   bf16x8* p2 = (bf16x8*)(base + HD / 2);
+  // position and cache slot first: the cos/sin loads hang off pos[t], so its
+  // latency overlaps the qkv / partial loads instead of following them
+  const int p = pos[t];
+  const int sl = slot[t];
   bf16x8 a, b;
   if constexpr (SK) {
     const long MN = tokens * nh * HD, e = t * nh * HD + (long)h * HD + 8 * c;
@@ -565,7 +569,6 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
     b = *p2;
   }
   if (h < H + HKV) {
-    const int p = pos[t];
     const f32x4* cp = (const f32x4*)(cosv + (long)p * (HD / 2) + 8 * c);
     const f32x4* sp = (const f32x4*)(sinv + (long)p * (HD / 2) + 8 * c);
     const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
@@ -584,7 +587,6 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
     b = o2;
   }
   if (h < H) return;
-  const int sl = slot[t];
   if (sl < 0) return;
   const int page = sl / PAGE, tau = sl - page * PAGE;
   const bool isv = h >= H + HKV;
