@@ -17,7 +17,11 @@ with the kubelet's device-plugin side played by the in-tree fake kubelet
   pod-first-gemm        start the pod entrypoint as a child with exactly the
                         Allocate response's envs, the GPUs restricted to the
                         allocated render minors (ROCR_VISIBLE_DEVICES), until its
-                        first 8192^3 GEMM result line
+                        first checked 8192^3 GEMM result line (``KGS_FIRST_GEMM``
+                        from the native probe, or the worker's result when the
+                        probe is not built)
+  pod-workload          (reported, not in the value) the rest of the pod's run:
+                        the torch workers' GEMM / all-reduce workload
 
 What is NOT in the number (needs docker/kind, docs/e2e.md): kind create, image
 build/pull, containerd's container start and the kubelet's own pod sync.
@@ -102,15 +106,42 @@ def run_nokind(gpus: int = 1, dev_root: str = "/", fake_gpus: int = 0, gemm_size
         if minors:
             env["ROCR_VISIBLE_DEVICES"] = visible_devices_for(minors, dev_root)
         res_path = os.path.join(d, "pod_result.json")
+        cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "1",
+               "--json-out", res_path]
+        err_path = os.path.join(d, "pod.stderr")
         with t.phase("pod-first-gemm") as rec:
-            cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "1",
-                   "--json-out", res_path]
-            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=REPO)
-            if r.returncode != 0:
-                raise RuntimeError(f"pod entrypoint failed ({r.returncode}): {r.stderr[-2000:]}")
+            with open(err_path, "w") as err:
+                pod = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=err, text=True, cwd=REPO)
+            try:
+                deadline = time.monotonic() + timeout
+                first = None
+                for line in pod.stdout:  # the readiness line, as soon as the pod prints it
+                    if line.startswith("KGS_FIRST_GEMM "):
+                        first = json.loads(line[len("KGS_FIRST_GEMM "):])
+                        break
+                    if time.monotonic() > deadline:
+                        raise TimeoutError("pod first GEMM not reached")
+                if first is not None:
+                    if not first.get("ok"):
+                        raise RuntimeError(f"pod first-GEMM probe failed: {first}")
+                    rec.update(source="kgs-gpuprobe", probe_ready_s=first.get("t_first_gemm_s"))
+                else:
+                    rec.update(source="worker")  # no probe: the clock stops when the pod's run ends
+                    pod.wait(timeout=max(1.0, deadline - time.monotonic()))
+            except BaseException:
+                pod.kill()
+                pod.wait()
+                raise
+        with t.phase("pod-workload") as rec:
+            pod.stdout.read()
+            rc = pod.wait(timeout=timeout)
+            pod.stdout.close()
+            if rc != 0:
+                with open(err_path) as f:
+                    raise RuntimeError(f"pod entrypoint failed ({rc}): {f.read()[-2000:]}")
             with open(res_path) as f:
                 result = json.load(f)
-            rec.update(mode=result.get("mode"), n_gpus=result.get("n_gpus"))
+            rec.update(mode=result.get("mode"), n_gpus=result.get("n_gpus"), in_value=False)
         t.meta.update(pod_result=result, gpus_requested=gpus, fake=bool(fake_gpus),
                       allocate_envs=envs, rocr_visible_devices=env.get("ROCR_VISIBLE_DEVICES"))
     finally:
@@ -125,8 +156,10 @@ def run_nokind(gpus: int = 1, dev_root: str = "/", fake_gpus: int = 0, gemm_size
         if not keep_dir:
             shutil.rmtree(d, ignore_errors=True)
     phases = {p["phase"]: p["seconds"] for p in t.phases}
+    workload_s = phases.pop("pod-workload", None)
     summary = {"metric": "device-plugin start -> first in-pod GEMM (no kind)", "value": round(sum(phases.values()), 4),
                "unit": "s", "gpus": gpus, "fake": bool(fake_gpus), "phases": phases,
+               "pod_workload_s": workload_s,
                "excluded": "kind create, image build/pull, containerd container start, kubelet pod sync"}
     if result.get("gemm_tflops_total"):
         summary["in_pod_gemm_tflops"] = result["gemm_tflops_total"]

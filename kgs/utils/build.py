@@ -6,6 +6,9 @@ Builds, with the ROCm toolchain in ``/opt/rocm``:
   GEMM, vector add, transpose, checksum, P2P all-reduce) behind a C ABI that
   ``kgs/ops/_lib.py`` loads with ctypes. Built with ``-fvisibility=hidden``:
   only the ``KGS_EXPORT`` production entry points are exported.
+* ``kgs/_native/kgs-gpuprobe`` -- the pod's first-GEMM readiness probe: HIP
+  host code linked against ``libkgs_kernels.so`` (no Python, no torch), one
+  thread per visible GPU running the production GEMM with a sampled check.
 * ``kgs/_native/libkgs_experiments.so`` -- ``native/experiments/*.hip``, the
   measured GEMM alternatives and timing probes (some wrong by construction),
   opt-in through ``kgs.ops.experiments`` and never loaded by production code.
@@ -118,6 +121,15 @@ def targets() -> list[Target]:
             HIPCC,
             flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
             headers=k_headers,
+        ),
+        Target(
+            "gpuprobe",
+            OUT / "kgs-gpuprobe",
+            [NATIVE / "probe" / "gpuprobe.hip"],
+            HIPCC,
+            flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-Wall"],
+            link_flags=[f"-L{OUT}", "-lkgs_kernels", "-Wl,-rpath,$ORIGIN", "-pthread"],
+            shared=False,
         ),
         Target(
             "experiments",

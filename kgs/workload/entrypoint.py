@@ -9,6 +9,10 @@ pods/rocm-gpu-test-pod.yaml runs ``python3 -m kgs.workload.entrypoint --pod``:
    device plugin passed in), then start one worker process per GPU with
    ``torch.distributed.run`` -- vector add, bf16 MFMA GEMM, RCCL all-reduce
    sweep (:mod:`kgs.workload.worker`) -- and print one JSON result line.
+   Before the workers, the native first-GEMM probe (``kgs-gpuprobe``,
+   native/probe/gpuprobe.hip: HIP + libkgs_kernels.so, no Python/torch start-up)
+   runs one checked 8192^3 GEMM per GPU and prints ``KGS_FIRST_GEMM {...}``:
+   the pod's readiness point, ~2 s earlier than the torch worker's first GEMM.
    ``--smoke`` (BASELINE config 2) runs ``rocminfo`` and the HIP vector add
    only: passthrough works and a kernel launches, nothing heavier.
 3. ``--pod`` keeps the container Running afterwards (``sleep 3600`` in the
@@ -61,6 +65,32 @@ def allocated_gpus() -> list:
         want = {int(x) for x in alloc.split(",") if x.strip()}
         gpus = [g for g in gpus if g.render_minor in want]
     return gpus
+
+
+def probe_binary() -> str | None:
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "kgs-gpuprobe")
+    return exe if os.access(exe, os.X_OK) else None
+
+
+def run_probe(size: int, timeout: int = 300) -> dict:
+    """Native first-GEMM probe over every GPU this process sees. Its
+    ``KGS_FIRST_GEMM`` line is echoed as soon as it arrives (the readiness
+    point ``kgs bench --no-kind`` stops its clock at)."""
+    exe = probe_binary()
+    if exe is None:
+        return {"ok": False, "error": "kgs-gpuprobe not built (python -m kgs.utils.build)"}
+    try:
+        r = subprocess.run([exe, "--size", str(size)], capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"ok": False, "error": f"kgs-gpuprobe timed out after {timeout}s"}
+    for line in r.stdout.splitlines():
+        if line.startswith("KGS_FIRST_GEMM "):
+            print(line, flush=True)
+            res = json.loads(line[len("KGS_FIRST_GEMM "):])
+            res["rc"] = r.returncode
+            return res
+    sys.stderr.write(r.stderr[-2000:])
+    return {"ok": False, "rc": r.returncode, "error": "no KGS_FIRST_GEMM line"}
 
 
 def rocminfo_agents(timeout: int = 60) -> dict:
@@ -117,6 +147,9 @@ def main(argv=None) -> int:
     ap.add_argument("--smoke", action="store_true", help="config 2: rocminfo + HIP vector add only")
     ap.add_argument("--fp8", action="store_true", help="also report the e4m3 GEMM TFLOPS")
     ap.add_argument("--p2p", action="store_true", help="multi-GPU pods: P2P all-reduce latency vs RCCL")
+    ap.add_argument("--no-probe", action="store_true", help="skip the native first-GEMM probe")
+    ap.add_argument("--probe-only", action="store_true",
+                    help="run the native first-GEMM probe and stop (no torch workers)")
     a = ap.parse_args(argv)
 
     gpus = allocated_gpus()
@@ -132,6 +165,12 @@ def main(argv=None) -> int:
         if a.smoke:
             result["rocminfo"] = rocminfo_agents()
             print(f"rocminfo GPU agents: {result['rocminfo'].get('gpu_agents')}", flush=True)
+        if not a.smoke and not a.no_probe and a.gemm_size % 256 == 0:
+            result["first_gemm"] = run_probe(a.gemm_size, a.timeout)
+            if not result["first_gemm"].get("ok"):
+                result["all_ok"] = False
+        if a.probe_only:
+            return _finish(a, result, rc=0 if result.get("all_ok", True) else 1)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env = dict(os.environ)
         env["PYTHONPATH"] = root + (":" + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
@@ -152,24 +191,31 @@ def main(argv=None) -> int:
             cmd += ["--fp8"]
         if a.p2p:
             cmd += ["--p2p"]
+        ok_before = result.get("all_ok", True)
         p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=a.timeout)
         sys.stderr.write(p.stderr[-4000:])
         for line in p.stdout.splitlines():
             if line.startswith("KGS_RESULT "):
                 result.update(json.loads(line[len("KGS_RESULT "):]))
+                result["all_ok"] = ok_before and result.get("all_ok", True)
             else:
                 print(line, flush=True)
         result["worker_rc"] = p.returncode
         if a.counters and p.returncode == 0:
             result["counters"] = collect_counters(a, env)
+    return _finish(a, result)
+
+
+def _finish(a, result: dict, rc: int | None = None) -> int:
     result["t_end"] = time.time()
     line = json.dumps(result)
     print(line, flush=True)
     if a.json_out:
         with open(a.json_out, "w") as f:
             f.write(line + "\n")
-    rc = 0 if result.get("worker_rc", 0) == 0 and result.get("all_ok", True) else 1
-    if a.smoke and n and not result.get("rocminfo", {}).get("ok"):
+    if rc is None:
+        rc = 0 if result.get("worker_rc", 0) == 0 and result.get("all_ok", True) else 1
+    if a.smoke and result.get("n_gpus") and not result.get("rocminfo", {}).get("ok"):
         rc = 1
     if a.pod:
         time.sleep(a.hold)

@@ -1,0 +1,213 @@
+// kgs-gpuprobe: the pod's first-GEMM readiness probe, without Python or torch.
+//
+// The rocm-gpu-test pod's first result is "this GPU runs a full-size bf16 MFMA
+// GEMM correctly" (kgs/workload/entrypoint.py). Through the torch worker that
+// line costs ~2.5 s, nearly all of it `import torch` and the caching
+// allocator's start-up. This probe reaches the same point directly on HIP:
+// one host thread per visible GPU (the pod's ROCR_VISIBLE_DEVICES view) fills
+// U[-1,1) bf16 operands on the device, runs the production four-wave GEMM from
+// libkgs_kernels.so (kgs_gemm_bf16_nt, the same entry the Python op uses),
+// checks sampled outputs against an fp32 host dot product of the same
+// operands, and prints one line:
+//
+//   KGS_FIRST_GEMM {"ok":true,"t_first_gemm_s":...,"devices":[...]}
+//
+// Stands in for the reference's "pod is Running" signal
+// (/root/reference/.github/workflows/rocm-ci.yaml:33-39 waits for Ready, then
+// greps the pod log) with a stricter one: the GPU computed a correct GEMM.
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+extern "C" int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K,
+                                int lda, int ldb, int ldc, int epi, int variant, hipStream_t stream);
+
+namespace {
+
+using clk = std::chrono::steady_clock;
+
+// Operand element i of matrix `seed`: a hashed U[-1,1) value rounded to bf16
+// (nearest-even). Host and device compute the same bits.
+__host__ __device__ inline unsigned short operand_bits(unsigned long long seed, unsigned long long i) {
+  unsigned long long z = i * 0x9E3779B97F4A7C15ull + seed * 0xD1B54A32D192ED03ull + 0x632BE59BD9B4E019ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  const float u = (float)(z >> 40) * (1.0f / 16777216.0f) * 2.0f - 1.0f;  // 24 random bits
+  unsigned int b;
+  __builtin_memcpy(&b, &u, 4);
+  return (unsigned short)((b + 0x7fffu + ((b >> 16) & 1u)) >> 16);
+}
+
+inline float bf16_to_float(unsigned short h) {
+  unsigned int b = (unsigned int)h << 16;
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+
+__global__ void fill_operand(unsigned short* __restrict__ p, unsigned long long n, unsigned long long seed) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    p[i] = operand_bits(seed, i);
+}
+
+struct DevResult {
+  int index = 0;
+  std::string arch;
+  int cus = 0;
+  double init_ms = 0, fill_ms = 0, first_gemm_ms = 0, tflops = 0, rel_err = 1, done_s = 0;
+  bool ok = false;
+  std::string error;
+};
+
+#define PROBE_CHECK(x)                                                         \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      r.error = std::string(#x) + ": " + hipGetErrorString(e_);                \
+      return;                                                                  \
+    }                                                                          \
+  } while (0)
+
+void probe_device(int dev, int n, int iters, clk::time_point t0, DevResult& r) {
+  r.index = dev;
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+  const auto ts = clk::now();
+  PROBE_CHECK(hipSetDevice(dev));
+  hipDeviceProp_t prop;
+  PROBE_CHECK(hipGetDeviceProperties(&prop, dev));
+  r.arch = prop.gcnArchName;
+  r.cus = prop.multiProcessorCount;
+  const size_t elems = (size_t)n * n;
+  unsigned short *A = nullptr, *B = nullptr, *C = nullptr;
+  PROBE_CHECK(hipMalloc(&A, elems * 2));
+  PROBE_CHECK(hipMalloc(&B, elems * 2));
+  PROBE_CHECK(hipMalloc(&C, elems * 2));
+  hipStream_t s;
+  PROBE_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  r.init_ms = ms_since(ts);
+
+  const auto tf = clk::now();
+  const int grid = 4 * r.cus;
+  hipLaunchKernelGGL(fill_operand, dim3(grid), dim3(256), 0, s, A, (unsigned long long)elems, 1ull);
+  hipLaunchKernelGGL(fill_operand, dim3(grid), dim3(256), 0, s, B, (unsigned long long)elems, 2ull);
+  PROBE_CHECK(hipGetLastError());
+  PROBE_CHECK(hipStreamSynchronize(s));
+  r.fill_ms = ms_since(tf);
+
+  const auto tg = clk::now();
+  int rc = kgs_gemm_bf16_nt(A, B, C, nullptr, n, n, n, n, n, n, 0, 0, s);
+  if (rc != 0) {
+    r.error = "kgs_gemm_bf16_nt returned " + std::to_string(rc);
+    return;
+  }
+  PROBE_CHECK(hipStreamSynchronize(s));
+  r.first_gemm_ms = ms_since(tg);
+
+  // sampled check: 4 rows x 64 columns against an fp32 host dot product
+  const int rows[4] = {0, n / 3 + 1, n / 2 + 5, n - 1};
+  std::vector<unsigned short> crow(n);
+  std::vector<float> arow(n), bcol(n);
+  double max_err = 0, max_ref = 0;
+  for (int ri = 0; ri < 4; ++ri) {
+    const int i = rows[ri];
+    PROBE_CHECK(hipMemcpy(crow.data(), C + (size_t)i * n, (size_t)n * 2, hipMemcpyDeviceToHost));
+    for (int k = 0; k < n; ++k) arow[k] = bf16_to_float(operand_bits(1, (unsigned long long)i * n + k));
+    for (int cj = 0; cj < 64; ++cj) {
+      const int j = (int)(((long long)cj * 131 + ri * 7) % n);
+      double acc = 0;
+      for (int k = 0; k < n; ++k)
+        acc += (double)arow[k] * bf16_to_float(operand_bits(2, (unsigned long long)j * n + k));
+      max_err = std::fmax(max_err, std::fabs(bf16_to_float(crow[j]) - acc));
+      max_ref = std::fmax(max_ref, std::fabs(acc));
+    }
+  }
+  r.rel_err = max_ref > 0 ? max_err / max_ref : 1.0;
+  r.ok = r.rel_err < 1e-2;
+  r.done_s = std::chrono::duration<double>(clk::now() - t0).count();
+
+  if (iters > 0) {  // throughput after the readiness point (does not delay it)
+    hipEvent_t e0, e1;
+    PROBE_CHECK(hipEventCreate(&e0));
+    PROBE_CHECK(hipEventCreate(&e1));
+    PROBE_CHECK(hipEventRecord(e0, s));
+    for (int it = 0; it < iters; ++it) kgs_gemm_bf16_nt(A, B, C, nullptr, n, n, n, n, n, n, 0, 0, s);
+    PROBE_CHECK(hipEventRecord(e1, s));
+    PROBE_CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    PROBE_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    r.tflops = 2.0 * n * (double)n * n * iters / (ms * 1e-3) / 1e12;
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+  }
+  hipStreamDestroy(s);
+  hipFree(A);
+  hipFree(B);
+  hipFree(C);
+}
+
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    if ((unsigned char)c >= 0x20) o += c;
+  }
+  return o;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const auto t0 = clk::now();
+  int n = 8192, iters = 5;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--size") && i + 1 < argc) n = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[++i]);
+    else {
+      fprintf(stderr, "usage: kgs-gpuprobe [--size N (multiple of 256)] [--iters K]\n");
+      return 2;
+    }
+  }
+  if (n <= 0 || n % 256 || n > 32768 || iters < 0) {
+    fprintf(stderr, "kgs-gpuprobe: --size must be a positive multiple of 256 up to 32768\n");
+    return 2;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    printf("KGS_FIRST_GEMM {\"ok\":false,\"error\":\"no HIP device visible\",\"devices\":[]}\n");
+    return 1;
+  }
+  std::vector<DevResult> res(ndev);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; ++d) th.emplace_back(probe_device, d, n, iters, t0, std::ref(res[d]));
+  for (auto& t : th) t.join();
+  bool ok = true;
+  double t_first = 0;
+  std::string devs;
+  for (auto& r : res) {
+    ok = ok && r.ok;
+    t_first = std::fmax(t_first, r.done_s);
+    char buf[512];
+    snprintf(buf, sizeof buf,
+             "{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"ok\":%s,\"init_ms\":%.2f,\"fill_ms\":%.2f,"
+             "\"first_gemm_ms\":%.2f,\"rel_err\":%.3e,\"tflops\":%.1f,\"ready_s\":%.4f",
+             r.index, json_escape(r.arch).c_str(), r.cus, r.ok ? "true" : "false", r.init_ms, r.fill_ms,
+             r.first_gemm_ms, r.rel_err, r.tflops, r.done_s);
+    if (!devs.empty()) devs += ",";
+    devs += buf;
+    if (!r.error.empty()) devs += ",\"error\":\"" + json_escape(r.error) + "\"";
+    devs += "}";
+  }
+  printf("KGS_FIRST_GEMM {\"ok\":%s,\"size\":%d,\"n_gpus\":%d,\"t_first_gemm_s\":%.4f,\"devices\":[%s]}\n",
+         ok ? "true" : "false", n, ndev, t_first, devs.c_str());
+  fflush(stdout);
+  return ok ? 0 : 1;
+}

@@ -373,6 +373,22 @@ def test_bench_no_kind_fake_chain(world, tmp_path, capsys):
     assert len(alloc["device_ids"]) == 2
 
 
+def test_gpuprobe_rejects_bad_sizes_before_touching_the_gpu():
+    """The native first-GEMM probe validates its shape on the host (the GEMM
+    grid assumes 256-multiples) and exits 2 without any HIP call."""
+    import subprocess
+
+    from kgs.workload.entrypoint import probe_binary
+
+    exe = probe_binary()
+    if exe is None:
+        pytest.skip("kgs-gpuprobe not built")
+    for bad in (["--size", "1000"], ["--size", "0"], ["--iters", "-1"], ["--bogus"]):
+        r = subprocess.run([exe, *bad], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 2, (bad, r.stdout, r.stderr)
+        assert "KGS_FIRST_GEMM" not in r.stdout
+
+
 def test_pod_verb_renders_static_pods_on_the_configured_registry(world, capsys):
     assert run("pod", "rocm-gpu-test", "--registry-port=5123") == 0
     doc = yaml.safe_load(capsys.readouterr().out)

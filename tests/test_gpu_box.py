@@ -81,6 +81,26 @@ def test_bench_no_kind_chain_on_the_box(tmp_path):
     assert t["pod_result"]["mode"] == "gpu" and t["pod_result"]["n_gpus"] == 1
     assert t["allocate_envs"]["KGS_RENDER_MINORS"] and t["rocr_visible_devices"] is not None
     assert s.get("in_pod_gemm_tflops", 0) > 300, s
+    # the clock stops at the native probe's checked first GEMM, not at the torch worker's
+    assert t["pod_result"]["first_gemm"]["ok"] is True, t["pod_result"]
+    first = [p for p in t["phases"] if p["phase"] == "pod-first-gemm"][0]
+    assert first["source"] == "kgs-gpuprobe", first
+    assert s["pod_workload_s"] is not None
+
+
+def test_gpuprobe_first_gemm_checked():
+    """kgs-gpuprobe: HIP + libkgs_kernels.so, no torch; one checked GEMM per GPU."""
+    from kgs.workload.entrypoint import probe_binary
+
+    exe = probe_binary()
+    assert exe is not None, "kgs-gpuprobe not built"
+    r = subprocess.run([exe, "--size", "1024", "--iters", "2"], capture_output=True, text=True, env=ENV, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("KGS_FIRST_GEMM ")][0]
+    res = json.loads(line.split(" ", 1)[1])
+    assert res["ok"] and res["n_gpus"] >= 1
+    d = res["devices"][0]
+    assert d["arch"].startswith("gfx950") and d["rel_err"] < 1e-2 and d["tflops"] > 0, d
 
 
 def test_device_plugin_self_test_allocates_real_paths():
