@@ -64,17 +64,6 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lo, const char* hi) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// value of lane l ^ 32 combined with lane l's own, by one VALU swap
-// (v_permlane32_swap) instead of an LDS round trip (ds_bpermute)
-__device__ __forceinline__ float xor32_max(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-__device__ __forceinline__ float xor32_sum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-
 __device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
   bf16x8 r;
 #pragma unroll
@@ -204,7 +193,7 @@ __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) 
       for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[t][r]);
-      mx = xor32_max(mx);
+      mx = xor32_max(mx);  // v_permlane32_swap (kgs_common.h), not an LDS round trip
       // deferred rescale (guide T13): the running max m only moves when a row's
       // new max exceeds it by more than RESCALE (log2 units after sl2), so most
       // tiles skip the 64-multiply O rescale; p = exp2(s sl2 - m sl2) then stays

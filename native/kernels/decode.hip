@@ -50,14 +50,9 @@ __host__ __device__ __forceinline__ int kv_v_index(int tau, int d) {
   return ((dt * 64) + g * 16 + m) * 8 + j;
 }
 
-__device__ __forceinline__ float wmax16(float v) {
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
-  return fmaxf(v, __shfl_xor(v, 32, 64));
-}
-__device__ __forceinline__ float wsum16(float v) {
-  v += __shfl_xor(v, 16, 64);
-  return v + __shfl_xor(v, 32, 64);
-}
+// over the four 16-lane rows (lanes of one column), on the permlane swaps
+__device__ __forceinline__ float wmax16(float v) { return xor32_max(xor16_max(v)); }
+__device__ __forceinline__ float wsum16(float v) { return xor32_sum(xor16_sum(v)); }
 
 // In-launch hand-offs (split-K slabs, attention split partials): producers store
 // WRITE-THROUGH (sc1 buffer stores) and drain, so they need no release fence (a
@@ -363,7 +358,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
     if (ep.mode & EPI_SWIGLU) {
       f32x4v u;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) u[i] = __shfl_xor(v[i], 32, 64);
+      for (int i = 0; i < 4; ++i) u[i] = lane_xor32(v[i]);
       if (m < M && g < 2) {
         f32x4v o;
 #pragma unroll
@@ -398,7 +393,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
       for (int i = 0; i < 4; ++i) vb[i] = bf2f(f2bf(v[i]));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) pb[i] = __shfl_xor(vb[i], 32, 64);
+      for (int i = 0; i < 4; ++i) pb[i] = lane_xor32(vb[i]);
       // original dim of element 0: rotated heads hold (d, d + 64) pairs in a tile
       const int d0 = rot ? (g < 2 ? 8 * t + 4 * g : 64 + 8 * t + 4 * (g - 2)) : 16 * t + 4 * g;
       if (m < M) {

@@ -43,6 +43,32 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
 }
 
+// Cross-lane exchanges on gfx950's half-swaps (one VALU op each, no LDS round
+// trip like the ds_bpermute behind __shfl_xor). With both operands = x,
+// permlane32_swap returns {x of lanes 0-31 in both halves, x of lanes 32-63 in
+// both halves}; permlane16_swap does the same for each pair of 16-lane rows.
+__device__ __forceinline__ float xor32_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), true, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), true, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor16_max(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), true, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor16_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), true, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// the value of lane l ^ 32
+__device__ __forceinline__ float lane_xor32(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), true, false);
+  return __uint_as_float((__lane_id() & 32) ? r[0] : r[1]);
+}
+
 // 16-byte LDS-DMA: each lane's 16 global bytes land at lds_base + lane*16
 // (lds_base must be wave-uniform). The swizzle, if any, is applied to the
 // per-lane *source* address (cdna_hip_programming.md rule 21).
