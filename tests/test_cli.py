@@ -389,6 +389,33 @@ def test_gpuprobe_rejects_bad_sizes_before_touching_the_gpu():
         assert "KGS_FIRST_GEMM" not in r.stdout
 
 
+def test_entrypoint_probe_line_parsing(tmp_path, monkeypatch, capsys):
+    """run_probe echoes the probe's KGS_FIRST_GEMM line and returns it parsed;
+    a probe that prints no line, or reports a failed check, makes the pod fail."""
+    from kgs.workload import entrypoint
+
+    def fake(body: str) -> str:
+        exe = tmp_path / f"probe{len(list(tmp_path.iterdir()))}"
+        exe.write_text("#!/bin/sh\n" + body + "\n")
+        exe.chmod(0o755)
+        return str(exe)
+
+    good = fake('echo \'KGS_FIRST_GEMM {"ok":true,"n_gpus":1,"t_first_gemm_s":0.25,"devices":[]}\'')
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: good)
+    res = entrypoint.run_probe(256, timeout=30)
+    assert res["ok"] is True and res["rc"] == 0 and res["t_first_gemm_s"] == 0.25
+    assert capsys.readouterr().out.startswith("KGS_FIRST_GEMM ")
+    bad = fake('echo \'KGS_FIRST_GEMM {"ok":false,"devices":[]}\'; exit 1')
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: bad)
+    assert entrypoint.run_probe(256, timeout=30)["ok"] is False
+    silent = fake("exit 3")
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: silent)
+    res = entrypoint.run_probe(256, timeout=30)
+    assert res["ok"] is False and res["rc"] == 3
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: None)
+    assert "not built" in entrypoint.run_probe(256)["error"]
+
+
 def test_pod_verb_renders_static_pods_on_the_configured_registry(world, capsys):
     assert run("pod", "rocm-gpu-test", "--registry-port=5123") == 0
     doc = yaml.safe_load(capsys.readouterr().out)
