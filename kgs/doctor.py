@@ -10,7 +10,10 @@ MI355X-specific pieces the reference never had to care about:
   this user (the kind node containers bind-mount them);
 * the native gpuinfo core finds the GPUs, they are gfx950, healthy, and the
   xGMI mesh is complete (every pair linked: what RCCL's rings need);
-* the local registry port is free or already ours.
+* the local registry port is free or already ours;
+* the in-tree native build (HIP kernels, first-GEMM probe, gpuinfo core) is
+  present and newer than its sources (WARN otherwise: the workload image
+  rebuilds it, but a host-side ``kgs bench --no-kind`` runs what is in the tree).
 
 Each check is OK / WARN / FAIL; exit status 1 if any FAIL. ``--json`` for tools.
 """
@@ -114,11 +117,28 @@ def check_registry_port(port: int, runner: Runner, runtime: str | None) -> Check
     return Check("registry port", "FAIL", f"{port} in use by something else (use --registry-port)")
 
 
+def check_native_build() -> Check:
+    from .utils import build
+
+    missing, stale = [], []
+    for t in build.targets():
+        if not t.output.exists():
+            (stale if t.optional else missing).append(t.name)
+        elif t.stale():
+            stale.append(t.name)
+    if missing:
+        return Check("native build", "WARN", f"not built: {', '.join(missing)} (python -m kgs.utils.build)")
+    if stale:
+        return Check("native build", "WARN", f"older than sources: {', '.join(stale)} (python -m kgs.utils.build)")
+    return Check("native build", "OK", f"{len(build.targets())} targets fresh for {build.ARCH}")
+
+
 def run_doctor(settings: C.Settings, as_json: bool = False, runner: Runner | None = None) -> int:
     runner = runner or Runner()
     checks = check_tools(runner, settings.runtime)
     checks += check_devices(settings.dev_root)
     checks.append(check_registry_port(settings.registry_port, runner, settings.runtime))
+    checks.append(check_native_build())
     failed = any(c.status == "FAIL" for c in checks)
     if as_json:
         print(json.dumps({"ok": not failed, "checks": [c.as_dict() for c in checks]}, indent=1))

@@ -467,6 +467,33 @@ def test_doctor_fake_mi355x_box(world, tmp_path, capsys):
     assert st["health"][0] == "OK"
 
 
+def test_doctor_native_build_check(monkeypatch):
+    """The native-build check reports missing and stale targets as WARN."""
+    from pathlib import Path
+
+    from kgs import doctor
+    from kgs.utils import build
+
+    class T:
+        def __init__(self, name, exists, stale, optional=False):
+            self.name, self.optional = name, optional
+            self.output = Path("/") if exists else Path("/nonexistent/kgs-x")
+            self._stale = stale
+
+        def stale(self):
+            return self._stale
+
+    monkeypatch.setattr(build, "targets", lambda: [T("kernels", True, False), T("gpuprobe", True, False)])
+    c = doctor.check_native_build()
+    assert c.status == "OK" and "2 targets fresh" in c.detail
+    monkeypatch.setattr(build, "targets", lambda: [T("kernels", True, True), T("gpuprobe", False, True)])
+    c = doctor.check_native_build()
+    assert c.status == "WARN" and "not built: gpuprobe" in c.detail
+    monkeypatch.setattr(build, "targets", lambda: [T("kernels", True, True), T("rccl-bench", False, True, True)])
+    c = doctor.check_native_build()
+    assert c.status == "WARN" and "older than sources: kernels, rccl-bench" in c.detail
+
+
 def test_doctor_missing_tools_fails(world, monkeypatch, capsys):
     monkeypatch.setenv("PATH", "/nonexistent")
     assert run("doctor", "--dev-root", world.nogpu, "--registry-port", "0") == 1
