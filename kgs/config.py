@@ -15,7 +15,12 @@ DEFAULT_REGISTRY_PORT = 5000
 # this mirror (kind-gpu-sim.sh:144-178, :5); here it is a build argument.
 BASE_MIRROR = "public.ecr.aws/docker/library"
 REGISTRY_IMAGE = f"{BASE_MIRROR}/registry:2"
-ROCM_BASE_IMAGE = "docker.io/rocm/pytorch:latest"
+# Pinned bases (the reference pins nothing for ROCm, Q6). gfx950 needs ROCm >= 7.0.
+ROCM_BASE_IMAGE = "docker.io/rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.8.0"
+ROCM_DEV_IMAGE = "docker.io/rocm/dev-ubuntu-22.04:7.0"          # amd-smi source of the plugin image
+PY_BUILD_IMAGE = "python:3.12.8-bookworm"
+PY_SLIM_IMAGE = "python:3.12.8-slim-bookworm"
+VLLM_ROCM_IMAGE = "docker.io/rocm/vllm:rocm7.0.0_vllm_0.10.2_20251006"
 DEFAULT_CLUSTER_NAME = "kind-gpu-sim"
 DEFAULT_IMAGE_NAME = "not-set"
 
@@ -87,6 +92,7 @@ class Settings:
     registry_image: str | None = None    # None = <base_mirror>/registry:2
     base_mirror: str = BASE_MIRROR       # C13: registry prefix for library base images
     rocm_base_image: str = ROCM_BASE_IMAGE
+    rocm_dev_image: str = ROCM_DEV_IMAGE
     kind_node_image: str | None = None
     config_file: str = CONFIG_FILE
     dry_run: bool = False
@@ -108,8 +114,9 @@ class Settings:
 
     def plugin_build_args(self) -> list[str]:
         """``--build-arg`` list for images/Dockerfile.deviceplugin."""
-        return ["--build-arg", f"PY_IMAGE={self.library_image('python:3.12-slim')}",
-                "--build-arg", f"BUILD_IMAGE={self.library_image('python:3.12')}"]
+        return ["--build-arg", f"PY_IMAGE={self.library_image(PY_SLIM_IMAGE)}",
+                "--build-arg", f"BUILD_IMAGE={self.library_image(PY_BUILD_IMAGE)}",
+                "--build-arg", f"ROCM_IMAGE={self.rocm_dev_image}"]
 
     @property
     def registry_host(self) -> str:

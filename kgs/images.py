@@ -26,7 +26,7 @@ def build_images(p, workload: bool = True, plugin: bool = True) -> int:
     if workload:
         if p.topology is None and p.s.fake_gpus is None:
             p.discover()
-        base = p.s.library_image("python:3.12-slim") if p.fake else p.s.rocm_base_image
+        base = p.s.library_image(C.PY_SLIM_IMAGE) if p.fake else p.s.rocm_base_image
         tag = f"{p.s.registry_host}/{C.WORKLOAD_IMAGE_REPO}:{C.WORKLOAD_IMAGE_TAG}"
         rt.cr("build", "-t", tag, "--build-arg", f"BASE_IMAGE={base}",
               "--build-arg", f"BUILD_NATIVE={'0' if p.fake else '1'}",

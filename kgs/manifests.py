@@ -196,6 +196,101 @@ def gpu_test_pod(image: str, gpus: int = 1, command: list | None = None, name: s
     }
 
 
+# Llama-3-8B architecture (config.json only: no weights, no tokenizer). vLLM
+# builds the model from it and --load-format=dummy random-initialises the
+# weights, so the pod starts on an offline host (BASELINE config 5, synthetic
+# weights). Kept in sync with kgs.models.llama.LlamaConfig.llama3_8b() by a test.
+LLAMA3_8B_HF_CONFIG = {
+    "architectures": ["LlamaForCausalLM"],
+    "model_type": "llama",
+    "attention_bias": False,
+    "attention_dropout": 0.0,
+    "bos_token_id": 128000,
+    "eos_token_id": 128001,
+    "hidden_act": "silu",
+    "hidden_size": 4096,
+    "initializer_range": 0.02,
+    "intermediate_size": 14336,
+    "max_position_embeddings": 8192,
+    "mlp_bias": False,
+    "num_attention_heads": 32,
+    "num_hidden_layers": 32,
+    "num_key_value_heads": 8,
+    "pretraining_tp": 1,
+    "rms_norm_eps": 1e-05,
+    "rope_scaling": None,
+    "rope_theta": 500000.0,
+    "tie_word_embeddings": False,
+    "torch_dtype": "bfloat16",
+    "use_cache": True,
+    "vocab_size": 128256,
+}
+VLLM_MODEL_DIR = "/models/llama3-8b"
+VLLM_CONFIGMAP = "vllm-llama3-8b-config"
+
+
+def vllm_rocm_pod(image: str = C.VLLM_ROCM_IMAGE) -> list:
+    """``pods/vllm-rocm-pod.yaml``: a ConfigMap holding the Llama-3-8B
+    ``config.json`` plus the serving Pod that mounts it at ``/models/llama3-8b``.
+
+    Mirrors /root/reference/pods/vllm-cpu-pod.yaml:1-38 (name pattern, port
+    8000, /dev/shm memory emptyDir, privileged, GPU nodeSelector/toleration with
+    the value quoted -- Q12) with a real ``amd.com/gpu: 1``. Offline by
+    construction: the model is a local path (no hub id), weights are
+    ``--load-format=dummy`` and ``--skip-tokenizer-init`` means no tokenizer is
+    needed (requests send token ids)."""
+    cm = {
+        "apiVersion": "v1",
+        "kind": "ConfigMap",
+        "metadata": {"name": VLLM_CONFIGMAP},
+        "data": {"config.json": json.dumps(LLAMA3_8B_HF_CONFIG, indent=2) + "\n"},
+    }
+    pod = {
+        "apiVersion": "v1",
+        "kind": "Pod",
+        "metadata": {"name": "vllm-rocm-pod"},
+        "spec": {
+            "containers": [{
+                "name": "vllm-rocm-container",
+                "image": image,
+                "ports": [{"containerPort": 8000}],
+                "env": [
+                    {"name": "HF_HUB_OFFLINE", "value": "1"},
+                    {"name": "TRANSFORMERS_OFFLINE", "value": "1"},
+                ],
+                "command": ["python3", "-m", "vllm.entrypoints.openai.api_server"],
+                "args": [
+                    f"--model={VLLM_MODEL_DIR}",
+                    "--served-model-name=llama3-8b",
+                    "--load-format=dummy",
+                    "--skip-tokenizer-init",
+                    "--dtype=bfloat16",
+                    "--tensor-parallel-size=1",
+                    "--max-model-len=8192",
+                    "--gpu-memory-utilization=0.90",
+                    "--port=8000",
+                ],
+                "resources": {"limits": {C.RESOURCE_NAME: 1}},
+                "readinessProbe": {"httpGet": {"path": "/health", "port": 8000},
+                                   "periodSeconds": 5, "failureThreshold": 120},
+                "volumeMounts": [
+                    {"name": "dshm", "mountPath": "/dev/shm"},
+                    {"name": "model-config", "mountPath": VLLM_MODEL_DIR, "readOnly": True},
+                ],
+                "securityContext": {"privileged": True},
+            }],
+            "nodeSelector": {C.LABEL_HARDWARE[0]: C.LABEL_HARDWARE[1]},
+            "tolerations": [{"key": C.TAINT[0], "operator": "Equal", "value": C.TAINT[1], "effect": C.TAINT[2]}],
+            "volumes": [
+                {"name": "dshm", "emptyDir": {"medium": "Memory", "sizeLimit": "16Gi"}},
+                {"name": "model-config", "configMap": {"name": VLLM_CONFIGMAP}},
+            ],
+            "restartPolicy": "Never",
+        },
+    }
+    return [cm, pod]
+
+
 STATIC_POD_REGISTRY = "localhost:5000"  # what pods/*.yaml are written against (the reference default port)
 
 

@@ -101,14 +101,38 @@ def _py_ext_suffix() -> str:
     return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
 
 
-def targets() -> list[Target]:
+# ``--only`` group names: the device-plugin image builds ``gpuinfo`` (the three
+# targets of the enumeration core) and nothing that needs hipcc.
+GROUPS = {
+    "gpuinfo": ("gpuinfo-lib", "gpuinfo-py", "gpuinfo-cli"),
+    "gpu": ("kernels", "gpuprobe", "experiments", "rccl-bench"),
+}
+
+
+def expand_only(only: list[str] | None) -> list[str] | None:
+    if not only:
+        return None
+    out: list[str] = []
+    for name in only:
+        for t in GROUPS.get(name, (name,)):
+            if t not in out:
+                out.append(t)
+    return out
+
+
+def amdsmi_header(rocm: Path | None = None) -> Path:
+    return (rocm or ROCM) / "include" / "amd_smi" / "amdsmi.h"
+
+
+def targets(out: Path | None = None) -> list[Target]:
+    odir = Path(out) if out is not None else OUT
     kdir = NATIVE / "kernels"
     gdir = NATIVE / "gpuinfo"
     rdir = NATIVE / "rccl_bench"
     sdir = NATIVE / "serve"
     k_headers = sorted(kdir.glob("*.h"))
     g_headers = sorted(gdir.glob("*.h"))
-    amdsmi_ok = (ROCM / "include" / "amd_smi" / "amdsmi.h").exists()
+    amdsmi_ok = amdsmi_header().exists()
     smi_flags = ["-DKGS_HAVE_AMDSMI=1", f"-I{ROCM / 'include'}"] if amdsmi_ok else []
     # amd-smi is dlopen'ed at run time (native/gpuinfo/smi.cpp): headers only, no link dependency
     smi_link = ["-ldl"]
@@ -116,7 +140,7 @@ def targets() -> list[Target]:
     ts = [
         Target(
             "kernels",
-            OUT / "libkgs_kernels.so",
+            odir / "libkgs_kernels.so",
             sorted(kdir.glob("*.hip")),
             HIPCC,
             flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
@@ -124,16 +148,16 @@ def targets() -> list[Target]:
         ),
         Target(
             "gpuprobe",
-            OUT / "kgs-gpuprobe",
+            odir / "kgs-gpuprobe",
             [NATIVE / "probe" / "gpuprobe.hip"],
             HIPCC,
             flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-Wall"],
-            link_flags=[f"-L{OUT}", "-lkgs_kernels", "-Wl,-rpath,$ORIGIN", "-pthread"],
+            link_flags=[f"-L{odir}", "-lkgs_kernels", "-Wl,-rpath,$ORIGIN", "-pthread"],
             shared=False,
         ),
         Target(
             "experiments",
-            OUT / "libkgs_experiments.so",
+            odir / "libkgs_experiments.so",
             sorted((NATIVE / "experiments").glob("*.hip")),
             HIPCC,
             flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
@@ -141,7 +165,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "gpuinfo-lib",
-            OUT / "libkgs_gpuinfo.so",
+            odir / "libkgs_gpuinfo.so",
             core + [gdir / "gpuinfo_capi.cpp"],
             CXX,
             flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{gdir}"] + smi_flags,
@@ -150,7 +174,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "gpuinfo-py",
-            OUT / f"_gpuinfo{_py_ext_suffix()}",
+            odir / f"_gpuinfo{_py_ext_suffix()}",
             core + [gdir / "gpuinfo_py.cpp"],
             CXX,
             flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{gdir}"] + smi_flags + _pybind_includes(),
@@ -159,7 +183,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "gpuinfo-cli",
-            OUT / "kgs-gpuinfo",
+            odir / "kgs-gpuinfo",
             core + [gdir / "gpuinfo_cli.cpp"],
             CXX,
             flags=["-O2", "-std=c++17", "-Wall", f"-I{gdir}"] + smi_flags,
@@ -169,7 +193,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "amdsmi-stub",
-            OUT / "libamd_smi_stub.so",
+            odir / "libamd_smi_stub.so",
             [gdir / "testing" / "amdsmi_stub.cpp"],
             CXX,
             flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{ROCM / 'include'}"],
@@ -177,7 +201,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "serve-py",
-            OUT / f"_serve{_py_ext_suffix()}",
+            odir / f"_serve{_py_ext_suffix()}",
             [sdir / "scheduler.cpp", sdir / "serve_py.cpp"],
             CXX,
             flags=["-O2", "-std=c++17", "-fPIC", "-Wall", f"-I{sdir}"] + _pybind_includes(),
@@ -185,7 +209,7 @@ def targets() -> list[Target]:
         ),
         Target(
             "rccl-bench",
-            OUT / "kgs-rccl-bench",
+            odir / "kgs-rccl-bench",
             [rdir / "rccl_bench.cpp"],
             HIPCC,
             flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", f"-I{ROCM / 'include'}"],
@@ -204,11 +228,11 @@ def _compile_one(t: Target, src: Path, obj: Path) -> None:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
 
 
-def build_target(t: Target, jobs: int = 8, verbose: bool = False) -> bool:
+def build_target(t: Target, jobs: int = 8, verbose: bool = False, objroot: Path | None = None) -> bool:
     """Build one target; returns True if it was (re)built."""
     if not t.stale():
         return False
-    objdir = REPO / "build" / "obj" / t.name
+    objdir = (objroot or REPO / "build" / "obj") / t.name
     objdir.mkdir(parents=True, exist_ok=True)
     objs = [objdir / (s.stem + ".o") for s in t.sources]
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
@@ -228,21 +252,38 @@ def build_target(t: Target, jobs: int = 8, verbose: bool = False) -> bool:
         raise RuntimeError(f"link failed: {' '.join(link)}\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, t.output)
     if verbose:
-        print(f"[kgs.build] built {t.output.relative_to(REPO)}", file=sys.stderr)
+        print(f"[kgs.build] built {t.output}", file=sys.stderr)
     return True
 
 
-def build_all(jobs: int | None = None, verbose: bool = True, only: list[str] | None = None) -> dict[str, str]:
-    """Build every native target. Returns {name: "built"|"fresh"|"skipped: why"}."""
-    if not Path(HIPCC).exists():
+def build_all(jobs: int | None = None, verbose: bool = True, only: list[str] | None = None,
+              out: str | os.PathLike | None = None, require_amdsmi: bool = False) -> dict[str, str]:
+    """Build every native target (or the ``only`` targets / groups) into
+    ``out`` (default ``kgs/_native``). Returns {name: "built"|"fresh"|"skipped: why"}.
+
+    This is the ONE build definition: ``images/Dockerfile.deviceplugin`` runs
+    ``python3 -m kgs.utils.build --only gpuinfo --require-amdsmi --out ...``
+    in its build stage instead of hand-written compiler lines.
+    """
+    only = expand_only(only)
+    outdir = Path(out).resolve() if out is not None else None
+    sel = [t for t in targets(outdir) if not only or t.name in only]
+    if only:
+        unknown = sorted(set(only) - {t.name for t in targets(outdir)})
+        if unknown:
+            raise RuntimeError(f"unknown build target(s) {unknown}; have {[t.name for t in targets(outdir)]} "
+                               f"and groups {sorted(GROUPS)}")
+    if any(t.compiler == HIPCC for t in sel) and not Path(HIPCC).exists():
         raise RuntimeError(f"hipcc not found at {HIPCC}; set ROCM_PATH")
+    if require_amdsmi and not amdsmi_header().exists():
+        raise RuntimeError(f"--require-amdsmi: {amdsmi_header()} not found (set ROCM_PATH to a tree with "
+                           "include/amd_smi); the device plugin's ECC/xGMI health needs it")
     jobs = jobs or min(8, os.cpu_count() or 4)
+    objroot = (outdir / ".obj") if outdir is not None else None
     status: dict[str, str] = {}
-    for t in targets():
-        if only and t.name not in only:
-            continue
+    for t in sel:
         try:
-            status[t.name] = "built" if build_target(t, jobs=jobs, verbose=verbose) else "fresh"
+            status[t.name] = "built" if build_target(t, jobs=jobs, verbose=verbose, objroot=objroot) else "fresh"
         except RuntimeError as e:
             if t.optional:
                 status[t.name] = f"skipped: {str(e).splitlines()[0]}"
@@ -268,11 +309,17 @@ def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(prog="python -m kgs.utils.build", description=__doc__.splitlines()[0])
     ap.add_argument("--clean", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
-    ap.add_argument("--only", nargs="*", default=None)
+    ap.add_argument("--only", nargs="*", default=None,
+                    help=f"targets or groups ({', '.join(sorted(GROUPS))})")
+    ap.add_argument("--out", default=None, help="output directory (default kgs/_native)")
+    ap.add_argument("--require-amdsmi", action="store_true",
+                    help="fail unless the amd-smi header is found (device-plugin image)")
     a = ap.parse_args(argv)
     if a.clean:
         clean()
-    st = build_all(jobs=a.jobs, only=a.only)
+    st = build_all(jobs=a.jobs, only=a.only, out=a.out, require_amdsmi=a.require_amdsmi)
+    if a.out is not None:
+        shutil.rmtree(Path(a.out) / ".obj", ignore_errors=True)
     for k, v in st.items():
         print(f"{k:14s} {v}")
     return 0

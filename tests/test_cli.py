@@ -436,8 +436,8 @@ def test_base_mirror_rewrites_base_images(world):
     (kind-gpu-sim.sh:144-178); kgs passes the mirror as build arguments."""
     assert run("create", "--dev-root", world.nogpu, "--base-mirror=mirror.example:5001/library") == 0
     build = world.calls("docker", "build")[0]
-    assert "PY_IMAGE=mirror.example:5001/library/python:3.12-slim" in build
-    assert "BUILD_IMAGE=mirror.example:5001/library/python:3.12" in build
+    assert "PY_IMAGE=mirror.example:5001/library/python:3.12.8-slim-bookworm" in build
+    assert "BUILD_IMAGE=mirror.example:5001/library/python:3.12.8-bookworm" in build
     reg = world.state()["containers"][C.REGISTRY_NAME]
     assert reg["image"] == "mirror.example:5001/library/registry:2"
 
@@ -445,7 +445,7 @@ def test_base_mirror_rewrites_base_images(world):
 def test_default_base_images_use_public_mirror(world):
     assert run("create", "--dev-root", world.nogpu) == 0
     build = world.calls("docker", "build")[0]
-    assert f"PY_IMAGE={C.BASE_MIRROR}/python:3.12-slim" in build
+    assert f"PY_IMAGE={C.BASE_MIRROR}/python:3.12.8-slim-bookworm" in build
 
 
 def test_doctor_cpu_only_host(world, capsys):

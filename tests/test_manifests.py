@@ -10,16 +10,25 @@ from kgs import manifests
 PODS = os.path.join(os.path.dirname(os.path.dirname(__file__)), "pods")
 
 
+def _docs(path):
+    with open(path) as f:
+        return [d for d in yaml.safe_load_all(f) if d]
+
+
 def _load(name):
-    with open(os.path.join(PODS, name)) as f:
-        return yaml.safe_load(f)
+    """The Pod document of pods/<name> (a file may add ConfigMaps it mounts)."""
+    pods = [d for d in _docs(os.path.join(PODS, name)) if d["kind"] == "Pod"]
+    assert len(pods) == 1, name
+    return pods[0]
 
 
 def test_every_pod_follows_reference_layout():
     files = sorted(glob.glob(os.path.join(PODS, "*.yaml")))
     assert len(files) >= 5
     for f in files:
-        doc = yaml.safe_load(open(f))
+        docs = _docs(f)
+        assert {d["kind"] for d in docs[:-1]} <= {"ConfigMap"}, f  # the Pod last, after what it mounts
+        doc = docs[-1]
         assert doc["kind"] == "Pod" and doc["apiVersion"] == "v1", f
         spec = doc["spec"]
         assert spec["nodeSelector"] == {"hardware-type": "gpu"}, f
@@ -50,11 +59,43 @@ def test_vllm_pod():
     doc = _load("vllm-rocm-pod.yaml")
     ctr = doc["spec"]["containers"][0]
     args = " ".join(ctr["args"])
-    assert "Meta-Llama-3-8B" in args and "--dtype=bfloat16" in args and "--tensor-parallel-size=1" in args
+    assert "--dtype=bfloat16" in args and "--tensor-parallel-size=1" in args
     assert ctr["resources"]["limits"] == {"amd.com/gpu": 1}
     assert ctr["securityContext"]["privileged"] is True
     assert doc["spec"]["restartPolicy"] == "Never"
     assert {"containerPort": 8000} in ctr["ports"]
+
+
+def test_vllm_pod_is_offline_and_pinned():
+    """no hub id, no :latest, the architecture config
+    mounted from a ConfigMap in the same file, dummy weights, no tokenizer."""
+    import json
+
+    docs = _docs(os.path.join(PODS, "vllm-rocm-pod.yaml"))
+    assert docs == manifests.vllm_rocm_pod()  # the file is the renderer's output
+    cm, pod = docs
+    ctr = pod["spec"]["containers"][0]
+    assert ":latest" not in ctr["image"] and ":" in ctr["image"].split("/")[-1]
+    args = ctr["args"]
+    model = [a.split("=", 1)[1] for a in args if a.startswith("--model=")]
+    assert model == [manifests.VLLM_MODEL_DIR] and "/" not in model[0].strip("/").split("/")[0] + ""
+    assert "--load-format=dummy" in args and "--skip-tokenizer-init" in args
+    assert not any("meta-llama" in a or "huggingface" in a for a in args)
+    env = {e["name"]: e["value"] for e in ctr["env"]}
+    assert env["HF_HUB_OFFLINE"] == "1"
+    # the ConfigMap the pod mounts at --model is the one in this file
+    vols = {v["name"]: v for v in pod["spec"]["volumes"]}
+    mounts = {m["mountPath"]: m["name"] for m in ctr["volumeMounts"]}
+    assert vols[mounts[manifests.VLLM_MODEL_DIR]]["configMap"]["name"] == cm["metadata"]["name"]
+    hf = json.loads(cm["data"]["config.json"])
+    assert hf["architectures"] == ["LlamaForCausalLM"]
+    # the same architecture the kgs.serve stand-in runs (kgs.models.llama)
+    from kgs.models.llama import LlamaConfig
+
+    c = LlamaConfig.llama3_8b()
+    assert (hf["hidden_size"], hf["intermediate_size"], hf["num_attention_heads"], hf["num_key_value_heads"],
+            hf["num_hidden_layers"], hf["vocab_size"], hf["rope_theta"], hf["rms_norm_eps"]) == \
+        (c.hidden, c.intermediate, c.heads, c.kv_heads, c.layers, c.vocab, c.rope_theta, c.eps)
 
 
 def test_daemonset_render():
@@ -114,10 +155,12 @@ def test_kgs_serve_pod():
     assert ctr["command"] == ["python3", "-m", "kgs.serve", "serve"]
     assert "--port=8000" in ctr["args"] and {"containerPort": 8000} in ctr["ports"]
     # same layout as the vLLM pod it stands in for
-    for key in ("resources", "volumeMounts", "securityContext"):
+    for key in ("resources", "securityContext"):
         assert ctr[key] == vctr[key]
-    for key in ("nodeSelector", "tolerations", "volumes", "restartPolicy"):
+    assert ctr["volumeMounts"][0] == vctr["volumeMounts"][0]  # /dev/shm
+    for key in ("nodeSelector", "tolerations", "restartPolicy"):
         assert doc["spec"][key] == vllm["spec"][key]
+    assert doc["spec"]["volumes"][0] == vllm["spec"]["volumes"][0]
     from kgs.serve.api import main  # the entrypoint the pod runs exists
 
     assert callable(main)
