@@ -1,12 +1,14 @@
 """``kgs`` command line -- drop-in for ``kind-gpu-sim.sh``.
 
   kgs create [rocm] [--registry-port=N] [--cluster-name=S] [--runtime=docker|podman]
-                    [--workers=N] [--gpu-partition=all-on-first|split] [--fake-gpus=N]
+                    [--gpus=N] [--workers=N] [--gpu-partition=all-on-first|split] [--fake-gpus=N]
                     [--fake-mode=patch|plugin] [--timings-json=F] [--dry-run] [--keep-on-fail]
   kgs delete [--cluster-name=S]
   kgs load   --image-name=IMG [--cluster-name=S]
   kgs status [--json]
-  kgs bench  [e2e options]          create -> gpu-rocm-test Running, per-phase JSON
+  kgs bench  [--gpus=N] [--pod-gpus=M] create --gpus N -> gpu-rocm-test (M GPUs, default N) Running,
+             [--sweep=1,2,4,8]        per-phase JSON; --sweep repeats it per advertised count
+             [--no-kind]              the docker-free chained tail instead (plugin -> pod -> GEMM)
   kgs images [--workload] [--plugin] build the in-tree images
   kgs pod NAME [--registry-port=N]   print pods/NAME.yaml with the image on the
                                      configured local registry (| kubectl create -f -)
@@ -65,7 +67,14 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
                     help="build the plugin image after the cluster (default: concurrently with kind create)")
     ap.add_argument("--json", action="store_true")
     # bench/images options
-    ap.add_argument("--gpus", type=int, default=1, help="bench: amd.com/gpu requested by the test pod")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="advertise exactly N of the host's healthy GPUs (one xGMI island, fewest NUMA nodes; "
+                         "default: all). bench: also the test pod's request unless --pod-gpus")
+    ap.add_argument("--pod-gpus", type=int, default=None,
+                    help="bench: amd.com/gpu requested by the test pod (default: --gpus, or 1)")
+    ap.add_argument("--sweep", default=None,
+                    help="bench: comma list of advertised GPU counts, e.g. 1,2,4,8 (one create..delete per count)")
+    ap.add_argument("--sweep-json", default=None, help="bench --sweep: write the per-count JSON here")
     ap.add_argument("--pod-timeout", type=int, default=C.TEST_POD_READY_TIMEOUT_S)
     ap.add_argument("--keep", action="store_true", help="bench: keep the cluster afterwards")
     ap.add_argument("--no-kind", action="store_true",
@@ -82,12 +91,22 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
 def settings_from(a) -> C.Settings:
     return C.Settings(
         registry_port=a.registry_port, cluster_name=a.cluster_name, image_name=a.image_name, runtime=a.runtime,
-        workers=a.workers, gpu_partition=a.gpu_partition, fake_gpus=a.fake_gpus, fake_mode=a.fake_mode,
+        workers=a.workers, gpus=a.gpus, gpu_partition=a.gpu_partition, fake_gpus=a.fake_gpus, fake_mode=a.fake_mode,
         registry_bind=a.registry_bind, kind_node_image=a.kind_node_image, dry_run=a.dry_run,
         keep_on_fail=a.keep_on_fail, skip_build=a.skip_build, timings_json=a.timings_json,
         plugin_image=a.plugin_image, ready_timeout_s=a.ready_timeout, dev_root=a.dev_root,
         base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image, extra={"serial": a.serial},
     )
+
+
+def _parse_counts(text: str) -> list:
+    try:
+        counts = [int(x) for x in text.replace(" ", "").split(",") if x]
+    except ValueError:
+        counts = []
+    if not counts or any(c < 1 for c in counts):
+        raise SystemExit(f"--sweep wants a comma list of GPU counts >= 1, e.g. 1,2,4,8 (got {text!r})")
+    return counts
 
 
 def main(argv=None, prog: str = "kgs") -> int:
@@ -122,15 +141,34 @@ def main(argv=None, prog: str = "kgs") -> int:
                 print(str(e), file=sys.stderr)
                 return 1
             return 0
+        if a.verb == "bench" and a.sweep:
+            from .e2e import run_sweep
+
+            counts = _parse_counts(a.sweep)
+            if a.no_kind:
+                kw = dict(dev_root=a.dev_root, fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
+                          timeout=max(60, a.pod_timeout * 10))
+                return run_sweep(None, counts, pod_gpus=a.pod_gpus, sweep_json=a.sweep_json, out=p.out,
+                                 no_kind=True, **kw)
+
+            def make(n):
+                st = settings_from(a)
+                st.gpus = n
+                st.timings_json = f"{a.timings_json}.gpus{n}.json" if a.timings_json else None
+                return Provisioner(st, runner=p.runner, out=p.out)
+
+            return run_sweep(make, counts, pod_gpus=a.pod_gpus, sweep_json=a.sweep_json, out=p.out,
+                             pod_timeout=a.pod_timeout, keep=False, workload_image=a.workload_image)
         if a.verb == "bench" and a.no_kind:
             from .e2e_nokind import run_nokind
 
-            return run_nokind(gpus=a.gpus, dev_root=a.dev_root, fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
+            return run_nokind(gpus=a.pod_gpus or a.gpus or 1, advertise=a.gpus, dev_root=a.dev_root,
+                              fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
                               timeout=max(60, a.pod_timeout * 10), timings_json=a.timings_json)
         if a.verb == "bench":
             from .e2e import run_e2e
 
-            return run_e2e(p, gpus=a.gpus, pod_timeout=a.pod_timeout, keep=a.keep,
+            return run_e2e(p, gpus=a.pod_gpus or a.gpus or 1, pod_timeout=a.pod_timeout, keep=a.keep,
                            workload_image=a.workload_image)
         if a.verb == "doctor":
             from .doctor import run_doctor

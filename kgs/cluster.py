@@ -72,6 +72,29 @@ def plan_partitions(gpus: list, workers: int, mode: str) -> list:
     return out
 
 
+def select_gpus(gpus: list, n: int | None) -> list:
+    """The ``n`` GPUs to advertise (``kgs create --gpus N``), out of the host's
+    healthy ones: one xGMI island first, then the fewest NUMA nodes, then the
+    lowest indices -- the device plugin's GetPreferredAllocation scoring
+    (kgs/deviceplugin/allocator.py), applied at cluster level. ``None`` = all.
+    The reference advertises a fixed count per worker (kind-gpu-sim.sh:113)."""
+    if n is None:
+        return list(gpus)
+    if n < 1:
+        raise ProvisionError(f"ERROR: --gpus must be >= 1 (got {n})")
+    if n > len(gpus):
+        raise ProvisionError(f"ERROR: --gpus {n} but the host has only {len(gpus)} healthy GPU(s) "
+                             f"(renderD{[g.render_minor for g in gpus]})")
+    from .deviceplugin.allocator import DevInfo, preferred
+
+    infos = {str(g.render_minor): DevInfo(str(g.render_minor), g.index, getattr(g, "numa_node", -1),
+                                          getattr(g, "node_id", -1), frozenset(g.xgmi_peers()))
+             for g in gpus}
+    ids = preferred([str(g.render_minor) for g in gpus], [], n, infos)
+    chosen = {int(i) for i in ids}
+    return [g for g in gpus if g.render_minor in chosen]
+
+
 class Provisioner:
     def __init__(self, settings: C.Settings, runner: Runner | None = None, timer: PhaseTimer | None = None,
                  workdir: str | os.PathLike | None = None, out=None):
@@ -84,6 +107,7 @@ class Provisioner:
         self.topology = None
         self.fake = False
         self.partitions: list = []
+        self.selected: list = []
         self.created_cluster = False
 
     # ------------------------------------------------------------ helpers ----
@@ -101,15 +125,28 @@ class Provisioner:
     def state_dir(self) -> Path:
         return self.workdir / ".kgs" / self.s.cluster_name
 
+    def generated_worker_names(self) -> list:
+        """kind's node names, in the order of the kind config's worker list
+        (``<cluster>-worker``, ``-worker2``, ... ``-worker10``): the order the
+        partition plan and the partition file use."""
+        return [f"{self.s.cluster_name}-worker"] + [f"{self.s.cluster_name}-worker{i}"
+                                                    for i in range(2, self.s.workers + 1)]
+
     def worker_names(self) -> list:
-        names = [f"{self.s.cluster_name}-worker"] + [f"{self.s.cluster_name}-worker{i}"
-                                                     for i in range(2, self.s.workers + 1)]
+        """The cluster's worker nodes in natural order. kubectl lists nodes
+        lexicographically (``worker, worker10, worker2``), which must not be
+        zipped with the partition plan."""
+        names = self.generated_worker_names()
         if self.runner.dry_run:
             return names
         r = self.kubectl("get", "nodes", "-o", "jsonpath={range .items[*]}{.metadata.name}{\"\\n\"}{end}",
                          mutating=False)
         got = [n for n in r.stdout.split() if n and "control-plane" not in n]
-        return got or names
+        return sorted(got, key=_natural_key) or names
+
+    def partition_of(self) -> dict:
+        """{worker node name: render minors} -- by name, never by list position."""
+        return dict(zip(self.generated_worker_names(), self.partitions))
 
     def cluster_exists(self) -> bool:
         r = self.kind("get", "clusters", check=False, mutating=False)
@@ -123,6 +160,9 @@ class Provisioner:
     # ------------------------------------------------------------ discover ---
     def discover(self) -> None:
         if self.s.fake_gpus is not None:
+            if self.s.gpus is not None:
+                raise ProvisionError("ERROR: --gpus selects real GPUs to advertise; with --fake-gpus the "
+                                     "count is --fake-gpus per worker")
             self.fake = True
             self.partitions = [[] for _ in range(self.s.workers)]
             return
@@ -136,11 +176,16 @@ class Provisioner:
         gpus = self.topology.gpus if self.topology else []
         usable = [g for g in gpus if g.render_minor >= 0 and g.healthy]
         if not self.topology or not self.topology.kfd_present or not usable:
+            if self.s.gpus is not None:
+                raise ProvisionError(f"ERROR: --gpus {self.s.gpus} needs real GPUs, but none were found under "
+                                     f"{self.s.dev_root} (/dev/kfd + gfx nodes); for the simulated path use "
+                                     "--fake-gpus N")
             self.fake = True
             self.partitions = [[] for _ in range(self.s.workers)]
             return
         self.fake = False
-        self.partitions = plan_partitions(usable, self.s.workers, self.s.gpu_partition)
+        self.selected = select_gpus(usable, self.s.gpus)
+        self.partitions = plan_partitions(self.selected, self.s.workers, self.s.gpu_partition)
 
     @property
     def fake_per_worker(self) -> int:
@@ -176,9 +221,7 @@ class Provisioner:
         if not self.runner.dry_run:
             host_dir.mkdir(parents=True, exist_ok=True)
             (host_dir / "hosts.toml").write_text(manifests.hosts_toml())
-            names = [f"{self.s.cluster_name}-worker"] + [f"{self.s.cluster_name}-worker{i}"
-                                                         for i in range(2, self.s.workers + 1)]
-            part.write_text(manifests.partition_file(dict(zip(names, self.partitions))))
+            part.write_text(manifests.partition_file(self.partition_of()))
         return str(certs.resolve()), str(part.resolve())
 
     def write_kind_config(self) -> Path:
@@ -205,8 +248,9 @@ class Provisioner:
         self.kubectl("label", "node", *workers, *labels, "--overwrite")
         self.kubectl("taint", "node", *workers, f"{C.TAINT[0]}={C.TAINT[1]}:{C.TAINT[2]}", "--overwrite")
         if not self.fake:
-            for w, p in zip(workers, self.partitions):
-                self.kubectl("label", "node", w, f"{C.LABEL_GPU_PARTITION}={len(p)}", "--overwrite")
+            owned = self.partition_of()
+            for w in workers:
+                self.kubectl("label", "node", w, f"{C.LABEL_GPU_PARTITION}={len(owned.get(w, []))}", "--overwrite")
         elif self.s.fake_mode == "patch":
             patch = json.dumps([{"op": "add", "path": "/status/capacity/amd.com~1gpu",
                                  "value": str(self.fake_per_worker)}])
@@ -412,14 +456,19 @@ class Provisioner:
                     self.created_cluster = True
                     self.write_shape()
             with t.phase("registry-network"):
-                self.ensure_runtime().network_connect(C.KIND_NETWORK, C.REGISTRY_NAME)
+                why = self.ensure_runtime().network_connect(C.KIND_NETWORK, C.REGISTRY_NAME)
+                if why is not None and not self.runner.dry_run:
+                    # without it the nodes cannot pull localhost:<port>/amdgpu-dp:dev and the
+                    # user would only see a 60 s "plugin pods not ready" timeout (Q5)
+                    raise ProvisionError(f"ERROR: could not attach {C.REGISTRY_NAME} to network "
+                                         f"{C.KIND_NETWORK}: {why}")
             with t.phase("nodes") as rec:
                 rec["workers"] = self.configure_nodes()
             prepull_images = self.s.extra.get("prepull") or []
             if prepull_images and not self.runner.dry_run:
                 # GPU pods only land on GPU workers; pull there while the plugin comes up
-                gpu_nodes = [w for w, part in zip(rec["workers"], self.partitions or [[1]] * len(rec["workers"]))
-                             if part] or rec["workers"]
+                owned = self.partition_of()
+                gpu_nodes = [w for w in rec["workers"] if self.fake or owned.get(w)] or rec["workers"]
                 pulls = _Background(lambda: self.prepull(gpu_nodes, prepull_images))
             else:
                 pulls = None
@@ -502,6 +551,13 @@ class Provisioner:
             for line in info.get("plugin_pods", []):
                 self.out(f"  {line}")
         return 0
+
+
+def _natural_key(name: str) -> list:
+    """``worker2`` < ``worker10`` (digit runs compare as numbers)."""
+    import re
+
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", name)]
 
 
 class _Background:

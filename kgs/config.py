@@ -85,6 +85,7 @@ class Settings:
     image_name: str = DEFAULT_IMAGE_NAME
     runtime: str | None = None           # docker | podman | None = autodetect
     workers: int = DEFAULT_WORKERS
+    gpus: int | None = None              # advertise exactly N of the host's GPUs (None = all healthy)
     gpu_partition: str = "all-on-first"  # all-on-first | split | fake
     fake_gpus: int | None = None         # force the fake path with N per worker
     fake_mode: str = "patch"             # patch (reference) | plugin (kgs fake plugin)

@@ -35,6 +35,15 @@ def workload_image(p) -> str:
 
 def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, keep: bool = False,
             workload_image: str | None = None, pod_command: list | None = None) -> int:
+    summary = e2e_once(p, gpus=gpus, pod_timeout=pod_timeout, keep=keep, workload_image=workload_image,
+                       pod_command=pod_command)
+    p.out(json.dumps(summary))
+    return 0
+
+
+def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, keep: bool = False,
+             workload_image: str | None = None, pod_command: list | None = None) -> dict:
+    """One create -> pod Running -> logs (-> delete) pass; returns the summary."""
     t = p.timer
     t_start = time.perf_counter()
     image = workload_image or globals()["workload_image"](p)
@@ -85,8 +94,53 @@ def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, kee
         if not keep and not p.runner.dry_run:
             p.delete()
     summary = {"metric": "cluster-create->GPU-pod-Running", "value": t.meta.get("create_to_running_s"),
-               "unit": "s", "gpus": gpus, "fake": p.fake, "phases": {ph["phase"]: ph["seconds"] for ph in t.phases}}
+               "unit": "s", "gpus": gpus, "advertised": p.expected_capacity, "fake": p.fake,
+               "phases": {ph["phase"]: ph["seconds"] for ph in t.phases}}
     if result.get("gemm_tflops_total"):
         summary["in_pod_gemm_tflops"] = result["gemm_tflops_total"]
-    p.out(json.dumps(summary))
-    return 0
+    return summary
+
+
+def run_sweep(make_provisioner, counts: list, pod_gpus: int | None = None, sweep_json: str | None = None,
+              out=print, no_kind: bool = False, **kw) -> int:
+    """``kgs bench --sweep 1,2,4,8``: the headline at each advertised-GPU count.
+
+    For every N: a fresh ``create --gpus N`` (exactly N GPUs advertised) ->
+    gpu-rocm-test pod requesting ``pod_gpus`` (default N: the pod takes all of
+    them, BASELINE config 4; ``--pod-gpus 1`` is config 3) -> Running -> logs
+    (in-pod GEMM TFLOPS) -> delete. With ``no_kind`` each point is the no-kind
+    chained tail instead (kgs/e2e_nokind.py). One JSON document: the per-N
+    points plus a ``table`` of create->Running seconds and in-pod TFLOPS.
+    A failing point is recorded with its error and the sweep goes on, so one
+    bad count does not hide the others; the exit status is then 1.
+    """
+    points = []
+    for n in counts:
+        want = pod_gpus or n
+        try:
+            if no_kind:
+                from .e2e_nokind import nokind_once
+
+                pt = nokind_once(gpus=want, advertise=n, **kw)
+            else:
+                pt = e2e_once(make_provisioner(n), gpus=want, **kw)
+            pt["ok"] = True
+        except Exception as e:  # noqa: BLE001 - recorded per point
+            pt = {"ok": False, "error": f"{type(e).__name__}: {e}"}
+        pt.update(advertised=n, pod_gpus=want)
+        points.append(pt)
+    doc = {
+        "metric": ("device-plugin start -> first in-pod GEMM (no kind)" if no_kind
+                   else "cluster-create->GPU-pod-Running"),
+        "unit": "s",
+        "sweep": list(counts),
+        "points": points,
+        "table": [{"advertised": pt["advertised"], "pod_gpus": pt["pod_gpus"], "seconds": pt.get("value"),
+                   "in_pod_gemm_tflops": pt.get("in_pod_gemm_tflops"), "ok": pt["ok"]} for pt in points],
+    }
+    text = json.dumps(doc, indent=1)
+    if sweep_json:
+        with open(sweep_json, "w") as f:
+            f.write(text + "\n")
+    out(text)
+    return 0 if all(pt["ok"] for pt in points) else 1

@@ -79,17 +79,19 @@ class ContainerRuntime:
         r = self.cr("ps", "-q", "-f", f"name=^{container}$", check=False, mutating=False)
         return r.stdout.strip() if r.ok else ""
 
-    def network_connect(self, network: str, container: str) -> bool:
-        """Connect; True if connected now or already. Errors other than
-        'already exists' are surfaced (the reference swallows all, Q5)."""
+    def network_connect(self, network: str, container: str) -> str | None:
+        """Connect; None if connected now or already, else the runtime's error
+        text. The reference swallows every error here (Q5,
+        kind-gpu-sim.sh:81,104); the caller turns one into a hard failure."""
         r = self.cr("network", "connect", network, container, check=False)
         if r.ok:
-            return True
+            return None
         msg = (r.stderr + r.stdout).lower()
         if "already exists" in msg or "already connected" in msg:
-            return True
-        log.warning("could not connect %s to network %s: %s", container, network, (r.stderr or r.stdout).strip())
-        return False
+            return None
+        why = (r.stderr or r.stdout).strip() or f"exit status {r.returncode}"
+        log.warning("could not connect %s to network %s: %s", container, network, why)
+        return why
 
     def image_exists(self, image: str) -> bool:
         r = self.cr("image", "inspect", image, check=False, mutating=False)

@@ -9,7 +9,8 @@ orchestrator's control flow: error strings for "already connected", exit codes
 for missing containers, kind node naming, kubelet-managed capacity once the
 device-plugin DaemonSet is applied (from the bind-mounted partition file), etc.
 Fault injection: $KGS_FAKE_FAIL = comma list of {plugin-ready, kind-create,
-push, pod-running}.
+push, pod-running, network-connect}. Node lists come back sorted by name, as
+the real kubectl prints them (worker, worker10, worker2, ...).
 """
 import fcntl
 import json
@@ -109,6 +110,8 @@ def container_tool():
         del cs[ARGS[1]]
     elif cmd == "network" and ARGS[1] == "connect":
         net, name = ARGS[2], ARGS[3]
+        if "network-connect" in FAIL:
+            err(f"Error response from daemon: failed to add interface to network {net}: permission denied")
         if net not in st["networks"]:
             err(f"Error response from daemon: network {net} not found")
         if net in cs[name]["networks"]:
@@ -230,10 +233,10 @@ def kubectl_tool():
             items = [{"metadata": {"name": n, "labels": v["labels"]},
                       "spec": {"taints": v["taints"]},
                       "status": {"capacity": v["capacity"], "allocatable": v["allocatable"]}}
-                     for n, v in c["nodes"].items()]
+                     for n, v in sorted(c["nodes"].items())]
             out(json.dumps({"items": items}))
         else:
-            out("\n".join(c["nodes"]) + "\n")
+            out("\n".join(sorted(c["nodes"])) + "\n")
     elif verb == "label":
         names = [x for x in a[2:] if "=" not in x and not x.startswith("-")]
         kvs = [x for x in a[2:] if "=" in x and not x.startswith("-")]

@@ -520,3 +520,160 @@ def test_serial_flag_keeps_reference_order(world):
     kind_create = next(i for i, e in enumerate(log) if e["tool"] == "kind" and e["argv"][:2] == ["create", "cluster"])
     build = next(i for i, e in enumerate(log) if e["tool"] == "docker" and e["argv"][:1] == ["build"])
     assert kind_create < build
+
+
+# ---- advertised-GPU count --------------------------------
+@pytest.mark.parametrize("n", [1, 2, 4, 8])
+def test_create_advertises_exactly_n_gpus(world, tmp_path, capsys, n):
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--gpus", str(n), "--dev-root", str(host)) == 0
+    assert f"({n} amd.com/gpu advertised)" in capsys.readouterr().out
+    cfg = yaml.safe_load((world.cwd / "kind-config.yaml").read_text())
+    renders = [m["containerPath"] for node in cfg["nodes"] for m in node.get("extraMounts", [])
+               if m["containerPath"].startswith("/dev/dri/renderD")]
+    assert len(renders) == n
+    part = json.loads((world.cwd / ".kgs" / "kind-gpu-sim" / "gpus.json").read_text())["nodes"]
+    chosen = part["kind-gpu-sim-worker"]
+    assert len(chosen) == n and part["kind-gpu-sim-worker2"] == []
+    # one NUMA node (4 GPUs per socket on the fake host), lowest indices: 128, 136, ...
+    assert chosen == [128 + 8 * i for i in range(n)]
+    st = world.state()["clusters"]["kind-gpu-sim"]
+    assert st["nodes"]["kind-gpu-sim-worker"]["allocatable"] == {"amd.com/gpu": str(n)}
+    assert st["nodes"]["kind-gpu-sim-worker"]["labels"]["kgs.amd.com/gpu-partition"] == str(n)
+
+
+def test_create_gpus_split_over_workers(world, tmp_path):
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--gpus", "4", "--gpu-partition", "split", "--dev-root", str(host)) == 0
+    part = json.loads((world.cwd / ".kgs" / "kind-gpu-sim" / "gpus.json").read_text())["nodes"]
+    assert sum(len(v) for v in part.values()) == 4 and all(len(v) == 2 for v in part.values())
+
+
+def test_create_gpus_changed_is_drift(world, tmp_path, capsys):
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--gpus", "2", "--dev-root", str(host)) == 0
+    assert run("create", "--gpus", "2", "--dev-root", str(host)) == 0  # same shape: reconcile
+    capsys.readouterr()
+    assert run("create", "--gpus", "4", "--dev-root", str(host)) == 1
+    err = capsys.readouterr().err
+    assert "different shape" in err and "GPU partition" in err
+
+
+def test_create_gpus_errors(world, tmp_path, capsys):
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--gpus", "9", "--dev-root", str(host)) == 1
+    assert "only 8 healthy GPU(s)" in capsys.readouterr().err
+    assert run("create", "--gpus", "1", "--dev-root", world.nogpu) == 1
+    assert "needs real GPUs" in capsys.readouterr().err
+    assert world.state().get("clusters", {}) == {}  # refused before anything was created
+
+
+def test_select_gpus_prefers_one_xgmi_island():
+    from kgs import gpuinfo
+    from kgs.cluster import select_gpus
+
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="kgs-sel", dir="/tmp")
+    gpus = gpuinfo.discover(str(make_fake_mi355x(os.path.join(d, "h"))), use_amdsmi=False).gpus
+    # drop every xGMI link of GPU 0: it must not be picked into a 2-GPU set
+    for g in gpus:
+        g.links = [lk for lk in g.links if lk.to_node != gpus[0].node_id] if g is not gpus[0] else \
+            [lk for lk in g.links if not lk.is_xgmi]
+    pick = select_gpus(gpus, 2)
+    assert gpus[0] not in pick and len(pick) == 2
+    assert select_gpus(gpus, None) == gpus
+
+
+def test_bench_sweep_dry_run_plan(world, tmp_path, capsys):
+    """`kgs bench --sweep 1,2,4,8 --dry-run`: one create (N renderD mounts) ->
+    pod (N GPUs) -> delete per count, nothing executed."""
+    host = make_fake_mi355x(tmp_path / "host8")
+    rc = run("bench", "--sweep", "1,2,4,8", "--dry-run", "--dev-root", str(host),
+             "--sweep-json", str(tmp_path / "sweep.json"))
+    cap = capsys.readouterr()
+    assert rc == 0, cap.err
+    assert world.log() == []
+    doc = json.loads((tmp_path / "sweep.json").read_text())
+    assert [p["advertised"] for p in doc["points"]] == [1, 2, 4, 8]
+    assert [p["pod_gpus"] for p in doc["points"]] == [1, 2, 4, 8]
+    assert all(p["ok"] for p in doc["points"]) and [t["advertised"] for t in doc["table"]] == [1, 2, 4, 8]
+    # the printed kind configs carry 1, 2, 4, 8 render nodes in order
+    cfgs = [c for c in cap.out.split("# ") if "kind: Cluster" in c]
+    counts = [c.count("containerPath: /dev/dri/renderD") for c in cfgs]
+    assert counts == [1, 2, 4, 8]
+    assert cap.err.count("kind create cluster --name kind-gpu-sim") == 4
+    pods = [c for c in cap.err.split("\n") if "kubectl" in c and "apply" in c]
+    assert len(pods) >= 4
+
+
+def test_bench_sweep_runs_each_count(world, tmp_path, capsys):
+    host = make_fake_mi355x(tmp_path / "host8")
+    rc = run("bench", "--sweep", "1,8", "--pod-gpus", "1", "--dev-root", str(host),
+             "--sweep-json", str(tmp_path / "s.json"))
+    assert rc == 0
+    doc = json.loads((tmp_path / "s.json").read_text())
+    assert [(p["advertised"], p["pod_gpus"], p["ok"]) for p in doc["points"]] == [(1, 1, True), (8, 1, True)]
+    assert all(p["value"] > 0 for p in doc["points"])
+    # each point created and deleted its own cluster
+    assert len(world.calls("kind", "create", "cluster")) == 2 and world.state()["clusters"] == {}
+    pods = [yaml.safe_load(o["stdin"]) for o in world.log() if o["tool"] == "kubectl" and o["stdin"]
+            and "kind: Pod" in o["stdin"]]
+    assert [p["spec"]["containers"][0]["resources"]["limits"]["amd.com/gpu"] for p in pods] == [1, 1]
+
+
+def test_bench_sweep_records_a_failing_point(world, tmp_path, monkeypatch):
+    host = make_fake_mi355x(tmp_path / "host8")
+    rc = run("bench", "--sweep", "2,16", "--dev-root", str(host), "--sweep-json", str(tmp_path / "s.json"))
+    assert rc == 1
+    pts = json.loads((tmp_path / "s.json").read_text())["points"]
+    assert pts[0]["ok"] and not pts[1]["ok"] and "only 8 healthy" in pts[1]["error"]
+
+
+# ---- create-path correctness (VERDICT r2 next-step 5) ------------------------------
+def test_registry_network_failure_is_an_error(world, monkeypatch, capsys):
+    monkeypatch.setenv("KGS_FAKE_FAIL", "network-connect")
+    assert run("create", "--dev-root", world.nogpu) == 1
+    err = capsys.readouterr().err
+    assert "could not attach kind-registry to network kind" in err and "permission denied" in err
+    assert world.state()["clusters"] == {}  # rolled back
+
+
+def test_ten_workers_partition_labels_match_the_file(world, tmp_path):
+    """kubectl lists worker, worker10, worker2 ...; labels must follow node
+    names, not list position."""
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("create", "--workers", "10", "--gpu-partition", "split", "--dev-root", str(host)) == 0
+    part = json.loads((world.cwd / ".kgs" / "kind-gpu-sim" / "gpus.json").read_text())["nodes"]
+    nodes = world.state()["clusters"]["kind-gpu-sim"]["nodes"]
+    assert len(part) == 10
+    for name, minors in part.items():
+        assert nodes[name]["labels"]["kgs.amd.com/gpu-partition"] == str(len(minors)), name
+        assert nodes[name]["allocatable"].get("amd.com/gpu", "0") in (str(len(minors)), "0")
+    assert part["kind-gpu-sim-worker10"] == [] and len(part["kind-gpu-sim-worker2"]) == 1
+
+
+def test_natural_worker_order():
+    from kgs.cluster import _natural_key
+
+    names = ["c-worker", "c-worker10", "c-worker2", "c-worker3"]
+    assert sorted(names, key=_natural_key) == ["c-worker", "c-worker2", "c-worker3", "c-worker10"]
+
+
+def test_bench_no_kind_advertises_the_same_selection(world, tmp_path, capsys):
+    """`kgs bench --no-kind --gpus 4 --pod-gpus 1` on the fake 8-GPU host: the
+    plugin process advertises exactly the 4 GPUs `create --gpus 4` would, and
+    the pod is allocated one of them (BASELINE config 3 shape)."""
+    host = make_fake_mi355x(tmp_path / "host8")
+    rc = run("bench", "--no-kind", "--gpus", "4", "--pod-gpus", "1", "--dev-root", str(host),
+             "--timings-json", str(tmp_path / "nk.json"))
+    assert rc == 0
+    s = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith('{"metric"')][-1])
+    assert s["advertised"] == 4 and s["gpus"] == 1
+    t = json.loads((tmp_path / "nk.json").read_text())
+    assert t["advertised_minors"] == [128, 136, 144, 152]
+    cap = [p for p in t["phases"] if p["phase"] == "capacity"][0]
+    assert cap["advertised"] == 4
+    alloc = [p for p in t["phases"] if p["phase"] == "allocate"][0]
+    assert len(alloc["device_ids"]) == 1
+    assert t["allocate_envs"]["KGS_RENDER_MINORS"] in {"128", "136", "144", "152"}
