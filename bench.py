@@ -24,6 +24,14 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
 With ``--gpus N > 1`` and no WORLD_SIZE in the environment the script launches
 itself: the parent (which never touches the GPU) spawns N ranks with the
 torchrun env contract (kgs.parallel.launch) and exits with their status.
+
+Failure is loud and bounded, under torchrun or the self-launch alike: the
+rendezvous has its own timeout (``--rendezvous-timeout``, 120 s), every rank
+checks it owns a distinct GPU before the RCCL communicator exists, and a
+per-rank watchdog ends the run after ``--launch-timeout`` (300 s). Whatever
+fails, ONE JSON line with ``"status": "error"``, the failing rank, the phase
+each rank reached and (self-launch) the failing rank's stderr tail is printed
+and the exit status is non-zero -- never a silent hang.
 """
 from __future__ import annotations
 
@@ -65,7 +73,25 @@ def parse(argv=None):
                          "1-GPU box, with --dist-backend gloo; not a benchmark configuration")
     ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
                     help="bf16 = the headline (BASELINE.json); fp8 = e4m3 operands on the scaled MFMA (extra)")
+    ap.add_argument("--launch-timeout", type=float, default=300.0,
+                    help="whole-run bound per rank (watchdog); the self-launch parent kills at +30 s")
+    ap.add_argument("--rendezvous-timeout", type=float, default=120.0,
+                    help="how long a rank waits for the others to join")
     return ap.parse_args(argv)
+
+
+def metric_name(dtype: str) -> str:
+    return ("in-pod bf16 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 MFMA GEMM + RCCL grad all-reduce)"
+            if dtype == "bf16" else
+            "in-pod fp8 e4m3 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 scaled-MFMA GEMM + RCCL all-reduce)")
+
+
+def error_report(args, world: int) -> dict:
+    """The fields of the success line that are known before the run, for the
+    error line (so a parser keyed on ``metric`` finds the failure)."""
+    return {"metric": metric_name(args.dtype), "value": None, "unit": "TFLOP/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+            "dtype": args.dtype if args.dtype == "bf16" else "fp8_e4m3"}
 
 
 def main(argv=None) -> int:
@@ -74,17 +100,56 @@ def main(argv=None) -> int:
 
     if launch.needs_self_launch(args.gpus):
         raw = list(sys.argv[1:] if argv is None else argv)
+        os.environ["KGS_LAUNCH_PARENT"] = "1"
         return launch.spawn_local(args.gpus, [os.path.abspath(__file__), *raw],
-                                  require_gpus=not (args.cpu or args.oversubscribe))
+                                  require_gpus=not (args.cpu or args.oversubscribe),
+                                  timeout_s=args.launch_timeout + 30, error_report=error_report(args, args.gpus))
 
+    env_rank = int(os.environ.get("RANK", "0") or 0)
+    env_world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    wd = launch.Watchdog(args.launch_timeout, env_rank, env_world, error_report(args, env_world))
+    if env_rank == 0 and env_world > 1 and not os.environ.get("KGS_LAUNCH_PARENT"):
+        # under torchrun: a peer's failure reaches rank 0 as SIGTERM from the agent
+        import signal
+
+        def _term(signum, frame):
+            print(json.dumps({**error_report(args, env_world), "status": "error", "exit_code": 128 + signum,
+                              "reason": f"rank 0 stopped by signal {signum} in phase {wd.phase!r} "
+                                        "(a peer rank failed or the launcher stopped the job)"}), flush=True)
+            os._exit(128 + signum)
+
+        signal.signal(signal.SIGTERM, _term)
+    try:
+        rc = run(args, wd)
+    except BaseException as e:
+        if env_rank == 0 and not (isinstance(e, SystemExit) and e.code in (0, None)):
+            print(json.dumps({**error_report(args, env_world), "status": "error", "exit_code": 1,
+                              "failing_rank": env_rank, "phase": wd.phase,
+                              "reason": f"{type(e).__name__}: {e}"}), flush=True)
+        raise
+    finally:
+        wd.cancel()
+    return rc
+
+
+def run(args, wd) -> int:
     import torch
     from kgs.models.gemm_workload import GemmWorkload
     from kgs.parallel import dist as kdist
+    from kgs.parallel import launch
 
+    wd.set_phase("rendezvous")
     ctx = kdist.init_from_env(expected_world=args.gpus, device_type="cpu" if args.cpu else None,
-                              backend=None if args.dist_backend == "auto" else args.dist_backend)
+                              backend=None if args.dist_backend == "auto" else args.dist_backend,
+                              rendezvous_timeout_s=args.rendezvous_timeout,
+                              timeout_s=max(args.launch_timeout, args.rendezvous_timeout),
+                              allow_shared_device=args.oversubscribe)
     rank, world = ctx.rank, ctx.world_size
     dev = ctx.device
+    if world > 1:
+        wd.store = ctx.store
+    wd.set_phase("setup")
+    launch.inject_fault(rank, "setup")
 
     def sync():
         if dev.type == "cuda":
@@ -110,19 +175,25 @@ def main(argv=None) -> int:
         if err > 2e-2:
             raise SystemExit(f"GEMM verification failed: rel err {err}")
 
+    launch.inject_fault(rank, "warmup")  # before the marker: a stalled rank stays behind in "setup"
+    wd.set_phase("warmup")
     for _ in range(args.warmup):
         wl.step()
     sync()
+    wd.set_phase("warmup-barrier")
     kdist.barrier(ctx)
     sync()
     wl.reset_stats()
+    wd.set_phase("timed")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
     sync()
+    wd.set_phase("timed-barrier")
     kdist.barrier(ctx)
     sync()
     elapsed = time.perf_counter() - t0
+    wd.set_phase("report")
 
     elapsed_max = kdist.max_over_ranks(ctx, elapsed)
     per_rank_ms = [round(t / max(1, args.steps) * 1e3, 4) for t in kdist.all_gather_object(ctx, elapsed)]
@@ -143,9 +214,7 @@ def main(argv=None) -> int:
 
     if rank == 0:
         out = {
-            "metric": "in-pod bf16 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 MFMA GEMM + RCCL grad all-reduce)"
-                      if args.dtype == "bf16" else
-                      "in-pod fp8 e4m3 GEMM TFLOPS (gpu-rocm-test workload, 8192^3 scaled-MFMA GEMM + RCCL all-reduce)",
+            "metric": metric_name(args.dtype),
             "value": round(total_tflops, 2),
             "unit": "TFLOP/s",
             "n_gpus": world,
@@ -176,6 +245,7 @@ def main(argv=None) -> int:
             **extra,
         }
         print(json.dumps(out), flush=True)
+    wd.set_phase("shutdown")
     kdist.shutdown(ctx)
     return 0
 

@@ -23,6 +23,7 @@ class DistContext:
     backend: str = "none"
     device: Any = None
     group: Any = None
+    store: Any = None  # the raw rendezvous TCPStore (unprefixed keys, e.g. kgs/phase/<rank>)
     initialized_here: bool = False
 
     @property
@@ -35,12 +36,69 @@ def _env_int(name: str, default: int) -> int:
     return int(v) if v not in (None, "") else default
 
 
-def init_from_env(expected_world: int | None = None, backend: str | None = None, timeout_s: float = 600.0,
-                  device_type: str | None = None) -> DistContext:
+class DeviceConflict(RuntimeError):
+    """Two ranks were bound to the same physical GPU."""
+
+
+def _rendezvous_store(rank: int, world: int, timeout_s: float):
+    """The TCPStore the process group is built on, created here so that the
+    rendezvous has its own (short) timeout and so ranks can exchange facts
+    before the RCCL communicator exists. Under torchrun the agent already
+    hosts the store on MASTER_PORT and every rank is a client (the same rule
+    torch's env:// rendezvous applies)."""
+    import torch.distributed as dist
+
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = os.environ.get("MASTER_PORT")
+    if not port:
+        raise RuntimeError("WORLD_SIZE > 1 but MASTER_PORT is not set (launch with torchrun or kgs.parallel.launch)")
+    agent = os.environ.get("TORCHELASTIC_USE_AGENT_STORE", "").lower() == "true"
+    return dist.TCPStore(host, int(port), world, is_master=(rank == 0 and not agent),
+                         timeout=datetime.timedelta(seconds=timeout_s), wait_for_workers=False)
+
+
+def device_identity(index: int) -> str | None:
+    """A physical identity of GPU ``index`` (PCI domain:bus:device, plus the
+    UUID when the runtime reports one); None if the runtime gives neither."""
+    import torch
+
+    p = torch.cuda.get_device_properties(index)
+    bus = getattr(p, "pci_bus_id", None)
+    uuid = str(getattr(p, "uuid", "") or "")
+    if bus is None and not uuid:
+        return None
+    return f"{getattr(p, 'pci_domain_id', 0)}:{bus}:{getattr(p, 'pci_device_id', 0)}/{uuid}"
+
+
+def check_distinct_devices(store, rank: int, world: int, ident: str | None, timeout_s: float) -> None:
+    """Every rank publishes its GPU identity; all ranks fail (DeviceConflict,
+    naming the ranks) if two of them hold the same GPU -- before the RCCL
+    communicator is created, where the same mistake hangs or corrupts."""
+    store.set(f"kgs/dev/{rank}", ident or "")
+    keys = [f"kgs/dev/{r}" for r in range(world)]
+    store.wait(keys, datetime.timedelta(seconds=timeout_s))
+    seen: dict = {}
+    for r in range(world):
+        v = store.get(keys[r]).decode()
+        if v:
+            seen.setdefault(v, []).append(r)
+    dup = {k: v for k, v in seen.items() if len(v) > 1}
+    if dup:
+        raise DeviceConflict("ranks share a GPU: " + "; ".join(f"ranks {v} on {k}" for k, v in dup.items())
+                             + " (one process per GPU; check HIP/ROCR_VISIBLE_DEVICES and LOCAL_RANK)")
+
+
+def init_from_env(expected_world: int | None = None, backend: str | None = None, timeout_s: float = 300.0,
+                  device_type: str | None = None, rendezvous_timeout_s: float = 120.0,
+                  allow_shared_device: bool = False) -> DistContext:
     """Initialise from torchrun-style env (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_*).
 
     With WORLD_SIZE unset (or 1) this is a single-process context and no process
     group is created. ``expected_world`` is a sanity check against ``--gpus``.
+    ``rendezvous_timeout_s`` bounds the wait for the other ranks (a missing
+    rank fails here, well inside any launcher's timeout); ``timeout_s`` bounds
+    each collective. On GPUs every rank must own a distinct device unless
+    ``allow_shared_device`` (the 1-GPU oversubscribed test mode).
     """
     import torch
     import torch.distributed as dist
@@ -59,6 +117,8 @@ def init_from_env(expected_world: int | None = None, backend: str | None = None,
     use_gpu = torch.cuda.is_available() if device_type is None else device_type == "cuda"
     if use_gpu:
         ndev = torch.cuda.device_count()
+        if local_rank >= ndev and not allow_shared_device:
+            raise DeviceConflict(f"LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible to this process")
         dev_index = local_rank % max(1, ndev)
         torch.cuda.set_device(dev_index)
         device = torch.device("cuda", dev_index)
@@ -70,12 +130,16 @@ def init_from_env(expected_world: int | None = None, backend: str | None = None,
         be = backend or ("nccl" if use_gpu else "gloo")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if not dist.is_initialized():
+            store = _rendezvous_store(rank, world, rendezvous_timeout_s)
+            if use_gpu and not allow_shared_device:
+                check_distinct_devices(store, rank, world, device_identity(device.index), rendezvous_timeout_s)
             kw = {}
             if be == "nccl":
                 kw["device_id"] = device
-            dist.init_process_group(be, rank=rank, world_size=world,
+            dist.init_process_group(be, store=store, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
             ctx.initialized_here = True
+            ctx.store = store
         ctx.backend = be
         ctx.group = dist.group.WORLD
     return ctx

@@ -308,3 +308,94 @@ def test_self_launch_refuses_missing_gpus():
     # this container has no GPU: asking for 2 real GPUs must fail fast, before spawning
     if launch.visible_gpu_count() < 2:
         assert launch.spawn_local(2, ["-c", "pass"], require_gpus=True) == 1
+
+
+def _bench_env(**extra):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "KGS_FAULT", "KGS_LAUNCH_PARENT")}
+    env["OMP_NUM_THREADS"] = "1"
+    env.update(extra)
+    return env
+
+
+_TINY = ["--cpu", "--backend", "torch", "--gemm-m", "64", "--gemm-n", "64", "--gemm-k", "64",
+         "--steps", "2", "--warmup", "1", "--allreduce-mb", "0.25"]
+
+
+def _error_line(stdout):
+    lines = [json.loads(ln) for ln in stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, stdout
+    return lines[0]
+
+
+def test_bench_stalled_rank_fails_fast_with_error_json():
+    """one of 8 gloo ranks stalls; the run ends inside
+    its launch timeout, exits non-zero and prints ONE error JSON line naming
+    the rank that is behind."""
+    import subprocess
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", *_TINY,
+                        "--launch-timeout", "25", "--rendezvous-timeout", "20"],
+                       capture_output=True, text=True, env=_bench_env(KGS_FAULT="warmup:5:stall:600"), timeout=200)
+    dt = time.monotonic() - t0
+    assert p.returncode != 0
+    assert dt < 25 + 30 + 30, dt
+    err = _error_line(p.stdout)
+    assert err["status"] == "error" and err["n_gpus"] == 8 and err["value"] is None
+    assert err["metric"].startswith("in-pod bf16 GEMM TFLOPS")
+    assert err["failing_rank"] == 5, err
+    assert err["rank_phases"]["5"].endswith(":setup") and err["rank_phases"]["0"].endswith(":warmup")
+    assert err["ranks_behind"] == [5]
+
+
+def test_bench_raising_rank_kills_all_within_seconds():
+    import subprocess
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", *_TINY,
+                        "--launch-timeout", "120"],
+                       capture_output=True, text=True, env=_bench_env(KGS_FAULT="setup:2:raise"), timeout=200)
+    dt = time.monotonic() - t0
+    assert p.returncode != 0
+    assert dt < 60, dt  # not the 120 s watchdog: the launcher stops the peers
+    err = _error_line(p.stdout)
+    assert err["status"] == "error" and err["failing_rank"] == 2
+    assert any("injected fault at setup on rank 2" in ln for ln in err["stderr_tail"]["2"])
+
+
+def test_bench_missing_rank_fails_at_rendezvous():
+    """torchrun-style launch where one rank never starts: the rendezvous
+    timeout (not the collective timeout) ends rank 0 with an error line."""
+    import subprocess
+
+    from kgs.parallel.launch import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = _bench_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                     MASTER_PORT=str(free_port()))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", *_TINY,
+                        "--rendezvous-timeout", "5", "--launch-timeout", "60"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    assert p.returncode != 0
+    err = _error_line(p.stdout)
+    assert err["status"] == "error" and err["phase"] == "rendezvous", err
+
+
+def test_distinct_device_check():
+    import datetime
+
+    import torch.distributed as dist
+
+    from kgs.parallel.dist import DeviceConflict, check_distinct_devices
+    from kgs.parallel.launch import free_port
+
+    store = dist.TCPStore("127.0.0.1", free_port(), 1, is_master=True, timeout=datetime.timedelta(seconds=5))
+    check_distinct_devices(store, 0, 1, "0:3:0/uuid-a", 5)
+    store.set("kgs/dev/1", "0:3:0/uuid-a")  # a second rank claiming the same GPU
+    with pytest.raises(DeviceConflict, match=r"ranks \[0, 1\]"):
+        check_distinct_devices(store, 0, 2, "0:3:0/uuid-a", 5)
