@@ -207,6 +207,9 @@ class AmdGpuDevicePlugin:
         self._cv = threading.Condition()
         self._version = 0          # bumps on every device-list change
         self._stop = threading.Event()
+        # serialises stop() with serve_forever's restart; re-entrant because
+        # stop() also runs from a SIGTERM handler on the serving thread
+        self._life = threading.RLock()
         self.registrations = 0
         self.allocations = 0
         self.health_flips = 0
@@ -311,12 +314,13 @@ class AmdGpuDevicePlugin:
         log.info("serving %s on %s", self.resource_name, self.socket_path)
 
     def stop(self, grace: float = 1.0) -> None:
-        self._stop.set()
-        with self._cv:
-            self._cv.notify_all()
-        if self._server is not None:
-            self._server.stop(grace).wait()
-            self._server = None
+        with self._life:
+            self._stop.set()
+            with self._cv:
+                self._cv.notify_all()
+            if self._server is not None:
+                self._server.stop(grace).wait()
+                self._server = None
         if os.path.exists(self.socket_path):
             try:
                 os.unlink(self.socket_path)
@@ -372,12 +376,16 @@ class AmdGpuDevicePlugin:
             if not os.path.exists(self.socket_path) or (cur is not None and cur != kubelet_id):
                 log.warning("kubelet restarted (socket %s); re-registering",
                             "gone" if not os.path.exists(self.socket_path) else "changed")
-                if self._server is not None:
-                    self._server.stop(0).wait()
-                    self._server = None
-                if self._stop.is_set():  # stop() raced the restart: do not come back up
+                with self._life:  # a stop() now either precedes the restart or tears it down
+                    if self._server is not None:
+                        self._server.stop(0).wait()
+                        self._server = None
+                    if self._stop.is_set():  # stop() raced the restart: do not come back up
+                        break
+                    self.start()
+                if self._stop.is_set():  # stop() ran inside the block (signal on this thread)
+                    self.stop(0)
                     break
-                self.start()
                 self._wait_kubelet_and_register()
                 kubelet_id = self._kubelet_id()
 

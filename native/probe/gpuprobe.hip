@@ -19,9 +19,12 @@
 
 #include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -65,7 +68,8 @@ struct DevResult {
   int cus = 0;
   double init_ms = 0, fill_ms = 0, first_gemm_ms = 0, tflops = 0, rel_err = 1, done_s = 0;
   bool ok = false;
-  std::string error;
+  std::string error;       // up to the readiness point (read by main after the latch)
+  std::string tput_error;  // the throughput loop, after it
 };
 
 #define PROBE_CHECK(x)                                                         \
@@ -77,7 +81,34 @@ struct DevResult {
     }                                                                          \
   } while (0)
 
-void probe_device(int dev, int n, int iters, clk::time_point t0, DevResult& r) {
+#define PROBE_CHECK_T(x)                                                       \
+  do {                                                                         \
+    hipError_t e_ = (x);                                                       \
+    if (e_ != hipSuccess) {                                                    \
+      r.tput_error = std::string(#x) + ": " + hipGetErrorString(e_);           \
+      return;                                                                  \
+    }                                                                          \
+  } while (0)
+
+// Readiness is announced as soon as every device has passed (or failed) its
+// checked first GEMM: main() prints KGS_FIRST_GEMM then, while the threads go
+// on to the throughput loop, which is reported afterwards as KGS_PROBE_TPUT.
+struct ReadyLatch {
+  std::mutex m;
+  std::condition_variable cv;
+  int pending;
+  explicit ReadyLatch(int n) : pending(n) {}
+  void arrive() {
+    std::lock_guard<std::mutex> g(m);
+    if (--pending == 0) cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> g(m);
+    cv.wait(g, [&] { return pending == 0; });
+  }
+};
+
+void probe_device(int dev, int n, int iters, clk::time_point t0, DevResult& r, const std::function<void()>& ready) {
   r.index = dev;
   auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   const auto ts = clk::now();
@@ -133,17 +164,18 @@ void probe_device(int dev, int n, int iters, clk::time_point t0, DevResult& r) {
   r.rel_err = max_ref > 0 ? max_err / max_ref : 1.0;
   r.ok = r.rel_err < 1e-2;
   r.done_s = std::chrono::duration<double>(clk::now() - t0).count();
+  ready();
 
   if (iters > 0) {  // throughput after the readiness point (does not delay it)
     hipEvent_t e0, e1;
-    PROBE_CHECK(hipEventCreate(&e0));
-    PROBE_CHECK(hipEventCreate(&e1));
-    PROBE_CHECK(hipEventRecord(e0, s));
+    PROBE_CHECK_T(hipEventCreate(&e0));
+    PROBE_CHECK_T(hipEventCreate(&e1));
+    PROBE_CHECK_T(hipEventRecord(e0, s));
     for (int it = 0; it < iters; ++it) kgs_gemm_bf16_nt(A, B, C, nullptr, n, n, n, n, n, n, 0, 0, s);
-    PROBE_CHECK(hipEventRecord(e1, s));
-    PROBE_CHECK(hipEventSynchronize(e1));
+    PROBE_CHECK_T(hipEventRecord(e1, s));
+    PROBE_CHECK_T(hipEventSynchronize(e1));
     float ms = 0;
-    PROBE_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PROBE_CHECK_T(hipEventElapsedTime(&ms, e0, e1));
     r.tflops = 2.0 * n * (double)n * n * iters / (ms * 1e-3) / 1e12;
     hipEventDestroy(e0);
     hipEventDestroy(e1);
@@ -187,8 +219,18 @@ int main(int argc, char** argv) {
   }
   std::vector<DevResult> res(ndev);
   std::vector<std::thread> th;
-  for (int d = 0; d < ndev; ++d) th.emplace_back(probe_device, d, n, iters, t0, std::ref(res[d]));
-  for (auto& t : th) t.join();
+  ReadyLatch latch(ndev);
+  for (int d = 0; d < ndev; ++d) {
+    th.emplace_back([&, d] {
+      std::once_flag once;
+      auto ready = [&] { std::call_once(once, [&] { latch.arrive(); }); };
+      probe_device(d, n, iters, t0, res[d], ready);
+      ready();  // an early error return still counts as "checked"
+    });
+  }
+  latch.wait();
+  // res[d] fields up to done_s are final once its thread arrived (the latch's
+  // mutex orders those writes before this read); tflops is written later.
   bool ok = true;
   double t_first = 0;
   std::string devs;
@@ -198,9 +240,9 @@ int main(int argc, char** argv) {
     char buf[512];
     snprintf(buf, sizeof buf,
              "{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"ok\":%s,\"init_ms\":%.2f,\"fill_ms\":%.2f,"
-             "\"first_gemm_ms\":%.2f,\"rel_err\":%.3e,\"tflops\":%.1f,\"ready_s\":%.4f",
+             "\"first_gemm_ms\":%.2f,\"rel_err\":%.3e,\"ready_s\":%.4f",
              r.index, json_escape(r.arch).c_str(), r.cus, r.ok ? "true" : "false", r.init_ms, r.fill_ms,
-             r.first_gemm_ms, r.rel_err, r.tflops, r.done_s);
+             r.first_gemm_ms, r.rel_err, r.done_s);
     if (!devs.empty()) devs += ",";
     devs += buf;
     if (!r.error.empty()) devs += ",\"error\":\"" + json_escape(r.error) + "\"";
@@ -208,6 +250,17 @@ int main(int argc, char** argv) {
   }
   printf("KGS_FIRST_GEMM {\"ok\":%s,\"size\":%d,\"n_gpus\":%d,\"t_first_gemm_s\":%.4f,\"devices\":[%s]}\n",
          ok ? "true" : "false", n, ndev, t_first, devs.c_str());
+  fflush(stdout);
+  for (auto& t : th) t.join();
+  std::string tput;
+  for (auto& r : res) {
+    char buf[96];
+    snprintf(buf, sizeof buf, "%s{\"device\":%d,\"tflops\":%.1f", tput.empty() ? "" : ",", r.index, r.tflops);
+    tput += buf;
+    if (!r.tput_error.empty()) tput += ",\"error\":\"" + json_escape(r.tput_error) + "\"";
+    tput += "}";
+  }
+  printf("KGS_PROBE_TPUT {\"iters\":%d,\"devices\":[%s]}\n", iters, tput.c_str());
   fflush(stdout);
   return ok ? 0 : 1;
 }

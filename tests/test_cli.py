@@ -413,7 +413,51 @@ def test_entrypoint_probe_line_parsing(tmp_path, monkeypatch, capsys):
     res = entrypoint.run_probe(256, timeout=30)
     assert res["ok"] is False and res["rc"] == 3
     monkeypatch.setattr(entrypoint, "probe_binary", lambda: None)
-    assert "not built" in entrypoint.run_probe(256)["error"]
+    assert "not built" in entrypoint.run_probe(256)["skipped"]
+
+
+def test_entrypoint_forwards_readiness_before_the_probe_exits(tmp_path, monkeypatch):
+    """the KGS_FIRST_GEMM line is forwarded when read, not when the
+    probe (which goes on to its throughput loop) has exited."""
+    import time
+
+    from kgs.workload import entrypoint
+
+    exe = tmp_path / "probe"
+    exe.write_text("#!/bin/sh\necho 'KGS_FIRST_GEMM {\"ok\":true,\"devices\":[]}'\nsleep 2\n"
+                   "echo 'KGS_PROBE_TPUT {\"iters\":5,\"devices\":[{\"device\":0,\"tflops\":1600.0}]}'\n")
+    exe.chmod(0o755)
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: str(exe))
+    writes = []
+
+    class Rec:
+        def write(self, text):
+            writes.append((time.monotonic(), text))
+
+        def flush(self):
+            pass
+
+    monkeypatch.setattr(sys, "stdout", Rec())
+    res = entrypoint.run_probe(256, timeout=30)
+    t_end = time.monotonic()
+    t_line = [t for t, x in writes if x.startswith("KGS_FIRST_GEMM")][0]
+    assert t_end - t_line > 1.5
+    assert res["ok"] and res["throughput"]["devices"][0]["tflops"] == 1600.0
+
+
+def test_entrypoint_missing_probe_does_not_fail_the_pod(tmp_path, monkeypatch):
+    from kgs.workload import entrypoint
+
+    class G:
+        render_minor, bdf, gfx_arch, cu_count, num_xcc, vram_bytes, numa_node = 128, "0000:05:00.0", "gfx950", \
+            256, 8, 288 << 30, 0
+
+    monkeypatch.setattr(entrypoint, "allocated_gpus", lambda: [G()])
+    monkeypatch.setattr(entrypoint, "probe_binary", lambda: None)
+    out = tmp_path / "r.json"
+    assert entrypoint.main(["--probe-only", "--json-out", str(out)]) == 0
+    r = json.loads(out.read_text())
+    assert "skipped" in r["first_gemm"] and r.get("all_ok", True)
 
 
 def test_pod_verb_renders_static_pods_on_the_configured_registry(world, capsys):
