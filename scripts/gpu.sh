@@ -20,6 +20,8 @@
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
+#   e2e_sweep    the same through `kgs bench --no-kind --sweep 1` (one point on a 1-GPU box)
+#   gemm_llm     kgs vs hipBLASLt on the Llama-shaped GEMMs ($SHAPES overrides)
 #   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
@@ -102,6 +104,10 @@ step() {
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
+        e2e_sweep) run e2e_sweep 300 python -m kgs bench --no-kind --sweep 1 --sweep-json "$O/e2e_sweep.json" ;;
+        gemm_llm) run gemm_llm 600 python bench/gemm_sweep.py \
+            --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \
+            --variants fast --rounds 7 --out "$O/gemm_llm.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
             --shapes ${SHAPES:-qkv,o,gate_up,down} --out "$O/w4x_sweep.jsonl" ;;

@@ -399,3 +399,34 @@ def test_distinct_device_check():
     store.set("kgs/dev/1", "0:3:0/uuid-a")  # a second rank claiming the same GPU
     with pytest.raises(DeviceConflict, match=r"ranks \[0, 1\]"):
         check_distinct_devices(store, 0, 2, "0:3:0/uuid-a", 5)
+
+
+def _torchrun(nproc, *extra, fault=None, timeout=240):
+    import subprocess
+
+    from kgs.parallel.launch import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = _bench_env(**({"KGS_FAULT": fault} if fault else {}))
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+                           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                           os.path.join(root, "bench.py"), "--gpus", str(nproc), *_TINY, *extra],
+                          capture_output=True, text=True, env=env, timeout=timeout, cwd="/tmp")
+
+
+def test_bench_under_torchrun_agent_store():
+    """The driver's launch (torch.distributed.run, static rendezvous: the agent
+    hosts the store and the ranks are its clients) works with our own store."""
+    p = _torchrun(2)
+    assert p.returncode == 0, p.stderr[-2000:]
+    j = _error_line(p.stdout)
+    assert j["n_gpus"] == 2 and "status" not in j
+
+
+def test_bench_under_torchrun_failing_rank_reports():
+    """torchrun tears the job down when a rank raises; rank 0 turns the agent's
+    SIGTERM into the error line, and the launcher exits non-zero."""
+    p = _torchrun(2, "--launch-timeout", "120", fault="setup:1:raise")
+    assert p.returncode != 0
+    j = _error_line(p.stdout)
+    assert j["status"] == "error" and j["value"] is None
