@@ -54,7 +54,9 @@ FP8 = {"gm8": 17, "gm16": 18, "gm2": 19}
 # per 128-MFMA K-step; name w4h_ORD_B1_R_P_X -> table id in gemm_w4h.hip (barrier 1 after MFMA B1, R
 # MFMAs after barrier 2, P reads per MFMA there)
 _W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (1, 24, 20, 1, 480000),
-            (1, 20, 20, 1, 160000), (1, 20, 24, 1, 320000))
+            (1, 20, 20, 1, 160000), (1, 20, 24, 1, 320000),
+            # round 3: GROUP_M 2 / 8 / 16 / 32 with the production schedule
+            (1, 24, 20, 1, 2), (1, 24, 20, 1, 8), (1, 24, 20, 1, 16), (1, 24, 20, 1, 32))
 W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
 
 

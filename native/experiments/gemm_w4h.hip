@@ -30,6 +30,10 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
     KGS_W4H(4, 24, 20, 1, 1, 480000)
     KGS_W4H(5, 20, 20, 1, 1, 160000)
     KGS_W4H(6, 20, 24, 1, 1, 320000)
+    KGS_W4H(7, 24, 20, 1, 1, 2)
+    KGS_W4H(8, 24, 20, 1, 1, 8)
+    KGS_W4H(9, 24, 20, 1, 1, 16)
+    KGS_W4H(10, 24, 20, 1, 1, 32)
     default: return KGS_ERR_ARG;
   }
 #undef KGS_W4H

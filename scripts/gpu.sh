@@ -21,6 +21,7 @@
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
 #   e2e_sweep    the same through `kgs bench --no-kind --sweep 1` (one point on a 1-GPU box)
+#   stride_probe per-K-step time vs K and row stride, GROUP_M variants ($CASES, $VARIANTS)
 #   gemm_llm     kgs vs hipBLASLt on the Llama-shaped GEMMs ($SHAPES overrides)
 #   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
@@ -104,6 +105,10 @@ step() {
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
+        stride_probe) run stride_probe 600 python bench/gemm_stride_probe.py \
+            --cases ${CASES:-8192x4096x14336,8192x4096x14336@16384,8192x4096x16384,8192x4096x8192,8192x8192x8192,4096x4096x4096} \
+            --variants ${VARIANTS:-fast,w4h_1_24_20_1_2,w4h_1_24_20_1_8,w4h_1_24_20_1_16,w4h_1_24_20_1_32} \
+            --out "$O/stride_probe.json" ;;
         e2e_sweep) run e2e_sweep 300 python -m kgs bench --no-kind --sweep 1 --sweep-json "$O/e2e_sweep.json" ;;
         gemm_llm) run gemm_llm 600 python bench/gemm_sweep.py \
             --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \

@@ -100,7 +100,12 @@ def test_gpuprobe_first_gemm_checked():
     res = json.loads(line.split(" ", 1)[1])
     assert res["ok"] and res["n_gpus"] >= 1
     d = res["devices"][0]
-    assert d["arch"].startswith("gfx950") and d["rel_err"] < 1e-2 and d["tflops"] > 0, d
+    assert d["arch"].startswith("gfx950") and d["rel_err"] < 1e-2, d
+    # the readiness line comes before the throughput loop, which reports after it
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith(("KGS_FIRST_GEMM ", "KGS_PROBE_TPUT "))]
+    assert [ln.split(" ", 1)[0] for ln in lines] == ["KGS_FIRST_GEMM", "KGS_PROBE_TPUT"], r.stdout
+    tput = json.loads(lines[1].split(" ", 1)[1])
+    assert tput["iters"] == 2 and tput["devices"][0]["tflops"] > 0, tput
 
 
 def test_device_plugin_self_test_allocates_real_paths():
