@@ -21,6 +21,7 @@
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
 #   e2e_sweep    the same through `kgs bench --no-kind --sweep 1` (one point on a 1-GPU box)
+#   gemm_l2      TCC hit/miss, FETCH_SIZE and kernel trace of kgs vs hipBLASLt at $MNK ($VAR: kgs variant)
 #   stride_probe per-K-step time vs K and row stride, GROUP_M variants ($CASES, $VARIANTS)
 #   gemm_llm     kgs vs hipBLASLt on the Llama-shaped GEMMs ($SHAPES overrides)
 #   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
@@ -105,6 +106,14 @@ step() {
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
+        gemm_l2) # L2 hit/miss + HBM bytes of kgs vs hipBLASLt at $MNK (two counter passes) + a kernel trace
+            local G="python3 bench/gemm_profile.py --mnk ${MNK:-8192x4096x14336} --iters 10 --torch --variant ${VAR:-auto}"
+            run l2_hit 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --output-format csv \
+                -d "$O/l2_hit_${MNK:-8192x4096x14336}" -o g -- $G &&
+            run l2_fetch 120 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv \
+                -d "$O/l2_fetch_${MNK:-8192x4096x14336}" -o g -- $G &&
+            run l2_trace 120 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$O/l2_trace_${MNK:-8192x4096x14336}" -o g -- $G ;;
         stride_probe) run stride_probe 600 python bench/gemm_stride_probe.py \
             --cases ${CASES:-8192x4096x14336,8192x4096x14336@16384,8192x4096x16384,8192x4096x8192,8192x8192x8192,4096x4096x4096} \
             --variants ${VARIANTS:-fast,w4h_1_24_20_1_2,w4h_1_24_20_1_8,w4h_1_24_20_1_16,w4h_1_24_20_1_32} \

@@ -15,7 +15,8 @@ from kgs.parallel.p2p_allreduce import P2PAllReduce  # noqa: E402
 
 
 def main():
-    ctx = kdist.init_from_env(backend="gloo")  # gloo: the handle exchange needs no RCCL
+    # gloo: the handle exchange needs no RCCL; both ranks may share the one GPU of a test box
+    ctx = kdist.init_from_env(backend="gloo", allow_shared_device=True)
     rank, world = ctx.rank, ctx.world_size
     ar = P2PAllReduce(group=ctx.group, max_bytes=4 << 20, device=ctx.device, timeout_s=5.0)
     ok = True
