@@ -124,7 +124,8 @@ __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
   }
 }
 
-// X: the knob bag of the kernel template (AUX = X / 100 % 100, SW = X / 10^6 % 10)
+// X: the knob bag of the kernel template (GROUP_M = X % 100, AUX = X / 100 % 100,
+// DMA window = X / 10^4 % 100, SW = X / 10^6 % 10, MAP = X / 10^7 % 10)
 template <int BM, int BN, int X>
 __device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
   constexpr int AUX = (X / 100) % 100;
@@ -311,6 +312,38 @@ struct Knobs<128, 128> {
 template <int MODE>
 constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
 
+// XCD-blocked tile map (X digit 10^7 = MAP, round 3). The default map
+// (xcd_remap + GROUP_M) gives XCD x a contiguous run of tile ids; with groups
+// along M that makes all eight XCDs of a wave work on the SAME B columns at the
+// same time (8192 x 4096: wave 1 = every A row x tn 0..7), so every B line is
+// requested by all eight XCDs at once and the wave's footprint (all of A + half
+// of B) is 294 MB at K = 14336, more than the 256 MB MALL. MAP 1..3 give each
+// wave (256 tiles, one per CU) a compact super-block and split it into eight
+// XCD blocks, so a line is shared by at most four XCDs:
+//   MAP 1: XCD block 8 (M) x 4 (N) tiles, XCD blocks 2 x 4   -> super-block 16 x 16
+//   MAP 2: XCD block 4 x 8,              XCD blocks 4 x 2   -> 16 x 16
+//   MAP 3: XCD block 8 x 4,              XCD blocks 4 x 2   -> 32 x 8
+// Waves walk super-blocks N-fastest, so consecutive waves share A rows. The
+// hardware dispatches workgroup b to XCD b % 8 and the first 256 workgroups
+// form wave 1, so XCD x's loc-th workgroup (loc = b / 8) takes tile loc % 32 of
+// its block loc / 32 of super-block loc / 32. Shapes whose tile grid is not a
+// whole number of super-blocks keep the default map (returns false).
+template <int MAP>
+__device__ __forceinline__ bool blocked_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
+  constexpr int XBM = MAP == 2 ? 4 : 8, XBN = MAP == 2 ? 8 : 4;  // XCD block, tiles
+  constexpr int AM = MAP == 1 ? 2 : 4, AN = 8 / AM;               // XCD blocks per super-block
+  constexpr int SBM = XBM * AM, SBN = XBN * AN, PER = XBM * XBN;
+  if (ntm % SBM || ntn % SBN) return false;
+  const int xcd = bid & 7, loc = bid >> 3;
+  const int sb = loc / PER, p = loc % PER;
+  const int nsbn = ntn / SBN;
+  const int sbm = sb / nsbn, sbn = sb - sbm * nsbn;
+  const int xm = xcd % AM, xn = xcd / AM;
+  tm = sbm * SBM + xm * XBM + p % XBM;
+  tn = sbn * SBN + xn * XBN + p / XBM;
+  return true;
+}
+
 template <int EPI, int BN = 256, int MODE = 0, int B1 = Knobs<tile_m<MODE>(), BN>::B1,
           int R = Knobs<tile_m<MODE>(), BN>::R, int P = Knobs<tile_m<MODE>(), BN>::P,
           int ORD = Knobs<tile_m<MODE>(), BN>::ORD, int X = Knobs<tile_m<MODE>(), BN>::X>
@@ -333,12 +366,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int slice = SPLITK ? wga / nwg : 0;
   const int wg = SPLITK ? wga - slice * nwg : wga;
   constexpr int G = (X % 100) ? X % 100 : GM;
-  const int per_group = G * ntn;
-  const int group = wg / per_group;
-  const int first_m = group * G;
-  const int gsz = min(ntm - first_m, G);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
+  constexpr int MAP = (X / 10000000) % 10;
+  int tm, tn;
+  if (MAP == 0 || SPLITK || !blocked_tile<MAP>(blockIdx.x, ntm, ntn, tm, tn)) {
+    const int per_group = G * ntn;
+    const int group = wg / per_group;
+    const int first_m = group * G;
+    const int gsz = min(ntm - first_m, G);
+    tm = first_m + (wg % per_group) % gsz;
+    tn = (wg % per_group) / gsz;
+  }
   const int rows_a = BNDM ? min(M - tm * BM, BM) : BM;
 
   Ctx c;
