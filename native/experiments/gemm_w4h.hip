@@ -37,6 +37,9 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
     KGS_W4H(11, 24, 20, 1, 1, 10000000)
     KGS_W4H(12, 24, 20, 1, 1, 20000000)
     KGS_W4H(13, 24, 20, 1, 1, 30000000)
+    KGS_W4H(14, 24, 20, 1, 1, 40000000)
+    KGS_W4H(15, 24, 20, 1, 1, 40000008)
+    KGS_W4H(16, 24, 20, 1, 1, 40000002)
     default: return KGS_ERR_ARG;
   }
 #undef KGS_W4H

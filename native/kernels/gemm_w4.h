@@ -323,6 +323,7 @@ constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
 //   MAP 1: XCD block 8 (M) x 4 (N) tiles, XCD blocks 2 x 4   -> super-block 16 x 16
 //   MAP 2: XCD block 4 x 8,              XCD blocks 4 x 2   -> 16 x 16
 //   MAP 3: XCD block 8 x 4,              XCD blocks 4 x 2   -> 32 x 8
+//   MAP 4: not blocked -- the default GROUP_M map with M and N exchanged
 // Waves walk super-blocks N-fastest, so consecutive waves share A rows. The
 // hardware dispatches workgroup b to XCD b % 8 and the first 256 workgroups
 // form wave 1, so XCD x's loc-th workgroup (loc = b / 8) takes tile loc % 32 of
@@ -330,6 +331,7 @@ constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
 // whole number of super-blocks keep the default map (returns false).
 template <int MAP>
 __device__ __forceinline__ bool blocked_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
+  static_assert(MAP >= 1 && MAP <= 3, "blocked maps are 1..3");
   constexpr int XBM = MAP == 2 ? 4 : 8, XBN = MAP == 2 ? 8 : 4;  // XCD block, tiles
   constexpr int AM = MAP == 1 ? 2 : 4, AN = 8 / AM;               // XCD blocks per super-block
   constexpr int SBM = XBM * AM, SBN = XBN * AN, PER = XBM * XBN;
@@ -367,8 +369,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int wg = SPLITK ? wga - slice * nwg : wga;
   constexpr int G = (X % 100) ? X % 100 : GM;
   constexpr int MAP = (X / 10000000) % 10;
-  int tm, tn;
-  if (MAP == 0 || SPLITK || !blocked_tile<MAP>(blockIdx.x, ntm, ntn, tm, tn)) {
+  int tm = 0, tn = 0;
+  bool mapped = false;
+  if constexpr (!SPLITK && MAP >= 1 && MAP <= 3) mapped = blocked_tile<MAP>(blockIdx.x, ntm, ntn, tm, tn);
+  if constexpr (!SPLITK && MAP == 4) {
+    // the default map mirrored: groups of G tile-COLUMNS walked down M. For
+    // M > N this is what the default map is for the transposed problem, e.g.
+    // 8192 x 4096 x 14336 then gets 4096 x 8192 x 14336's order.
+    const int per_group = G * ntm;
+    const int group = wg / per_group;
+    const int first_n = group * G;
+    const int gsz = min(ntn - first_n, G);
+    tn = first_n + (wg % per_group) % gsz;
+    tm = (wg % per_group) / gsz;
+    mapped = true;
+  }
+  if (!mapped) {
     const int per_group = G * ntn;
     const int group = wg / per_group;
     const int first_m = group * G;
