@@ -197,3 +197,18 @@ def test_bench_two_ranks_on_one_gpu():
     assert s["n_gpus"] == 2 and s["config"]["parallelism"] == "dp2" and s["value"] > 0
     assert len(s["per_rank_ms_per_step"]) == 2 and s["allreduce_busbw_gbs"] > 0
     assert s["gemm_path"].startswith("kgs gemm_nt_w4")
+
+
+def test_device_identity_is_informative():
+    """The distinct-device check before RCCL init (kgs.parallel.dist) compares
+    these strings across ranks; on the MI355X they must carry a real PCI bus id
+    and UUID, never a placeholder that would make every GPU look the same."""
+    from kgs.parallel.dist import device_identity
+
+    ident = device_identity(0)
+    print("device_identity(0) =", ident)
+    assert ident is not None
+    bus_part, _, uuid = ident.partition("/")
+    dom, bus, dev = bus_part.split(":")
+    assert bus not in ("None", "-1"), ident
+    assert uuid and uuid.strip("0-") != "", ident
