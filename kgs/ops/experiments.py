@@ -60,7 +60,10 @@ _W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (
             # round 3: XCD-blocked tile maps (gemm_w4.h blocked_tile) MAP 1 / 2 / 3
             (1, 24, 20, 1, 10000000), (1, 24, 20, 1, 20000000), (1, 24, 20, 1, 30000000),
             # MAP 4: GROUP_N (the default map with M and N exchanged), G = 4 / 8 / 2
-            (1, 24, 20, 1, 40000000), (1, 24, 20, 1, 40000008), (1, 24, 20, 1, 40000002))
+            (1, 24, 20, 1, 40000000), (1, 24, 20, 1, 40000008), (1, 24, 20, 1, 40000002),
+            # DMA operand order (X / 10^8): B first / interleaved, with MAP 4 and with the default map
+            (1, 24, 20, 1, 140000000), (1, 24, 20, 1, 240000000), (1, 24, 20, 1, 100000000),
+            (1, 24, 20, 1, 200000000))
 W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
 
 

@@ -40,6 +40,10 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
     KGS_W4H(14, 24, 20, 1, 1, 40000000)
     KGS_W4H(15, 24, 20, 1, 1, 40000008)
     KGS_W4H(16, 24, 20, 1, 1, 40000002)
+    KGS_W4H(17, 24, 20, 1, 1, 140000000)
+    KGS_W4H(18, 24, 20, 1, 1, 240000000)
+    KGS_W4H(19, 24, 20, 1, 1, 100000000)
+    KGS_W4H(20, 24, 20, 1, 1, 200000000)
     default: return KGS_ERR_ARG;
   }
 #undef KGS_W4H
