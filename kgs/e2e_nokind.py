@@ -159,7 +159,7 @@ def nokind_once(gpus: int = 1, dev_root: str = "/", fake_gpus: int = 0, gemm_siz
         if minors:
             env["ROCR_VISIBLE_DEVICES"] = visible_devices_for(minors, dev_root)
         res_path = os.path.join(d, "pod_result.json")
-        cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "1",
+        cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "10",
                "--json-out", res_path]
         err_path = os.path.join(d, "pod.stderr")
         with t.phase("pod-first-gemm") as rec:

@@ -50,7 +50,7 @@ run() {
     return $rc
 }
 
-PMC_GEMM="python3 bench/gemm_profile.py --iters 5 --torch"
+PMC_GEMM="python3 bench/gemm_profile.py --iters 5 --torch --mnk ${MNK:-8192} --variant ${VAR:-auto}"
 
 step() {
     case "$1" in
