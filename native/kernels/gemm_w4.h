@@ -338,7 +338,7 @@ constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
 // its block loc / 32 of super-block loc / 32. Shapes whose tile grid is not a
 // whole number of super-blocks keep the default map (returns false).
 template <int MAP>
-__device__ __forceinline__ bool blocked_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
+__host__ __device__ __forceinline__ bool blocked_tile(int bid, int ntm, int ntn, int& tm, int& tn) {
   static_assert(MAP >= 1 && MAP <= 3, "blocked maps are 1..3");
   constexpr int XBM = MAP == 2 ? 4 : 8, XBN = MAP == 2 ? 8 : 4;  // XCD block, tiles
   constexpr int AM = MAP == 1 ? 2 : 4, AN = 8 / AM;               // XCD blocks per super-block
@@ -352,6 +352,44 @@ __device__ __forceinline__ bool blocked_tile(int bid, int ntm, int ntn, int& tm,
   tm = sbm * SBM + xm * XBM + p % XBM;
   tn = sbn * SBN + xn * XBN + p / XBM;
   return true;
+}
+
+// Workgroup -> (split-K slice, tile row, tile column): the default map
+// (xcd_remap + GROUP_M), a blocked map (MAP 1..3) or GROUP_N (MAP 4). A
+// bijection from [0, grid) onto slices x tiles for every MAP
+// (tests/test_gemm_tile_map.py checks it on the host).
+template <int X, bool SPLITK>
+__host__ __device__ __forceinline__ void tile_of(int bid, int grid, int ntm, int ntn, int& slice, int& tm, int& tn) {
+  const int nwg = ntm * ntn;
+  // split-K: remap over the whole grid, so the blocks of one XCD share a slice
+  const int nslice = SPLITK ? grid / nwg : 1;
+  const int wga = SPLITK ? xcd_remap(bid, nwg * nslice) : xcd_remap(bid, nwg);
+  slice = SPLITK ? wga / nwg : 0;
+  const int wg = SPLITK ? wga - slice * nwg : wga;
+  constexpr int G = (X % 100) ? X % 100 : GM;
+  constexpr int MAP = (X / 10000000) % 10;
+  bool mapped = false;
+  if constexpr (!SPLITK && MAP >= 1 && MAP <= 3) mapped = blocked_tile<MAP>(bid, ntm, ntn, tm, tn);
+  if constexpr (!SPLITK && MAP == 4) {
+    // the default map mirrored: groups of G tile-COLUMNS walked down M. For
+    // M > N this is what the default map is for the transposed problem, e.g.
+    // 8192 x 4096 x 14336 then gets 4096 x 8192 x 14336's order.
+    const int per_group = G * ntm;
+    const int group = wg / per_group;
+    const int first_n = group * G;
+    const int gsz = ntn - first_n < G ? ntn - first_n : G;
+    tn = first_n + (wg % per_group) % gsz;
+    tm = (wg % per_group) / gsz;
+    mapped = true;
+  }
+  if (!mapped) {
+    const int per_group = G * ntn;
+    const int group = wg / per_group;
+    const int first_m = group * G;
+    const int gsz = ntm - first_m < G ? ntm - first_m : G;
+    tm = first_m + (wg % per_group) % gsz;
+    tn = (wg % per_group) / gsz;
+  }
 }
 
 template <int EPI, int BN = 256, int MODE = 0, int B1 = Knobs<tile_m<MODE>(), BN>::B1,
@@ -369,37 +407,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ __attribute__((aligned(1024))) char smem[S::LDS_BYTES];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int ntm = BNDM ? (M + BM - 1) / BM : M / BM, ntn = N / BN, nwg = ntm * ntn;
-  // split-K: remap over the whole grid, so the blocks of one XCD share a slice
-  const int nslice = SPLITK ? gridDim.x / nwg : 1;
-  const int wga = SPLITK ? xcd_remap(blockIdx.x, nwg * nslice) : xcd_remap(blockIdx.x, nwg);
-  const int slice = SPLITK ? wga / nwg : 0;
-  const int wg = SPLITK ? wga - slice * nwg : wga;
-  constexpr int G = (X % 100) ? X % 100 : GM;
-  constexpr int MAP = (X / 10000000) % 10;
-  int tm = 0, tn = 0;
-  bool mapped = false;
-  if constexpr (!SPLITK && MAP >= 1 && MAP <= 3) mapped = blocked_tile<MAP>(blockIdx.x, ntm, ntn, tm, tn);
-  if constexpr (!SPLITK && MAP == 4) {
-    // the default map mirrored: groups of G tile-COLUMNS walked down M. For
-    // M > N this is what the default map is for the transposed problem, e.g.
-    // 8192 x 4096 x 14336 then gets 4096 x 8192 x 14336's order.
-    const int per_group = G * ntm;
-    const int group = wg / per_group;
-    const int first_n = group * G;
-    const int gsz = min(ntn - first_n, G);
-    tn = first_n + (wg % per_group) % gsz;
-    tm = (wg % per_group) / gsz;
-    mapped = true;
-  }
-  if (!mapped) {
-    const int per_group = G * ntn;
-    const int group = wg / per_group;
-    const int first_m = group * G;
-    const int gsz = min(ntm - first_m, G);
-    tm = first_m + (wg % per_group) % gsz;
-    tn = (wg % per_group) / gsz;
-  }
+  const int ntm = BNDM ? (M + BM - 1) / BM : M / BM, ntn = N / BN;
+  int slice, tm, tn;
+  tile_of<X, SPLITK>((int)blockIdx.x, (int)gridDim.x, ntm, ntn, slice, tm, tn);
   const int rows_a = BNDM ? min(M - tm * BM, BM) : BM;
 
   Ctx c;

@@ -79,7 +79,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_base) {
 // Bijective XCD-aware remap of a 1-D grid: blocks that the dispatcher deals to
 // the same XCD (bid % 8 equal) get a contiguous range of logical ids, so
 // neighbouring output tiles share that XCD's L2 (guide T1).
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+__host__ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, loc = bid >> 3;
   const int q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
