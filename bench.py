@@ -74,7 +74,8 @@ def parse(argv=None):
     ap.add_argument("--dtype", choices=("bf16", "fp8"), default="bf16",
                     help="bf16 = the headline (BASELINE.json); fp8 = e4m3 operands on the scaled MFMA (extra)")
     ap.add_argument("--launch-timeout", type=float, default=300.0,
-                    help="whole-run bound per rank (watchdog); the self-launch parent kills at +30 s")
+                    help="per-rank bound from `import torch` to the end (watchdog); the self-launch parent, whose "
+                         "clock includes the ranks' imports, kills at +180 s")
     ap.add_argument("--rendezvous-timeout", type=float, default=120.0,
                     help="how long a rank waits for the others to join")
     return ap.parse_args(argv)
@@ -103,19 +104,23 @@ def main(argv=None) -> int:
         os.environ["KGS_LAUNCH_PARENT"] = "1"
         return launch.spawn_local(args.gpus, [os.path.abspath(__file__), *raw],
                                   require_gpus=not (args.cpu or args.oversubscribe),
-                                  timeout_s=args.launch_timeout + 30, error_report=error_report(args, args.gpus))
+                                  timeout_s=args.launch_timeout + 180, error_report=error_report(args, args.gpus))
 
     env_rank = int(os.environ.get("RANK", "0") or 0)
     env_world = int(os.environ.get("WORLD_SIZE", "1") or 1)
+    # the watchdog's clock starts after `import torch`, which alone can take 1-2
+    # minutes on a freshly booted box (image paging), so that cost never reads as a hang
+    import torch  # noqa: F401
+
     wd = launch.Watchdog(args.launch_timeout, env_rank, env_world, error_report(args, env_world))
     if env_rank == 0 and env_world > 1 and not os.environ.get("KGS_LAUNCH_PARENT"):
         # under torchrun: a peer's failure reaches rank 0 as SIGTERM from the agent
         import signal
 
         def _term(signum, frame):
-            print(json.dumps({**error_report(args, env_world), "status": "error", "exit_code": 128 + signum,
-                              "reason": f"rank 0 stopped by signal {signum} in phase {wd.phase!r} "
-                                        "(a peer rank failed or the launcher stopped the job)"}), flush=True)
+            launch.report_once({**error_report(args, env_world), "status": "error", "exit_code": 128 + signum,
+                                "reason": f"rank 0 stopped by signal {signum} in phase {wd.phase!r} "
+                                          "(a peer rank failed or the launcher stopped the job)"})
             os._exit(128 + signum)
 
         signal.signal(signal.SIGTERM, _term)
@@ -123,9 +128,8 @@ def main(argv=None) -> int:
         rc = run(args, wd)
     except BaseException as e:
         if env_rank == 0 and not (isinstance(e, SystemExit) and e.code in (0, None)):
-            print(json.dumps({**error_report(args, env_world), "status": "error", "exit_code": 1,
-                              "failing_rank": env_rank, "phase": wd.phase,
-                              "reason": f"{type(e).__name__}: {e}"}), flush=True)
+            launch.report_once({**error_report(args, env_world), "status": "error", "exit_code": 1,
+                                "failing_rank": env_rank, "phase": wd.phase, "reason": f"{type(e).__name__}: {e}"})
         raise
     finally:
         wd.cancel()
@@ -244,7 +248,7 @@ def run(args, wd) -> int:
             "backend": args.backend,
             **extra,
         }
-        print(json.dumps(out), flush=True)
+        launch.report_once(out)  # the one JSON line (a later signal cannot add an error line)
     wd.set_phase("shutdown")
     kdist.shutdown(ctx)
     return 0

@@ -189,6 +189,23 @@ def inject_fault(rank: int, where: str) -> None:
         raise RuntimeError(f"injected fault at {where} on rank {rank}")
 
 
+_report_lock = threading.RLock()  # re-entrant: the SIGTERM handler runs on the main thread
+_reported = False
+
+
+def report_once(obj: dict) -> bool:
+    """Print ``obj`` as THE error line of this process unless one was already
+    printed (an exception handler, the SIGTERM handler and the watchdog can
+    all race to report the same failure). True if this call printed."""
+    global _reported
+    with _report_lock:
+        if _reported:
+            return False
+        _reported = True
+        print(json.dumps(obj), flush=True)
+        return True
+
+
 class Watchdog:
     """Bounds one rank's whole run: after ``timeout_s`` it reports where every
     rank was (rank 0: one JSON error line on stdout) and hard-exits 124, so a
@@ -210,6 +227,9 @@ class Watchdog:
         self.store = None
         self._t = None
         if timeout_s:
+            # rank 0 fires first: it writes the one report (with every rank's
+            # phase); the others only end their process, a little later
+            timeout_s = timeout_s if rank == 0 else timeout_s + 15.0
             self._t = threading.Timer(timeout_s, self._fire, args=(timeout_s,))
             self._t.daemon = True
             self._t.start()
@@ -255,7 +275,7 @@ class Watchdog:
                         rep["failing_rank"] = behind[0]
                         rep["ranks_behind"] = behind
             rep.setdefault("failing_rank", self.rank)
-            print(json.dumps(rep), flush=True)
+            report_once(rep)
         os._exit(124)
 
     def cancel(self) -> None:
