@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--table-pages", type=int, default=64, help="block-table width (the graph bucket)")
     ap.add_argument("--splits", default="1,2,4,8,16")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--pipe", default="auto", help="auto | 0 | 1 | both: the two-page register pipeline")
     a = ap.parse_args()
     from kgs.ops.decode import PAGE, PagedKVCache, decode_splits, paged_decode_attention
 
@@ -37,21 +38,22 @@ def main():
         q = (torch.randn(b, H * 128, device=dev)).bfloat16()
         kv_bytes = b * math.ceil(a.ctx / PAGE) * PAGE * HKV * 128 * 2 * 2
         auto = decode_splits(b, HKV, tp)
-        for ns in [int(x) for x in a.splits.split(",")]:
+        pipes = {"auto": [None], "0": [False], "1": [True], "both": [False, True]}[a.pipe]
+        for ns, pipe in [(int(x), p) for x in a.splits.split(",") for p in pipes]:
             pps = math.ceil(tp / ns)
             for _ in range(3):
-                paged_decode_attention(q, lay, bt, ctx, H, HKV, pages_per_split=pps)
+                paged_decode_attention(q, lay, bt, ctx, H, HKV, pages_per_split=pps, pipe=pipe)
             ts = []
             for _ in range(a.iters):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                paged_decode_attention(q, lay, bt, ctx, H, HKV, pages_per_split=pps)
+                paged_decode_attention(q, lay, bt, ctx, H, HKV, pages_per_split=pps, pipe=pipe)
                 e.record()
                 e.synchronize()
                 ts.append(s.elapsed_time(e) * 1e3)
             us = statistics.median(ts)
             print(json.dumps({"batch": b, "nsplit": math.ceil(tp / pps), "pps": pps, "us": round(us, 2),
-                              "TBps": round(kv_bytes / us / 1e6, 2), "auto_pps_nsplit": auto}), flush=True)
+                              "TBps": round(kv_bytes / us / 1e6, 2), "auto_pps_nsplit": auto, "pipe": pipe}), flush=True)
         del cache, lay
         torch.cuda.empty_cache()
 

@@ -525,7 +525,8 @@ _AWS: dict = {}
 
 def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tables: torch.Tensor,
                            ctx_lens: torch.Tensor, heads: int, kv_heads: int, out: torch.Tensor | None = None,
-                           scale: float | None = None, pages_per_split: int | None = None) -> torch.Tensor:
+                           scale: float | None = None, pages_per_split: int | None = None,
+                           pipe: bool | None = None) -> torch.Tensor:
     """One query token per sequence: ``q`` rows ``[B, >= H*128]`` (e.g. the rotated
     q heads at the front of the fused QKV rows), ``block_tables`` int32
     ``[B, max_pages]``, ``ctx_lens`` int32 ``[B]`` (cached tokens incl. the new
@@ -556,12 +557,14 @@ def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tab
             cnt = torch.zeros(max(b * kv_heads, 4096), dtype=torch.int32, device=q.device)
             _AWS[key] = (po, pml, cnt)
     scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
-    rc = _lib.lib().kgs_paged_decode_bf16(q.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(),
-                                          ctx_lens.data_ptr(), out.data_ptr(), po.data_ptr() if po is not None else None,
-                                          pml.data_ptr() if pml is not None else None,
-                                          cnt.data_ptr() if cnt is not None else None, b, heads, kv_heads, HEAD_DIM,
-                                          max_pages, pps, nsplit, q.stride(0), out.stride(0), float(scale),
-                                          1 if cache_layer.dtype == FP8 else 0, _lib.stream_handle(q.device))
+    rc = _lib.lib().kgs_paged_decode_bf16_ex(q.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(),
+                                             ctx_lens.data_ptr(), out.data_ptr(),
+                                             po.data_ptr() if po is not None else None,
+                                             pml.data_ptr() if pml is not None else None,
+                                             cnt.data_ptr() if cnt is not None else None, b, heads, kv_heads, HEAD_DIM,
+                                             max_pages, pps, nsplit, q.stride(0), out.stride(0), float(scale),
+                                             1 if cache_layer.dtype == FP8 else 0,
+                                             -1 if pipe is None else int(bool(pipe)), _lib.stream_handle(q.device))
     _lib.check(rc, "paged_decode_attention")
     return out
 

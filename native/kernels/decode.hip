@@ -1119,10 +1119,25 @@ KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* si
 // [B, max_pages] int32; ctx_lens [B] int32 (>= 1). nsplit > 1 needs po
 // (B*H*nsplit*128 f32), pml (B*H*nsplit*2 f32) and cnt (B*HKV zeroed ints, left
 // zeroed); the splits are merged in the same launch.
+KGS_EXPORT int kgs_paged_decode_bf16_ex(const void* q, const void* cache, const int* block_tables,
+                                       const int* ctx_lens, void* o, float* po, float* pml, int* cnt, int B, int H,
+                                       int HKV, int hd, int max_pages, int pages_per_split, int nsplit, long ldq,
+                                       long ldo, float scale, int kv8, int pipe_mode, hipStream_t s);
+
 KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int* block_tables, const int* ctx_lens,
                                     void* o, float* po, float* pml, int* cnt, int B, int H, int HKV, int hd,
                                     int max_pages, int pages_per_split, int nsplit, long ldq, long ldo, float scale,
                                     int kv8, hipStream_t s) {
+  return kgs_paged_decode_bf16_ex(q, cache, block_tables, ctx_lens, o, po, pml, cnt, B, H, HKV, hd, max_pages,
+                                  pages_per_split, nsplit, ldq, ldo, scale, kv8, -1, s);
+}
+
+// pipe_mode: -1 = automatic (the two-page register pipeline for small grids),
+// 0 / 1 = force it off / on (measurement)
+KGS_EXPORT int kgs_paged_decode_bf16_ex(const void* q, const void* cache, const int* block_tables,
+                                       const int* ctx_lens, void* o, float* po, float* pml, int* cnt, int B, int H,
+                                       int HKV, int hd, int max_pages, int pages_per_split, int nsplit, long ldq,
+                                       long ldo, float scale, int kv8, int pipe_mode, hipStream_t s) {
   using namespace kgs::dec;
   if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 16 || hd != HD) return KGS_ERR_SHAPE;
   if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0) return KGS_ERR_SHAPE;
@@ -1139,7 +1154,7 @@ KGS_EXPORT int kgs_paged_decode_bf16(const void* q, const void* cache, const int
              pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
   // a grid of at most 2 waves per CU cannot hide page latency across waves:
   // pipeline inside the wave there
-  const bool pipe = nwg <= 512;
+  const bool pipe = pipe_mode < 0 ? nwg <= 512 : pipe_mode != 0;
   if (kv8) {
     if (pipe) hipLaunchKernelGGL((paged_decode<true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((paged_decode<true, false>), dim3((unsigned)nwg), dim3(64), 0, s, a);

@@ -85,7 +85,8 @@ step() {
         decode_trace_b128) run decode_trace_b128 300 rocprofv3 --kernel-trace --stats --output-format csv \
             -d "$O/dtrace128" -o d -- python3 -m kgs.serve bench --requests 128 --input-len 512 --output-len 32 \
             --max-batch 128 --max-model-len 2048 ;;
-        paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py ;;
+        paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py --batches ${BATCHES:-64,128,256} \
+            --ctx ${CTX:-528} --splits ${SPLITS:-1,2,4} --pipe ${PIPE:-both} ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
             --max-batch 1 --max-model-len 2048 ;;
         serve_b1_f8) run serve_b1_f8 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
