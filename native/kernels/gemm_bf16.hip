@@ -158,7 +158,19 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   // at 4096^3..16384^2x8192 in interleaved A/B, profiles/gemm_tuning.md).
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
   if (variant == 3) {
-    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI>), grid256, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+    using Kn = w4::Knobs<256, 256>;
+    if (M > N) {
+      // tall problems run the mirror image of the default schedule: GROUP_N tile
+      // order (MAP 4) and B's DMAs first. The kernel is then what the default one
+      // is for the transposed problem, which is the faster orientation: at
+      // 8192x4096x14336 the default order made all eight XCDs of a wave read the
+      // same B columns (1456-1531 TFLOP/s); the mirror runs 1587, as fast as
+      // 4096x8192x14336 (profiles/r3/gemm_long_k.md)
+      hipLaunchKernelGGL((w4::gemm_nt_w4<EPI, 256, 0, Kn::B1, Kn::R, Kn::P, Kn::ORD, 140000000>), grid256, dim3(256),
+                         0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+    } else {
+      hipLaunchKernelGGL((w4::gemm_nt_w4<EPI>), grid256, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+    }
   } else if (variant == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7>), grid256, dim3(512), 0, s, A, B, C, bias, M, N, K, lda, ldb,
                        ldc, 1.0f, nullptr);
