@@ -525,3 +525,26 @@ def test_gemm_w4x_swiglu_epilogue(M, I, K, bn, bm):
     gu = a.float() @ w.float().T
     r32 = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
     assert ((fused.float() - r32).abs().max() / r32.abs().max()).item() < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 640), (2048, 256, 1024), (768, 256, 384)])
+def test_gemm_tall_mirrored_schedule_is_bitwise_the_default(M, N, K):
+    """M > N runs the mirrored schedule (GROUP_N order, B's DMAs first, round 3):
+    only tile order and DMA issue order differ, so the result must be bitwise
+    the default schedule's (experiment w4h_1_24_20_1_0) and match fp32."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    fast = gemm_nt(a, b, variant="fast")
+    default = _gemm_v(a, b, "w4h_1_24_20_1_0")
+    assert torch.equal(fast, default)
+    assert _rel_err(fast, _ref_nt(a, b)) < 1e-2
+    # an asymmetric exact check: B^T stacked under itself, A = [I; I]
+    a2 = torch.zeros(M, K, device=DEV).bfloat16()
+    idx = torch.arange(M, device=DEV)
+    a2[idx, idx % min(N, K)] = 1.0
+    b2 = ((torch.arange(N, device=DEV)[:, None] * 3 + torch.arange(K, device=DEV)[None, :] * 7) % 61 - 30).float()
+    c = gemm_nt(a2, b2.bfloat16(), variant="fast")
+    ref = b2.T[idx % min(N, K)]  # row i of C = row (i mod min(N,K)) of B^T
+    torch.testing.assert_close(c.float(), ref, rtol=0, atol=0)
