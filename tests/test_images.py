@@ -51,10 +51,12 @@ def test_final_stage_ships_all_three_gpuinfo_targets_and_amdsmi(plugin_image):
     assert "libkgs_gpuinfo.so" in names and "kgs-gpuinfo" in names
     assert any(n.startswith("_gpuinfo") and n.endswith(".so") for n in names), names
     libs = os.listdir(os.path.join(final, "opt", "kgs", "lib"))
-    assert "libamd_smi.so" in libs, libs
+    assert "libamd_smi.so" in libs and "libdrm_amdgpu.so.1" in libs and "libdrm.so.2" in libs, libs
     # RTLD_NOW: any unresolved symbol (the r2 SmiSession link failure) raises here
     ctypes.CDLL(os.path.join(nat, "libkgs_gpuinfo.so"), mode=os.RTLD_NOW)
     ctypes.CDLL(os.path.join(final, "opt", "kgs", "lib", "libamd_smi.so"), mode=os.RTLD_NOW)
+    ctypes.CDLL(os.path.join(final, "opt", "kgs", "lib", "libdrm.so.2"), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+    ctypes.CDLL(os.path.join(final, "opt", "kgs", "lib", "libdrm_amdgpu.so.1"), mode=os.RTLD_NOW)
     r = subprocess.run([os.path.join(nat, "kgs-gpuinfo"), "--root", "/nonexistent", "--no-amdsmi", "--json"],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
