@@ -505,13 +505,20 @@ class Provisioner:
             self.out(C.SUCCESS_FMT_REAL.format(gpu_type=gpu_type, n=self.expected_capacity))
         return 0
 
-    def delete(self) -> int:
+    def delete(self, keep_registry: bool = False) -> int:
+        """Delete the cluster, then stop and remove the registry
+        (kind-gpu-sim.sh:338-361). ``keep_registry`` leaves the registry and
+        the images pushed to it (``kgs bench --sweep`` between its points)."""
         rt = self.ensure_runtime()
         if self.cluster_exists() or self.runner.dry_run:
             self.out(f"Deleting kind cluster '{self.s.cluster_name}'...")
             self.kind("delete", "cluster", "--name", self.s.cluster_name)
         else:
             self.out(f"Kind cluster '{self.s.cluster_name}' does not exist. Skipping delete.")
+        if keep_registry:
+            if not self.runner.dry_run:
+                shutil.rmtree(self.state_dir, ignore_errors=True)
+            return 0
         name = C.REGISTRY_NAME
         self.out(f"Stopping {name} (if running)...")
         if rt.running_id(name) or self.runner.dry_run:  # Q10: test the output, not the exit code

@@ -42,8 +42,11 @@ def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, kee
 
 
 def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, keep: bool = False,
-             workload_image: str | None = None, pod_command: list | None = None) -> dict:
-    """One create -> pod Running -> logs (-> delete) pass; returns the summary."""
+             workload_image: str | None = None, pod_command: list | None = None,
+             keep_registry: bool = False) -> dict:
+    """One create -> pod Running -> logs (-> delete) pass; returns the summary.
+    ``keep_registry``: the final delete leaves the local registry (and the
+    images in it) for the next pass."""
     t = p.timer
     t_start = time.perf_counter()
     image = workload_image or globals()["workload_image"](p)
@@ -53,6 +56,13 @@ def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, ke
             rec["provided"] = True  # a user-supplied image: their registry, their build
         elif p.runner.dry_run or p.ensure_runtime().image_exists(image):
             rec["cached"] = True
+            if not p.runner.dry_run and p.ensure_runtime().name == "docker":
+                # built earlier, but the registry may be a fresh one (kgs delete
+                # removes it): the nodes pull from the registry, so push (a no-op
+                # upload when the registry already has the layers)
+                p.start_registry()
+                p.ensure_runtime().cr("push", image)
+                rec["pushed"] = True
         else:
             from .images import build_images
 
@@ -92,7 +102,7 @@ def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, ke
     finally:
         t.write(p.s.timings_json)
         if not keep and not p.runner.dry_run:
-            p.delete()
+            p.delete(keep_registry=keep_registry)
     summary = {"metric": "cluster-create->GPU-pod-Running", "value": t.meta.get("create_to_running_s"),
                "unit": "s", "gpus": gpus, "advertised": p.expected_capacity, "fake": p.fake,
                "phases": {ph["phase"]: ph["seconds"] for ph in t.phases}}
@@ -115,7 +125,8 @@ def run_sweep(make_provisioner, counts: list, pod_gpus: int | None = None, sweep
     bad count does not hide the others; the exit status is then 1.
     """
     points = []
-    for n in counts:
+    last = None
+    for i, n in enumerate(counts):
         want = pod_gpus or n
         try:
             if no_kind:
@@ -123,12 +134,17 @@ def run_sweep(make_provisioner, counts: list, pod_gpus: int | None = None, sweep
 
                 pt = nokind_once(gpus=want, advertise=n, **kw)
             else:
-                pt = e2e_once(make_provisioner(n), gpus=want, **kw)
+                # the registry (with the plugin and workload images) outlives
+                # the points; the last one removes it as `kgs delete` does
+                last = make_provisioner(n)
+                pt = e2e_once(last, gpus=want, keep_registry=i < len(counts) - 1, **kw)
             pt["ok"] = True
         except Exception as e:  # noqa: BLE001 - recorded per point
             pt = {"ok": False, "error": f"{type(e).__name__}: {e}"}
         pt.update(advertised=n, pod_gpus=want)
         points.append(pt)
+    if last is not None and not points[-1]["ok"] and not last.runner.dry_run:
+        last.delete()  # a failed last point: still leave no registry behind
     doc = {
         "metric": ("device-plugin start -> first in-pod GEMM (no kind)" if no_kind
                    else "cluster-create->GPU-pod-Running"),

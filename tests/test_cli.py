@@ -721,3 +721,18 @@ def test_bench_no_kind_advertises_the_same_selection(world, tmp_path, capsys):
     alloc = [p for p in t["phases"] if p["phase"] == "allocate"][0]
     assert len(alloc["device_ids"]) == 1
     assert t["allocate_envs"]["KGS_RENDER_MINORS"] in {"128", "136", "144", "152"}
+
+
+def test_bench_sweep_keeps_the_registry_between_points(world, tmp_path):
+    """The nodes pull the workload image from the local registry: the sweep
+    must not remove the registry between points (a fresh, empty one would leave
+    every later pod in ImagePullBackOff), and a locally cached image is pushed
+    again. After the last point the registry is gone, as after `kgs delete`."""
+    host = make_fake_mi355x(tmp_path / "host8")
+    assert run("bench", "--sweep", "1,2,4", "--dev-root", str(host)) == 0
+    runs = world.calls("docker", "run")
+    assert len([a for a in runs if "kind-registry" in a]) == 1  # started once, reused by points 2 and 3
+    assert world.calls("docker", "rm") == [["rm", "kind-registry"]]  # removed once, at the end
+    pushes = [a for a in world.calls("docker", "push") if a[1].endswith("kgs-rocm-test:dev")]
+    assert len(pushes) == 3  # built + pushed once, re-pushed (cached) by the next two points
+    assert "kind-registry" not in world.state()["containers"]
