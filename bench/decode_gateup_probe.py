@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Decode gate|up + SwiGLU at batch 128-512 (Llama-3-8B: [M, 4096] x [28672, 4096]^T):
+routing candidates vs hipBLASLt, weights streamed from HBM (a ring of copies
+larger than the MALL, as a 32-layer decode step sees them).
+
+Candidates (gate|up at batch 256 was 67 us, ~58 % of
+the weight-streaming floor):
+  swiglu_bmXXX_bnYYY  the four-wave kernel with SwiGLU in its epilogue
+  sk_bnYYY_sS         split-K S slices (fp32 partials, reduce) + silu_mul
+  hipblaslt           torch.matmul + silu_mul
+One JSON line per (batch, variant): median us, weight GB/s, max rel err vs
+hipBLASLt + silu_mul.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batches", default="128,256,512")
+    ap.add_argument("--inter", type=int, default=14336)
+    ap.add_argument("--hidden", type=int, default=4096)
+    ap.add_argument("--ring-gb", type=float, default=1.5)
+    ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--variants", default="swiglu_bm256_bn128,swiglu_bm256_bn256,swiglu_bm128_bn256,"
+                                          "swiglu_bm128_bn128,sk_bn256_s2,sk_bn256_s4,sk_bn128_s2,hipblaslt")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu, reserve_splitk_workspace
+    from kgs.ops.transformer import silu_mul
+
+    dev = torch.device("cuda", 0)
+    N, K = 2 * a.inter, a.hidden
+    wbytes = N * K * 2
+    ring = max(2, int(a.ring_gb * 1e9 // wbytes))
+    ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(ring)]
+    reserve_splitk_workspace(dev, 4 * 512 * N)
+
+    def make(v, x):
+        if v == "hipblaslt":
+            return lambda w: silu_mul(torch.matmul(x, w.T))
+        if v.startswith("swiglu_"):
+            bm, bn = (int(t[2:]) for t in v.split("_")[1:3])
+            return lambda w: gemm_nt_w4x_swiglu(x, w, bn=bn, bm=bm)
+        bn, s = int(v.split("_")[1][2:]), int(v.split("_")[2][1:])
+        return lambda w: silu_mul(gemm_nt_w4x(x, w, bn=bn, nslice=s))
+
+    res = []
+    for m in (int(t) for t in a.batches.split(",")):
+        x = (torch.randn(m, K, device=dev)).bfloat16()
+        ref = silu_mul(torch.matmul(x, ws[0].T)).float()
+        for v in a.variants.split(","):
+            fn = make(v, x)
+            try:
+                got = fn(ws[0]).float()
+            except Exception as e:  # a shape the variant does not take
+                print(json.dumps({"batch": m, "variant": v, "error": str(e)[:200]}), flush=True)
+                continue
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            for i in range(ring):
+                fn(ws[i])
+            torch.cuda.synchronize()
+            ts = []
+            for it in range(a.iters):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn(ws[it % ring])
+                e.record()
+                e.synchronize()
+                ts.append(s.elapsed_time(e) * 1e3)
+            us = statistics.median(ts)
+            r = {"batch": m, "variant": v, "us": round(us, 2), "weight_TBps": round(wbytes / us / 1e6, 2),
+                 "rel_err": round(err, 5)}
+            print(json.dumps(r), flush=True)
+            res.append(r)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

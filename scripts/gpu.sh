@@ -23,6 +23,7 @@
 #   e2e_sweep    the same through `kgs bench --no-kind --sweep 1` (one point on a 1-GPU box)
 #   gemm_l2      TCC hit/miss, FETCH_SIZE and kernel trace of kgs vs hipBLASLt at $MNK ($VAR: kgs variant)
 #   stride_probe per-K-step time vs K and row stride, GROUP_M variants ($CASES, $VARIANTS)
+#   gateup_probe decode gate|up + SwiGLU routing candidates vs hipBLASLt, HBM-streamed weights
 #   gemm_llm     kgs vs hipBLASLt on the Llama-shaped GEMMs ($SHAPES overrides)
 #   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
@@ -85,6 +86,8 @@ step() {
         decode_trace_b128) run decode_trace_b128 300 rocprofv3 --kernel-trace --stats --output-format csv \
             -d "$O/dtrace128" -o d -- python3 -m kgs.serve bench --requests 128 --input-len 512 --output-len 32 \
             --max-batch 128 --max-model-len 2048 ;;
+        gateup_probe) run gateup_probe 400 python bench/decode_gateup_probe.py --batches ${BATCHES:-128,256,512} \
+            --out "$O/gateup_probe.json" ;;
         paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py --batches ${BATCHES:-64,128,256} \
             --ctx ${CTX:-528} --splits ${SPLITS:-1,2,4} --pipe ${PIPE:-both} ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \
