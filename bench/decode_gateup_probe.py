@@ -7,6 +7,7 @@ Candidates (gate|up at batch 256 was 67 us, ~58 % of
 the weight-streaming floor):
   swiglu_bmXXX_bnYYY  the four-wave kernel with SwiGLU in its epilogue
   sk_bnYYY_sS         split-K S slices (fp32 partials, reduce) + silu_mul
+  skf_bnYYY_sS        split-K S slices + ONE fused reduce-and-SwiGLU pass
   hipblaslt           torch.matmul + silu_mul
 One JSON line per (batch, variant): median us, weight GB/s, max rel err vs
 hipBLASLt + silu_mul.
@@ -29,11 +30,12 @@ def main():
     ap.add_argument("--hidden", type=int, default=4096)
     ap.add_argument("--ring-gb", type=float, default=1.5)
     ap.add_argument("--iters", type=int, default=30)
-    ap.add_argument("--variants", default="swiglu_bm256_bn128,swiglu_bm256_bn256,swiglu_bm128_bn256,"
-                                          "swiglu_bm128_bn128,sk_bn256_s2,sk_bn256_s4,sk_bn128_s2,hipblaslt")
+    ap.add_argument("--variants", default=(
+        "swiglu_bm256_bn128,swiglu_bm256_bn256,swiglu_bm128_bn256,swiglu_bm128_bn128,"
+        "sk_bn256_s2,sk_bn256_s4,sk_bn128_s2,skf_bn256_s2,skf_bn256_s4,skf_bn128_s2,hipblaslt"))
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu, reserve_splitk_workspace
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_splitk_swiglu, gemm_nt_w4x_swiglu, reserve_splitk_workspace
     from kgs.ops.transformer import silu_mul
 
     dev = torch.device("cuda", 0)
@@ -50,6 +52,8 @@ def main():
             bm, bn = (int(t[2:]) for t in v.split("_")[1:3])
             return lambda w: gemm_nt_w4x_swiglu(x, w, bn=bn, bm=bm)
         bn, s = int(v.split("_")[1][2:]), int(v.split("_")[2][1:])
+        if v.startswith("skf_"):  # split-K partials + fused reduce-and-SwiGLU
+            return lambda w: gemm_nt_w4x_splitk_swiglu(x, w, bn=bn, nslice=s)
         return lambda w: silu_mul(gemm_nt_w4x(x, w, bn=bn, nslice=s))
 
     res = []

@@ -90,6 +90,7 @@ _SIGS = {
                                                                               ctypes.c_float, _c_void_p], _c_int),
     "kgs_paged_decode_bf16": ([_c_void_p] * 8 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_int, _c_void_p],
                               _c_int),
+    "kgs_splitk_reduce_swiglu_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_paged_decode_bf16_ex": ([_c_void_p] * 8 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_int, _c_int,
                                                                    _c_void_p], _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)

@@ -215,6 +215,22 @@ def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
     return out
 
 
+def gemm_nt_w4x_splitk_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 256, nslice: int = 2,
+                              bm: int = 256, out: torch.Tensor | None = None) -> torch.Tensor:
+    """SwiGLU over a fused gate|up weight as a split-K GEMM (fp32 partials in the
+    split-K workspace) + one reduce-and-SwiGLU pass: returns ``[M, I]`` with the
+    roundings of ``gemm_nt`` + ``silu_mul``. For decode batches where the
+    epilogue-fused kernel (:func:`gemm_nt_w4x_swiglu`) leaves CUs idle."""
+    parts = gemm_nt_w4x_partials(a, w_gate_up, bn=bn, nslice=nslice, bm=bm)
+    M, N = a.shape[0], w_gate_up.shape[0]
+    if out is None:
+        out = torch.empty((M, N // 2), dtype=torch.bfloat16, device=a.device)
+    rc = _lib.lib().kgs_splitk_reduce_swiglu_bf16(parts.data_ptr(), out.data_ptr(), int(nslice), M, N // 2,
+                                                  out.stride(0), _lib.stream_handle(a.device))
+    _lib.check(rc, f"splitk_reduce_swiglu[{nslice}x{M}x{N // 2}]")
+    return out
+
+
 def gemm_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
     """SwiGLU MLP input projection ``silu(a @ gate.T) * (a @ up.T)`` -> ``[M, I]``:
     fused into the four-wave GEMM's epilogue (256x256 tiles; 256x128 when

@@ -472,6 +472,62 @@ __global__ __launch_bounds__(256) void splitk_reduce(const float* __restrict__ P
   *(uint4*)(C + (long)row * ldc + col) = o;
 }
 
+// SwiGLU consumer of a split-K gate|up GEMM (round 3): P holds nslice fp32
+// partials [M][2I] of a fused gate|up product (gate columns [0, I), up [I, 2I));
+// out[m][j] = silu(g) * u with g, u the slice sums rounded to bf16 first -- the
+// roundings of gemm_nt + silu_mul. One thread: 8 consecutive outputs.
+template <int NSL>
+__global__ __launch_bounds__(256) void splitk_reduce_swiglu(const float* __restrict__ P,
+                                                            unsigned short* __restrict__ out, int M, int I, int ldo,
+                                                            int nslice) {
+  const long e = ((long)blockIdx.x * 256 + threadIdx.x) * 8;  // index into [M][I]
+  const long MI = (long)M * I, MN = 2 * MI;
+  if (e >= MI) return;
+  const int row = (int)(e / I), col = (int)(e - (long)row * I);
+  const float* pg = P + (long)row * 2 * I + col;
+  const float* pu = pg + I;
+  f32x4 g0, g1, u0, u1;
+  if constexpr (NSL > 0) {
+    f32x4 a[NSL][4];
+#pragma unroll
+    for (int s = 0; s < NSL; ++s) {
+      a[s][0] = *(const f32x4*)(pg + s * MN);
+      a[s][1] = *(const f32x4*)(pg + s * MN + 4);
+      a[s][2] = *(const f32x4*)(pu + s * MN);
+      a[s][3] = *(const f32x4*)(pu + s * MN + 4);
+    }
+    g0 = a[0][0], g1 = a[0][1], u0 = a[0][2], u1 = a[0][3];
+#pragma unroll
+    for (int s = 1; s < NSL; ++s) {
+      g0 += a[s][0];
+      g1 += a[s][1];
+      u0 += a[s][2];
+      u1 += a[s][3];
+    }
+  } else {
+    g0 = *(const f32x4*)pg, g1 = *(const f32x4*)(pg + 4), u0 = *(const f32x4*)pu, u1 = *(const f32x4*)(pu + 4);
+    for (int s = 1; s < nslice; ++s) {
+      g0 += *(const f32x4*)(pg + s * MN);
+      g1 += *(const f32x4*)(pg + s * MN + 4);
+      u0 += *(const f32x4*)(pu + s * MN);
+      u1 += *(const f32x4*)(pu + s * MN + 4);
+    }
+  }
+  float r[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float g = bf2f(f2bf(k < 4 ? g0[k] : g1[k - 4]));
+    const float u = bf2f(f2bf(k < 4 ? u0[k] : u1[k - 4]));
+    r[k] = g / (1.0f + __expf(-g)) * u;
+  }
+  uint4 o;
+  o.x = pack_bf16x2(r[0], r[1]);
+  o.y = pack_bf16x2(r[2], r[3]);
+  o.z = pack_bf16x2(r[4], r[5]);
+  o.w = pack_bf16x2(r[6], r[7]);
+  *(uint4*)(out + (long)row * ldo + col) = o;
+}
+
 inline void launch_splitk_reduce(const float* P, unsigned short* C, int M, int N, int ldc, int nslice,
                                  hipStream_t s) {
   const dim3 g((unsigned)(((long)M * N / 8 + 255) / 256)), b(256);
@@ -647,4 +703,21 @@ KGS_EXPORT int kgs_gemm_bf16(const void* A, const void* B, void* C, const void* 
     default: return KGS_ERR_ARG;
   }
   return (int)e;
+}
+
+// out[M][I] = silu(sum_s P[s][:, :I]) * sum_s P[s][:, I:] (bf16-rounded sums): the
+// consumer of kgs_gemm_bf16_nt_w4x(C = nullptr, ...) on a fused gate|up weight.
+KGS_EXPORT int kgs_splitk_reduce_swiglu_bf16(const float* P, void* out, int nslice, int M, int I, int ldo,
+                                            hipStream_t s) {
+  using namespace kgs;
+  if (nslice <= 0 || M <= 0 || I <= 0 || I % 8 || ldo < I || ldo % 8) return KGS_ERR_SHAPE;
+  if ((uintptr_t)P % 16 || (uintptr_t)out % 16) return KGS_ERR_ALIGN;
+  const dim3 g((unsigned)(((long)M * I / 8 + 255) / 256)), b(256);
+  auto o = (unsigned short*)out;
+  switch (nslice) {
+    case 2: hipLaunchKernelGGL(splitk_reduce_swiglu<2>, g, b, 0, s, P, o, M, I, ldo, nslice); break;
+    case 4: hipLaunchKernelGGL(splitk_reduce_swiglu<4>, g, b, 0, s, P, o, M, I, ldo, nslice); break;
+    default: hipLaunchKernelGGL(splitk_reduce_swiglu<0>, g, b, 0, s, P, o, M, I, ldo, nslice); break;
+  }
+  return (int)hipGetLastError();
 }

@@ -548,3 +548,21 @@ def test_gemm_tall_mirrored_schedule_is_bitwise_the_default(M, N, K):
     c = gemm_nt(a2, b2.bfloat16(), variant="fast")
     ref = b2.T[idx % min(N, K)]  # row i of C = row (i mod min(N,K)) of B^T
     torch.testing.assert_close(c.float(), ref, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("M,I,K,bn,nslice", [(256, 1024, 4096, 256, 2), (200, 768, 1024, 128, 4), (64, 512, 2048, 256, 3)])
+def test_gemm_splitk_swiglu_matches_gemm_then_silu_mul(M, I, K, bn, nslice):
+    """Split-K gate|up + the fused reduce-and-SwiGLU pass: the roundings of
+    gemm_nt + silu_mul (products rounded to bf16 first), close to fp32."""
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_splitk_swiglu
+    from kgs.ops.transformer import silu_mul
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * 0.05).bfloat16()
+    got = gemm_nt_w4x_splitk_swiglu(a, w, bn=bn, nslice=nslice)
+    # same partials reduced by the plain split-K path, then silu_mul: bitwise
+    want = silu_mul(gemm_nt_w4x(a, w, bn=bn, nslice=nslice))
+    assert torch.equal(got, want)
+    ref = a.float() @ w.float().T
+    ref = torch.nn.functional.silu(ref[:, :I]) * ref[:, I:]
+    assert _rel_err(got, ref) < 2e-2
