@@ -500,22 +500,28 @@ def rope_cache_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, positio
 def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS, min_pages: int = 4) -> tuple[int, int]:
     """(pages_per_split, nsplit) for a block-table width of ``max_pages``.
 
-    Fewer (sequence, KV head) groups than 3/4 of the CUs: split each context
-    so the grid has about 2 waves per CU, every split at least ``min_pages``
-    pages (a one-page split is all launch and merge overhead: 52 us for batch
-    1 x 4096 tokens with 1-page splits, profiles/decode_kernels.md); batch 16
-    takes 4 splits of 528 tokens, batch 1-8 eight. From there up, a split
-    costs more (partial writes + the merge pass) than the extra waves give back
-    unless it keeps >= 32 pages and the grid stays <= 8 waves per CU: at 528
-    cached tokens one split is fastest for batch 24-256 (batch 64: 32.7 vs
-    44.0 us with the old 8-waves-per-CU rule), at 2000 tokens two splits win
-    at batch 32 and 128 (profiles/r2/paged_split_sweep.md)."""
+    Split each context so that the grid holds about two waves per CU:
+    ``nsplit = ceil(2 * CUs / (batch * kv_heads))``. Every split keeps at least
+    ``min_pages`` pages (a one-page split is all launch and merge overhead: 52
+    us for batch 1 x 4096 tokens with 1-page splits, profiles/decode_kernels.md).
+    So batch 1-8 takes eight splits, batch 16 four and batch 32 two. From batch
+    64 up, one split per (sequence, KV head) is fastest. It is paired with the
+    two-page register pipeline, which the kernel runs for grids of up to 1024
+    waves (``kgs_paged_decode_bf16``).
+
+    Round-3 measurements (``profiles/r3/decode/paged_sweep_ctx*.log``, table
+    width 64 pages):
+
+    * 1024 cached tokens: batch 64 52 us (was 100 with the old rule of two
+      splits and no pipeline); batch 128 92 us (was 124);
+    * 528 tokens: batch 64 30 us (was 59), batch 128 50 us (was 72);
+    * 2000 tokens: within 2 % of the best split everywhere.
+
+    The old rule split large batches whenever the table held 64 pages or more;
+    without the pipeline, each split paid one page latency per page."""
     groups = max(1, batch * kv_heads)
-    if 4 * groups < 3 * cus:
-        want = max(1, math.ceil(2 * cus / groups))
-        nsplit = max(1, min(math.ceil(max_pages / min_pages), want))
-    else:
-        nsplit = max(1, min(max_pages // 32, (8 * cus) // groups))
+    want = max(1, math.ceil(2 * cus / groups))
+    nsplit = max(1, min(math.ceil(max_pages / min_pages), want))
     pps = math.ceil(max_pages / nsplit)
     return pps, math.ceil(max_pages / pps)
 

@@ -1152,9 +1152,11 @@ KGS_EXPORT int kgs_paged_decode_bf16_ex(const void* q, const void* cache, const 
   const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
              pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
-  // a grid of at most 2 waves per CU cannot hide page latency across waves:
-  // pipeline inside the wave there
-  const bool pipe = pipe_mode < 0 ? nwg <= 512 : pipe_mode != 0;
+  // up to 4 waves per CU (1024 on the chip) other waves cannot hide a page's
+  // latency: pipeline inside the wave there. Round 3 measured the pipeline at
+  // 1.2-1.9x for 512-1024-wave grids (batch 64-128 at 528-2000 cached
+  // tokens) and +-2 % at 2048 waves (profiles/r3/decode/paged_sweep_ctx*.log)
+  const bool pipe = pipe_mode < 0 ? nwg <= 1024 : pipe_mode != 0;
   if (kv8) {
     if (pipe) hipLaunchKernelGGL((paged_decode<true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((paged_decode<true, false>), dim3((unsigned)nwg), dim3(64), 0, s, a);

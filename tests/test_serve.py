@@ -679,6 +679,10 @@ def test_decode_routing_tables_cpu():
             assert (k // kpc) % ks == 0 and n % D.skinny_geometry(1, v)[0] == 0
     pps, ns = D.decode_splits(1, 8, 128)
     assert pps >= 4 and pps * ns >= 128
+    # round 3: about two waves per CU -- batch 16 four splits, 32 two, >= 64 one
+    # (paired with the kernel's two-page pipeline up to 1024 waves)
+    assert [D.decode_splits(b, 8, 64)[1] for b in (16, 32, 64, 128, 256)] == [4, 2, 1, 1, 1]
+    assert D.decode_splits(1, 8, 8) == (4, 2)  # >= 4 pages per split
 
 
 def test_splitk_routing_table_cpu():
