@@ -194,9 +194,10 @@ _reported = False
 
 
 def report_once(obj: dict) -> bool:
-    """Print ``obj`` as THE error line of this process unless one was already
-    printed (an exception handler, the SIGTERM handler and the watchdog can
-    all race to report the same failure). True if this call printed."""
+    """Print ``obj`` as THE JSON line of this process (the result, or the
+    error) unless one was already printed: an exception handler, the SIGTERM
+    handler and the watchdog can all race to report the same failure, and a
+    signal after the result must not add an error line. True if this printed."""
     global _reported
     with _report_lock:
         if _reported:
