@@ -49,7 +49,7 @@ BF16 = {
     "vgpr_stage": Experiment(21, "VGPR staging, 4 phases in flight"),
     "vgpr_stage2": Experiment(22, "VGPR staging, 2 phases in flight"),
 }
-FP8 = {"gm8": 17, "gm16": 18, "gm2": 19}
+FP8 = {"gm8": 17, "gm16": 18, "gm2": 19, "gn4": 20, "gn8": 21, "gn2": 22}
 # gemm_w4h (native/experiments/gemm_w4h.hip): 4 waves x 128x128, two barriers
 # per 128-MFMA K-step; name w4h_ORD_B1_R_P_X -> table id in gemm_w4h.hip (barrier 1 after MFMA B1, R
 # MFMAs after barrier 2, P reads per MFMA there)

@@ -742,11 +742,12 @@ KGS_EXPORT int kgs_exp_gemm_bf16_nt(const void* A, const void* B, void* C, const
 }
 
 // fp8 e4m3 tile-group height experiments (aligned shapes, no epilogue):
-// 17 = GROUP_M 8, 18 = GROUP_M 16, 19 = GROUP_M 2. Lengths in fp8 elements.
+// 17 = GROUP_M 8, 18 = GROUP_M 16, 19 = GROUP_M 2; round 3: 20 / 21 / 22 = GROUP_N
+// 4 / 8 / 2 (S bit 21). Lengths in fp8 elements.
 KGS_EXPORT int kgs_exp_gemm_fp8_nt(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                    int ldc, float alpha, int variant, hipStream_t s) {
   using namespace kgs;
-  if (variant < 17 || variant > 19) return KGS_ERR_ARG;
+  if (variant < 17 || variant > 22) return KGS_ERR_ARG;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if (M % 256 || N % 256 || K % 256 || lda % 16 || ldb % 16 || ldc % 8) return KGS_ERR_ALIGN;
   if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
@@ -764,6 +765,15 @@ KGS_EXPORT int kgs_exp_gemm_fp8_nt(const void* A, const void* B, void* C, int M,
   if (variant == 19)
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 15 + 1024>), grid, dim3(512), 0, s, a, b, c, nullptr, M, N, Kw,
                        ldaw, ldbw, ldc, alpha, nullptr);
+  if (variant == 20)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 7 + 1024 + 2097152>), grid, dim3(512), 0, s, a, b, c, nullptr, M,
+                       N, Kw, ldaw, ldbw, ldc, alpha, nullptr);
+  if (variant == 21)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 3 + 1024 + 2097152>), grid, dim3(512), 0, s, a, b, c, nullptr, M,
+                       N, Kw, ldaw, ldbw, ldc, alpha, nullptr);
+  if (variant == 22)
+    hipLaunchKernelGGL((g256::gemm_nt_256<EPI_NONE, 15 + 1024 + 2097152>), grid, dim3(512), 0, s, a, b, c, nullptr, M,
+                       N, Kw, ldaw, ldbw, ldc, alpha, nullptr);
   return (int)hipGetLastError();
 }
 

@@ -10,7 +10,7 @@
 //   7 one barrier per phase (with 6)                     8 narrow store tail
 //   9 bounded (buffer-resource zero fill, any M/N)       10 fp8 e4m3 (scaled MFMA)
 //   11 A stored [K][M]   12 B stored [K][N]  (ds_read_b64_tr_b16 fragments)
-//   13/14 probes for 11   15 persistent tile walk
+//   13/14 probes for 11   15 persistent tile walk      21 GROUP_N order (tall problems)
 // Production bf16 = 7 (balanced, no setprio, GROUP_M 4).
 #pragma once
 
@@ -510,12 +510,18 @@ __global__ __launch_bounds__(512) void gemm_nt_256(const unsigned short* __restr
   const int wg = SPLITK ? wga - slice * nwg : xcd_remap(blockIdx.x, nwg);
   // S bits 2-3 select the tile-group height (experiment knob): 8, 4, 16, 2
   constexpr int GM = ((S >> 2) & 3) == 0 ? GROUP_M : ((S >> 2) & 3) == 1 ? 4 : ((S >> 2) & 3) == 2 ? 16 : 2;
-  const int per_group = GM * ntn;
+  // S bit 21: the same grouped order with M and N exchanged (groups of GM
+  // tile-columns walked down M) -- tall problems, cf. gemm_w4.h MAP 4 and
+  // profiles/r3/gemm_long_k.md
+  constexpr bool GN = (S & 2097152) != 0;
+  const int ngrp = GN ? ntn : ntm, nalong = GN ? ntm : ntn;
+  const int per_group = GM * nalong;
   const int group = wg / per_group;
-  const int first_m = group * GM;
-  const int gsz = min(ntm - first_m, GM);
-  const int tm = first_m + (wg % per_group) % gsz;
-  const int tn = (wg % per_group) / gsz;
+  const int first = group * GM;
+  const int gsz = min(ngrp - first, GM);
+  const int tg = first + (wg % per_group) % gsz, ta = (wg % per_group) / gsz;
+  const int tm = GN ? ta : tg;
+  const int tn = GN ? tg : ta;
 
   Ctx c;
   c.smem = smem;
