@@ -106,7 +106,7 @@ class Settings:
     extra: dict = field(default_factory=dict)
 
     def library_image(self, name: str) -> str:
-        """``name`` (e.g. ``python:3.12-slim``) from the configured library mirror."""
+        """``name`` (e.g. ``python:3.12.8-slim-bookworm``) from the configured library mirror."""
         return f"{self.base_mirror.rstrip('/')}/{name}"
 
     @property
