@@ -257,8 +257,12 @@ def kubectl_tool():
             key = op["path"].split("/")[-1].replace("~1", "/")
             c["nodes"][n]["capacity"][key] = op["value"]
             c["nodes"][n]["allocatable"][key] = op["value"]
-    elif verb == "apply":
-        for doc in yaml.safe_load_all(stdin or ""):
+    elif verb in ("apply", "create"):
+        text = stdin or ""
+        if "-f" in a and a[a.index("-f") + 1] != "-":
+            with open(a[a.index("-f") + 1]) as f:
+                text = f.read()
+        for doc in yaml.safe_load_all(text):
             if not doc:
                 continue
             c["objects"].append(doc)
