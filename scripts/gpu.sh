@@ -123,6 +123,8 @@ step() {
             --variants ${VARIANTS:-fast,w4h_1_24_20_1_2,w4h_1_24_20_1_8,w4h_1_24_20_1_16,w4h_1_24_20_1_32} \
             --out "$O/stride_probe.json" ;;
         e2e_sweep) run e2e_sweep 300 python -m kgs bench --no-kind --sweep 1 --sweep-json "$O/e2e_sweep.json" ;;
+        gemm_power) run gemm_power 200 python bench/gemm_power.py --mnk ${MNK:-8192} --seconds 2 --rounds 2 \
+            --out "$O/gemm_power.json" ;;
         fp8_tall) run fp8_tall 400 python bench/gemm_sweep.py --dtype fp8 --data normal \
             --shapes ${SHAPES:-8192x4096x14336,16384x4096x14336,4096x8192x14336,8192x28672x4096,8192} \
             --variants ${VARIANTS:-fast,gn4,gn8,gn2} --rounds 7 --out "$O/fp8_tall.json" ;;
