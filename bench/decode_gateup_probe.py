@@ -9,6 +9,10 @@ the weight-streaming floor):
   sk_bnYYY_sS         split-K S slices (fp32 partials, reduce) + silu_mul
   skf_bnYYY_sS        split-K S slices + ONE fused reduce-and-SwiGLU pass
   hipblaslt           torch.matmul + silu_mul
+  p<any of the above> the same on weights packed tile-panel major
+                      (kgs.ops.gemm.pack_w4x_weight, PACKB), e.g. pswiglu_bm256_bn128
+With ``--proj down`` (x [M, 14336] . W [4096, 14336]^T, no SwiGLU) the
+candidates are w4x_bmXXX_bnYYY[_sS], pw4x_... and hipblaslt.
 One JSON line per (batch, variant): median us, weight GB/s, max rel err vs
 hipBLASLt + silu_mul.
 """
@@ -33,49 +37,71 @@ def main():
     ap.add_argument("--variants", default=(
         "swiglu_bm256_bn128,swiglu_bm256_bn256,swiglu_bm128_bn256,swiglu_bm128_bn128,"
         "sk_bn256_s2,sk_bn256_s4,sk_bn128_s2,skf_bn256_s2,skf_bn256_s4,skf_bn128_s2,hipblaslt"))
+    ap.add_argument("--proj", choices=("gateup", "down"), default="gateup")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_splitk_swiglu, gemm_nt_w4x_swiglu, reserve_splitk_workspace
+    from kgs.ops.gemm import (gemm_nt_w4x, gemm_nt_w4x_splitk_swiglu, gemm_nt_w4x_swiglu, pack_w4x_weight,
+                              reserve_splitk_workspace)
     from kgs.ops.transformer import silu_mul
 
     dev = torch.device("cuda", 0)
-    N, K = 2 * a.inter, a.hidden
+    down = a.proj == "down"
+    N, K = (a.hidden, a.inter) if down else (2 * a.inter, a.hidden)
     wbytes = N * K * 2
     ring = max(2, int(a.ring_gb * 1e9 // wbytes))
     ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(ring)]
     reserve_splitk_workspace(dev, 4 * 512 * N)
+    packed = {}  # (bn, swiglu) -> ring of packed copies
+
+    def ring_of(bn, sw):
+        if (bn, sw) not in packed:
+            packed.clear()  # one packed ring at a time (HBM)
+            torch.cuda.empty_cache()
+            packed[(bn, sw)] = [pack_w4x_weight(w, bn, swiglu=sw) for w in ws]
+        return packed[(bn, sw)]
 
     def make(v, x):
         if v == "hipblaslt":
-            return lambda w: silu_mul(torch.matmul(x, w.T))
-        if v.startswith("swiglu_"):
-            bm, bn = (int(t[2:]) for t in v.split("_")[1:3])
-            return lambda w: gemm_nt_w4x_swiglu(x, w, bn=bn, bm=bm)
-        bn, s = int(v.split("_")[1][2:]), int(v.split("_")[2][1:])
-        if v.startswith("skf_"):  # split-K partials + fused reduce-and-SwiGLU
-            return lambda w: gemm_nt_w4x_splitk_swiglu(x, w, bn=bn, nslice=s)
-        return lambda w: silu_mul(gemm_nt_w4x(x, w, bn=bn, nslice=s))
+            return (lambda i: torch.matmul(x, ws[i].T)) if down else (lambda i: silu_mul(torch.matmul(x, ws[i].T)))
+        pk = v.startswith("p")
+        v = v[1:] if pk else v
+        f = v.split("_")
+        if f[0] in ("swiglu", "w4x"):
+            bm, bn = int(f[1][2:]), int(f[2][2:])
+            s = int(f[3][1:]) if len(f) > 3 else 1
+        else:
+            bm, bn, s = 256, int(f[1][2:]), int(f[2][1:])
+        sw = f[0] == "swiglu"
+        w = (lambda i: ring_of(bn, sw)[i]) if pk else (lambda i: ws[i])
+        if sw:
+            return lambda i: gemm_nt_w4x_swiglu(x, w(i), bn=bn, bm=bm)
+        if f[0] == "skf":  # split-K partials + fused reduce-and-SwiGLU
+            return lambda i: gemm_nt_w4x_splitk_swiglu(x, w(i), bn=bn, nslice=s)
+        if down:
+            return lambda i: gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm)
+        return lambda i: silu_mul(gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm))
 
     res = []
     for m in (int(t) for t in a.batches.split(",")):
         x = (torch.randn(m, K, device=dev)).bfloat16()
-        ref = silu_mul(torch.matmul(x, ws[0].T)).float()
+        ref = torch.matmul(x, ws[0].T)
+        ref = (ref if down else silu_mul(ref)).float()
         for v in a.variants.split(","):
-            fn = make(v, x)
             try:
-                got = fn(ws[0]).float()
+                fn = make(v, x)
+                got = fn(0).float()
             except Exception as e:  # a shape the variant does not take
                 print(json.dumps({"batch": m, "variant": v, "error": str(e)[:200]}), flush=True)
                 continue
             err = ((got - ref).abs().max() / ref.abs().max()).item()
             for i in range(ring):
-                fn(ws[i])
+                fn(i)
             torch.cuda.synchronize()
             ts = []
             for it in range(a.iters):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
-                fn(ws[it % ring])
+                fn(it % ring)
                 e.record()
                 e.synchronize()
                 ts.append(s.elapsed_time(e) * 1e3)

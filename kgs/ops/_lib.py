@@ -41,6 +41,7 @@ _SIGS = {
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_splitk": ([_c_void_p] * 4 + [_c_int] * 7 + [_c_void_p], _c_int),
     "kgs_gemm_bf16_nt_w4x": ([_c_void_p] * 4 + [_c_int] * 9 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_w4x_ex": ([_c_void_p] * 4 + [_c_int] * 10 + [_c_void_p], _c_int),
     "kgs_gemm_fp8_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [ctypes.c_float, _c_int, _c_int,
                                                                                      _c_void_p], _c_int),
     "kgs_gemm_fp8_nt_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 7, _c_int),
@@ -82,6 +83,7 @@ _SIGS = {
     "kgs_rope_cache_bf16": ([_c_void_p] * 6 + [_c_long, _c_int, _c_int, _c_int, _c_long, _c_int, _c_void_p, _c_int,
                                                   _c_void_p], _c_int),
     "kgs_gemm_bf16_nt_w4x_swiglu": ([_c_void_p] * 3 + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_w4x_swiglu_ex": ([_c_void_p] * 3 + [_c_int] * 9 + [_c_void_p], _c_int),
     "kgs_skinny_gemm_bf16_rope": ([_c_void_p] * 5 + [_c_int] * 3 + [_c_long, _c_long] + [_c_int] * 3 +
                                   [_c_void_p, ctypes.c_float, ctypes.c_float] + [_c_void_p] * 5 + [_c_int, _c_int,
                                                                                                   _c_void_p], _c_int),

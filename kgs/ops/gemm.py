@@ -134,18 +134,67 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
     return out
 
 
-def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1,
+W4X_BK = 64  # the four-wave kernel's K-tile (gemm_w4.h BK)
+
+
+class PackedWeight:
+    """A ``[N, K]`` bf16 weight re-laid out tile-panel major for the four-wave
+    kernel's PACKB mode (``native/kernels/gemm_w4.h``): ``[N / bn][K / 64][bn][64]``,
+    so each K-step's ``bn x 64`` B block is one contiguous run in HBM. For a
+    fused gate|up weight packed with ``swiglu=True`` each panel holds the
+    tile's gate / up 32-row groups interleaved, as the SwiGLU epilogue stages
+    them. Only valid with the ``bn`` it was packed for."""
+
+    def __init__(self, data: torch.Tensor, n: int, k: int, bn: int, swiglu: bool):
+        self.data, self.shape, self.bn, self.swiglu = data, (n, k), bn, swiglu
+
+    def __repr__(self):
+        return f"PackedWeight(shape={self.shape}, bn={self.bn}, swiglu={self.swiglu})"
+
+
+def pack_w4x_weight(w: torch.Tensor, bn: int, swiglu: bool = False) -> PackedWeight:
+    """Pack ``w [N, K]`` for :func:`gemm_nt_w4x` / :func:`gemm_nt_w4x_swiglu`
+    with ``packed=`` (see :class:`PackedWeight`). ``N % bn == 0``, ``K % 64 == 0``;
+    with ``swiglu`` the rows are ``[gate; up]`` (``N = 2I``) and ``bn % 64 == 0``."""
+    if w.dim() != 2 or w.dtype != torch.bfloat16:
+        raise ValueError("pack_w4x_weight: a 2-D bf16 weight")
+    N, K = w.shape
+    if bn not in (128, 256) or N % bn or K % W4X_BK:
+        raise ValueError(f"pack_w4x_weight: [{N}, {K}] does not tile by {bn} x {W4X_BK}")
+    if swiglu:
+        # panel tn, 32-row group g: gate rows (even g) / up rows (odd g) of the
+        # tile's bn / 2 output columns, in the order the kernel's DMA j stages them
+        i, h = N // 2, bn // 2
+        gate = w[:i].reshape(i // h, h // 32, 32, K)
+        up = w[i:].reshape(i // h, h // 32, 32, K)
+        w = torch.stack((gate, up), dim=2).reshape(N, K)
+    data = w.reshape(N // bn, bn, K // W4X_BK, W4X_BK).permute(0, 2, 1, 3).contiguous()
+    return PackedWeight(data, N, K, bn, swiglu)
+
+
+def _packed_operand(b, bn, swiglu):
+    if not isinstance(b, PackedWeight):
+        return b, b.shape, b.stride(0), 0
+    if b.bn != bn or b.swiglu != swiglu:
+        raise ValueError(f"{b!r} used with bn={bn}, swiglu={swiglu}")
+    return b.data, b.shape, b.shape[1], 1
+
+
+def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
                 out: torch.Tensor | None = None, bm: int = 256) -> torch.Tensor:
     """``a @ b.T`` on the four-wave kernel with ``bm`` x ``bn`` tiles (256 or 128
     each), any M (rows past M read as zeros), over ``nslice`` K-slices (fp32
     partials + reduce when > 1): the decode-batch GEMM path.
-    ``N % bn == 0`` and ``(K / nslice) % 128 == 0``."""
+    ``N % bn == 0`` and ``(K / nslice) % 128 == 0``. ``b`` is a ``[N, K]`` tensor
+    or a :class:`PackedWeight` packed with the same ``bn``."""
     _check_operand(a, "a")
-    _check_operand(b, "b")
+    b, bshape, ldb, packed = _packed_operand(b, bn, False)
+    if not packed:
+        _check_operand(b, "b")
     M, K = a.shape
-    N, K2 = b.shape
+    N, K2 = bshape
     if K != K2:
-        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(bshape)}")
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
     ws_ptr = None
@@ -159,9 +208,9 @@ def gemm_nt_w4x(a: torch.Tensor, b: torch.Tensor, bn: int = 256, nslice: int = 1
                 raise RuntimeError("gemm_nt_w4x: reserve_splitk_workspace() before hipGraph capture")
             ws = reserve_splitk_workspace(a.device, need)
         ws_ptr = ws.data_ptr()
-    rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws_ptr, M, N, K, a.stride(0),
-                                         b.stride(0), out.stride(0), int(bn), int(nslice), int(bm),
-                                         _lib.stream_handle(a.device))
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws_ptr, M, N, K, a.stride(0),
+                                            ldb, out.stride(0), int(bn), int(nslice), int(bm), packed,
+                                            _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return out
 
@@ -193,24 +242,27 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int,
     return ws[:need].view(nslice, M, N)
 
 
-def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor, bn: int = 128,
+def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up, bn: int = 128,
                        out: torch.Tensor | None = None, bm: int = 256) -> torch.Tensor:
     """``silu(a @ gate.T) * (a @ up.T)`` for a fused gate|up weight ``[2I, K]``
     (gate rows first) on the four-wave kernel, the SwiGLU applied in the GEMM
     epilogue: returns ``[M, I]`` (both products rounded to bf16 first, as
     ``gemm_nt`` + ``kgs.ops.transformer.silu_mul`` round them). Any M;
-    ``2I % bn == 0``, ``K % 128 == 0``."""
+    ``2I % bn == 0``, ``K % 128 == 0``. ``w_gate_up`` may be a
+    :class:`PackedWeight` from ``pack_w4x_weight(w, bn, swiglu=True)``."""
     _check_operand(a, "a")
-    _check_operand(w_gate_up, "w_gate_up")
+    w, wshape, ldb, packed = _packed_operand(w_gate_up, bn, True)
+    if not packed:
+        _check_operand(w, "w_gate_up")
     M, K = a.shape
-    N, K2 = w_gate_up.shape
+    N, K2 = wshape
     if K != K2:
-        raise ValueError(f"inner dims differ: a {tuple(a.shape)} w {tuple(w_gate_up.shape)}")
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} w {tuple(wshape)}")
     if out is None:
         out = torch.empty((M, N // 2), dtype=torch.bfloat16, device=a.device)
-    rc = _lib.lib().kgs_gemm_bf16_nt_w4x_swiglu(a.data_ptr(), w_gate_up.data_ptr(), out.data_ptr(), M, N, K,
-                                                a.stride(0), w_gate_up.stride(0), out.stride(0), int(bn), int(bm),
-                                                _lib.stream_handle(a.device))
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x_swiglu_ex(a.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K,
+                                                   a.stride(0), ldb, out.stride(0), int(bn), int(bm), packed,
+                                                   _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x_swiglu[{M}x{N}x{K} {bm}x{bn}]")
     return out
 

@@ -548,40 +548,69 @@ inline void launch_splitk_reduce(const float* P, unsigned short* C, int M, int N
 // kgs_rope_cache_bf16, which read ws directly). Requirements:
 // N % bn == 0, (K / nslice) % 128 == 0, lda/ldb/ldc % 8, 16-B aligned pointers.
 namespace {
-template <int BN, int TM>
-void launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
-                int M, int N, int ks, int lda, int ldb, int ld, int mode) {
+template <int BN, int TM, int X>
+void launch_w4x_x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
+                  int M, int N, int ks, int lda, int ldb, int ld, int mode) {
   using namespace kgs;
+  using Kn = w4::Knobs<w4::tile_m<TM>(), BN>;
+#define KGS_W4X(MD)                                                                                               \
+  hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | MD, Kn::B1, Kn::R, Kn::P, Kn::ORD, X>), grid, dim3(256), 0, s, \
+                     a, b, out, nullptr, M, N, ks, lda, ldb, ld)
   switch (mode) {
-    case 0: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 0>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
-                               ks, lda, ldb, ld); break;
-    case 1: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 1>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
-                               ks, lda, ldb, ld); break;
-    case 2: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 2>), grid, dim3(256), 0, s, a, b, out, nullptr, M, N,
-                               ks, lda, ldb, ld); break;
-    default: hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 3>), grid, dim3(256), 0, s, a, b, out, nullptr, M,
-                                N, ks, lda, ldb, ld); break;
+    case 0: KGS_W4X(0); break;
+    case 1: KGS_W4X(1); break;
+    case 2: KGS_W4X(2); break;
+    default: KGS_W4X(3); break;
   }
+#undef KGS_W4X
 }
 
+// packed: B stored tile-panel major ([N / bn][K / 64][bn][64], gemm_w4.h PACKB)
 template <int BN, int TM>
-void launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c, int M,
-                 int N, int K, int lda, int ldb, int ldc, bool aligned_m) {
+void launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
+                int M, int N, int ks, int lda, int ldb, int ld, int mode, bool packed) {
+  if (packed) launch_w4x_x<BN, TM, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+  else launch_w4x_x<BN, TM, 0>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+}
+
+template <int BN, int TM, int X>
+void launch_w4sw_x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c,
+                   int M, int N, int K, int lda, int ldb, int ldc, bool aligned_m) {
   using namespace kgs;
   constexpr int BM = w4::tile_m<TM>();
   using Kn = w4::Knobs<BM, BN>;
   if (aligned_m)
-    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM, Kn::B1, Kn::R, Kn::P, Kn::ORD, 1000000>), grid, dim3(256), 0,
-                       s, a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM, Kn::B1, Kn::R, Kn::P, Kn::ORD, X>), grid, dim3(256), 0, s, a,
+                       b, c, nullptr, M, N, K, lda, ldb, ldc);
   else
-    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 1, Kn::B1, Kn::R, Kn::P, Kn::ORD, 1000000>), grid, dim3(256),
-                       0, s, a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_NONE, BN, TM | 1, Kn::B1, Kn::R, Kn::P, Kn::ORD, X>), grid, dim3(256), 0, s,
+                       a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+}
+
+template <int BN, int TM>
+void launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c, int M,
+                 int N, int K, int lda, int ldb, int ldc, bool aligned_m, bool packed) {
+  if (packed) launch_w4sw_x<BN, TM, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+  else launch_w4sw_x<BN, TM, 1000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
 }
 }  // namespace
 
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
+                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int packed,
+                                       hipStream_t stream);
+
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
                                     int ldb, int ldc, int bn, int nslice, int bm, hipStream_t stream) {
+  return kgs_gemm_bf16_nt_w4x_ex(A, B, C, ws, M, N, K, lda, ldb, ldc, bn, nslice, bm, 0, stream);
+}
+
+// packed != 0: B is the tile-panel-major copy of a [N, K] weight
+// ([N / bn][K / 64][bn][64], kgs.ops.gemm.pack_w4x_weight) and ldb must be K
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
+                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int packed,
+                                       hipStream_t stream) {
   using namespace kgs;
+  if (packed && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
@@ -599,12 +628,13 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
   unsigned short* out = nslice > 1 ? (unsigned short*)ws : c;
   const int ld = nslice > 1 ? N : ldc;
   const int mode = (M % bm == 0 ? 0 : 1) | (nslice > 1 ? 2 : 0);
+  const bool pk = packed != 0;
   if (bm == 256) {
-    if (bn == 256) launch_w4x<256, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
-    else launch_w4x<128, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    if (bn == 256) launch_w4x<256, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
+    else launch_w4x<128, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
   } else {
-    if (bn == 256) launch_w4x<256, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
-    else launch_w4x<128, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    if (bn == 256) launch_w4x<256, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
+    else launch_w4x<128, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
   }
   if (nslice > 1 && c != nullptr) launch_splitk_reduce(ws, c, M, N, ldc, nslice, stream);
   return (int)hipGetLastError();
@@ -615,9 +645,20 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
 // both products rounded to bf16 first (the roundings of gemm + silu_mul). Any
 // M; tiles bm x bn (256 / 128 each); N % bn == 0, K % 128 == 0, lda/ldb/ldc % 8,
 // 16-B aligned pointers.
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                                              int ldb, int ldc, int bn, int bm, int packed, hipStream_t stream);
+
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C, int M, int N, int K, int lda,
                                            int ldb, int ldc, int bn, int bm, hipStream_t stream) {
+  return kgs_gemm_bf16_nt_w4x_swiglu_ex(A, B, C, M, N, K, lda, ldb, ldc, bn, bm, 0, stream);
+}
+
+// packed != 0: B is the SwiGLU-packed copy of the fused gate|up weight
+// (kgs.ops.gemm.pack_w4x_weight(..., swiglu=True)); ldb must be K
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
+                                              int ldb, int ldc, int bn, int bm, int packed, hipStream_t stream) {
   using namespace kgs;
+  if (packed && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N / 2) return KGS_ERR_SHAPE;
   if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
   if (N % bn || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
@@ -628,12 +669,13 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C
   auto c = (unsigned short*)C;
   const dim3 grid(((M + bm - 1) / bm) * (N / bn));
   const bool aligned_m = M % bm == 0;
+  const bool pk = packed != 0;
   if (bm == 256) {
-    if (bn == 256) launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
-    else launch_w4sw<128, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    if (bn == 256) launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
+    else launch_w4sw<128, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
   } else {
-    if (bn == 256) launch_w4sw<256, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
-    else launch_w4sw<128, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    if (bn == 256) launch_w4sw<256, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
+    else launch_w4sw<128, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
   }
   return (int)hipGetLastError();
 }

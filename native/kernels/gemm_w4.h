@@ -110,11 +110,16 @@ __device__ __forceinline__ void bar() {
 // K-tile starting at k0 into stage st: rows j*32 + w*8 + lane/8, 1 KiB = 8 rows
 // of 128 B. AUX: cache-policy bits of the load (0 = default; 16 = sc1). SW:
 // SwiGLU staging of B (groups alternate gate / up, see the MODE notes above).
-template <int BM, int BN, int OP, int AUX = 0, bool SW = false>
+template <int BM, int BN, int OP, int AUX = 0, bool SW = false, bool PK = false>
 __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
   using S = Shape<BM, BN>;
   char* dst = c.smem + st * S::STAGE + OP * S::OPA + (j * 4 + c.w) * 1024;
-  if constexpr (OP == 1 && SW) {
+  if constexpr (OP == 1 && PK) {
+    // packed B ([N/BN][K/BK][BN][BK], see PACKB): K-tile k0 / BK of this
+    // panel is one contiguous BN x 128 B block
+    const int so = j * c.sb32 + k0 * BN * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rb, (KGS_LDS void*)dst, 16, c.vob, so, 0, AUX);
+  } else if constexpr (OP == 1 && SW) {
     const int so = (j >> 1) * c.sb32 + k0 * 2;
     __builtin_amdgcn_raw_ptr_buffer_load_lds((j & 1) ? c.rb2 : c.rb, (KGS_LDS void*)dst, 16, c.vob, so, 0, AUX);
   } else {
@@ -126,19 +131,20 @@ __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
 
 // X: the knob bag of the kernel template (GROUP_M = X % 100, AUX = X / 100 % 100,
 // DMA window = X / 10^4 % 100, SW = X / 10^6 % 10, MAP = X / 10^7 % 10,
-// DMA operand order = X / 10^8 % 10)
+// DMA operand order = X / 10^8 % 10, packed B = X / 10^9 == 1)
 template <int BM, int BN, int X>
 __device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
   constexpr int AUX = (X / 100) % 100;
   constexpr bool SW = (X / 1000000) % 10 != 0;
   constexpr int ORDB = (X / 100000000) % 10;  // 1: the B operand's DMAs first, 2: A and B interleaved
+  constexpr bool PK = (X / 1000000000) == 1;  // B packed by K-tile (PACKB)
   constexpr int JA = BM / 32, JB = BN / 32;
   if constexpr (ORDB == 1) {
-    if (j < JB) dma<BM, BN, 1, AUX, SW>(c, st, j, k0); else dma<BM, BN, 0, AUX>(c, st, j - JB, k0);
+    if (j < JB) dma<BM, BN, 1, AUX, SW, PK>(c, st, j, k0); else dma<BM, BN, 0, AUX>(c, st, j - JB, k0);
   } else if constexpr (ORDB == 2 && JA == JB) {
-    if (j & 1) dma<BM, BN, 1, AUX, SW>(c, st, j >> 1, k0); else dma<BM, BN, 0, AUX>(c, st, j >> 1, k0);
+    if (j & 1) dma<BM, BN, 1, AUX, SW, PK>(c, st, j >> 1, k0); else dma<BM, BN, 0, AUX>(c, st, j >> 1, k0);
   } else {
-    if (j < JA) dma<BM, BN, 0, AUX>(c, st, j, k0); else dma<BM, BN, 1, AUX, SW>(c, st, j - JA, k0);
+    if (j < JA) dma<BM, BN, 0, AUX>(c, st, j, k0); else dma<BM, BN, 1, AUX, SW, PK>(c, st, j - JA, k0);
   }
 }
 
@@ -404,6 +410,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr bool SW = (X / 1000000) % 10 != 0;
   static_assert(!SW || (EPI == EPI_NONE && (MODE & 2) == 0), "SwiGLU: no bias epilogue, no split-K");
   constexpr bool BNDM = (MODE & 1) != 0, SPLITK = (MODE & 2) != 0;
+  // X digit 10^9 = 1, PACKB (round 3, decode weights): B is stored tile-panel
+  // major, [N / BN][K / BK][BN][BK], so each K-step's B block is ONE contiguous
+  // BN x 128 B run in HBM instead of BN rows 128 B each, K * 2 bytes apart. For
+  // SwiGLU the panel already holds the gate / up 32-row groups interleaved.
+  constexpr bool PACKB = (X / 1000000000) == 1;
   __shared__ __attribute__((aligned(1024))) char smem[S::LDS_BYTES];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -420,7 +431,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   c.nt = K / BK;
   const long koff = SPLITK ? (long)slice * K : 0;  // split-K: K is the slice length
   c.ra = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda + koff), 0, rows_a * lda * 2, 0x00020000);
-  if constexpr (SW) {
+  if constexpr (PACKB) {
+    // B packed by K-tile: tile column tn's panel is (ldb / BK) blocks of BN x BK
+    // (ldb = the full K), slice s starts at block s K / BK; rows 128 B apart
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb + koff * BN), 0, K * BN * 2,
+                                             0x00020000);
+  } else if constexpr (SW) {
     c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * (BN / 2) * ldb + koff), 0, (BN / 2) * ldb * 2,
                                              0x00020000);
     c.rb2 = __builtin_amdgcn_make_buffer_rsrc((void*)(B + ((long)N / 2 + (long)tn * (BN / 2)) * ldb + koff), 0,
@@ -429,12 +445,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb + koff), 0, BN * ldb * 2, 0x00020000);
   }
   c.sa32 = 32 * lda * 2;
-  c.sb32 = 32 * ldb * 2;
+  c.sb32 = 32 * (PACKB ? BK : ldb) * 2;
   {
     const int row = w * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
     c.voa = (row * lda + ch * 8) * 2;
-    c.vob = (row * ldb + ch * 8) * 2;
+    c.vob = (row * (PACKB ? BK : ldb) + ch * 8) * 2;
     const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
     c.ro0 = fr * 128 + ((fq ^ f) * 16);
     c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);

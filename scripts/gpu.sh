@@ -87,7 +87,7 @@ step() {
             -d "$O/dtrace128" -o d -- python3 -m kgs.serve bench --requests 128 --input-len 512 --output-len 32 \
             --max-batch 128 --max-model-len 2048 ;;
         gateup_probe) run gateup_probe 400 python bench/decode_gateup_probe.py --batches ${BATCHES:-128,256,512} \
-            --out "$O/gateup_probe.json" ;;
+            --proj ${PROJ:-gateup} ${VARIANTS:+--variants $VARIANTS} --out "$O/gateup_probe_${PROJ:-gateup}.json" ;;
         paged_sweep) run paged_sweep 300 python bench/paged_split_sweep.py --batches ${BATCHES:-64,128,256} \
             --ctx ${CTX:-528} --splits ${SPLITS:-1,2,4} --pipe ${PIPE:-both} ;;
         serve_b1) run serve_b1 300 python -u -m kgs.serve bench --requests 2 --input-len 512 --output-len 256 \

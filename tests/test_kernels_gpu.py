@@ -566,3 +566,32 @@ def test_gemm_splitk_swiglu_matches_gemm_then_silu_mul(M, I, K, bn, nslice):
     ref = a.float() @ w.float().T
     ref = torch.nn.functional.silu(ref[:, :I]) * ref[:, I:]
     assert _rel_err(got, ref) < 2e-2
+
+
+@pytest.mark.parametrize("M,N,K,bn,bm,nslice", [(256, 1024, 4096, 256, 256, 1), (200, 768, 1024, 128, 256, 1),
+                                                (72, 512, 1024, 128, 128, 1), (64, 1024, 2048, 256, 256, 2),
+                                                (130, 512, 3072, 128, 256, 3)])
+def test_gemm_w4x_packed_weight_is_bitwise_the_unpacked(M, N, K, bn, bm, nslice):
+    """PACKB (round 3): a weight packed tile-panel major gives the same bits as
+    the row-major weight (only the B addresses change), incl. split-K slices."""
+    from kgs.ops.gemm import gemm_nt_w4x, pack_w4x_weight
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device=DEV) * 2 - 1) * 0.05).bfloat16()
+    pw = pack_w4x_weight(w, bn)
+    got = gemm_nt_w4x(a, pw, bn=bn, nslice=nslice, bm=bm)
+    assert torch.equal(got, gemm_nt_w4x(a, w, bn=bn, nslice=nslice, bm=bm))
+    assert _rel_err(got, _ref_nt(a, w)) < 1e-2
+    with pytest.raises(ValueError):
+        gemm_nt_w4x(a, pw, bn=384 - bn, nslice=nslice, bm=bm)
+
+
+@pytest.mark.parametrize("M,I,K,bn,bm", [(256, 1024, 4096, 128, 256), (200, 768, 1024, 128, 256),
+                                         (512, 1024, 2048, 256, 256), (72, 512, 1024, 128, 128)])
+def test_gemm_w4x_swiglu_packed_weight_is_bitwise_the_unpacked(M, I, K, bn, bm):
+    from kgs.ops.gemm import gemm_nt_w4x_swiglu, pack_w4x_weight
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * K ** -0.5).bfloat16()
+    got = gemm_nt_w4x_swiglu(a, pack_w4x_weight(w, bn, swiglu=True), bn=bn, bm=bm)
+    assert torch.equal(got, gemm_nt_w4x_swiglu(a, w, bn=bn, bm=bm))
