@@ -227,6 +227,12 @@ def w4x_route(m: int, n: int, k: int):
     return W4X_TUNED.get((b, n, k))
 
 
+def w4x_split_bns(n: int, k: int) -> set:
+    """Tile widths the split-K four-wave routes use for an ``[n, k]`` weight
+    (the bn a tile-panel copy must be packed with)."""
+    return {r[0] for (_, rn, rk), r in W4X_TUNED.items() if (rn, rk) == (n, k) and r[1] > 1}
+
+
 def splitk_slices(m: int, n: int, k: int) -> int | None:
     """K slices for a decode GEMM of batch m (bucketed to a power of two), or
     None when the split-K kernel is not the measured winner."""

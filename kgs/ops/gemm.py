@@ -137,7 +137,7 @@ def gemm_nt_splitk(a: torch.Tensor, b: torch.Tensor, nslice: int, out: torch.Ten
 W4X_BK = 64  # the four-wave kernel's K-tile (gemm_w4.h BK)
 
 
-class PackedWeight:
+class PanelWeight:
     """A ``[N, K]`` bf16 weight re-laid out tile-panel major for the four-wave
     kernel's PACKB mode (``native/kernels/gemm_w4.h``): ``[N / bn][K / 64][bn][64]``,
     so each K-step's ``bn x 64`` B block is one contiguous run in HBM. For a
@@ -149,12 +149,12 @@ class PackedWeight:
         self.data, self.shape, self.bn, self.swiglu = data, (n, k), bn, swiglu
 
     def __repr__(self):
-        return f"PackedWeight(shape={self.shape}, bn={self.bn}, swiglu={self.swiglu})"
+        return f"PanelWeight(shape={self.shape}, bn={self.bn}, swiglu={self.swiglu})"
 
 
-def pack_w4x_weight(w: torch.Tensor, bn: int, swiglu: bool = False) -> PackedWeight:
+def pack_w4x_weight(w: torch.Tensor, bn: int, swiglu: bool = False) -> PanelWeight:
     """Pack ``w [N, K]`` for :func:`gemm_nt_w4x` / :func:`gemm_nt_w4x_swiglu`
-    with ``packed=`` (see :class:`PackedWeight`). ``N % bn == 0``, ``K % 64 == 0``;
+    with ``packed=`` (see :class:`PanelWeight`). ``N % bn == 0``, ``K % 64 == 0``;
     with ``swiglu`` the rows are ``[gate; up]`` (``N = 2I``) and ``bn % 64 == 0``."""
     if w.dim() != 2 or w.dtype != torch.bfloat16:
         raise ValueError("pack_w4x_weight: a 2-D bf16 weight")
@@ -169,11 +169,11 @@ def pack_w4x_weight(w: torch.Tensor, bn: int, swiglu: bool = False) -> PackedWei
         up = w[i:].reshape(i // h, h // 32, 32, K)
         w = torch.stack((gate, up), dim=2).reshape(N, K)
     data = w.reshape(N // bn, bn, K // W4X_BK, W4X_BK).permute(0, 2, 1, 3).contiguous()
-    return PackedWeight(data, N, K, bn, swiglu)
+    return PanelWeight(data, N, K, bn, swiglu)
 
 
 def _packed_operand(b, bn, swiglu):
-    if not isinstance(b, PackedWeight):
+    if not isinstance(b, PanelWeight):
         return b, b.shape, b.stride(0), 0
     if b.bn != bn or b.swiglu != swiglu:
         raise ValueError(f"{b!r} used with bn={bn}, swiglu={swiglu}")
@@ -186,7 +186,7 @@ def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
     each), any M (rows past M read as zeros), over ``nslice`` K-slices (fp32
     partials + reduce when > 1): the decode-batch GEMM path.
     ``N % bn == 0`` and ``(K / nslice) % 128 == 0``. ``b`` is a ``[N, K]`` tensor
-    or a :class:`PackedWeight` packed with the same ``bn``."""
+    or a :class:`PanelWeight` packed with the same ``bn``."""
     _check_operand(a, "a")
     b, bshape, ldb, packed = _packed_operand(b, bn, False)
     if not packed:
@@ -215,7 +215,7 @@ def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
     return out
 
 
-def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int, bm: int = 256) -> torch.Tensor:
+def gemm_nt_w4x_partials(a: torch.Tensor, b, bn: int, nslice: int, bm: int = 256) -> torch.Tensor:
     """The split-K four-wave GEMM WITHOUT its reduce: returns the fp32 partial
     products ``[nslice, M, N]`` (a view of the per-GPU split-K workspace, valid
     until the next split-K call on the stream) for a fused consumer --
@@ -223,11 +223,13 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int,
     if nslice < 2:
         raise ValueError("partials need nslice >= 2")
     _check_operand(a, "a")
-    _check_operand(b, "b")
+    b, bshape, ldb, packed = _packed_operand(b, bn, False)
+    if not packed:
+        _check_operand(b, "b")
     M, K = a.shape
-    N, K2 = b.shape
+    N, K2 = bshape
     if K != K2:
-        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(b.shape)}")
+        raise ValueError(f"inner dims differ: a {tuple(a.shape)} b {tuple(bshape)}")
     from .decode import device_key
 
     need = nslice * M * N
@@ -236,8 +238,9 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b: torch.Tensor, bn: int, nslice: int,
         if torch.cuda.is_current_stream_capturing():
             raise RuntimeError("gemm_nt_w4x_partials: reserve_splitk_workspace() before hipGraph capture")
         ws = reserve_splitk_workspace(a.device, need)
-    rc = _lib.lib().kgs_gemm_bf16_nt_w4x(a.data_ptr(), b.data_ptr(), None, ws.data_ptr(), M, N, K, a.stride(0),
-                                         b.stride(0), N, int(bn), int(nslice), int(bm), _lib.stream_handle(a.device))
+    rc = _lib.lib().kgs_gemm_bf16_nt_w4x_ex(a.data_ptr(), b.data_ptr(), None, ws.data_ptr(), M, N, K, a.stride(0),
+                                            ldb, N, int(bn), int(nslice), int(bm), packed,
+                                            _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x_partials[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return ws[:need].view(nslice, M, N)
 
@@ -249,7 +252,7 @@ def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up, bn: int = 128,
     epilogue: returns ``[M, I]`` (both products rounded to bf16 first, as
     ``gemm_nt`` + ``kgs.ops.transformer.silu_mul`` round them). Any M;
     ``2I % bn == 0``, ``K % 128 == 0``. ``w_gate_up`` may be a
-    :class:`PackedWeight` from ``pack_w4x_weight(w, bn, swiglu=True)``."""
+    :class:`PanelWeight` from ``pack_w4x_weight(w, bn, swiglu=True)``."""
     _check_operand(a, "a")
     w, wshape, ldb, packed = _packed_operand(w_gate_up, bn, True)
     if not packed:

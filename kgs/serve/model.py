@@ -93,6 +93,18 @@ class ServingModel:
                             "down": D.PackedWeight(lw["down"], fp8=f8)} for i, lw in enumerate(self.w)]
             self.packed_lm = D.PackedWeight(self.w_lm, fold=self.norm, fp8=f8)
             D.reserve_workspace(self.device)
+        # split-K decode projections (qkv, o, down from batch 64 up, kgs.ops.decode
+        # W4X_TUNED) read a third copy laid out tile-panel major, so each K-step's
+        # weight block is one contiguous HBM run (PACKB): 5-6 % off the down
+        # projection at batch 128/256 (profiles/r3/decode/README.md). 6.4 GB for
+        # Llama-3-8B; kept only with the other decode copies
+        self.w4x_panels = None
+        if self.fuse_splitk and packed_decode:
+            from kgs.ops.gemm import pack_w4x_weight
+
+            bns = {n: D.w4x_split_bns(*self.w[0][n].shape) for n in ("qkv", "o", "down")}
+            self.w4x_panels = [{(n, bn): pack_w4x_weight(lw[n], bn) for n in bns for bn in bns[n]}
+                               for lw in self.w]
         if prefill_weights not in ("bf16", "fp8"):
             raise ValueError(f"prefill_weights must be bf16 or fp8, got {prefill_weights!r}")
         self.prefill_f8 = None
@@ -159,6 +171,15 @@ class ServingModel:
         if name in ("o", "down") and self.cfg.hidden % 2048:
             return None
         return r
+
+    def _w4x_weight(self, layer: int, name: str, bn: int):
+        """The weight a split-K four-wave projection reads: its tile-panel
+        copy when there is one for ``bn``, else the row-major weight."""
+        if self.w4x_panels is not None:
+            p = self.w4x_panels[layer].get((name, bn))
+            if p is not None:
+                return p
+        return self.w[layer][name]
 
     def _swiglu_route(self, m: int):
         """(bn, 1) when the decode gate|up projection runs unsplit on the
@@ -400,7 +421,7 @@ class ServingModel:
             from kgs.ops.transformer import splitk_add_rmsnorm
         for i in range(c.layers):
             if rq:
-                part = gemm_nt_w4x_partials(y, self.w[i]["qkv"], *rq)
+                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)
                 qkv = torch.empty((m, part.shape[2]), dtype=torch.bfloat16, device=x.device)
                 D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(i), c.heads, c.kv_heads,
                               partials=part)
@@ -414,7 +435,8 @@ class ServingModel:
                 a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                              pages_per_split=pages_per_split)
             if ro:
-                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self.w[i]["o"], *ro), x, self.ln2[i], c.eps)
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self._w4x_weight(i, "o", ro[0]), *ro), x, self.ln2[i],
+                                       c.eps)
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
             if rg:
@@ -423,7 +445,8 @@ class ServingModel:
                 act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             if rd:
-                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self.w[i]["down"], *rd), x, nxt, c.eps)
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self._w4x_weight(i, "down", rd[0]), *rd), x, nxt,
+                                       c.eps)
             else:
                 y = self._norm(x, self._proj(act, i, "down", True), nxt)
         return self._proj(y, None, "lm", True)
