@@ -46,7 +46,7 @@ def run_engine(a) -> dict:
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
                       packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights,
-                      fuse_splitk=not a.no_fuse_splitk)
+                      fuse_splitk=not a.no_fuse_splitk, w4x_panels=not a.no_w4x_panels)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -76,7 +76,7 @@ def run_engine(a) -> dict:
         "max_batch": a.max_batch, "layers": a.layers, "num_pages": eng.num_pages, "cuda_graphs": not a.no_graphs,
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "kv_cache_dtype": a.kv_cache_dtype, "prefill_weights": a.prefill_weights,
-        "fuse_splitk": not a.no_fuse_splitk,
+        "fuse_splitk": not a.no_fuse_splitk, "w4x_panels": not a.no_w4x_panels,
         "chunked_prefill": a.chunked_prefill,
         "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
         "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
@@ -211,6 +211,8 @@ def main(argv=None) -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-fuse-splitk", action="store_true",
                     help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
+    ap.add_argument("--no-w4x-panels", action="store_true",
+                    help="split-K decode projections read the row-major weights (A/B against the panel copies)")
     ap.add_argument("--fused-max-batch", type=int, default=48,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",

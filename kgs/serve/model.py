@@ -49,7 +49,7 @@ class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 48,
                  decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True,
-                 prefill_weights: str = "bf16", fuse_splitk: bool = True):
+                 prefill_weights: str = "bf16", fuse_splitk: bool = True, w4x_panels: bool = True):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -99,7 +99,7 @@ class ServingModel:
         # projection at batch 128/256 (profiles/r3/decode/README.md). 6.4 GB for
         # Llama-3-8B; kept only with the other decode copies
         self.w4x_panels = None
-        if self.fuse_splitk and packed_decode:
+        if self.fuse_splitk and packed_decode and w4x_panels:
             from kgs.ops.gemm import pack_w4x_weight
 
             bns = {n: D.w4x_split_bns(*self.w[0][n].shape) for n in ("qkv", "o", "down")}

@@ -144,6 +144,12 @@ step() {
                 run serve_b256_kv8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 &&
                 run serve_b256_f8 300 $SB --requests 256 --max-batch 256 --kv-cache-dtype fp8 --prefill-weights fp8 &&
                 run serve_b512_f8 300 $SB --requests 512 --max-batch 512 --kv-cache-dtype fp8 --prefill-weights fp8 ;;
+        panels_ab)  # tile-panel decode weights on / off, batch 128 and 256
+            local SB="python -u -m kgs.serve bench --input-len 512 --output-len 256 --max-model-len 2048"
+            run serve_b128_panels 300 $SB --requests 128 --max-batch 128 &&
+                run serve_b128_rowmajor 300 $SB --requests 128 --max-batch 128 --no-w4x-panels &&
+                run serve_b256_panels 300 $SB --requests 256 --max-batch 256 &&
+                run serve_b256_rowmajor 300 $SB --requests 256 --max-batch 256 --no-w4x-panels ;;
         online_sweep)
             local OB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 --max-batch 256"
             OB="$OB --max-model-len 2048 --chunked-prefill 2048"
