@@ -130,7 +130,7 @@ step() {
             --variants ${VARIANTS:-fast,gn4,gn8,gn2} --rounds 7 --out "$O/fp8_tall.json" ;;
         gemm_llm) run gemm_llm 600 python bench/gemm_sweep.py \
             --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \
-            --variants fast --rounds 7 --out "$O/gemm_llm.json" ;;
+            --variants ${VARIANTS:-fast} --rounds 7 --out "$O/gemm_llm.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
             --shapes ${SHAPES:-qkv,o,gate_up,down} --out "$O/w4x_sweep.jsonl" ;;
