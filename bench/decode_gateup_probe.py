@@ -11,6 +11,7 @@ the weight-streaming floor):
   hipblaslt           torch.matmul + silu_mul
   p<any of the above> the same on weights packed tile-panel major
                       (kgs.ops.gemm.pack_w4x_weight, PACKB), e.g. pswiglu_bm256_bn128
+A ``_tT`` suffix runs the four-wave kernel with T LDS stages (3 or 4).
 With ``--proj down`` (x [M, 14336] . W [4096, 14336]^T, no SwiGLU) the
 candidates are w4x_bmXXX_bnYYY[_sS], pw4x_... and hipblaslt.
 One JSON line per (batch, variant): median us, weight GB/s, max rel err vs
@@ -66,20 +67,21 @@ def main():
         pk = v.startswith("p")
         v = v[1:] if pk else v
         f = v.split("_")
+        opt = {t[0]: int(t[1:]) for t in f[1:] if t[0] in "st"}  # sS: K slices, tT: LDS stages
+        s, st = opt.get("s", 1), opt.get("t", 2)
         if f[0] in ("swiglu", "w4x"):
             bm, bn = int(f[1][2:]), int(f[2][2:])
-            s = int(f[3][1:]) if len(f) > 3 else 1
         else:
-            bm, bn, s = 256, int(f[1][2:]), int(f[2][1:])
+            bm, bn = 256, int(f[1][2:])
         sw = f[0] == "swiglu"
         w = (lambda i: ring_of(bn, sw)[i]) if pk else (lambda i: ws[i])
         if sw:
-            return lambda i: gemm_nt_w4x_swiglu(x, w(i), bn=bn, bm=bm)
+            return lambda i: gemm_nt_w4x_swiglu(x, w(i), bn=bn, bm=bm, stages=st)
         if f[0] == "skf":  # split-K partials + fused reduce-and-SwiGLU
             return lambda i: gemm_nt_w4x_splitk_swiglu(x, w(i), bn=bn, nslice=s)
         if down:
-            return lambda i: gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm)
-        return lambda i: silu_mul(gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm))
+            return lambda i: gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm, stages=st)
+        return lambda i: silu_mul(gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm, stages=st))
 
     res = []
     for m in (int(t) for t in a.batches.split(",")):

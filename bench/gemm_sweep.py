@@ -28,13 +28,14 @@ def _gemm(v):
 
     if v in VARIANTS:
         return lambda A, B, out: gemm_nt(A, B, out=out, variant=v)
-    if v.startswith("w4x_"):  # w4x_bmX_bnY[_sS]: the four-wave kernel, X x Y tiles, S K-slices
+    if v.startswith("w4x_"):  # w4x_bmX_bnY[_sS][_tT]: four-wave kernel, X x Y tiles, S K-slices, T stages
         from kgs.ops.gemm import gemm_nt_w4x
 
         f = v.split("_")
         bm, bn = int(f[1][2:]), int(f[2][2:])
-        s = int(f[3][1:]) if len(f) > 3 else 1
-        return lambda A, B, out: gemm_nt_w4x(A, B, bn=bn, nslice=s, out=out, bm=bm)
+        opt = {t[0]: int(t[1:]) for t in f[3:]}  # sS: K slices, tT: LDS stages
+        s, st = opt.get("s", 1), opt.get("t", 2)
+        return lambda A, B, out: gemm_nt_w4x(A, B, bn=bn, nslice=s, out=out, bm=bm, stages=st)
     return lambda A, B, out: experiments.gemm_nt(A, B, v, out=out, allow_wrong=True)
 
 

@@ -565,12 +565,38 @@ void launch_w4x_x(dim3 grid, hipStream_t s, const unsigned short* a, const unsig
 #undef KGS_W4X
 }
 
-// packed: B stored tile-panel major ([N / bn][K / 64][bn][64], gemm_w4.h PACKB)
+// LDS stages of the w4x entries: flags bits 4-5 = stages - 2 (gemm_w4.h
+// stages<MODE>), only where NS stages fit in 160 KiB
+constexpr bool stages_fit(int bm, int bn, int ns) { return ns * (bm + bn) * 128 <= 160 * 1024; }
+
+// flags bit 0 (packed): B stored tile-panel major ([N / bn][K / 64][bn][64],
+// gemm_w4.h PACKB); bits 4-5: extra LDS stages
 template <int BN, int TM>
-void launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
-                int M, int N, int ks, int lda, int ldb, int ld, int mode, bool packed) {
-  if (packed) launch_w4x_x<BN, TM, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
-  else launch_w4x_x<BN, TM, 0>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+int launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* out,
+               int M, int N, int ks, int lda, int ldb, int ld, int mode, int flags) {
+  constexpr int BM = kgs::w4::tile_m<TM>();
+  const bool packed = flags & 1;
+  switch (flags & 0x30) {
+    case 0x00:
+      if (packed) launch_w4x_x<BN, TM, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+      else launch_w4x_x<BN, TM, 0>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+      return 0;
+    case 0x10:
+      if constexpr (stages_fit(BM, BN, 3)) {
+        if (packed) launch_w4x_x<BN, TM | 0x10, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+        else launch_w4x_x<BN, TM | 0x10, 0>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+        return 0;
+      }
+      break;
+    case 0x20:
+      if constexpr (stages_fit(BM, BN, 4)) {
+        if (packed) launch_w4x_x<BN, TM | 0x20, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+        else launch_w4x_x<BN, TM | 0x20, 0>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+        return 0;
+      }
+      break;
+  }
+  return KGS_ERR_ARG;
 }
 
 template <int BN, int TM, int X>
@@ -588,15 +614,36 @@ void launch_w4sw_x(dim3 grid, hipStream_t s, const unsigned short* a, const unsi
 }
 
 template <int BN, int TM>
-void launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c, int M,
-                 int N, int K, int lda, int ldb, int ldc, bool aligned_m, bool packed) {
-  if (packed) launch_w4sw_x<BN, TM, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
-  else launch_w4sw_x<BN, TM, 1000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+int launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c, int M,
+                int N, int K, int lda, int ldb, int ldc, bool aligned_m, int flags) {
+  constexpr int BM = kgs::w4::tile_m<TM>();
+  const bool packed = flags & 1;
+  switch (flags & 0x30) {
+    case 0x00:
+      if (packed) launch_w4sw_x<BN, TM, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+      else launch_w4sw_x<BN, TM, 1000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+      return 0;
+    case 0x10:
+      if constexpr (stages_fit(BM, BN, 3)) {
+        if (packed) launch_w4sw_x<BN, TM | 0x10, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+        else launch_w4sw_x<BN, TM | 0x10, 1000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+        return 0;
+      }
+      break;
+    case 0x20:
+      if constexpr (stages_fit(BM, BN, 4)) {
+        if (packed) launch_w4sw_x<BN, TM | 0x20, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+        else launch_w4sw_x<BN, TM | 0x20, 1000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+        return 0;
+      }
+      break;
+  }
+  return KGS_ERR_ARG;
 }
 }  // namespace
 
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
-                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int packed,
+                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int flags,
                                        hipStream_t stream);
 
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float* ws, int M, int N, int K, int lda,
@@ -604,13 +651,15 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
   return kgs_gemm_bf16_nt_w4x_ex(A, B, C, ws, M, N, K, lda, ldb, ldc, bn, nslice, bm, 0, stream);
 }
 
-// packed != 0: B is the tile-panel-major copy of a [N, K] weight
-// ([N / bn][K / 64][bn][64], kgs.ops.gemm.pack_w4x_weight) and ldb must be K
+// flags bit 0: B is the tile-panel-major copy of a [N, K] weight
+// ([N / bn][K / 64][bn][64], kgs.ops.gemm.pack_w4x_weight) and ldb must be K;
+// bits 4-5: LDS stages - 2 (0..2, where they fit in 160 KiB)
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
-                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int packed,
+                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int flags,
                                        hipStream_t stream) {
   using namespace kgs;
-  if (packed && ldb != K) return KGS_ERR_SHAPE;
+  if (flags & ~0x31 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
+  if ((flags & 1) && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
   if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
@@ -628,14 +677,15 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
   unsigned short* out = nslice > 1 ? (unsigned short*)ws : c;
   const int ld = nslice > 1 ? N : ldc;
   const int mode = (M % bm == 0 ? 0 : 1) | (nslice > 1 ? 2 : 0);
-  const bool pk = packed != 0;
+  int rc;
   if (bm == 256) {
-    if (bn == 256) launch_w4x<256, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
-    else launch_w4x<128, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
+    if (bn == 256) rc = launch_w4x<256, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, flags);
+    else rc = launch_w4x<128, 0>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, flags);
   } else {
-    if (bn == 256) launch_w4x<256, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
-    else launch_w4x<128, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, pk);
+    if (bn == 256) rc = launch_w4x<256, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, flags);
+    else rc = launch_w4x<128, 8>(grid, stream, a, b, out, M, N, ks, lda, ldb, ld, mode, flags);
   }
+  if (rc) return rc;
   if (nslice > 1 && c != nullptr) launch_splitk_reduce(ws, c, M, N, ldc, nslice, stream);
   return (int)hipGetLastError();
 }
@@ -646,19 +696,21 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
 // M; tiles bm x bn (256 / 128 each); N % bn == 0, K % 128 == 0, lda/ldb/ldc % 8,
 // 16-B aligned pointers.
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
-                                              int ldb, int ldc, int bn, int bm, int packed, hipStream_t stream);
+                                              int ldb, int ldc, int bn, int bm, int flags, hipStream_t stream);
 
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C, int M, int N, int K, int lda,
                                            int ldb, int ldc, int bn, int bm, hipStream_t stream) {
   return kgs_gemm_bf16_nt_w4x_swiglu_ex(A, B, C, M, N, K, lda, ldb, ldc, bn, bm, 0, stream);
 }
 
-// packed != 0: B is the SwiGLU-packed copy of the fused gate|up weight
-// (kgs.ops.gemm.pack_w4x_weight(..., swiglu=True)); ldb must be K
+// flags bit 0: B is the SwiGLU-packed copy of the fused gate|up weight
+// (kgs.ops.gemm.pack_w4x_weight(..., swiglu=True)), ldb must be K; bits 4-5:
+// LDS stages - 2 (as kgs_gemm_bf16_nt_w4x_ex)
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
-                                              int ldb, int ldc, int bn, int bm, int packed, hipStream_t stream) {
+                                              int ldb, int ldc, int bn, int bm, int flags, hipStream_t stream) {
   using namespace kgs;
-  if (packed && ldb != K) return KGS_ERR_SHAPE;
+  if (flags & ~0x31 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
+  if ((flags & 1) && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N / 2) return KGS_ERR_SHAPE;
   if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;
   if (N % bn || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
@@ -669,14 +721,15 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void
   auto c = (unsigned short*)C;
   const dim3 grid(((M + bm - 1) / bm) * (N / bn));
   const bool aligned_m = M % bm == 0;
-  const bool pk = packed != 0;
+  int rc;
   if (bm == 256) {
-    if (bn == 256) launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
-    else launch_w4sw<128, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
+    if (bn == 256) rc = launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, flags);
+    else rc = launch_w4sw<128, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, flags);
   } else {
-    if (bn == 256) launch_w4sw<256, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
-    else launch_w4sw<128, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, pk);
+    if (bn == 256) rc = launch_w4sw<256, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, flags);
+    else rc = launch_w4sw<128, 8>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, flags);
   }
+  if (rc) return rc;
   return (int)hipGetLastError();
 }
 

@@ -229,6 +229,10 @@ template <int N>
 __device__ __forceinline__ void wait_vm() {
   if constexpr (N == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
   else if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if constexpr (N == 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+  else if constexpr (N == 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else if constexpr (N == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
   else {
     static_assert(N == 8, "unsupported vmcnt");
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -239,9 +243,9 @@ __device__ __forceinline__ void wait_vm() {
 //   k < NR              ds_read f1 (k-sub 1 of this K-tile) read k
 //   k == B1 - 1         lgkmcnt(0) + barrier 1 (stage ST free)
 //   k in [B1, KM - R)   the ND LDS-DMA issues of K-tile t+2, evenly spread
-//   k == KM - R - 1     vmcnt(ND) + barrier 2 (K-tile t+1 visible)
+//   k == KM - R - 1     vmcnt((NS - 1) ND) + barrier 2 (K-tile t+1 visible)
 //   k >= KM - R         P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
-template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int K>
+template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int NS, int K>
 __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM / 32, BN / 32>& f0,
                                       Frag<BM / 32, BN / 32>& f1, f32x4 (&acc)[BM / 32][BN / 32]) {
   using S = Shape<BM, BN>;
@@ -275,18 +279,18 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM 
       bar();
     }
     if constexpr (K == KM - R - 1) {
-      // own DMA of K-tile t+1 landed (the ND issued after it belong to t+2)
-      wait_vm<ND>();
+      // own DMA of K-tile t+1 landed (the (NS - 1) ND issued after it belong to t+2 .. t+NS)
+      wait_vm<(NS - 1) * ND>();
       bar();
     }
-    kbody<BM, BN, ST, B1, R, P, ORD, X, K + 1>(c, sp, f0, f1, acc);
+    kbody<BM, BN, ST, B1, R, P, ORD, X, NS, K + 1>(c, sp, f0, f1, acc);
   }
 }
 
 // One K-step: a single pinned sequence of KM MFMAs (the first half on f0 = k-sub 0,
 // the second on f1 = k-sub 1) with the reads, DMA issues and the two barriers
 // placed between them (kbody).
-template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X>
+template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int NS = 2>
 __device__ __forceinline__ void kstep(const Ctx& c, Frag<BM / 32, BN / 32>& f0, Frag<BM / 32, BN / 32>& f1,
                                       f32x4 (&acc)[BM / 32][BN / 32], int t) {
   using S = Shape<BM, BN>;
@@ -294,12 +298,12 @@ __device__ __forceinline__ void kstep(const Ctx& c, Frag<BM / 32, BN / 32>& f0, 
   StepPtrs sp;
   sp.pa1 = abase<BM, BN, 1>(c, ST);
   sp.pb1 = bbase<BM, BN, 1>(c, ST);
-  sp.pa0 = abase<BM, BN, 0>(c, ST ^ 1);
-  sp.pb0 = bbase<BM, BN, 0>(c, ST ^ 1);
-  int tl = t + 2;
+  sp.pa0 = abase<BM, BN, 0>(c, (ST + 1) % NS);
+  sp.pb0 = bbase<BM, BN, 0>(c, (ST + 1) % NS);
+  int tl = t + NS;
   tl = tl < c.nt ? tl : c.nt - 1;  // past the end: harmless re-load into the free stage
   sp.k0 = tl * BK;
-  kbody<BM, BN, ST, B1, R, P, ORD, X, 0>(c, sp, f0, f1, acc);
+  kbody<BM, BN, ST, B1, R, P, ORD, X, NS, 0>(c, sp, f0, f1, acc);
 }
 
 // Production knobs per tile shape: barrier 1 after MFMA B1, R MFMAs after
@@ -325,6 +329,13 @@ struct Knobs<128, 128> {
 
 template <int MODE>
 constexpr int tile_m() { return (MODE & 8) ? 128 : 256; }
+
+// MODE bits 4-5: LDS stages - 2 (round 3, decode GEMMs). With NS stages the
+// DMAs of K-tile t + NS are issued during K-step t, so NS - 1 K-tiles are in
+// flight while one is consumed: for the short-M, weight-streaming shapes the
+// K-step is bound by load latency, not by the MFMAs.
+template <int MODE>
+constexpr int stages() { return 2 + ((MODE >> 4) & 3); }
 
 // XCD-blocked tile map (X digit 10^7 = MAP, round 3). The default map
 // (xcd_remap + GROUP_M) gives XCD x a contiguous run of tile ids; with groups
@@ -415,7 +426,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // BN x 128 B run in HBM instead of BN rows 128 B each, K * 2 bytes apart. For
   // SwiGLU the panel already holds the gate / up 32-row groups interleaved.
   constexpr bool PACKB = (X / 1000000000) == 1;
-  __shared__ __attribute__((aligned(1024))) char smem[S::LDS_BYTES];
+  constexpr int NS = stages<MODE>();
+  static_assert(NS * S::STAGE <= 160 * 1024, "LDS stages exceed 160 KiB");
+  __shared__ __attribute__((aligned(1024))) char smem[NS * S::STAGE];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntm = BNDM ? (M + BM - 1) / BM : M / BM, ntn = N / BN;
@@ -462,13 +475,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
     for (int n = 0; n < NB; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: K-tiles 0 and 1 into stages 0 and 1, k-sub 0 of K-tile 0 into f0
+  // prologue: K-tiles 0 .. NS-1 into stages 0 .. NS-1, k-sub 0 of K-tile 0 into f0
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BM, BN, X>(c, 0, j, 0);
-  const int k1 = (c.nt > 1 ? 1 : 0) * BK;
+  for (int st = 0; st < NS; ++st) {
+    const int kt = (st < c.nt ? st : c.nt - 1) * BK;
 #pragma unroll
-  for (int j = 0; j < ND; ++j) dma_any<BM, BN, X>(c, 1, j, k1);
-  wait_vm<ND>();
+    for (int j = 0; j < ND; ++j) dma_any<BM, BN, X>(c, st, j, kt);
+  }
+  wait_vm<(NS - 1) * ND>();
   bar();
   Frag<MA, NB> f0, f1;
   {
@@ -484,9 +498,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // the preheader's scalar loads into the loop header and waits lgkmcnt(0) there
   __builtin_amdgcn_s_waitcnt(0xc07f);
 
-  for (int t = 0; t < c.nt; t += 2) {
-    kstep<BM, BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
-    kstep<BM, BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
+  if constexpr (NS == 2) {
+    for (int t = 0; t < c.nt; t += 2) {
+      kstep<BM, BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
+      kstep<BM, BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
+    }
+  } else {
+    // K-tile t lives in stage t % NS; the tail steps of a partial round are
+    // skipped uniformly by the whole workgroup
+    for (int t = 0; t < c.nt; t += NS) {
+      kstep<BM, BN, 0, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t);
+      if (t + 1 < c.nt) kstep<BM, BN, 1, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 1);
+      if (t + 2 < c.nt) kstep<BM, BN, 2 % NS, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 2);
+      if constexpr (NS == 4)
+        if (t + 3 < c.nt) kstep<BM, BN, 3, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 3);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read hazard

@@ -595,3 +595,39 @@ def test_gemm_w4x_swiglu_packed_weight_is_bitwise_the_unpacked(M, I, K, bn, bm):
     w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * K ** -0.5).bfloat16()
     got = gemm_nt_w4x_swiglu(a, pack_w4x_weight(w, bn, swiglu=True), bn=bn, bm=bm)
     assert torch.equal(got, gemm_nt_w4x_swiglu(a, w, bn=bn, bm=bm))
+
+
+@pytest.mark.parametrize("M,N,K,bn,bm,nslice,stages", [
+    (256, 1024, 640, 128, 256, 1, 3), (200, 768, 1024, 128, 256, 2, 3), (72, 512, 1152, 128, 128, 1, 4),
+    (128, 1024, 2048, 128, 128, 4, 4), (130, 512, 1152, 256, 128, 1, 3), (256, 512, 768, 128, 128, 3, 3)])
+def test_gemm_w4x_lds_stages_are_bitwise_two_stage(M, N, K, bn, bm, nslice, stages):
+    """3 / 4 LDS stages (more K-tiles in flight) change only when tiles are
+    loaded: bitwise the two-stage result, incl. K-tile counts that are not a
+    multiple of the stage count, split-K and packed weights."""
+    from kgs.ops.gemm import gemm_nt_w4x, pack_w4x_weight
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(N, K, device=DEV) * 2 - 1) * 0.05).bfloat16()
+    want = gemm_nt_w4x(a, w, bn=bn, nslice=nslice, bm=bm)
+    assert torch.equal(gemm_nt_w4x(a, w, bn=bn, nslice=nslice, bm=bm, stages=stages), want)
+    pw = pack_w4x_weight(w, bn)
+    assert torch.equal(gemm_nt_w4x(a, pw, bn=bn, nslice=nslice, bm=bm, stages=stages), want)
+    assert _rel_err(want, _ref_nt(a, w)) < 1e-2
+
+
+@pytest.mark.parametrize("M,I,K,bn,bm,stages", [(256, 1024, 640, 128, 256, 3), (72, 512, 1024, 128, 128, 4),
+                                                (200, 768, 1152, 128, 128, 3)])
+def test_gemm_w4x_swiglu_lds_stages_are_bitwise_two_stage(M, I, K, bn, bm, stages):
+    from kgs.ops.gemm import gemm_nt_w4x_swiglu
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV) * 2 - 1) * K ** -0.5).bfloat16()
+    assert torch.equal(gemm_nt_w4x_swiglu(a, w, bn=bn, bm=bm, stages=stages), gemm_nt_w4x_swiglu(a, w, bn=bn, bm=bm))
+
+
+def test_gemm_w4x_stages_that_do_not_fit_are_refused():
+    from kgs.ops.gemm import gemm_nt_w4x
+
+    a = torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        gemm_nt_w4x(a, a, bn=256, bm=256, stages=3)  # 3 x 64 KiB > 160 KiB
