@@ -223,9 +223,17 @@ KGS_EXPORT int kgs_gemm_bf16_nt_bounded_ok(const void* A, const void* B, const v
   return 1;
 }
 
+KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
+                                       int lda, int ldb, int ldc, int bn, int nslice, int bm, int flags,
+                                       hipStream_t stream);
+
 // variant: 0 = auto, 1 = force the 256x256 8-wave ping-pong, 2 = force generic,
-//          3 = force the four-wave kernel, 16 = force the bounded 256x256
-//          pipeline. Anything else is rejected.
+//          3 = force the four-wave kernel (256x256 tiles), 16 = force the
+//          bounded 256x256 pipeline. Anything else is rejected.
+// Auto on a grid of at most 128 256x256 tiles (half the CUs or fewer) runs the
+// four-wave kernel on smaller tiles: 256x128 / 128x256 up to 128 tiles, 128x128
+// up to 64 -- 1.13-1.23x hipBLASLt there, where 256x256 tiles leave CUs idle
+// (profiles/r3/gemm_small_grid.json).
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                 int ldb, int ldc, int epi, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;
@@ -243,6 +251,15 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;
   else return KGS_ERR_ARG;
+  if (variant == 0 && v == 3 && epi == kgs::EPI_NONE) {
+    const long tiles = (long)(M / 256) * (N / 256);
+    if (tiles <= 64) return kgs_gemm_bf16_nt_w4x_ex(A, B, C, nullptr, M, N, K, lda, ldb, ldc, 128, 1, 128, 0, stream);
+    if (tiles <= 128) {
+      const bool wide = M < N;
+      return kgs_gemm_bf16_nt_w4x_ex(A, B, C, nullptr, M, N, K, lda, ldb, ldc, wide ? 256 : 128, 1, wide ? 128 : 256,
+                                     0, stream);
+    }
+  }
   auto a = (const unsigned short*)A;
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;

@@ -631,3 +631,18 @@ def test_gemm_w4x_stages_that_do_not_fit_are_refused():
     a = torch.zeros(256, 256, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         gemm_nt_w4x(a, a, bn=256, bm=256, stages=3)  # 3 x 64 KiB > 160 KiB
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 1024, 1024), (1024, 2048, 512), (512, 512, 768), (4096, 2048, 256),
+                                   (2048, 4096, 512), (768, 2048, 1280)])
+def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
+    """Auto routes grids of <= 128 256x256 tiles to 256x128 / 128x256 / 128x128
+    four-wave tiles (round 3): same per-element MFMA chain, so bitwise the
+    forced 256x256 result, and close to fp32."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    auto = gemm_nt(a, b)
+    assert torch.equal(auto, gemm_nt(a, b, variant="fast"))
+    assert _rel_err(auto, _ref_nt(a, b)) < 1e-2
