@@ -74,7 +74,7 @@ class GemmWorkload:
             return "torch.matmul"
         from kgs.ops import fast_path_ok
 
-        return "kgs gemm_nt_w4 (4-wave 256x256 LDS-DMA pipeline)" if fast_path_ok(self.a, self.b, self.c[0]) else \
+        return "kgs gemm_nt_w4p (persistent 4-wave 256x256 LDS-DMA pipeline)" if fast_path_ok(self.a, self.b, self.c[0]) else \
             "kgs gemm_nt_generic"
 
     def _allreduce(self):

@@ -65,6 +65,9 @@ _W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (
             (1, 24, 20, 1, 140000000), (1, 24, 20, 1, 240000000), (1, 24, 20, 1, 100000000),
             (1, 24, 20, 1, 200000000))
 W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
+# round 3: the persistent four-wave kernel (native/kernels/gemm_w4p.h, named accumulator AGPRs),
+# default tile map / the tall mirror; K >= 256
+W4H.update({"w4p_0": 101, "w4p_140000000": 102})
 
 
 @lru_cache(maxsize=1)

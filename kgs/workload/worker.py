@@ -79,7 +79,7 @@ def gemm_check(dev, size: int, iters: int) -> dict:
     ms = s.elapsed_time(e) / iters
     return {"size": size, "rel_err": err, "ok": err < 2e-2, "ms": round(ms, 4),
             "tflops": round(2.0 * size ** 3 / (ms * 1e-3) / 1e12, 1),
-            "kernel": "gemm_nt_w4" if fast_path_ok(A, B, C) else "gemm_nt_generic"}
+            "kernel": "gemm_nt_w4p" if fast_path_ok(A, B, C) else "gemm_nt_generic"}
 
 
 def gemm_fp8_check(dev, size: int, iters: int) -> dict:

@@ -590,6 +590,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // invisible to hipcc's hazard recognizer), drain the tail prefetches.
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int n = 0; n < 8; ++n) asm volatile("" : "+a"(f.acc[i][n]));  // reads stay after the padding
 
   const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll

@@ -3,6 +3,17 @@
 // opt-in libkgs_experiments.so; names and ids in kgs/ops/experiments.py (W4H),
 // numbers in profiles/gemm_tuning.md ("Four-wave kernel").
 #include "gemm_w4.h"
+#include "gemm_w4p.h"
+
+static int cu_count() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
 
 // variant = table id below; template <B1, R, P, ORD, X>, X = 10000 W + 100 AUX + GROUP_M
 // (W = DMA window in MFMAs, AUX = DMA cache bits, 0 = default). Aligned shapes
@@ -23,6 +34,20 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
                        nullptr, M, N, K, lda, ldb, ldc);                                                      \
     break;
   // ids: kgs/ops/experiments.py W4H (name = w4h_ORD_B1_R_P_X)
+  // ids 101 / 102: the persistent kernel (gemm_w4p.h), default map / the tall
+  // mirror (GROUP_N + B's DMAs first); K >= 256, one workgroup per CU
+  if (variant == 101 || variant == 102) {
+    if (K < 256) return KGS_ERR_SHAPE;
+    const int ntiles = (M / 256) * (N / 256);
+    const dim3 pg(ntiles < cu_count() ? ntiles : cu_count());
+    if (variant == 101)
+      hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0>), pg, dim3(256), 0, s, a, b, c, nullptr, M, N, K,
+                         lda, ldb, ldc);
+    else
+      hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000000>), pg, dim3(256), 0, s, a, b, c, nullptr, M,
+                         N, K, lda, ldb, ldc);
+    return (int)hipGetLastError();
+  }
   switch (variant) {
     KGS_W4H(1, 24, 20, 1, 1, 0)
     KGS_W4H(2, 24, 20, 1, 1, 160000)

@@ -61,6 +61,7 @@
 // the in-pod hot path required by BASELINE.json configs 3-4.
 #include "gemm_pipeline.h"
 #include "gemm_w4.h"
+#include "gemm_w4p.h"
 
 namespace kgs {
 
@@ -150,6 +151,18 @@ __global__ __launch_bounds__(256) void gemm_nt_generic(const unsigned short* __r
 
 }  // namespace gen
 
+// Compute units of the current device (the persistent grid size), cached per device.
+static int cu_count() {
+  static int n[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  if (!n[dev]) {
+    int v = 0;
+    n[dev] = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) ? v : 256;
+  }
+  return n[dev];
+}
+
 template <int EPI>
 static hipError_t launch(int variant, const unsigned short* A, const unsigned short* B, unsigned short* C,
                          const unsigned short* bias, int M, int N, int K, int lda, int ldb, int ldc,
@@ -157,7 +170,20 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   // Production S = 7: balanced schedule, no s_setprio, GROUP_M 4 (measured best
   // at 4096^3..16384^2x8192 in interleaved A/B, profiles/gemm_tuning.md).
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
-  if (variant == 3) {
+  if (variant == 3 && K >= 256) {
+    // the persistent four-wave kernel (gemm_w4p.h, round 3): one workgroup per
+    // CU walking tiles, the next tile's first K-tiles loaded under the current
+    // tile's last K-steps; bitwise the one-shot kernel. Interleaved medians vs
+    // the one-shot grid: 8192^3 1643 vs 1616, 16384^2x8192 1618 vs 1586,
+    // 8192x28672x4096 1589 vs 1545 TFLOP/s (profiles/r3/gemm_persistent.json)
+    const int tiles = (M / 256) * (N / 256), cus = cu_count();
+    const dim3 pg(tiles < cus ? tiles : cus);
+    if (M > N)
+      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 140000000>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb,
+                         ldc);
+    else
+      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc);
+  } else if (variant == 3 || variant == 4) {
     using Kn = w4::Knobs<256, 256>;
     if (M > N) {
       // tall problems run the mirror image of the default schedule: GROUP_N tile
@@ -228,8 +254,10 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
                                        hipStream_t stream);
 
 // variant: 0 = auto, 1 = force the 256x256 8-wave ping-pong, 2 = force generic,
-//          3 = force the four-wave kernel (256x256 tiles), 16 = force the
-//          bounded 256x256 pipeline. Anything else is rejected.
+//          3 = force the four-wave kernel (256x256 tiles; persistent when
+//          K >= 256), 4 = the four-wave kernel's one-shot grid (one workgroup
+//          per tile), 16 = force the bounded 256x256 pipeline. Anything else
+//          is rejected.
 // Auto on a grid of at most 128 256x256 tiles (half the CUs or fewer) runs the
 // four-wave kernel on smaller tiles: 256x128 / 128x256 up to 128 tiles, 128x128
 // up to 64 -- 1.13-1.23x hipBLASLt there, where 256x256 tiles leave CUs idle
@@ -246,7 +274,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
   const int bounded = kgs_gemm_bf16_nt_bounded_ok(A, B, C, M, N, K, lda, ldb, ldc) && bias_ok;
   int v;
   if (variant == 0) v = w4 ? 3 : fast ? 1 : bounded ? 16 : 2;
-  else if (variant == 3) { if (!w4) return KGS_ERR_ALIGN; v = 3; }
+  else if (variant == 3 || variant == 4) { if (!w4) return KGS_ERR_ALIGN; v = variant; }
   else if (variant == 16) { if (!bounded) return KGS_ERR_ALIGN; v = 16; }
   else if (variant == 1) { if (!fast) return KGS_ERR_ALIGN; v = 1; }
   else if (variant == 2) v = 2;

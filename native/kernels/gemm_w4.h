@@ -29,12 +29,21 @@
 // The LDS image is the 8-wave kernel's (128-B rows, 16-B chunk c of row r at
 // c ^ ((r >> 1) & 7)): conflict-free ds_read_b128 fragments.
 //
-// Register allocation: the accumulators MUST stay tied. With the builtin MFMA
-// hipcc renames accumulators between the two unrolled K-steps and repairs the
-// loop with ~700 v_accvgpr moves per iteration; the asm form with a "+a"
-// operand keeps each accumulator in place (0 moves, checked in the ISA).
+// Register allocation: the accumulators are NAMED AGPRs (acc_regs.h: fragment
+// (i, n) in a[4q : 4q+3], q = NB i + n), reserved by KGS_ACC_RESERVE and
+// touched only by asm. With the builtin MFMA hipcc renames accumulators between
+// the two unrolled K-steps and repairs the loop with ~700 v_accvgpr moves per
+// iteration; tied "+a" C++ operands (rounds 2-3) kept them in place inside the
+// loop but let the allocator shuffle them at the loop exit, before the s_nop
+// hazard padding (v_accvgpr_read of a[248:251] four instructions after the MFMA
+// that wrote it; the SiLU-epilogue instantiation returned stale fragments).
+// Named registers leave the allocator nothing to move, and the epilogue's asm
+// reads stay after the padding (volatile asm keeps program order).
 #pragma once
 
+#include <type_traits>
+
+#include "acc_regs.h"
 #include "kgs_common.h"
 
 
@@ -159,16 +168,31 @@ __device__ __forceinline__ const char* bbase(const Ctx& c, int st) {
   return c.smem + st * Shape<BM, BN>::STAGE + Shape<BM, BN>::OPA + c.wc * (BN / 2) * 128 + (SUB ? c.ro1 : c.ro0);
 }
 
-// One MFMA on an accumulator pinned to AGPRs: the tied "+a" operand keeps each
-// accumulator in one place across the K-loop (the builtin form lets the
-// register allocator rename accumulators and then repair the loop with
-// hundreds of v_accvgpr moves per K-step). Operands swapped (B first) so a lane
+// One MFMA on the named accumulator (I, N). Operands swapped (B first) so a lane
 // holds C[m = lane&15][n = 4*(lane>>4)+e]. asm MFMAs are invisible to the
 // hazard recognizer: the only hazard left (AGPR results read by VALU) is padded
 // before the epilogue.
-template <int MA, int NB>
-__device__ __forceinline__ void mma(f32x4 (&acc)[MA][NB], const Frag<MA, NB>& f, int i, int n) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc[i][n]) : "v"(f.b[n]), "v"(f.a[i]));
+template <int MA, int NB, int I, int N>
+__device__ __forceinline__ void mma(const Frag<MA, NB>& f) {
+  accr::mfma<I * NB + N>(f.b[N], f.a[I]);
+}
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Row I of the wave's accumulator grid (NB fragments) into VGPRs.
+template <int NB, int I, int N = 0>
+__device__ __forceinline__ void read_row(f32x4 (&v)[NB]) {
+  if constexpr (N < NB) {
+    v[N] = accr::read<I * NB + N>();
+    read_row<NB, I, N + 1>(v);
+  }
 }
 
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
@@ -247,12 +271,12 @@ __device__ __forceinline__ void wait_vm() {
 //   k >= KM - R         P ds_reads of f0 (K-tile t+1, k-sub 0) after each MFMA
 template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int NS, int K>
 __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM / 32, BN / 32>& f0,
-                                      Frag<BM / 32, BN / 32>& f1, f32x4 (&acc)[BM / 32][BN / 32]) {
+                                      Frag<BM / 32, BN / 32>& f1) {
   using S = Shape<BM, BN>;
   constexpr int MA = S::MA, NB = S::NB, KM = S::KM, HM = S::HM, NR = S::NR, ND = dma_per_stage<BM, BN>();
   if constexpr (K < KM) {
     constexpr int mi = Order<ORD, MA, NB>::o.i[K % HM], mn = Order<ORD, MA, NB>::o.n[K % HM];
-    if constexpr (K < HM) mma<MA, NB>(acc, f0, mi, mn); else mma<MA, NB>(acc, f1, mi, mn);
+    if constexpr (K < HM) mma<MA, NB, mi, mn>(f0); else mma<MA, NB, mi, mn>(f1);
     if constexpr (K < NR) {
       constexpr int x = rd_idx(ORD, MA, NB, K);
       if constexpr (rd_isa(ORD, MA, NB, K)) f1.a[x] = frag(sp.pa1 + x * 2048); else f1.b[x] = frag(sp.pb1 + x * 2048);
@@ -283,7 +307,7 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM 
       wait_vm<(NS - 1) * ND>();
       bar();
     }
-    kbody<BM, BN, ST, B1, R, P, ORD, X, NS, K + 1>(c, sp, f0, f1, acc);
+    kbody<BM, BN, ST, B1, R, P, ORD, X, NS, K + 1>(c, sp, f0, f1);
   }
 }
 
@@ -292,7 +316,7 @@ __device__ __forceinline__ void kbody(const Ctx& c, const StepPtrs& sp, Frag<BM 
 // placed between them (kbody).
 template <int BM, int BN, int ST, int B1, int R, int P, int ORD, int X, int NS = 2>
 __device__ __forceinline__ void kstep(const Ctx& c, Frag<BM / 32, BN / 32>& f0, Frag<BM / 32, BN / 32>& f1,
-                                      f32x4 (&acc)[BM / 32][BN / 32], int t) {
+                                      int t) {
   using S = Shape<BM, BN>;
   static_assert(B1 >= S::NR && B1 + dma_per_stage<BM, BN>() <= S::KM - R && S::NR <= R * P, "bad K-step schedule");
   StepPtrs sp;
@@ -303,7 +327,7 @@ __device__ __forceinline__ void kstep(const Ctx& c, Frag<BM / 32, BN / 32>& f0, 
   int tl = t + NS;
   tl = tl < c.nt ? tl : c.nt - 1;  // past the end: harmless re-load into the free stage
   sp.k0 = tl * BK;
-  kbody<BM, BN, ST, B1, R, P, ORD, X, NS, 0>(c, sp, f0, f1, acc);
+  kbody<BM, BN, ST, B1, R, P, ORD, X, NS, 0>(c, sp, f0, f1);
 }
 
 // Production knobs per tile shape: barrier 1 after MFMA B1, R MFMAs after
@@ -469,11 +493,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
   }
 
-  f32x4 acc[MA][NB];
-#pragma unroll
-  for (int i = 0; i < MA; ++i)
-#pragma unroll
-    for (int n = 0; n < NB; ++n) acc[i][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+  KGS_ACC_RESERVE();
+  static_for<0, MA * NB>([](auto q) { accr::zero<decltype(q)::value>(); });
 
   // prologue: K-tiles 0 .. NS-1 into stages 0 .. NS-1, k-sub 0 of K-tile 0 into f0
 #pragma unroll
@@ -500,18 +521,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   if constexpr (NS == 2) {
     for (int t = 0; t < c.nt; t += 2) {
-      kstep<BM, BN, 0, B1, R, P, ORD, X>(c, f0, f1, acc, t);
-      kstep<BM, BN, 1, B1, R, P, ORD, X>(c, f0, f1, acc, t + 1);
+      kstep<BM, BN, 0, B1, R, P, ORD, X>(c, f0, f1, t);
+      kstep<BM, BN, 1, B1, R, P, ORD, X>(c, f0, f1, t + 1);
     }
   } else {
     // K-tile t lives in stage t % NS; the tail steps of a partial round are
     // skipped uniformly by the whole workgroup
     for (int t = 0; t < c.nt; t += NS) {
-      kstep<BM, BN, 0, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t);
-      if (t + 1 < c.nt) kstep<BM, BN, 1, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 1);
-      if (t + 2 < c.nt) kstep<BM, BN, 2 % NS, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 2);
+      kstep<BM, BN, 0, B1, R, P, ORD, X, NS>(c, f0, f1, t);
+      if (t + 1 < c.nt) kstep<BM, BN, 1, B1, R, P, ORD, X, NS>(c, f0, f1, t + 1);
+      if (t + 2 < c.nt) kstep<BM, BN, 2 % NS, B1, R, P, ORD, X, NS>(c, f0, f1, t + 2);
       if constexpr (NS == 4)
-        if (t + 3 < c.nt) kstep<BM, BN, 3, B1, R, P, ORD, X, NS>(c, f0, f1, acc, t + 3);
+        if (t + 3 < c.nt) kstep<BM, BN, 3, B1, R, P, ORD, X, NS>(c, f0, f1, t + 3);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
@@ -521,31 +542,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if constexpr (SPLITK) {
     // fp32 partial tile, row-major [M][N]: one 16-B store per lane per fragment
     float* part = (float*)C + (long)slice * M * N;
-#pragma unroll
-    for (int i = 0; i < MA; ++i) {
+    static_for<0, MA>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
       const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
-      if (BNDM && row >= M) continue;
+      f32x4 v[NB];
+      read_row<NB, i>(v);
+      if (BNDM && row >= M) return;
 #pragma unroll
       for (int n = 0; n < NB; ++n)
-        *(f32x4*)(part + (long)row * N + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4) = acc[i][n];
-    }
+        *(f32x4*)(part + (long)row * N + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4) = v[n];
+    });
     return;
   }
   if constexpr (SW) {
     // out fragment q (16 columns) = silu(gate fragment ng) * up fragment ng + 2,
     // ng = 4 (q / 2) + q % 2; pairs (q, q + 1) share one 16-B store per lane
-#pragma unroll
-    for (int i = 0; i < MA; ++i) {
+    static_for<0, MA>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
       const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
       unsigned short* crow = C + (long)row * ldc;
       const bool row_ok = !BNDM || row < M;
+      f32x4 v[NB];
+      read_row<NB, i>(v);
 #pragma unroll
       for (int q = 0; q < NB / 2; q += 2) {
         uint2 o[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int ng = 4 * ((q + h) / 2) + (q + h) % 2;
-          const f32x4 g = acc[i][ng], u = acc[i][ng + 2];
+          const f32x4 g = v[ng], u = v[ng + 2];
           float r[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -561,7 +586,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         const int col0 = tn * (BN / 2) + c.wc * (BN / 4) + q * 16;
         if (row_ok) *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
       }
-    }
+    });
     return;
   }
   // epilogue: bias + activation, then pair n-tiles (n, n+1) with
@@ -577,17 +602,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int e = 0; e < 4; ++e) bv[n][e] = bf2f((unsigned short)bb[e]);
     }
   }
-#pragma unroll
-  for (int i = 0; i < MA; ++i) {
+  static_for<0, MA>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
     const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
     unsigned short* crow = C + (long)row * ldc;
     const bool row_ok = !BNDM || row < M;
+    f32x4 vr[NB];
+    read_row<NB, i>(vr);
 #pragma unroll
     for (int n = 0; n < NB; n += 2) {
       uint2 o[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const f32x4 v = acc[i][n + h];
+        const f32x4 v = vr[n + h];
         o[h].x = pack_bf16x2(epilogue<EPI>(v[0], bv[n + h][0]), epilogue<EPI>(v[1], bv[n + h][1]));
         o[h].y = pack_bf16x2(epilogue<EPI>(v[2], bv[n + h][2]), epilogue<EPI>(v[3], bv[n + h][3]));
       }
@@ -597,7 +624,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
       if (row_ok) *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
     }
-  }
+  });
 }
 
 }  // namespace w4

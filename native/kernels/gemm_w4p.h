@@ -1,0 +1,240 @@
+// gemm_w4p: the four-wave 256x256x64 bf16 NT GEMM of gemm_w4.h made PERSISTENT.
+//
+// One workgroup per CU walks tiles v, v + G, v + 2G, ... (G = gridDim.x) in the
+// production tile order (tile_of, so every tile lands on the same XCD as in the
+// one-shot grid, and the tiles in flight at any moment are the same set). The
+// LDS-DMA stream does not stop at a tile boundary: the last two K-steps of a
+// tile load K-tiles 0 and 1 of the NEXT tile into the stages they free, and the
+// last R MFMAs read the next tile's first fragments, exactly as they read K-tile
+// t + 1 inside a tile. Between two tiles a wave only runs its epilogue (256
+// v_accvgpr_read, bf16 packing, 32 16-byte stores) while the next tile's first
+// two K-tiles are already on their way. The one-shot grid instead drains,
+// exits, dispatches a new workgroup, recomputes addresses and waits for two
+// K-tiles from memory before its first MFMA, at every tile.
+//
+// Why a separate kernel: with the accumulators as C++ values ("+a" operands),
+// an outer tile loop makes the register allocator move them (round 2: 124-132
+// v_accvgpr_mov inside the MFMA loop and wrong results, profiles/gemm_tuning.md
+// "Persistent four-wave kernel"). Here the accumulator tile is NAMED: q = 8 i + n
+// lives in a[4q : 4q+3] (acc_regs.h), reserved by KGS_ACC_RESERVE and touched
+// only by asm, so the allocator has nothing to rename. The first k-sub of a
+// tile's first K-step writes with C = 0 (mfma0), which is the reset.
+//
+// K-step schedule, LDS image, DMA placement, barriers and MFMA order are
+// gemm_w4.h's (Knobs<256, 256>: B1 24, R 20, P 1, growing-square order), so the
+// result is bitwise the one-shot kernel's (tests/test_kernels_gpu.py).
+#pragma once
+
+#include "acc_regs.h"
+#include "gemm_w4.h"
+
+namespace kgs {
+namespace w4p {
+
+using w4::BK;
+using w4::Ctx;
+using w4::Frag;
+using w4::StepPtrs;
+
+constexpr int BM = 256, BN = 256;
+using S = w4::Shape<BM, BN>;
+using Kn = w4::Knobs<BM, BN>;
+constexpr int MA = S::MA, NB = S::NB;
+
+template <bool ZERO, int I, int N>
+__device__ __forceinline__ void pmma(const Frag<MA, NB>& f) {
+  if constexpr (ZERO) accr::mfma0<I * NB + N>(f.b[N], f.a[I]);
+  else accr::mfma<I * NB + N>(f.b[N], f.a[I]);
+}
+
+// gemm_w4.h's kbody with named accumulators: MFMA K of the K-step plus what
+// follows it. The DMA issues use `cd` (this tile's or the next tile's buffer
+// resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`.
+template <int ST, int X, bool ZERO, int K>
+__device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
+                                      Frag<MA, NB>& f1) {
+  constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = Kn::ORD;
+  constexpr int KM = S::KM, HM = S::HM, NR = S::NR, ND = w4::dma_per_stage<BM, BN>();
+  if constexpr (K < KM) {
+    constexpr int mi = w4::Order<ORD, MA, NB>::o.i[K % HM], mn = w4::Order<ORD, MA, NB>::o.n[K % HM];
+    if constexpr (K < HM) pmma<ZERO, mi, mn>(f0); else pmma<false, mi, mn>(f1);
+    if constexpr (K < NR) {
+      constexpr int x = w4::rd_idx(ORD, MA, NB, K);
+      if constexpr (w4::rd_isa(ORD, MA, NB, K)) f1.a[x] = w4::frag(sp.pa1 + x * 2048);
+      else f1.b[x] = w4::frag(sp.pb1 + x * 2048);
+    }
+    if constexpr (K >= B1 && K < KM - R) {
+      constexpr int NW = KM - R - B1;
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        if (B1 + (j * NW) / ND == K) w4::dma_any<BM, BN, X>(cd, ST, j, sp.k0);
+      }
+    }
+    if constexpr (K >= KM - R) {
+      constexpr int q = K - (KM - R);
+#pragma unroll
+      for (int e = q * P; e < (q + 1) * P && e < NR; ++e) {
+        const int x = w4::rd_idx(ORD, MA, NB, e);
+        if (w4::rd_isa(ORD, MA, NB, e)) f0.a[x] = w4::frag(sp.pa0 + x * 2048);
+        else f0.b[x] = w4::frag(sp.pb0 + x * 2048);
+      }
+    }
+    w4::fence();
+    if constexpr (K == B1 - 1) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage ST retired
+      w4::bar();
+    }
+    if constexpr (K == KM - R - 1) {
+      w4::wait_vm<ND>();  // own DMA of the next K-tile landed
+      w4::bar();
+    }
+    pbody<ST, X, ZERO, K + 1>(c, cd, sp, f0, f1);
+  }
+}
+
+// One K-step on stage ST; its DMAs bring K-tile kd (of cd's tile) into ST.
+template <int ST, int X, bool ZERO>
+__device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd) {
+  StepPtrs sp;
+  sp.pa1 = w4::abase<BM, BN, 1>(c, ST);
+  sp.pb1 = w4::bbase<BM, BN, 1>(c, ST);
+  sp.pa0 = w4::abase<BM, BN, 0>(c, ST ^ 1);
+  sp.pb0 = w4::bbase<BM, BN, 0>(c, ST ^ 1);
+  sp.k0 = kd * BK;
+  pbody<ST, X, ZERO, 0>(c, cd, sp, f0, f1);
+}
+
+// Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
+// bias + activation, pack to bf16, pair n-tiles with v_permlane16_swap -> one
+// 16-B store per lane (the one-shot kernel's epilogue, reading named AGPRs).
+template <int EPI, int Q>
+__device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn,
+                                     const float (&bv)[NB][4]) {
+  if constexpr (Q < MA * NB) {
+    constexpr int i = Q / NB, n = Q % NB;
+    const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+    const f32x4 v0 = accr::read<Q>(), v1 = accr::read<Q + 1>();
+    uint2 o[2];
+    o[0].x = pack_bf16x2(epilogue<EPI>(v0[0], bv[n][0]), epilogue<EPI>(v0[1], bv[n][1]));
+    o[0].y = pack_bf16x2(epilogue<EPI>(v0[2], bv[n][2]), epilogue<EPI>(v0[3], bv[n][3]));
+    o[1].x = pack_bf16x2(epilogue<EPI>(v1[0], bv[n + 1][0]), epilogue<EPI>(v1[1], bv[n + 1][1]));
+    o[1].y = pack_bf16x2(epilogue<EPI>(v1[2], bv[n + 1][2]), epilogue<EPI>(v1[3], bv[n + 1][3]));
+    auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+    auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+    const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
+    const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
+    *(uint4*)(C + (long)row * ldc + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
+    pepi<EPI, Q + 2>(c, C, ldc, tm, tn, bv);
+  }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_a(const unsigned short* A, int tm, int lda) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda), 0, BM * lda * 2, 0x00020000);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B, int tn, int ldb) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb), 0, BN * ldb * 2, 0x00020000);
+}
+
+// Aligned shapes only (M, N % 256, K % 128 with K >= 256; 16-B operands); the
+// grid is at most the tile count. X: gemm_w4.h's knob bag (tile map, DMA order).
+template <int EPI, int X = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
+    const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
+    const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+  constexpr int ND = w4::dma_per_stage<BM, BN>();
+  __shared__ __attribute__((aligned(1024))) char smem[2 * S::STAGE];
+  KGS_ACC_RESERVE();
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ntm = M / BM, ntn = N / BN, ntiles = ntm * ntn;
+
+  Ctx c;
+  c.smem = smem;
+  c.w = w;
+  c.wr = w >> 1;
+  c.wc = w & 1;
+  c.nt = K / BK;
+  c.sa32 = 32 * lda * 2;
+  c.sb32 = 32 * ldb * 2;
+  {
+    const int row = w * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    c.voa = (row * lda + ch * 8) * 2;
+    c.vob = (row * ldb + ch * 8) * 2;
+    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
+    c.ro0 = fr * 128 + ((fq ^ f) * 16);
+    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+  }
+  int v = blockIdx.x, sl, tm, tn;
+  w4::tile_of<X, false>(v, ntiles, ntm, ntn, sl, tm, tn);
+  c.ra = rsrc_a(A, tm, lda);
+  c.rb = rsrc_b(B, tn, ldb);
+
+  // prologue: K-tiles 0, 1 of the first tile into stages 0, 1; k-sub 0 of K-tile 0 into f0
+#pragma unroll
+  for (int st = 0; st < 2; ++st)
+#pragma unroll
+    for (int j = 0; j < ND; ++j) w4::dma_any<BM, BN, X>(c, st, j, st * BK);
+  w4::wait_vm<ND>();
+  w4::bar();
+  Frag<MA, NB> f0, f1;
+  {
+    const char* pa = w4::abase<BM, BN, 0>(c, 0);
+    const char* pb = w4::bbase<BM, BN, 0>(c, 0);
+#pragma unroll
+    for (int e = 0; e < S::NR; ++e) {
+      const int x = w4::rd_idx(Kn::ORD, MA, NB, e);
+      if (w4::rd_isa(Kn::ORD, MA, NB, e)) f0.a[x] = w4::frag(pa + x * 2048);
+      else f0.b[x] = w4::frag(pb + x * 2048);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);
+
+  const int nt = c.nt;
+  for (;;) {
+    const int vn = v + (int)gridDim.x;
+    const bool more = vn < ntiles;
+    int tmn = tm, tnn = tn;
+    if (more) w4::tile_of<X, false>(vn, ntiles, ntm, ntn, sl, tmn, tnn);
+    Ctx cn = c;
+    cn.ra = rsrc_a(A, tmn, lda);
+    cn.rb = rsrc_b(B, tnn, ldb);
+    pstep<0, X, true>(c, c, f0, f1, 2);
+    pstep<1, X, false>(c, c, f0, f1, 3);
+    for (int t = 2; t < nt - 2; t += 2) {
+      pstep<0, X, false>(c, c, f0, f1, t + 2);
+      pstep<1, X, false>(c, c, f0, f1, t + 3);
+    }
+    // the last two K-steps bring the next tile's K-tiles 0 and 1 (no next tile:
+    // harmless re-loads of this tile's last K-tile into the freed stages)
+    pstep<0, X, false>(c, cn, f0, f1, more ? 0 : nt - 1);
+    pstep<1, X, false>(c, cn, f0, f1, more ? 1 : nt - 1);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read
+    float bv[NB][4];
+    {
+      const int fq = lane >> 4;
+#pragma unroll
+      for (int n = 0; n < NB; ++n) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[n][e] = 0.f;
+        if constexpr (EPI != EPI_NONE) {
+          const bf16x4 bb = *(const bf16x4*)(bias + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bv[n][e] = bf2f((unsigned short)bb[e]);
+        }
+      }
+    }
+    pepi<EPI, 0>(c, C, ldc, tm, tn, bv);
+    if (!more) break;
+    v = vn;
+    tm = tmn;
+    tn = tnn;
+    c.ra = cn.ra;
+    c.rb = cn.rb;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
+}
+
+}  // namespace w4p
+}  // namespace kgs

@@ -16,11 +16,14 @@ pytestmark = pytest.mark.skipif(not Path(HIPCC).exists() and shutil.which("hipcc
                                 reason="hipcc not available")
 
 
-def _resources(src: str, tmp_path) -> dict:
+def _compile(src: str, odir: Path, save_temps: bool = False) -> tuple[dict, str]:
+    """Resource remarks per kernel (and, with save_temps, the device assembly)."""
     cmd = [HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c",
-           str(ROOT / "native" / "kernels" / src), "-o", str(tmp_path / (src + ".o")),
+           str(ROOT / "native" / "kernels" / src), "-o", str(odir / (src + ".o")),
            "-Rpass-analysis=kernel-resource-usage"]
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    if save_temps:
+        cmd.append("-save-temps=obj")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=odir)
     assert out.returncode == 0, out.stderr[-2000:]
     res, name = {}, None
     for line in out.stderr.splitlines():
@@ -32,17 +35,63 @@ def _resources(src: str, tmp_path) -> dict:
         m = re.search(r"remark:\s+([A-Za-z ]+?)(?: \[bytes/\w+\])?: (\d+)", line)
         if m and name:
             res[name][m.group(1).strip()] = int(m.group(2))
-    return res
+    asm = ""
+    if save_temps:
+        (s_file,) = list(odir.glob(f"{Path(src).stem}-hip-amdgcn-amd-amdhsa-gfx950.s"))
+        asm = s_file.read_text()
+    return res, asm
 
 
-def test_gemm_production_kernels_do_not_spill(tmp_path):
-    res = _resources("gemm_bf16.hip", tmp_path)
+def _resources(src: str, tmp_path) -> dict:
+    return _compile(src, tmp_path)[0]
+
+
+@pytest.fixture(scope="module")
+def gemm_build(tmp_path_factory):
+    return _compile("gemm_bf16.hip", tmp_path_factory.mktemp("gemm"), save_temps=True)
+
+
+def test_gemm_production_kernels_do_not_spill(gemm_build):
+    res, _ = gemm_build
     prod = [n for n in res if re.search(r"gemm_nt_256ILi[0-4]ELi(7|519|263)E", n)]
     prod += [n for n in res if re.search(r"gemm_nt_256ILi[0-2]ELi(1031|1543)E", n)]
     prod += [n for n in res if re.search(r"gemm_nt_256ILi[01]ELi(525319|525831)E", n)]
-    assert len(prod) >= 19, list(res)[:20]
+    prod += [n for n in res if "gemm_nt_w4" in n]
+    assert len(prod) >= 19 + 10, list(res)[:20]
     bad = {n: r.get("VGPRs Spill") for n, r in res.items() if n in prod and r.get("VGPRs Spill", 0)}
     assert not bad, bad
+
+
+def _functions(asm: str, pattern: str) -> dict:
+    out = {}
+    for m in re.finditer(r"\n(_Z\S+):", asm):
+        if re.search(pattern, m.group(1)):
+            out[m.group(1)] = asm[m.end():asm.find(".Lfunc_end", m.end())]
+    return out
+
+
+def test_four_wave_gemms_touch_agprs_only_through_named_asm(gemm_build):
+    """The four-wave GEMMs keep their accumulators in NAMED AGPRs (acc_regs.h).
+    Guard the two ways that went wrong before (gemm_w4.h header): the register
+    allocator moving accumulators (any v_accvgpr_mov, or a v_accvgpr_write that
+    is not the zero reset), and an AGPR read before the s_nop padding that
+    follows the last MFMA (a stale fragment: the MFMA -> VALU hazard is not
+    checked by hipcc for asm MFMAs)."""
+    _, asm = gemm_build
+    funcs = _functions(asm, r"gemm_nt_w4p?I")
+    assert len(funcs) >= 10 + 2 * 5, sorted(funcs)[:5]
+    for name, body in funcs.items():
+        lines = body.splitlines()
+        assert not any("v_accvgpr_mov" in ln for ln in lines), name
+        writes = [ln for ln in lines if "v_accvgpr_write" in ln]
+        assert all(re.search(r"v_accvgpr_write_b32 a\d+, 0\b", ln) for ln in writes), (name, writes[:3])
+        pads = [i for i, ln in enumerate(lines) if "s_nop 7" in ln]
+        assert pads, name
+        for i, ln in enumerate(lines):
+            if "v_accvgpr_read" in ln:
+                # every read follows a padding that follows every MFMA before it
+                last_mfma = max((j for j in range(i) if "v_mfma" in lines[j]), default=-1)
+                assert any(last_mfma < p < i for p in pads), (name, i, ln)
 
 
 def test_attention_fits_two_workgroups_per_cu(tmp_path):

@@ -135,7 +135,7 @@ def test_gemm_strided_operands(variant):
 
 
 @pytest.mark.parametrize("act", ["bias", "gelu", "relu", "silu"])
-@pytest.mark.parametrize("variant", ["fast", "pingpong", "generic", "w4_bk32", "p32"])
+@pytest.mark.parametrize("variant", ["fast", "w4_oneshot", "pingpong", "generic", "w4_bk32", "p32"])
 def test_gemm_epilogues(act, variant):
     from kgs.ops import gemm_nt
 
@@ -646,3 +646,41 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
     auto = gemm_nt(a, b)
     assert torch.equal(auto, gemm_nt(a, b, variant="fast"))
     assert _rel_err(auto, _ref_nt(a, b)) < 1e-2
+
+
+@pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 256, "w4p_0"), (4608, 4096, 384, "w4p_0"),
+                                           (8192, 2304, 512, "w4p_140000000"), (1024, 768, 1024, "w4p_0")])
+def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
+    """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
+    tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
+    K-steps) runs gemm_w4.h's K-step, so it must reproduce the one-shot kernel
+    bit for bit -- with several tiles per workgroup (1024 / 288 / 288 tiles on
+    256 CUs: 4 each, 1-2 each, 1-2 in the mirrored tall order) and with fewer
+    tiles than CUs (12)."""
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    one_shot = _gemm_v(a, b, "w4h_1_24_20_1_0")
+    pers = _gemm_v(a, b, variant)
+    assert torch.equal(pers, one_shot)
+    assert _rel_err(pers, _ref_nt(a, b)) < 1e-2
+    # run twice more on other data: nothing carried over between launches/tiles
+    a2 = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    assert torch.equal(_gemm_v(a2, b, variant), _gemm_v(a2, b, "w4h_1_24_20_1_0"))
+
+
+@pytest.mark.parametrize("act", [None, "bias", "gelu", "silu"])
+@pytest.mark.parametrize("M,N,K", [(4096, 4608, 512), (4608, 2048, 256)])
+def test_gemm_fast_persistent_is_bitwise_the_one_shot_grid(M, N, K, act):
+    """Production "fast" launches the persistent grid (K >= 256); "w4_oneshot" the
+    one-workgroup-per-tile grid of the same K-step: bitwise equal with every
+    epilogue, several tiles per workgroup (288 / 144 tiles), tall and wide."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    kw = {} if act is None else {"bias": torch.randn(N, device=DEV).bfloat16(),
+                                 "act": None if act == "bias" else act}
+    fast = gemm_nt(a, b, variant="fast", **kw)
+    assert torch.equal(fast, gemm_nt(a, b, variant="w4_oneshot", **kw))
+    ref = _ref_nt(a, b, kw.get("bias"), kw.get("act"))
+    torch.testing.assert_close(fast.float(), ref, rtol=2e-2, atol=2e-2)
