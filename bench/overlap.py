@@ -54,10 +54,10 @@ def measure(args) -> dict:
 
     def gemms():
         for i in range(args.gemms):
-            gemm_nt(a, b, out=c[i & 1])
+            gemm_nt(a, b, out=c[i & 1], variant=args.variant)
 
     def comm():
-        comm_standin(dst, src, blocks=args.blocks, passes=args.passes)
+        comm_standin(dst, src, blocks=args.blocks, passes=args.passes, lds_kb=args.standin_lds_kb)
 
     def on(stream, fn):
         stream.wait_stream(main)
@@ -107,8 +107,9 @@ def measure(args) -> dict:
     med = {k: statistics.median(v) for k, v in times.items()}
     tg, tc = med["gemm"], med["comm"]
     out = {
-        "config": {"gemm": f"{args.gemms} x {m}^3 bf16 (kgs gemm_nt)", "comm_standin_mb": args.bucket_mb,
-                   "comm_blocks": args.blocks, "comm_passes": args.passes, "iters": args.iters},
+        "config": {"gemm": f"{args.gemms} x {m}^3 bf16 (kgs gemm_nt, variant {args.variant})",
+                   "comm_standin_mb": args.bucket_mb, "comm_blocks": args.blocks, "comm_passes": args.passes,
+                   "comm_lds_kb": args.standin_lds_kb, "iters": args.iters},
         "ms_median": {k: round(v, 4) for k, v in med.items()},
         "hidden_fraction": {k: round((tg + tc - med[k]) / tc, 3) for k in ("serial", "side", "side_prio", "late_prio")},
         "overlap_efficiency": {k: round(med[k] / (tg + tc), 3) for k in ("serial", "side", "side_prio", "late_prio")},
@@ -124,6 +125,9 @@ def main(argv=None) -> int:
     ap.add_argument("--blocks", type=int, default=32, help="stand-in workgroups (RCCL channels)")
     ap.add_argument("--passes", type=int, default=3, help="stand-in passes (scales its duration)")
     ap.add_argument("--iters", type=int, default=15)
+    ap.add_argument("--variant", default="auto", help="kgs GEMM variant (auto = persistent; w4_oneshot)")
+    ap.add_argument("--standin-lds-kb", type=int, default=0,
+                    help="LDS per stand-in workgroup (> 32: it needs a CU of its own, like a collective kernel)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     res = measure(args)

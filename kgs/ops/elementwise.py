@@ -36,15 +36,18 @@ def vector_add(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None
     return out
 
 
-def comm_standin(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32, passes: int = 1) -> torch.Tensor:
+def comm_standin(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32, passes: int = 1,
+                 lds_kb: int = 0) -> torch.Tensor:
     """``dst += src`` (f32) on a fixed number of workgroups, ``passes`` times: the
     footprint of a ring collective's kernel (a few tens of long-lived,
-    memory-bound workgroups) on one GPU, for GEMM/comm overlap measurements."""
+    memory-bound workgroups) on one GPU, for GEMM/comm overlap measurements.
+    ``lds_kb`` > 32 reserves enough LDS that a workgroup needs a CU of its own
+    (cannot share one with a 128 KiB GEMM workgroup)."""
     _dev_check(dst, src)
     if dst.dtype != torch.float32 or src.dtype != torch.float32 or dst.shape != src.shape:
         raise ValueError("comm_standin needs two f32 tensors of one shape")
     _lib.check(_lib.lib().kgs_comm_standin_f32(dst.data_ptr(), src.data_ptr(), dst.numel(), int(blocks), int(passes),
-                                               _lib.stream_handle(dst.device)), "comm_standin")
+                                               int(lds_kb) * 1024, _lib.stream_handle(dst.device)), "comm_standin")
     return dst
 
 

@@ -66,8 +66,11 @@ _W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (
             (1, 24, 20, 1, 200000000))
 W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
 # round 3: the persistent four-wave kernel (native/kernels/gemm_w4p.h, named accumulator AGPRs),
-# default tile map / the tall mirror; K >= 256
-W4H.update({"w4p_0": 101, "w4p_140000000": 102})
+# name w4p_X -> id 101.. (X: gemm_w4.h knob bag: tile map, DMA operand order); K >= 256
+_W4P_X = (0, 140000000, 8, 10000000, 140000008, 40000000, 100000000, 200000000, 140000002)
+W4H.update({f"w4p_{x}": 101 + i for i, x in enumerate(_W4P_X)})
+# the same with the static tile walk (no ticket queue): w4ps_X -> 121..
+W4H.update({f"w4ps_{x}": 121 + i for i, x in enumerate((0, 140000000, 8, 140000008))})
 
 
 @lru_cache(maxsize=1)

@@ -4,6 +4,7 @@
 // numbers in profiles/gemm_tuning.md ("Four-wave kernel").
 #include "gemm_w4.h"
 #include "gemm_w4p.h"
+#include "tile_queue.h"
 
 static int cu_count() {
   static int n = 0;
@@ -34,18 +35,38 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
                        nullptr, M, N, K, lda, ldb, ldc);                                                      \
     break;
   // ids: kgs/ops/experiments.py W4H (name = w4h_ORD_B1_R_P_X)
-  // ids 101 / 102: the persistent kernel (gemm_w4p.h), default map / the tall
-  // mirror (GROUP_N + B's DMAs first); K >= 256, one workgroup per CU
-  if (variant == 101 || variant == 102) {
+  // ids 101..: the persistent kernel (gemm_w4p.h) with knob bag X (tile map,
+  // DMA order; see gemm_w4.h tile_of / dma_any); K >= 256, one workgroup per CU
+  if (variant > 100) {
     if (K < 256) return KGS_ERR_SHAPE;
     const int ntiles = (M / 256) * (N / 256);
     const dim3 pg(ntiles < cu_count() ? ntiles : cu_count());
-    if (variant == 101)
-      hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0>), pg, dim3(256), 0, s, a, b, c, nullptr, M, N, K,
-                         lda, ldb, ldc);
-    else
-      hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000000>), pg, dim3(256), 0, s, a, b, c, nullptr, M,
-                         N, K, lda, ldb, ldc);
+    int* tq = kgs::tile_queue(s);
+    if (!tq) return KGS_ERR_ARG;
+#define KGS_W4P(ID, X, DYN)                                                                                    \
+  case ID:                                                                                                          \
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, X, DYN>), pg, dim3(256), 0, s, a, b, c, nullptr, M, N, K, \
+                       lda, ldb, ldc, tq);                                                                              \
+    break;
+    // ids: kgs/ops/experiments.py W4P
+    switch (variant) {
+      KGS_W4P(101, 0, true)
+      KGS_W4P(102, 140000000, true)
+      KGS_W4P(103, 8, true)
+      KGS_W4P(104, 10000000, true)
+      KGS_W4P(105, 140000008, true)
+      KGS_W4P(106, 40000000, true)
+      KGS_W4P(107, 100000000, true)
+      KGS_W4P(108, 200000000, true)
+      KGS_W4P(109, 140000002, true)
+      // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
+      KGS_W4P(121, 0, false)
+      KGS_W4P(122, 140000000, false)
+      KGS_W4P(123, 8, false)
+      KGS_W4P(124, 140000008, false)
+      default: return KGS_ERR_ARG;
+    }
+#undef KGS_W4P
     return (int)hipGetLastError();
   }
   switch (variant) {

@@ -262,10 +262,15 @@ KGS_EXPORT int kgs_vector_add_bf16_v(const void* a, const void* b, void* c, long
 }
 
 // dst += src (f32, n % 4 == 0, 16-B aligned) on `nblocks` workgroups, `passes` times.
-KGS_EXPORT int kgs_comm_standin_f32(void* dst, const void* src, long n, int nblocks, int passes, hipStream_t s) {
+// lds_bytes: dynamic LDS reserved per workgroup (unused by the kernel) -- with
+// more than 32 KiB a workgroup cannot share a CU with a 128 KiB GEMM workgroup,
+// like a collective kernel that needs its own CU.
+KGS_EXPORT int kgs_comm_standin_f32(void* dst, const void* src, long n, int nblocks, int passes, int lds_bytes,
+                                    hipStream_t s) {
   if (n <= 0 || n % 4 || nblocks <= 0 || passes <= 0) return KGS_ERR_SHAPE;
+  if (lds_bytes < 0 || lds_bytes > 160 * 1024) return KGS_ERR_ARG;
   if ((uintptr_t)dst % 16 || (uintptr_t)src % 16) return KGS_ERR_ALIGN;
-  hipLaunchKernelGGL(kgs::comm_standin_f32, dim3(nblocks), dim3(kgs::EW_THREADS), 0, s, (f32x4*)dst,
+  hipLaunchKernelGGL(kgs::comm_standin_f32, dim3(nblocks), dim3(kgs::EW_THREADS), lds_bytes, s, (f32x4*)dst,
                      (const f32x4*)src, n / 4, passes);
   return (int)hipGetLastError();
 }

@@ -1,7 +1,7 @@
 // gemm_w4p: the four-wave 256x256x64 bf16 NT GEMM of gemm_w4.h made PERSISTENT.
 //
-// One workgroup per CU walks tiles v, v + G, v + 2G, ... (G = gridDim.x) in the
-// production tile order (tile_of, so every tile lands on the same XCD as in the
+// One workgroup per CU takes tiles from a per-XCD ticket queue (below) in the
+// production tile order (tile_of, so every tile lands on the XCD it had in the
 // one-shot grid, and the tiles in flight at any moment are the same set). The
 // LDS-DMA stream does not stop at a tile boundary: the last two K-steps of a
 // tile load K-tiles 0 and 1 of the NEXT tile into the stages they free, and the
@@ -19,6 +19,18 @@
 // lives in a[4q : 4q+3] (acc_regs.h), reserved by KGS_ACC_RESERVE and touched
 // only by asm, so the allocator has nothing to rename. The first k-sub of a
 // tile's first K-step writes with C = 0 (mfma0), which is the reset.
+//
+// Tiles are handed out dynamically, not as v, v + G, v + 2G: a workgroup that
+// starts late (its CU held by another kernel, e.g. an RCCL all-reduce launched
+// on a side stream just before the GEMM) must not keep its share of tiles
+// waiting, or the whole GEMM waits for it. Workgroup b serves XCD label
+// x = b & 7 (the dispatcher deals workgroups to XCDs round robin), whose tiles
+// are the one-shot ids v = x + 8 t, t = 0, 1, ...; ticket t comes from
+// atomicAdd(q[x]). Wave 0 fetches the next tile's ticket at the top of a tile
+// and publishes it in LDS after the first K-step (its vmcnt wait has covered
+// the atomic by then); the other waves read it after the second. The last
+// workgroup to leave (exit counter q[8]) zeroes q[0..8] for the next launch on
+// the stream (tile_queue.h hands every stream its own slot).
 //
 // K-step schedule, LDS image, DMA placement, barriers and MFMA order are
 // gemm_w4.h's (Knobs<256, 256>: B1 24, R 20, P 1, growing-square order), so the
@@ -138,12 +150,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 
 // Aligned shapes only (M, N % 256, K % 128 with K >= 256; 16-B operands); the
 // grid is at most the tile count. X: gemm_w4.h's knob bag (tile map, DMA order).
-template <int EPI, int X = 0>
+// q: this stream's zeroed ticket slot (tile_queue.h), zero again on return.
+// DYN = false: the static walk v, v + G, v + 2G (q unused), for measurements.
+template <int EPI, int X = 0, bool DYN = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
-    const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc) {
+    const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
   constexpr int ND = w4::dma_per_stage<BM, BN>();
-  __shared__ __attribute__((aligned(1024))) char smem[2 * S::STAGE];
+  // the two stages plus one int at the end: the next tile's ticket, from wave 0.
+  // One LDS object, not a second __shared__ variable: with two, hipcc's LDS-DMA
+  // alias tracking put an s_waitcnt vmcnt(0) before every K-step's first
+  // fragment read (all DMAs in flight drained).
+  __shared__ __attribute__((aligned(1024))) char smem[2 * S::STAGE + 16];
+  int& tslot = *(int*)(smem + 2 * S::STAGE);
   KGS_ACC_RESERVE();
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -166,8 +185,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.ro0 = fr * 128 + ((fq ^ f) * 16);
     c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
   }
-  int v = blockIdx.x, sl, tm, tn;
-  w4::tile_of<X, false>(v, ntiles, ntm, ntn, sl, tm, tn);
+  const int x = blockIdx.x & 7;             // XCD label
+  const int ntx = (ntiles - x + 7) >> 3;     // its tiles: v = x + 8 t, t < ntx
+  // DYN: t is a ticket of label x (tile v = x + 8 t, t < ntx); static: t = v
+  const int lim = DYN ? ntx : ntiles;
+  int t = blockIdx.x;
+  if constexpr (DYN) {
+    if (threadIdx.x == 0) tslot = atomicAdd(q + x, 1);
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(tslot);
+    if (t >= ntx) {  // nothing left for this workgroup (it started late)
+      if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
+        for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
+      return;
+    }
+  }
+  int sl, tm, tn;
+  w4::tile_of<X, false>(DYN ? x + 8 * t : t, ntiles, ntm, ntn, sl, tm, tn);
   c.ra = rsrc_a(A, tm, lda);
   c.rb = rsrc_b(B, tn, ldb);
 
@@ -192,16 +226,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __builtin_amdgcn_s_waitcnt(0xc07f);
 
   const int nt = c.nt;
+  // The in-loop ticket fetch goes through an address hipcc cannot prove
+  // uniform: for a uniform one its atomic optimizer broadcasts the result with
+  // v_readfirstlane right after the atomic, i.e. an s_waitcnt vmcnt(0) (every
+  // DMA in flight) at the top of each tile. This way the first use, after
+  // K-step 0, waits only for the atomic.
+  int vzero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+  int* const qx = q + x + vzero;
   for (;;) {
-    const int vn = v + (int)gridDim.x;
-    const bool more = vn < ntiles;
+    int tk = 0;
+    if constexpr (DYN) {
+      if (threadIdx.x == 0) tk = atomicAdd(qx, 1);  // the next tile's ticket
+    }
+    pstep<0, X, true>(c, c, f0, f1, 2);
+    if constexpr (DYN) {
+      if (threadIdx.x == 0) tslot = tk;  // K-step 0's vmcnt wait covered the atomic
+    }
+    pstep<1, X, false>(c, c, f0, f1, 3);  // its barrier 1 publishes tslot
+    const int tnx = DYN ? __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
+    const bool more = tnx < lim;
     int tmn = tm, tnn = tn;
-    if (more) w4::tile_of<X, false>(vn, ntiles, ntm, ntn, sl, tmn, tnn);
+    if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
     Ctx cn = c;
     cn.ra = rsrc_a(A, tmn, lda);
     cn.rb = rsrc_b(B, tnn, ldb);
-    pstep<0, X, true>(c, c, f0, f1, 2);
-    pstep<1, X, false>(c, c, f0, f1, 3);
     for (int t = 2; t < nt - 2; t += 2) {
       pstep<0, X, false>(c, c, f0, f1, t + 2);
       pstep<1, X, false>(c, c, f0, f1, t + 3);
@@ -227,13 +276,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     pepi<EPI, 0>(c, C, ldc, tm, tn, bv);
     if (!more) break;
-    v = vn;
+    t = tnx;
     tm = tmn;
     tn = tnn;
     c.ra = cn.ra;
     c.rb = cn.rb;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
+  if constexpr (DYN) {
+    if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)  // last one out resets the queue
+      for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
+  }
 }
 
 }  // namespace w4p

@@ -100,3 +100,20 @@ def test_attention_fits_two_workgroups_per_cu(tmp_path):
     assert r.get("VGPRs Spill", 0) == 0
     assert r["VGPRs"] + r.get("AGPRs", 0) <= 256  # 2 waves / SIMD
     assert r["LDS Size"] <= 80 * 1024            # 2 workgroups / CU (160 KiB)
+
+
+def test_persistent_gemm_k_loop_has_no_full_vmcnt_drain(gemm_build):
+    """The persistent kernel's K-steps keep one K-tile of LDS-DMA in flight; a
+    compiler-inserted ``s_waitcnt vmcnt(0)`` in the loop would drain it every
+    K-step. Two ways it crept in while gemm_w4p.h was written: a second
+    __shared__ object (LDS-DMA alias tracking then waits before every fragment
+    read) and a uniform-address ticket atomic (the atomic optimizer's broadcast
+    waits right after it). Only the prologue's and the exit's may remain."""
+    _, asm = gemm_build
+    funcs = _functions(asm, r"gemm_nt_w4pILi0E")
+    assert funcs
+    for name, body in funcs.items():
+        lines = body.splitlines()
+        full = [i for i, ln in enumerate(lines)
+                if re.search(r"s_waitcnt vmcnt\(0\)", ln) and "ASMSTART" not in lines[i - 1]]
+        assert len(full) <= 3, (name, full)

@@ -669,11 +669,12 @@ def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
 
 
 @pytest.mark.parametrize("act", [None, "bias", "gelu", "silu"])
-@pytest.mark.parametrize("M,N,K", [(4096, 4608, 512), (4608, 2048, 256)])
+@pytest.mark.parametrize("M,N,K", [(4096, 4608, 512), (8192, 2560, 256), (4608, 4096, 8320), (8192, 2304, 8448)])
 def test_gemm_fast_persistent_is_bitwise_the_one_shot_grid(M, N, K, act):
-    """Production "fast" launches the persistent grid (K >= 256); "w4_oneshot" the
+    """Production "fast" launches the persistent grid (K >= 256, more tiles than CUs); "w4_oneshot" the
     one-workgroup-per-tile grid of the same K-step: bitwise equal with every
-    epilogue, several tiles per workgroup (288 / 144 tiles), tall and wide."""
+    epilogue, more tiles than CUs (288 / 320 / 288 / 288), tall and wide, and
+    the long-K (> 8192) tile-group-8 maps."""
     from kgs.ops import gemm_nt
 
     a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
@@ -684,3 +685,34 @@ def test_gemm_fast_persistent_is_bitwise_the_one_shot_grid(M, N, K, act):
     assert torch.equal(fast, gemm_nt(a, b, variant="w4_oneshot", **kw))
     ref = _ref_nt(a, b, kw.get("bias"), kw.get("act"))
     torch.testing.assert_close(fast.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+def test_gemm_persistent_with_cus_held_by_another_kernel():
+    """A side-stream kernel whose workgroups need a CU each (the RCCL all-reduce
+    of the bench step, here the comm stand-in with 64 KiB of LDS) launched just
+    before the persistent GEMM: the GEMM's late workgroups find their tiles
+    taken by the others (per-XCD ticket queue), the result is exact, and the
+    queue is reset for the next launches on both streams."""
+    from kgs.ops import gemm_nt
+    from kgs.ops.elementwise import comm_standin
+
+    a = (torch.rand(4096, 2048, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(4608, 2048, device=DEV) * 2 - 1).bfloat16()
+    ref = gemm_nt(a, b, variant="w4_oneshot")
+    dst = torch.zeros(1 << 22, device=DEV)
+    src = torch.ones(1 << 22, device=DEV)
+    side = torch.cuda.Stream(device=DEV)
+    main = torch.cuda.current_stream(DEV)
+    outs = []
+    for _ in range(3):
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            comm_standin(dst, src, blocks=48, passes=4, lds_kb=64)
+        outs.append(gemm_nt(a, b, variant="fast"))
+        with torch.cuda.stream(side):  # a persistent GEMM on the side stream too (its own ticket slot)
+            outs.append(gemm_nt(a, b, variant="fast"))
+        main.wait_stream(side)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, ref)
+    assert torch.equal(dst, torch.full_like(dst, 12.0))

@@ -21,7 +21,8 @@ def _overlap():
 
 def test_side_stream_comm_overlaps_gemm():
     mod = _overlap()
-    args = types.SimpleNamespace(m=4096, gemms=6, bucket_mb=32.0, blocks=32, passes=2, iters=7)
+    args = types.SimpleNamespace(m=4096, gemms=6, bucket_mb=32.0, blocks=32, passes=2, iters=7, variant="auto",
+                                 standin_lds_kb=0)
     r = mod.measure(args)
     hidden = r["hidden_fraction"]
     # serial is the no-overlap reference; the bench's side stream hides a good
