@@ -66,7 +66,7 @@ _W4H_CFG = ((1, 24, 20, 1, 0), (1, 24, 20, 1, 160000), (1, 24, 20, 1, 320000), (
             (1, 24, 20, 1, 200000000))
 W4H = {f"w4h_{o}_{b}_{r}_{p}_{x}": i + 1 for i, (o, b, r, p, x) in enumerate(_W4H_CFG)}
 # round 3: the persistent four-wave kernel (native/kernels/gemm_w4p.h, named accumulator AGPRs),
-# name w4p_X -> id 101.. (X: gemm_w4.h knob bag: tile map, DMA operand order); K >= 256
+# name w4p_X -> id 101.. (X: gemm_w4.h knob bag: tile map, DMA operand order); K >= 384
 _W4P_X = (0, 140000000, 8, 10000000, 140000008, 40000000, 100000000, 200000000, 140000002)
 W4H.update({f"w4p_{x}": 101 + i for i, x in enumerate(_W4P_X)})
 # the same with the static tile walk (no ticket queue): w4ps_X -> 121..

@@ -19,7 +19,7 @@ EPI = {None: 0, "none": 0, "bias": 1, "gelu": 2, "relu": 3, "silu": 4}
 # Production kernels only; the measured alternatives and timing probes are in
 # kgs.ops.experiments (a separate, opt-in library).
 # "fast" = the four-wave kernel (gemm_w4.h), the aligned hot path, launched as the
-# persistent grid (gemm_w4p.h) when K >= 256; "w4_oneshot" = its one-shot grid
+# persistent grid (gemm_w4p.h) when K >= 384; "w4_oneshot" = its one-shot grid
 # (one workgroup per tile, for A/B and tests); "pingpong" =
 # the 8-wave kernel it replaced there (still behind bounded / fp8 / K-major).
 VARIANTS = {"auto": 0, "fast": 3, "w4": 3, "w4_oneshot": 4, "pingpong": 1, "generic": 2, "bounded": 16}

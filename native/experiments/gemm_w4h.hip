@@ -36,9 +36,9 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
     break;
   // ids: kgs/ops/experiments.py W4H (name = w4h_ORD_B1_R_P_X)
   // ids 101..: the persistent kernel (gemm_w4p.h) with knob bag X (tile map,
-  // DMA order; see gemm_w4.h tile_of / dma_any); K >= 256, one workgroup per CU
+  // DMA order; see gemm_w4.h tile_of / dma_any); K >= 384, one workgroup per CU
   if (variant > 100) {
-    if (K < 256) return KGS_ERR_SHAPE;
+    if (K < 384) return KGS_ERR_SHAPE;
     const int ntiles = (M / 256) * (N / 256);
     const dim3 pg(ntiles < cu_count() ? ntiles : cu_count());
     int* tq = kgs::tile_queue(s);

@@ -61,7 +61,6 @@
 // the in-pod hot path required by BASELINE.json configs 3-4.
 #include "gemm_pipeline.h"
 #include "gemm_w4.h"
-#include "gemm_w4p.h"
 #include "tile_queue.h"
 
 namespace kgs {
@@ -164,6 +163,11 @@ static int cu_count() {
   return n[dev];
 }
 
+// gemm_persistent.hip
+template <int EPI>
+hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned short* C, const unsigned short* bias,
+                      int M, int N, int K, int lda, int ldb, int ldc, int cus, int* tq, hipStream_t s);
+
 template <int EPI>
 static hipError_t launch(int variant, const unsigned short* A, const unsigned short* B, unsigned short* C,
                          const unsigned short* bias, int M, int N, int K, int lda, int ldb, int ldc,
@@ -173,30 +177,12 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
   const dim3 grid256((M / g256::BM) * (N / g256::BN));
   // persistent only with more tiles than CUs: with one tile per workgroup it
   // saves nothing and its ticket fetch costs (4096^3: 1483 vs 1543 one-shot)
-  const bool pers = variant == 3 && K >= 256 && (M / 256) * (N / 256) > cu_count();
+  const bool pers = variant == 3 && K >= 384 && (M / 256) * (N / 256) > cu_count();
   int* tq = pers ? tile_queue(s) : nullptr;
   if (tq) {
-    // the persistent four-wave kernel (gemm_w4p.h, round 3): one workgroup per
-    // CU walking tiles, the next tile's first K-tiles loaded under the current
-    // tile's last K-steps; bitwise the one-shot kernel. Interleaved medians vs
-    // the one-shot grid: 8192^3 1643 vs 1616, 16384^2x8192 1618 vs 1586,
-    // 8192x28672x4096 1589 vs 1545 TFLOP/s (profiles/r3/gemm_persistent.json)
-    // Long K (> 8192) takes tile groups of 8 instead of 4: 4096x8192x14336 1616
-    // vs 1590, 8192x4096x14336 (mirror) 1612 vs 1597 TFLOP/s; at K = 8192 the
-    // two are even (profiles/r3/gemm_persistent_maps_long_k.json)
-    const int tiles = (M / 256) * (N / 256), cus = cu_count();
-    const dim3 pg(tiles < cus ? tiles : cus);
-    const bool tall = M > N, longk = K > 8192;
-    if (tall && longk)
-      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 140000008>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                         ldc, tq);
-    else if (tall)
-      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 140000000>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb,
-                         ldc, tq);
-    else if (longk)
-      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 8>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
-    else
-      hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
+    // the persistent four-wave kernel (gemm_persistent.hip, round 3)
+    const hipError_t e = launch_w4p<EPI>(A, B, C, bias, M, N, K, lda, ldb, ldc, cu_count(), tq, s);
+    if (e != hipSuccess) return e;
   } else if (variant == 3 || variant == 4) {
     using Kn = w4::Knobs<256, 256>;
     if (M > N) {
@@ -269,7 +255,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
 
 // variant: 0 = auto, 1 = force the 256x256 8-wave ping-pong, 2 = force generic,
 //          3 = force the four-wave kernel (256x256 tiles; persistent when
-//          K >= 256 and there are more tiles than CUs), 4 = the four-wave
+//          K >= 384 and there are more tiles than CUs), 4 = the four-wave
 //          kernel's one-shot grid (one workgroup
 //          per tile), 16 = force the bounded 256x256 pipeline. Anything else
 //          is rejected.

@@ -1,0 +1,48 @@
+// Launcher of the persistent four-wave bf16 GEMM (gemm_w4p.h) for the aligned
+// fast path of kgs_gemm_bf16_nt (gemm_bf16.hip, variant 3 with K >= 256 and
+// more 256x256 tiles than CUs). A separate translation unit so that it and
+// gemm_bf16.hip compile in parallel.
+//
+// Measured routing (interleaved medians, TFLOP/s):
+//  * persistent vs the one-shot grid of the same K-step: 8192^3 1654 vs 1628,
+//    16384^2x8192 1628 vs 1602, 8192x28672x4096 1600 vs 1559
+//    (profiles/r3/gemm_persistent_production.json);
+//  * tall problems (M > N) take the mirrored order (GROUP_N, B's DMAs first),
+//    as the one-shot kernel does (profiles/r3/gemm_long_k.md);
+//  * long K (> 8192) takes tile groups of 8 instead of 4: 4096x8192x14336 1616
+//    vs 1590, 8192x4096x14336 (mirror) 1612 vs 1597; at K = 8192 the two are
+//    even (profiles/r3/gemm_persistent_maps_long_k.json).
+#include "gemm_w4p.h"
+
+namespace kgs {
+
+template <int EPI>
+hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned short* C, const unsigned short* bias,
+                      int M, int N, int K, int lda, int ldb, int ldc, int cus, int* tq, hipStream_t s) {
+  const int tiles = (M / 256) * (N / 256);
+  const dim3 pg(tiles < cus ? tiles : cus);
+  const bool tall = M > N, longk = K > 8192;
+  if (tall && longk)
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 140000008>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
+                       tq);
+  else if (tall)
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 140000000>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc,
+                       tq);
+  else if (longk)
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 8>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
+  else
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
+  return hipGetLastError();
+}
+
+#define KGS_LAUNCH_W4P(EPI)                                                                                         \
+  template hipError_t launch_w4p<EPI>(const unsigned short*, const unsigned short*, unsigned short*,              \
+                                      const unsigned short*, int, int, int, int, int, int, int, int*, hipStream_t);
+KGS_LAUNCH_W4P(EPI_NONE)
+KGS_LAUNCH_W4P(EPI_BIAS)
+KGS_LAUNCH_W4P(EPI_BIAS_GELU)
+KGS_LAUNCH_W4P(EPI_BIAS_RELU)
+KGS_LAUNCH_W4P(EPI_BIAS_SILU)
+#undef KGS_LAUNCH_W4P
+
+}  // namespace kgs

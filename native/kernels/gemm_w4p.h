@@ -25,10 +25,11 @@
 // on a side stream just before the GEMM) must not keep its share of tiles
 // waiting, or the whole GEMM waits for it. Workgroup b serves XCD label
 // x = b & 7 (the dispatcher deals workgroups to XCDs round robin), whose tiles
-// are the one-shot ids v = x + 8 t, t = 0, 1, ...; ticket t comes from
-// atomicAdd(q[x]). Wave 0 fetches the next tile's ticket at the top of a tile
-// and publishes it in LDS after the first K-step (its vmcnt wait has covered
-// the atomic by then); the other waves read it after the second. The last
+// are the one-shot ids v = x + 8 t, t = 0, 1, .... Its first ticket is its rank
+// among the workgroups of label x; every later one is that count plus
+// atomicAdd(q[x]) (struct Tick: issued after barrier 2 of the tile's first
+// K-step, stored to LDS after barrier 2 of the second, read by every wave
+// before the last two K-steps, which load the next tile). The last
 // workgroup to leave (exit counter q[8]) zeroes q[0..8] for the next launch on
 // the stream (tile_queue.h hands every stream its own slot).
 //
@@ -59,12 +60,25 @@ __device__ __forceinline__ void pmma(const Frag<MA, NB>& f) {
   else accr::mfma<I * NB + N>(f.b[N], f.a[I]);
 }
 
+// The next tile's ticket (DYN): wave 0 lane 0 issues the atomic right after
+// barrier 2 of a tile's K-step 0 -- after that K-step's DMAs, so the vmcnt wait
+// that barrier needs does not include it -- and stores the ticket to LDS right
+// after barrier 2 of K-step 1, whose vmcnt wait did include it (no stall if it
+// took less than a K-step). All waves read the slot before the tile's last two
+// K-steps, at least one barrier later (K >= 384).
+struct Tick {
+  int* qx;    // this label's counter (through a non-uniform address, see the kernel)
+  int* slot;  // LDS
+  int tk;
+};
+
 // gemm_w4.h's kbody with named accumulators: MFMA K of the K-step plus what
 // follows it. The DMA issues use `cd` (this tile's or the next tile's buffer
-// resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`.
-template <int ST, int X, bool ZERO, int K>
+// resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`. TK: 1 =
+// issue the ticket atomic after barrier 2, 2 = publish the ticket there.
+template <int ST, int X, bool ZERO, int TK, int K>
 __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
-                                      Frag<MA, NB>& f1) {
+                                      Frag<MA, NB>& f1, Tick& tq) {
   constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = Kn::ORD;
   constexpr int KM = S::KM, HM = S::HM, NR = S::NR, ND = w4::dma_per_stage<BM, BN>();
   if constexpr (K < KM) {
@@ -99,21 +113,27 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
     if constexpr (K == KM - R - 1) {
       w4::wait_vm<ND>();  // own DMA of the next K-tile landed
       w4::bar();
+      if constexpr (TK == 1) {
+        if (threadIdx.x == 0) tq.tk = atomicAdd(tq.qx, 1);
+      } else if constexpr (TK == 2) {
+        if (threadIdx.x == 0) *tq.slot = tq.tk;
+      }
     }
-    pbody<ST, X, ZERO, K + 1>(c, cd, sp, f0, f1);
+    pbody<ST, X, ZERO, TK, K + 1>(c, cd, sp, f0, f1, tq);
   }
 }
 
 // One K-step on stage ST; its DMAs bring K-tile kd (of cd's tile) into ST.
-template <int ST, int X, bool ZERO>
-__device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd) {
+template <int ST, int X, bool ZERO, int TK = 0>
+__device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd,
+                                      Tick& tq) {
   StepPtrs sp;
   sp.pa1 = w4::abase<BM, BN, 1>(c, ST);
   sp.pb1 = w4::bbase<BM, BN, 1>(c, ST);
   sp.pa0 = w4::abase<BM, BN, 0>(c, ST ^ 1);
   sp.pb0 = w4::bbase<BM, BN, 0>(c, ST ^ 1);
   sp.k0 = kd * BK;
-  pbody<ST, X, ZERO, 0>(c, cd, sp, f0, f1);
+  pbody<ST, X, ZERO, TK, 0>(c, cd, sp, f0, f1, tq);
 }
 
 // Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
@@ -148,7 +168,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
   return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb), 0, BN * ldb * 2, 0x00020000);
 }
 
-// Aligned shapes only (M, N % 256, K % 128 with K >= 256; 16-B operands); the
+// Aligned shapes only (M, N % 256, K % 128 with K >= 384; 16-B operands); the
 // grid is at most the tile count. X: gemm_w4.h's knob bag (tile map, DMA order).
 // q: this stream's zeroed ticket slot (tile_queue.h), zero again on return.
 // DYN = false: the static walk v, v + G, v + 2G (q unused), for measurements.
@@ -187,18 +207,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   const int x = blockIdx.x & 7;             // XCD label
   const int ntx = (ntiles - x + 7) >> 3;     // its tiles: v = x + 8 t, t < ntx
-  // DYN: t is a ticket of label x (tile v = x + 8 t, t < ntx); static: t = v
+  // DYN: t is a ticket of label x (tile v = x + 8 t, t < ntx). The first one is
+  // static, the workgroup's rank in its label (no atomic + barrier before the
+  // first DMA: that cost 1.2 % at 3 tiles per CU); the queue numbers the rest
+  // from nwx on. Static walk: t = v.
+  const int nwx = ((int)gridDim.x - x + 7) >> 3;  // workgroups of label x
   const int lim = DYN ? ntx : ntiles;
-  int t = blockIdx.x;
-  if constexpr (DYN) {
-    if (threadIdx.x == 0) tslot = atomicAdd(q + x, 1);
-    __syncthreads();
-    t = __builtin_amdgcn_readfirstlane(tslot);
-    if (t >= ntx) {  // nothing left for this workgroup (it started late)
-      if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
-        for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
-      return;
-    }
+  int t = DYN ? (int)blockIdx.x >> 3 : (int)blockIdx.x;
+  if (t >= lim) {  // (never with the host's grid <= tiles)
+    if (DYN && threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
+      for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
+    return;
   }
   int sl, tm, tn;
   w4::tile_of<X, false>(DYN ? x + 8 * t : t, ntiles, ntm, ntn, sl, tm, tn);
@@ -233,32 +252,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // K-step 0, waits only for the atomic.
   int vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-  int* const qx = q + x + vzero;
+  Tick tq{q + x + vzero, &tslot, 0};
   for (;;) {
-    int tk = 0;
-    if constexpr (DYN) {
-      if (threadIdx.x == 0) tk = atomicAdd(qx, 1);  // the next tile's ticket
+    pstep<0, X, true, DYN ? 1 : 0>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
+    pstep<1, X, false, DYN ? 2 : 0>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
+    for (int t = 2; t < nt - 2; t += 2) {
+      pstep<0, X, false>(c, c, f0, f1, t + 2, tq);
+      pstep<1, X, false>(c, c, f0, f1, t + 3, tq);
     }
-    pstep<0, X, true>(c, c, f0, f1, 2);
-    if constexpr (DYN) {
-      if (threadIdx.x == 0) tslot = tk;  // K-step 0's vmcnt wait covered the atomic
-    }
-    pstep<1, X, false>(c, c, f0, f1, 3);  // its barrier 1 publishes tslot
-    const int tnx = DYN ? __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
+    const int tnx = DYN ? nwx + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
     const bool more = tnx < lim;
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
     Ctx cn = c;
     cn.ra = rsrc_a(A, tmn, lda);
     cn.rb = rsrc_b(B, tnn, ldb);
-    for (int t = 2; t < nt - 2; t += 2) {
-      pstep<0, X, false>(c, c, f0, f1, t + 2);
-      pstep<1, X, false>(c, c, f0, f1, t + 3);
-    }
     // the last two K-steps bring the next tile's K-tiles 0 and 1 (no next tile:
     // harmless re-loads of this tile's last K-tile into the freed stages)
-    pstep<0, X, false>(c, cn, f0, f1, more ? 0 : nt - 1);
-    pstep<1, X, false>(c, cn, f0, f1, more ? 1 : nt - 1);
+    pstep<0, X, false>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
+    pstep<1, X, false>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read
     float bv[NB][4];
     {

@@ -48,7 +48,14 @@ def _resources(src: str, tmp_path) -> dict:
 
 @pytest.fixture(scope="module")
 def gemm_build(tmp_path_factory):
-    return _compile("gemm_bf16.hip", tmp_path_factory.mktemp("gemm"), save_temps=True)
+    """gemm_bf16.hip (one-shot kernels) + gemm_persistent.hip (the persistent
+    launcher), resources and assembly merged."""
+    res, asm = {}, ""
+    for src in ("gemm_bf16.hip", "gemm_persistent.hip"):
+        r, a = _compile(src, tmp_path_factory.mktemp(Path(src).stem), save_temps=True)
+        res.update(r)
+        asm += a
+    return res, asm
 
 
 def test_gemm_production_kernels_do_not_spill(gemm_build):

@@ -648,7 +648,7 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
     assert _rel_err(auto, _ref_nt(a, b)) < 1e-2
 
 
-@pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 256, "w4p_0"), (4608, 4096, 384, "w4p_0"),
+@pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 384, "w4p_0"), (4608, 4096, 384, "w4p_0"),
                                            (8192, 2304, 512, "w4p_140000000"), (1024, 768, 1024, "w4p_0")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
@@ -669,9 +669,9 @@ def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
 
 
 @pytest.mark.parametrize("act", [None, "bias", "gelu", "silu"])
-@pytest.mark.parametrize("M,N,K", [(4096, 4608, 512), (8192, 2560, 256), (4608, 4096, 8320), (8192, 2304, 8448)])
+@pytest.mark.parametrize("M,N,K", [(4096, 4608, 512), (8192, 2560, 384), (4608, 4096, 8320), (8192, 2304, 8448)])
 def test_gemm_fast_persistent_is_bitwise_the_one_shot_grid(M, N, K, act):
-    """Production "fast" launches the persistent grid (K >= 256, more tiles than CUs); "w4_oneshot" the
+    """Production "fast" launches the persistent grid (K >= 384, more tiles than CUs); "w4_oneshot" the
     one-workgroup-per-tile grid of the same K-step: bitwise equal with every
     epilogue, more tiles than CUs (288 / 320 / 288 / 288), tall and wide, and
     the long-K (> 8192) tile-group-8 maps."""
