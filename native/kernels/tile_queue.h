@@ -5,8 +5,9 @@
 // kernel ends, so the next launch on the same stream starts from zero without a
 // memset. Launches on DIFFERENT streams may run concurrently, so each
 // (device, stream) pair gets its own 64-byte slot. The pool is allocated and
-// zeroed once per device, on first use (do the first launch outside stream
-// capture); a process that uses more than SLOTS streams per device wraps
+// zeroed once per device, on first use (a first use inside hipGraph capture
+// returns nullptr and the caller runs the one-shot grid); a process that uses
+// more than SLOTS streams per device wraps
 // around, which is only safe if the wrapped streams never overlap.
 #pragma once
 
@@ -29,6 +30,10 @@ inline int* tile_queue(hipStream_t stream) {
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= TQ_DEVICES) return nullptr;
   std::lock_guard<std::mutex> lock(mu);
   if (!pool[dev]) {
+    // no allocation or device-wide sync while the stream is being captured
+    // into a hipGraph: the caller falls back to the one-shot grid
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     int* p = nullptr;
     if (hipMalloc(&p, sizeof(int) * TQ_INTS * TQ_SLOTS) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, sizeof(int) * TQ_INTS * TQ_SLOTS) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {

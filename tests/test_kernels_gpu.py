@@ -716,3 +716,25 @@ def test_gemm_persistent_with_cus_held_by_another_kernel():
     for o in outs:
         assert torch.equal(o, ref)
     assert torch.equal(dst, torch.full_like(dst, 12.0))
+
+
+def test_gemm_persistent_in_a_hip_graph_replays():
+    """The persistent GEMM captured into a hipGraph (the serving engine captures
+    its decode step, LM head included): its ticket slot is baked into the graph
+    and reset by the kernel itself, so every replay computes the full product."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(2304, 1024, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(8192, 1024, device=DEV) * 2 - 1).bfloat16()  # 9 x 32 = 288 tiles
+    ref = gemm_nt(a, b, variant="w4_oneshot")
+    out = torch.empty_like(ref)
+    gemm_nt(a, b, out=out)  # warm-up outside capture (allocates the ticket pool)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gemm_nt(a, b, out=out)
+    for _ in range(3):
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
