@@ -314,7 +314,9 @@ def gemm_swiglu(a: torch.Tensor, w_gate_up: torch.Tensor) -> torch.Tensor:
 
 FP8_DTYPE = torch.float8_e4m3fn  # OCP e4m3 -- gfx950's MFMA fp8 format (not MI300's fnuz)
 FP8_MAX = 448.0
-FP8_VARIANTS = {"auto": 0, "fast": 1, "bounded": 16}
+# fp8: "fast" = the 8-wave aligned pipeline; "w4p" = the four-wave persistent
+# kernel (gemm_w4f8.h: K >= 768, "auto" takes it with more 256x256 tiles than CUs)
+FP8_VARIANTS = {"auto": 0, "fast": 1, "w4p": 3, "bounded": 16}
 
 
 def quantize_fp8(x: torch.Tensor, scale: float | None = None) -> tuple[torch.Tensor, float]:

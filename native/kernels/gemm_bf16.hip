@@ -313,14 +313,29 @@ KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const voi
 // variant 0 = auto, 1 = aligned (M, N % 256, K % 256), 16 = bounded (any M, N;
 // K % 16). Lengths and leading dimensions are in fp8 elements (= bytes).
 // ---------------------------------------------------------------------------
+namespace kgs {
+// gemm_persistent.hip: the four-wave persistent fp8 kernel (gemm_w4f8.h)
+template <int EPI>
+hipError_t launch_fp8_w4p(const unsigned short* A, const unsigned short* B, unsigned short* C,
+                          const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
+                          const float* alpha_ptr, int cus, int* tq, hipStream_t s);
+}  // namespace kgs
+
 namespace {
 
+// v 3: the four-wave persistent kernel (aligned, Kw >= 384 words, more tiles
+// than CUs); falls back to the 8-wave aligned kernel without a ticket slot
 template <int EPI>
 hipError_t launch_fp8(int v, const unsigned short* A, const unsigned short* B, unsigned short* C,
                       const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
                       const float* alpha_ptr, hipStream_t s) {
   using namespace kgs;
   const dim3 grid_al((M / g256::BM) * (N / g256::BN));
+  if (v == 3) {
+    if (int* tq = tile_queue(s))
+      return launch_fp8_w4p<EPI>(A, B, C, bias, M, N, Kw, ldaw, ldbw, ldc, alpha, alpha_ptr, cu_count(), tq, s);
+    v = 1;
+  }
   if (v == 1) {
     hipLaunchKernelGGL((g256::gemm_nt_256<EPI, 7 + 1024>), grid_al, dim3(512), 0, s, A, B, C, bias, M, N, Kw, ldaw,
                        ldbw, ldc, alpha, alpha_ptr);
@@ -354,9 +369,13 @@ KGS_EXPORT int kgs_gemm_fp8_nt_dev(const void* A, const void* B, void* C, const 
   if (epi != kgs::EPI_NONE && (bias == nullptr || (uintptr_t)bias % 8)) return KGS_ERR_ARG;
   const int fast = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 0);
   const int bounded = kgs_gemm_fp8_nt_ok(A, B, C, M, N, K, lda, ldb, ldc, 1);
+  // the four-wave persistent kernel: K >= 768 fp8 (384 words), 32-bit offsets
+  // over a 256-row panel, more tiles than CUs (round 3, gemm_w4f8.h)
+  const int w4p = fast && K >= 768 && (long)(lda / 2) * 512 < (1L << 31) && (long)(ldb / 2) * 512 < (1L << 31);
   int v;
-  if (variant == 0) v = fast ? 1 : 16;
+  if (variant == 0) v = w4p && (M / 256) * (N / 256) > kgs::cu_count() ? 3 : fast ? 1 : 16;
   else if (variant == 1 || variant == 16) v = variant;
+  else if (variant == 3) { if (!w4p) return KGS_ERR_ALIGN; v = 3; }
   else return KGS_ERR_ARG;
   if (!(v == 16 ? bounded : fast)) return KGS_ERR_ALIGN;
   auto a = (const unsigned short*)A;

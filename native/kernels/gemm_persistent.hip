@@ -12,6 +12,7 @@
 //  * long K (> 8192) takes tile groups of 8 instead of 4: 4096x8192x14336 1616
 //    vs 1590, 8192x4096x14336 (mirror) 1612 vs 1597; at K = 8192 the two are
 //    even (profiles/r3/gemm_persistent_maps_long_k.json).
+#include "gemm_w4f8.h"
 #include "gemm_w4p.h"
 
 namespace kgs {
@@ -44,5 +45,41 @@ KGS_LAUNCH_W4P(EPI_BIAS_GELU)
 KGS_LAUNCH_W4P(EPI_BIAS_RELU)
 KGS_LAUNCH_W4P(EPI_BIAS_SILU)
 #undef KGS_LAUNCH_W4P
+
+// fp8 (e4m3): lengths and leading dimensions of A / B in 16-bit words
+template <int EPI>
+hipError_t launch_fp8_w4p(const unsigned short* A, const unsigned short* B, unsigned short* C,
+                          const unsigned short* bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
+                          const float* alpha_ptr, int cus, int* tq, hipStream_t s) {
+  // the bf16 kernel's maps, by bytes: tall problems the mirrored order, rows
+  // longer than 16 KiB (Kw > 8192 words) tile groups of 8
+  const int tiles = (M / 256) * (N / 256);
+  const dim3 pg(tiles < cus ? tiles : cus);
+  const bool tall = M > N, longk = Kw > 8192;
+  if (tall && longk)
+    hipLaunchKernelGGL((w4f8::gemm_fp8_w4p<EPI, 140000008>), pg, dim3(256), 0, s, A, B, C, bias, M, N, Kw, ldaw,
+                       ldbw, ldc, alpha, alpha_ptr, tq);
+  else if (tall)
+    hipLaunchKernelGGL((w4f8::gemm_fp8_w4p<EPI, 140000000>), pg, dim3(256), 0, s, A, B, C, bias, M, N, Kw, ldaw,
+                       ldbw, ldc, alpha, alpha_ptr, tq);
+  else if (longk)
+    hipLaunchKernelGGL((w4f8::gemm_fp8_w4p<EPI, 8>), pg, dim3(256), 0, s, A, B, C, bias, M, N, Kw, ldaw, ldbw, ldc,
+                       alpha, alpha_ptr, tq);
+  else
+    hipLaunchKernelGGL((w4f8::gemm_fp8_w4p<EPI, 0>), pg, dim3(256), 0, s, A, B, C, bias, M, N, Kw, ldaw, ldbw, ldc,
+                       alpha, alpha_ptr, tq);
+  return hipGetLastError();
+}
+
+#define KGS_LAUNCH_FP8(EPI)                                                                                      \
+  template hipError_t launch_fp8_w4p<EPI>(const unsigned short*, const unsigned short*, unsigned short*,        \
+                                          const unsigned short*, int, int, int, int, int, int, float,           \
+                                          const float*, int, int*, hipStream_t);
+KGS_LAUNCH_FP8(EPI_NONE)
+KGS_LAUNCH_FP8(EPI_BIAS)
+KGS_LAUNCH_FP8(EPI_BIAS_GELU)
+KGS_LAUNCH_FP8(EPI_BIAS_RELU)
+KGS_LAUNCH_FP8(EPI_BIAS_SILU)
+#undef KGS_LAUNCH_FP8
 
 }  // namespace kgs

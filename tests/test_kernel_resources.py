@@ -85,8 +85,8 @@ def test_four_wave_gemms_touch_agprs_only_through_named_asm(gemm_build):
     follows the last MFMA (a stale fragment: the MFMA -> VALU hazard is not
     checked by hipcc for asm MFMAs)."""
     _, asm = gemm_build
-    funcs = _functions(asm, r"gemm_nt_w4p?I")
-    assert len(funcs) >= 10 + 2 * 5, sorted(funcs)[:5]
+    funcs = _functions(asm, r"gemm_nt_w4p?I|gemm_fp8_w4pI")
+    assert len(funcs) >= 10 + 2 * 5 + 5, sorted(funcs)[:5]
     for name, body in funcs.items():
         lines = body.splitlines()
         assert not any("v_accvgpr_mov" in ln for ln in lines), name
@@ -117,8 +117,8 @@ def test_persistent_gemm_k_loop_has_no_full_vmcnt_drain(gemm_build):
     read) and a uniform-address ticket atomic (the atomic optimizer's broadcast
     waits right after it). Only the prologue's and the exit's may remain."""
     _, asm = gemm_build
-    funcs = _functions(asm, r"gemm_nt_w4pILi0E")
-    assert funcs
+    funcs = _functions(asm, r"gemm_nt_w4pILi0E|gemm_fp8_w4pILi0E")
+    assert len(funcs) >= 2
     for name, body in funcs.items():
         lines = body.splitlines()
         full = [i for i, ln in enumerate(lines)

@@ -738,3 +738,26 @@ def test_gemm_persistent_in_a_hip_graph_replays():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("act", [None, "bias", "gelu"])
+@pytest.mark.parametrize("M,N,K", [(4096, 4608, 1024), (4608, 4096, 768), (2048, 1024, 4096)])
+def test_gemm_fp8_four_wave_persistent_equals_eight_wave(M, N, K, act):
+    """The four-wave persistent fp8 kernel (gemm_w4f8.h: one 16x16x128 MFMA per
+    accumulator and K-tile, the K-step split by A rows) accumulates each output
+    over the same K-tiles in the same order as the 8-wave kernel: bitwise equal,
+    with epilogues, more tiles than CUs (288) and fewer (32), and the device
+    activation scale."""
+    from kgs.ops import gemm_fp8_nt
+
+    qa, sa, qb, sb = _fp8_pair(M, N, K, seed=5)
+    kw = {} if act is None else {"bias": torch.randn(N, device=DEV).bfloat16(), "act": None if act == "bias" else act}
+    ref8 = gemm_fp8_nt(qa, qb, sa, sb, variant="fast", **kw)
+    c = gemm_fp8_nt(qa, qb, sa, sb, variant="w4p", **kw)
+    assert torch.equal(c, ref8)
+    assert torch.equal(gemm_fp8_nt(qa, qb, sa, sb, **kw), ref8)  # auto
+    torch.testing.assert_close(c.float(), _fp8_ref(qa, sa, qb, sb, kw.get("bias"), kw.get("act")),
+                               rtol=2e-2, atol=2e-2)
+    dev_scale = torch.tensor([sa], device=DEV, dtype=torch.float32)
+    assert torch.equal(gemm_fp8_nt(qa, qb, dev_scale, sb, variant="w4p", **kw),
+                       gemm_fp8_nt(qa, qb, dev_scale, sb, variant="fast", **kw))
