@@ -50,6 +50,11 @@ BF16 = {
     "vgpr_stage2": Experiment(22, "VGPR staging, 2 phases in flight"),
 }
 FP8 = {"gm8": 17, "gm16": 18, "gm2": 19, "gn4": 20, "gn8": 21, "gn2": 22}
+# fp8 four-wave persistent kernel (gemm_w4f8.h, native/experiments/gemm_w4h.hip):
+# w4f8_X_B1_R_P -> id 40..
+_W4F8_CFG = ((0, 12, 24, 1), (0, 12, 12, 2), (0, 10, 12, 2), (0, 16, 24, 1), (0, 10, 24, 1), (0, 12, 20, 2),
+             (8, 12, 24, 1), (140000000, 12, 24, 1), (0, 14, 12, 2), (0, 12, 8, 3), (0, 10, 8, 3), (0, 12, 6, 4))
+W4F8 = {f"w4f8_{x}_{b1}_{r}_{p}": 40 + i for i, (x, b1, r, p) in enumerate(_W4F8_CFG)}
 # gemm_w4h (native/experiments/gemm_w4h.hip): 4 waves x 128x128, two barriers
 # per 128-MFMA K-step; name w4h_ORD_B1_R_P_X -> table id in gemm_w4h.hip (barrier 1 after MFMA B1, R
 # MFMAs after barrier 2, P reads per MFMA there)
@@ -89,6 +94,8 @@ def lib() -> ctypes.CDLL:
     so.kgs_gemm_stamp_n.restype = i
     so.kgs_exp_gemm_w4h.argtypes = [vp] * 3 + [i] * 7 + [vp]
     so.kgs_exp_gemm_w4h.restype = i
+    so.kgs_exp_gemm_fp8_w4f8.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
+    so.kgs_exp_gemm_fp8_w4f8.restype = i
     return so
 
 
@@ -136,6 +143,12 @@ def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, scale_a: float, scale_b: float
     N = b.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=a.device)
+    if variant in W4F8:
+        rc = lib().kgs_exp_gemm_fp8_w4f8(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
+                                         b.stride(0), out.stride(0), float(scale_a) * float(scale_b), W4F8[variant],
+                                         _lib.stream_handle(a.device))
+        _lib.check(rc, f"fp8 experiment {variant}[{M}x{N}x{K}]")
+        return out
     rc = lib().kgs_exp_gemm_fp8_nt(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0), b.stride(0),
                                    out.stride(0), float(scale_a) * float(scale_b), FP8[variant],
                                    _lib.stream_handle(a.device))

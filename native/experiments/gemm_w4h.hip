@@ -3,6 +3,7 @@
 // opt-in libkgs_experiments.so; names and ids in kgs/ops/experiments.py (W4H),
 // numbers in profiles/gemm_tuning.md ("Four-wave kernel").
 #include "gemm_w4.h"
+#include "gemm_w4f8.h"
 #include "gemm_w4p.h"
 #include "tile_queue.h"
 
@@ -93,5 +94,51 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
     default: return KGS_ERR_ARG;
   }
 #undef KGS_W4H
+  return (int)hipGetLastError();
+}
+
+// fp8 four-wave persistent kernel (gemm_w4f8.h) with schedule knobs B1 / R / P
+// and tile-map X; ids 40.. (kgs/ops/experiments.py W4F8). Aligned shapes,
+// K (fp8) >= 768 and % 256; lengths in fp8 elements.
+template <int B1_, int R_, int P_>
+struct FK {
+  static constexpr int B1 = B1_, R = R_, P = P_;
+};
+
+KGS_EXPORT int kgs_exp_gemm_fp8_w4f8(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                     int ldc, float alpha, int variant, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K < 768 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (M % 256 || N % 256 || K % 256 || lda % 16 || ldb % 16 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16) return KGS_ERR_ALIGN;
+  if ((long)(lda / 2) * 512 >= (1L << 31) || (long)(ldb / 2) * 512 >= (1L << 31)) return KGS_ERR_SHAPE;
+  int* tq = kgs::tile_queue(s);
+  if (!tq) return KGS_ERR_ARG;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  const int Kw = K / 2, ldaw = lda / 2, ldbw = ldb / 2;
+  const int ntiles = (M / 256) * (N / 256);
+  const dim3 pg(ntiles < cu_count() ? ntiles : cu_count());
+#define KGS_W4F8(ID, X, B1, R, P)                                                                                   \
+  case ID:                                                                                                          \
+    hipLaunchKernelGGL((kgs::w4f8::gemm_fp8_w4p<kgs::EPI_NONE, X, FK<B1, R, P>>), pg, dim3(256), 0, s, a, b, c,     \
+                       nullptr, M, N, Kw, ldaw, ldbw, ldc, alpha, nullptr, tq);                                     \
+    break;
+  switch (variant) {
+    KGS_W4F8(40, 0, 12, 24, 1)
+    KGS_W4F8(41, 0, 12, 12, 2)
+    KGS_W4F8(42, 0, 10, 12, 2)
+    KGS_W4F8(43, 0, 16, 24, 1)
+    KGS_W4F8(44, 0, 10, 24, 1)
+    KGS_W4F8(45, 0, 12, 20, 2)
+    KGS_W4F8(46, 8, 12, 24, 1)
+    KGS_W4F8(47, 140000000, 12, 24, 1)
+    KGS_W4F8(48, 0, 14, 12, 2)
+    KGS_W4F8(49, 0, 12, 8, 3)
+    KGS_W4F8(50, 0, 10, 8, 3)
+    KGS_W4F8(51, 0, 12, 6, 4)
+    default: return KGS_ERR_ARG;
+  }
+#undef KGS_W4F8
   return (int)hipGetLastError();
 }

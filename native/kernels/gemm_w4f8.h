@@ -21,7 +21,7 @@
 //   the 16 DMAs of K-tile t + 2 spread up to barrier 2 (vmcnt: K-tile t + 1
 //   landed, KM - R - 1), then the 24 reads of K-tile t + 1 that H1 needs first
 //   (B rows 0..7 into the other B set, A rows 0..3, whose last use was H1)
-//   one per MFMA over the last R = 24.
+//   P per MFMA over the last R (FKnobs: B1 12, R 12, P 2).
 // A: 8 x 32 B (64 VGPRs), B: two sets of 8 x 32 B (128 VGPRs): ~220 VGPRs
 // next to the 256 named accumulator AGPRs (acc_regs.h).
 #pragma once
@@ -40,10 +40,14 @@ using w4p::Tick;
 constexpr int BM = 256, BN = 256, MA = 8, NB = 8;
 using S = w4::Shape<BM, BN>;
 constexpr int KM = 64;   // MFMAs per K-step
-constexpr int B1 = 12;   // barrier 1 after MFMA B1 - 1
-constexpr int R = 24;    // MFMAs after barrier 2 (one read of K-tile t + 1 after each)
 constexpr int ND = w4::dma_per_stage<BM, BN>();
-static_assert(B1 >= 8 + 1 && KM - R >= 32 + 8, "A rows 0..3 are re-read only after H1");
+// Schedule knobs: barrier 1 after MFMA B1 - 1, R MFMAs after barrier 2, P reads
+// of K-tile t + 1 after each of them (24 reads). Production 12 / 12 / 2: the
+// DMA window grows from 28 to 40 MFMAs; 8192^3 3426 vs 3378 (12 / 24 / 1),
+// 8192x6144x4096 3129 vs 3068 TFLOP/s (profiles/r3/gemm_fp8_w4f8_knobs.json).
+struct FKnobs {
+  static constexpr int B1 = 12, R = 12, P = 2;
+};
 
 struct FragF8 {
   bf16x8 a[MA][2];     // this K-tile's A rows (two 16-byte halves)
@@ -75,8 +79,9 @@ __device__ __forceinline__ void h1_read(FragF8& f, const char* const (&pa)[2], c
 }
 
 // One MFMA slot K of the K-step on stage ST (= B set) and what follows it.
-template <int ST, int X, bool ZERO, int TK, int K>
+template <int ST, int X, bool ZERO, int TK, int B1, int R, int P, int K>
 __device__ __forceinline__ void fbody(const Ctx& c, const Ctx& cd, int k0, FragF8& f, Tick& tq) {
+  static_assert(B1 >= 8 + 1 && KM - R >= 32 + 8 && R * P >= 24, "A rows 0..3 are re-read only after H1");
   if constexpr (K < KM) {
     if constexpr (K < 32) {
       constexpr int i = w4::Order<1, 4, NB>::o.i[K], n = w4::Order<1, 4, NB>::o.n[K];
@@ -94,10 +99,11 @@ __device__ __forceinline__ void fbody(const Ctx& c, const Ctx& cd, int k0, FragF
       for (int j = 0; j < ND; ++j)
         if (B1 + (j * NW) / ND == K) w4::dma_any<BM, BN, X>(cd, ST, j, k0);
     }
-    if constexpr (K >= KM - R) {  // H1 operands of K-tile t + 1 (stage ST ^ 1, B set ST ^ 1)
+    if constexpr (K >= KM - R && (K - (KM - R)) * P < 24) {  // H1 operands of K-tile t + 1 (stage / B set ST ^ 1)
       const char* const pa[2] = {w4::abase<BM, BN, 0>(c, ST ^ 1), w4::abase<BM, BN, 1>(c, ST ^ 1)};
       const char* const pb[2] = {w4::bbase<BM, BN, 0>(c, ST ^ 1), w4::bbase<BM, BN, 1>(c, ST ^ 1)};
-      h1_read<ST ^ 1, K - (KM - R)>(f, pa, pb);
+      constexpr int e0 = (K - (KM - R)) * P;
+      w4::static_for<e0, (e0 + P < 24 ? e0 + P : 24)>([&](auto e) { h1_read<ST ^ 1, decltype(e)::value>(f, pa, pb); });
     }
     w4::fence();
     if constexpr (K == B1 - 1) {
@@ -113,13 +119,13 @@ __device__ __forceinline__ void fbody(const Ctx& c, const Ctx& cd, int k0, FragF
         if (threadIdx.x == 0) *tq.slot = tq.tk;
       }
     }
-    fbody<ST, X, ZERO, TK, K + 1>(c, cd, k0, f, tq);
+    fbody<ST, X, ZERO, TK, B1, R, P, K + 1>(c, cd, k0, f, tq);
   }
 }
 
-template <int ST, int X, bool ZERO, int TK = 0>
+template <int ST, int X, bool ZERO, int TK, class KN>
 __device__ __forceinline__ void fstep(const Ctx& c, const Ctx& cd, FragF8& f, int kd, Tick& tq) {
-  fbody<ST, X, ZERO, TK, 0>(c, cd, kd * BK, f, tq);
+  fbody<ST, X, ZERO, TK, KN::B1, KN::R, KN::P, 0>(c, cd, kd * BK, f, tq);
 }
 
 // epilogue: alpha * acc (+ bias, activation), bf16, paired n-tiles, 16-B stores
@@ -150,7 +156,7 @@ __device__ __forceinline__ void fepi(const Ctx& c, unsigned short* __restrict__ 
 // Kw / ldaw / ldbw are in 16-bit words (fp8 elements / 2); ldc in bf16
 // elements. alpha *= *alpha_ptr when alpha_ptr is given (dynamic activation
 // scale). q: this stream's ticket slot (tile_queue.h). Grid <= tiles.
-template <int EPI, int X = 0>
+template <int EPI, int X = 0, class KN = FKnobs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_fp8_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int Kw, int ldaw, int ldbw, int ldc, float alpha,
@@ -213,11 +219,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   Tick tq{q + x + vzero, &tslot, 0};
   for (;;) {
-    fstep<0, X, true, 1>(c, c, f, 2, tq);
-    fstep<1, X, false, 2>(c, c, f, 3, tq);
+    fstep<0, X, true, 1, KN>(c, c, f, 2, tq);
+    fstep<1, X, false, 2, KN>(c, c, f, 3, tq);
     for (int k = 2; k < nt - 2; k += 2) {
-      fstep<0, X, false>(c, c, f, k + 2, tq);
-      fstep<1, X, false>(c, c, f, k + 3, tq);
+      fstep<0, X, false, 0, KN>(c, c, f, k + 2, tq);
+      fstep<1, X, false, 0, KN>(c, c, f, k + 3, tq);
     }
     const int tnx = nwx + __builtin_amdgcn_readfirstlane(tslot);
     const bool more = tnx < ntx;
@@ -226,8 +232,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     Ctx cn = c;
     cn.ra = w4p::rsrc_a(A, tmn, ldaw);
     cn.rb = w4p::rsrc_b(B, tnn, ldbw);
-    fstep<0, X, false>(c, cn, f, more ? 0 : nt - 1, tq);
-    fstep<1, X, false>(c, cn, f, more ? 1 : nt - 1, tq);
+    fstep<0, X, false, 0, KN>(c, cn, f, more ? 0 : nt - 1, tq);
+    fstep<1, X, false, 0, KN>(c, cn, f, more ? 1 : nt - 1, tq);
     // MFMA -> v_accvgpr_read: the 16x16x128 fp8 MFMA has more passes than the bf16 one
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
     float bv[NB][4];
