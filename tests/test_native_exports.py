@@ -32,8 +32,9 @@ def test_public_variants_are_production_only():
     from kgs.ops import experiments
     from kgs.ops.gemm import FP8_VARIANTS, VARIANTS
 
-    assert set(VARIANTS) == {"auto", "fast", "w4", "pingpong", "generic", "bounded"}
-    assert set(FP8_VARIANTS) == {"auto", "fast", "bounded"}
+    # w4_oneshot: the four-wave kernel on its one-shot grid (the persistent grid's A/B partner)
+    assert set(VARIANTS) == {"auto", "fast", "w4", "w4_oneshot", "pingpong", "generic", "bounded"}
+    assert set(FP8_VARIANTS) == {"auto", "fast", "w4p", "bounded"}  # w4p: four-wave persistent e4m3
     probes = {k for k, e in experiments.BF16.items() if e.probe}
     assert probes == {"probe_2xmfma", "probe_l2"}
     assert not probes & set(VARIANTS)
