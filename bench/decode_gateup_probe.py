@@ -12,8 +12,9 @@ the weight-streaming floor):
   p<any of the above> the same on weights packed tile-panel major
                       (kgs.ops.gemm.pack_w4x_weight, PACKB), e.g. pswiglu_bm256_bn128
 A ``_tT`` suffix runs the four-wave kernel with T LDS stages (3 or 4).
-With ``--proj down`` (x [M, 14336] . W [4096, 14336]^T, no SwiGLU) the
-candidates are w4x_bmXXX_bnYYY[_sS], pw4x_... and hipblaslt.
+With ``--proj down`` (x [M, 14336] . W [4096, 14336]^T, no SwiGLU), ``qkv``
+([6144, 4096]) or ``o`` ([4096, 4096]) the candidates are w4x_bmXXX_bnYYY[_sS][_tT],
+pw4x_... and hipblaslt.
 One JSON line per (batch, variant): median us, weight GB/s, max rel err vs
 hipBLASLt + silu_mul.
 """
@@ -38,7 +39,8 @@ def main():
     ap.add_argument("--variants", default=(
         "swiglu_bm256_bn128,swiglu_bm256_bn256,swiglu_bm128_bn256,swiglu_bm128_bn128,"
         "sk_bn256_s2,sk_bn256_s4,sk_bn128_s2,skf_bn256_s2,skf_bn256_s4,skf_bn128_s2,hipblaslt"))
-    ap.add_argument("--proj", choices=("gateup", "down"), default="gateup")
+    ap.add_argument("--proj", choices=("gateup", "down", "qkv", "o"), default="gateup",
+                    help="down / qkv / o: a plain projection (no SwiGLU), Llama-3-8B shapes")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from kgs.ops.gemm import (gemm_nt_w4x, gemm_nt_w4x_splitk_swiglu, gemm_nt_w4x_swiglu, pack_w4x_weight,
@@ -46,8 +48,9 @@ def main():
     from kgs.ops.transformer import silu_mul
 
     dev = torch.device("cuda", 0)
-    down = a.proj == "down"
-    N, K = (a.hidden, a.inter) if down else (2 * a.inter, a.hidden)
+    down = a.proj != "gateup"  # plain projection
+    N, K = {"down": (a.hidden, a.inter), "qkv": (a.hidden + 2 * 1024, a.hidden), "o": (a.hidden, a.hidden),
+            "gateup": (2 * a.inter, a.hidden)}[a.proj]
     wbytes = N * K * 2
     ring = max(2, int(a.ring_gb * 1e9 // wbytes))
     ws = [(torch.randn(N, K, device=dev) * 0.02).bfloat16() for _ in range(ring)]

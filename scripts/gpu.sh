@@ -132,6 +132,15 @@ step() {
             --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \
             --variants ${VARIANTS:-fast} --rounds 7 --out "$O/gemm_llm.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
+        stages_probe)  # LDS stages (t2/t3/t4) x tiles on all four decode projections, HBM-streamed weights
+            run st_gateup 300 python bench/decode_gateup_probe.py --batches ${BATCHES:-128,256} \
+                --variants swiglu_bm256_bn128,swiglu_bm256_bn128_t3,pswiglu_bm256_bn128,pswiglu_bm256_bn128_t3,swiglu_bm128_bn128,swiglu_bm128_bn128_t3,swiglu_bm128_bn128_t4,swiglu_bm128_bn256_t3 \
+                --out "$O/st_gateup.json" &&
+            for P in down qkv o; do
+                run st_$P 300 python bench/decode_gateup_probe.py --proj $P --batches ${BATCHES:-128,256} \
+                    --variants pw4x_bm256_bn128_s8,pw4x_bm256_bn128_s8_t3,pw4x_bm256_bn128_s4,pw4x_bm256_bn128_s4_t3,pw4x_bm128_bn128_s8,pw4x_bm128_bn128_s8_t3,pw4x_bm128_bn128_s8_t4,pw4x_bm128_bn128_s4_t4,pw4x_bm128_bn128_s2_t4,hipblaslt \
+                    --out "$O/st_$P.json" || return 1
+            done ;;
         w4x_sweep) run w4x_sweep 600 python bench/decode_w4x_sweep.py --batches ${BATCHES:-128,256,512} \
             --shapes ${SHAPES:-qkv,o,gate_up,down} --out "$O/w4x_sweep.jsonl" ;;
         serve_sweep)
