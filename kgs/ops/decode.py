@@ -21,6 +21,7 @@ on CPU too and define the cache layout for tests).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -218,13 +219,41 @@ W4X_TUNED: dict = {
 }
 
 
+def _apply_w4x_override(spec: str) -> None:
+    """``KGS_W4X_ROUTES="256,4096,4096=128,4,128,4;..."``: (bucket, N, K) =
+    (bn, slices, bm[, stages]) entries replacing W4X_TUNED's, for same-box
+    routing A/B runs (scripts/gpu.sh route_ab); ``=none`` removes an entry."""
+    for item in filter(None, (s.strip() for s in spec.split(";"))):
+        key, _, val = item.partition("=")
+        k = tuple(int(t) for t in key.split(","))
+        if len(k) != 3 or k[0] not in _W4X_BUCKETS:
+            raise ValueError(f"KGS_W4X_ROUTES: bad key {key!r}")
+        if val.strip() == "none":
+            W4X_TUNED.pop(k, None)
+            continue
+        v = tuple(int(t) for t in val.split(","))
+        if len(v) not in (3, 4):
+            raise ValueError(f"KGS_W4X_ROUTES: bad route {val!r}")
+        W4X_TUNED[k] = v
+
+
+if os.environ.get("KGS_W4X_ROUTES"):
+    _apply_w4x_override(os.environ["KGS_W4X_ROUTES"])
+
+
 def w4x_route(m: int, n: int, k: int):
-    """(tile width, K slices, tile height) of the four-wave decode GEMM for
-    batch m, or None."""
+    """(tile width, K slices, tile height[, LDS stages]) of the four-wave
+    decode GEMM for batch m, or None. The tuple's order is
+    ``gemm_nt_w4x_partials``'s (bn, nslice, bm, stages) positional order."""
     if m < W4X_MIN_BATCH or m > 512:
         return None
     b = next(x for x in _W4X_BUCKETS if m <= x)
     return W4X_TUNED.get((b, n, k))
+
+
+def w4x_stages(route) -> int:
+    """LDS stages of a W4X_TUNED route (2 unless the entry names 3 or 4)."""
+    return route[3] if len(route) > 3 else 2
 
 
 def w4x_split_bns(n: int, k: int) -> set:

@@ -136,7 +136,7 @@ class ServingModel:
             if route is not None:
                 from kgs.ops.gemm import gemm_nt_w4x
 
-                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1], bm=route[2])
+                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1], bm=route[2], stages=D.w4x_stages(route))
         if decode:
             ns = D.splitk_slices(m, w.shape[0], w.shape[1])
             if ns == 1:
@@ -440,7 +440,7 @@ class ServingModel:
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
             if rg:
-                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], bn=rg[0], bm=rg[2])
+                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], bn=rg[0], bm=rg[2], stages=D.w4x_stages(rg))
             else:
                 act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm

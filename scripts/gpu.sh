@@ -132,6 +132,22 @@ step() {
             --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \
             --variants ${VARIANTS:-fast} --rounds 7 --out "$O/gemm_llm.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
+        route_ab)  # 128-row tiles for the split-K decode projections at 192-384 rows, then serving A/B/A
+            # with $ROUTES (KGS_W4X_ROUTES syntax) and a kernel trace of the B routes
+            for P in o qkv down; do
+                run rt_$P 300 python bench/decode_gateup_probe.py --proj $P --batches ${BATCHES:-192,256,384} \
+                    --variants pw4x_bm256_bn128_s8,pw4x_bm256_bn128_s4,pw4x_bm128_bn128_s8,pw4x_bm128_bn128_s4,pw4x_bm128_bn128_s4_t4,pw4x_bm128_bn128_s2,pw4x_bm128_bn128_s2_t4 \
+                    --out "$O/rt_$P.json" || return 1
+            done &&
+            run serve_a1 300 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
+                --max-batch 256 --max-model-len 2048 &&
+            (export KGS_W4X_ROUTES="$ROUTES"; run serve_b 300 python -u -m kgs.serve bench --requests 256 \
+                --input-len 512 --output-len 256 --max-batch 256 --max-model-len 2048) &&
+            run serve_a2 300 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
+                --max-batch 256 --max-model-len 2048 &&
+            (export KGS_W4X_ROUTES="$ROUTES"; run dtrace_b 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$O/dtrace_b" -o d -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 \
+                --max-batch 256 --max-model-len 2048) ;;
         stages_probe)  # LDS stages (t2/t3/t4) x tiles on all four decode projections, HBM-streamed weights
             run st_gateup 300 python bench/decode_gateup_probe.py --batches ${BATCHES:-128,256} \
                 --variants swiglu_bm256_bn128,swiglu_bm256_bn128_t3,pswiglu_bm256_bn128,pswiglu_bm256_bn128_t3,swiglu_bm128_bn128,swiglu_bm128_bn128_t3,swiglu_bm128_bn128_t4,swiglu_bm128_bn256_t3 \

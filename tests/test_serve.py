@@ -714,8 +714,11 @@ def test_w4x_routing_table_cpu():
     split-K workspace reserved before graph capture."""
     from kgs.ops import decode as D
 
-    for (m, n, k), (bn, ns, bm) in D.W4X_TUNED.items():
+    for (m, n, k), r in D.W4X_TUNED.items():
+        bn, ns, bm = r[:3]
+        st = D.w4x_stages(r)
         assert m in D._W4X_BUCKETS and bn in (128, 256) and bm in (128, 256), (m, n, k)
+        assert len(r) in (3, 4) and st in (2, 3, 4) and st * (bm + bn) * 128 <= 160 * 1024, (m, n, k, r)
         assert n % bn == 0 and k % ns == 0 and (k // ns) % 128 == 0, (m, n, k, ns)
         assert ns == 1 or ns * m * n <= D.SPLITK_WS_FLOATS, (m, n, k, ns)
         assert bm == 256 or m <= 128, (m, bm)  # 128-row tiles only where they pad less
