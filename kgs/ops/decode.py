@@ -211,7 +211,9 @@ W4X_TUNED: dict = {
     (64, *_DOWN): (128, 8, 128), (96, *_DOWN): (128, 8, 128), (128, *_DOWN): (128, 8, 128),  # 1.75/2.07/2.29
     (64, *_LM): (256, 1, 128), (96, *_LM): (256, 1, 128), (128, *_LM): (256, 1, 128),  # 1.18/1.22/1.24
     (192, *_QKV): (128, 4, 256), (256, *_QKV): (128, 4, 256), (384, *_QKV): (128, 2, 256),  # 1.39/1.49/1.06
-    (192, *_O): (128, 8, 256), (256, *_O): (128, 8, 256), (384, *_O): (128, 4, 256),  # 1.62/1.05/1.02
+    # o at 192-256 rows: 128-row tiles, 4 slices (half the fp32 partials of 256-row tiles x 8 slices;
+    # probe 29.6 / 30.6 vs 32.9 / 33.7 us, serving b256 +0.8 % A/B/A, profiles/r3/decode/route_ab)
+    (192, *_O): (128, 4, 128), (256, *_O): (128, 4, 128), (384, *_O): (128, 4, 256),  # -/-/1.02
     (512, *_O): (128, 4, 256),  # 1.10
     (192, *_GU): (128, 1, 256), (256, *_GU): (128, 1, 256), (512, *_GU): (256, 1, 256),  # 1.07/1.06/1.06
     (192, *_DOWN): (128, 8, 256), (256, *_DOWN): (128, 8, 256), (384, *_DOWN): (128, 4, 256),  # 2.7/1.5/1.4

@@ -264,7 +264,7 @@ def test_fp8_prefill_with_chunked_prefill():
     _oracle_check(eng, prompts, outs, tol=0.12)
 
 
-@pytest.mark.parametrize("b", [64, 128, 256])
+@pytest.mark.parametrize("b", [64, 128, 192, 256])
 def test_splitk_fused_decode_llama8b_layer(b):
     """Decode through one Llama-3-8B-shaped layer, where qkv / o / down run
     split-K on the four-wave kernel (and gate|up unsplit): with
