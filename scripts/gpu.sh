@@ -138,7 +138,8 @@ step() {
                 run rt_$P 300 python bench/decode_gateup_probe.py --proj $P --batches ${BATCHES:-192,256,384} \
                     --variants pw4x_bm256_bn128_s8,pw4x_bm256_bn128_s4,pw4x_bm128_bn128_s8,pw4x_bm128_bn128_s4,pw4x_bm128_bn128_s4_t4,pw4x_bm128_bn128_s2,pw4x_bm128_bn128_s2_t4 \
                     --out "$O/rt_$P.json" || return 1
-            done &&
+            done && step serve_ab ;;
+        serve_ab)  # batch-256 serving A/B/A: production table, $ROUTES (KGS_W4X_ROUTES), production; trace of B
             run serve_a1 300 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
                 --max-batch 256 --max-model-len 2048 &&
             (export KGS_W4X_ROUTES="$ROUTES"; run serve_b 300 python -u -m kgs.serve bench --requests 256 \
