@@ -750,3 +750,23 @@ def test_rope_packing_cpu():
     assert torch.equal(p.unpacked(), w)
     with pytest.raises(ValueError):
         D.rope_rows(n + 128, heads, hkv)
+
+
+def test_w4x_route_override_cpu():
+    """KGS_W4X_ROUTES replaces / removes W4X_TUNED entries (same-box routing A/B)
+    and rejects malformed specs."""
+    import pytest as _pytest
+
+    from kgs.ops import decode as D
+
+    saved = dict(D.W4X_TUNED)
+    try:
+        D._apply_w4x_override("256,4096,4096=128,4,128,3; 128,6144,4096=none")
+        assert D.w4x_route(256, 4096, 4096) == (128, 4, 128, 3) and D.w4x_stages(D.w4x_route(256, 4096, 4096)) == 3
+        assert D.w4x_route(128, 6144, 4096) is None
+        for bad in ("255,4096,4096=128,4,128", "256,4096=128,4,128", "256,4096,4096=128,4"):
+            with _pytest.raises(ValueError):
+                D._apply_w4x_override(bad)
+    finally:
+        D.W4X_TUNED.clear()
+        D.W4X_TUNED.update(saved)
