@@ -95,6 +95,8 @@ _SIGS = {
     "kgs_splitk_reduce_swiglu_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_paged_decode_bf16_ex": ([_c_void_p] * 8 + [_c_int] * 7 + [_c_long, _c_long, ctypes.c_float, _c_int, _c_int,
                                                                    _c_void_p], _c_int),
+    "kgs_paged_decode_rope_bf16": ([_c_void_p, _c_int] + [_c_void_p] * 11 + [_c_int] * 7 +
+                                   [_c_long, ctypes.c_float, _c_int, _c_int, _c_void_p], _c_int),
     # peer-to-peer all-reduce (native/kernels/allreduce_p2p.hip)
     "kgs_ar_signal_bytes": ([], _c_int),
     "kgs_ar_max_blocks": ([], _c_int),

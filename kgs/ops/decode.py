@@ -566,6 +566,73 @@ def decode_splits(batch: int, kv_heads: int, max_pages: int, cus: int = CUS, min
 _AWS: dict = {}
 
 
+def _attn_workspace(b: int, heads: int, kv_heads: int, nsplit: int, device) -> tuple:
+    """(po, pml, cnt) split-merge workspace of the paged decode attention
+    (None x 3 for one split); grown on demand, one per device."""
+    if nsplit <= 1:
+        return None, None, None
+    need = b * heads * nsplit
+    key = device_key(device)
+    po, pml, cnt = _AWS.get(key, (None, None, None))
+    if po is None or po.numel() < need * HEAD_DIM or cnt.numel() < b * kv_heads:
+        retire(po, pml, cnt)
+        po = torch.empty(max(need, 1 << 14) * HEAD_DIM, dtype=torch.float32, device=device)
+        pml = torch.empty(max(need, 1 << 14) * 2, dtype=torch.float32, device=device)
+        cnt = torch.zeros(max(b * kv_heads, 4096), dtype=torch.int32, device=device)
+        _AWS[key] = (po, pml, cnt)
+    return po, pml, cnt
+
+
+def rope_paged_decode_attention(partials: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
+                                positions: torch.Tensor, slots: torch.Tensor, cache_layer: torch.Tensor,
+                                block_tables: torch.Tensor, ctx_lens: torch.Tensor, heads: int, kv_heads: int,
+                                out: torch.Tensor | None = None, scale: float | None = None,
+                                pages_per_split: int | None = None, pipe: bool | None = None) -> torch.Tensor:
+    """:func:`rope_cache_` (partials form) and :func:`paged_decode_attention` in
+    ONE launch (``kgs_paged_decode_rope_bf16``): ``partials`` fp32
+    ``[nslice, B, (H + 2 HKV) * 128]`` from ``gemm_nt_w4x_partials`` of the
+    fused qkv projection. Each attention wave reduces, rotates and caches its
+    own (sequence, KV head) rows, so the rotated q never goes through memory
+    and the rope_cache launch disappears. Same cache contents and output as the
+    two launches. ``slots[b]`` must lie in the last page of ``ctx_lens[b]``
+    (the engine's assignment)."""
+    nh = heads + 2 * kv_heads
+    if partials.dtype != torch.float32 or partials.dim() != 3 or not partials.is_contiguous() or \
+            partials.shape[2] != nh * HEAD_DIM or not partials.is_cuda:
+        raise ValueError("partials must be contiguous fp32 GPU [nslice, B, (H + 2 HKV) * 128]")
+    b = partials.shape[1]
+    if heads % kv_heads or heads // kv_heads > 6:
+        raise ValueError("rope_paged_decode_attention: GQA group of at most 6 q heads per KV head")
+    for v, name in ((positions, "positions"), (slots, "slots"), (ctx_lens, "ctx_lens")):
+        if v.dtype != torch.int32 or not v.is_contiguous() or v.numel() != b:
+            raise ValueError(f"{name} must be a contiguous int32 vector of length {b}")
+    for v in (cos, sin):
+        if v.dtype != torch.float32 or not v.is_contiguous() or v.shape[-1] != HEAD_DIM // 2:
+            raise ValueError("cos/sin must be contiguous fp32 [max_pos, 64]")
+    if cache_layer.dtype not in (torch.bfloat16, FP8) or not cache_layer.is_contiguous():
+        raise ValueError("cache_layer must be a contiguous bf16 or e4m3 page array")
+    if block_tables.dtype != torch.int32 or not block_tables.is_contiguous() or block_tables.shape[0] != b:
+        raise ValueError("block_tables must be contiguous int32 [B, max_pages]")
+    max_pages = block_tables.shape[1]
+    if pages_per_split is None:
+        pps, nsplit = decode_splits(b, kv_heads, max_pages)
+    else:
+        pps, nsplit = pages_per_split, math.ceil(max_pages / pages_per_split)
+    if out is None:
+        out = torch.empty((b, heads * HEAD_DIM), dtype=torch.bfloat16, device=partials.device)
+    po, pml, cnt = _attn_workspace(b, heads, kv_heads, nsplit, partials.device)
+    scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
+    rc = _lib.lib().kgs_paged_decode_rope_bf16(
+        partials.data_ptr(), partials.shape[0], cos.data_ptr(), sin.data_ptr(), positions.data_ptr(),
+        slots.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(), ctx_lens.data_ptr(), out.data_ptr(),
+        po.data_ptr() if po is not None else None, pml.data_ptr() if pml is not None else None,
+        cnt.data_ptr() if cnt is not None else None, b, heads, kv_heads, HEAD_DIM, max_pages, pps, nsplit,
+        out.stride(0), float(scale), 1 if cache_layer.dtype == FP8 else 0, -1 if pipe is None else int(bool(pipe)),
+        _lib.stream_handle(partials.device))
+    _lib.check(rc, "rope_paged_decode_attention")
+    return out
+
+
 def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tables: torch.Tensor,
                            ctx_lens: torch.Tensor, heads: int, kv_heads: int, out: torch.Tensor | None = None,
                            scale: float | None = None, pages_per_split: int | None = None,
@@ -588,17 +655,7 @@ def paged_decode_attention(q: torch.Tensor, cache_layer: torch.Tensor, block_tab
         pps, nsplit = pages_per_split, math.ceil(max_pages / pages_per_split)
     if out is None:
         out = torch.empty((b, heads * HEAD_DIM), dtype=torch.bfloat16, device=q.device)
-    po = pml = cnt = None
-    if nsplit > 1:
-        need = b * heads * nsplit
-        key = device_key(q.device)
-        po, pml, cnt = _AWS.get(key, (None, None, None))
-        if po is None or po.numel() < need * HEAD_DIM or cnt.numel() < b * kv_heads:
-            retire(po, pml, cnt)
-            po = torch.empty(max(need, 1 << 14) * HEAD_DIM, dtype=torch.float32, device=q.device)
-            pml = torch.empty(max(need, 1 << 14) * 2, dtype=torch.float32, device=q.device)
-            cnt = torch.zeros(max(b * kv_heads, 4096), dtype=torch.int32, device=q.device)
-            _AWS[key] = (po, pml, cnt)
+    po, pml, cnt = _attn_workspace(b, heads, kv_heads, nsplit, q.device)
     scale = 1.0 / math.sqrt(HEAD_DIM) if scale is None else scale
     rc = _lib.lib().kgs_paged_decode_bf16_ex(q.data_ptr(), cache_layer.data_ptr(), block_tables.data_ptr(),
                                              ctx_lens.data_ptr(), out.data_ptr(),

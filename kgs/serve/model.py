@@ -38,6 +38,8 @@ the full-recompute oracle the tests compare generations against.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from kgs.models.llama import LlamaConfig, LlamaModel, _rms_norm
@@ -58,6 +60,8 @@ class ServingModel:
         # qkv, residual add + RMSNorm after o and down) instead of a reduce
         # launch, and an unsplit gate|up applies SwiGLU in its epilogue
         self.fuse_splitk = fuse_splitk and backend == "kgs"
+        # split-K qkv decode layers: reduce + RoPE + KV write inside the attention launch
+        self.rope_attn = os.environ.get("KGS_ROPE_ATTN", "1") != "0"
         base = LlamaModel(cfg, device=device, backend="torch" if backend == "ref" else "kgs", seed=seed)
         self.oracle = base  # same weights, full-recompute forward (tests)
         self.embed, self.norm = base.embed, base.norm
@@ -419,8 +423,16 @@ class ServingModel:
         if rq or ro or rd or rg:
             from kgs.ops.gemm import gemm_nt_w4x_partials, gemm_nt_w4x_swiglu
             from kgs.ops.transformer import splitk_add_rmsnorm
+        # split-K qkv: its reduce + RoPE + KV write run inside the attention
+        # launch (one launch per layer fewer) unless KGS_ROPE_ATTN=0
+        fused_attn = bool(rq) and self.backend == "kgs" and self.rope_attn and c.heads // c.kv_heads <= 6
         for i in range(c.layers):
-            if rq:
+            if fused_attn:
+                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)
+                a = D.rope_paged_decode_attention(part, self.cos, self.sin, positions, slots, self.cache.layer(i),
+                                                  block_tables, ctx_lens, c.heads, c.kv_heads,
+                                                  pages_per_split=pages_per_split)
+            elif rq:
                 part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)
                 qkv = torch.empty((m, part.shape[2]), dtype=torch.bfloat16, device=x.device)
                 D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(i), c.heads, c.kv_heads,
@@ -428,7 +440,9 @@ class ServingModel:
             else:
                 qkv = self._proj(y, i, "qkv", True)
                 self._rope_cache(qkv, i, positions, slots)
-            if self.backend == "ref":
+            if fused_attn:
+                pass
+            elif self.backend == "ref":
                 a = D.ref_paged_decode(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads,
                                        c.kv_heads).to(torch.bfloat16)
             else:

@@ -498,6 +498,50 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 // ---------------------------------------------------------------------------
 // RoPE + KV-cache write
 // ---------------------------------------------------------------------------
+// k / v head h (H <= h < H + 2 HKV), dims (8c.., 64+8c..) = (a, b), into cache
+// slot sl (page sl / 32, offset sl % 32) in the MFMA operand order of the pages
+template <bool KV8>
+__device__ __forceinline__ void kv_write(void* __restrict__ cache, int sl, int h, int H, int HKV, int c, bf16x8 a,
+                                         bf16x8 b) {
+  const int page = sl / PAGE, tau = sl - page * PAGE;
+  const bool isv = h >= H + HKV;
+  const int kvh = isv ? h - H - HKV : h - H;
+  const long region = (((long)page * HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
+  const int d1 = 8 * c, d2 = HD / 2 + 8 * c;
+  if constexpr (KV8) {
+    unsigned char* pg = (unsigned char*)cache + region;
+    float fa[8], fb[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      fa[e] = bf2f((unsigned short)a[e]);
+      fb[e] = bf2f((unsigned short)b[e]);
+    }
+    if (!isv) {
+      *(uint2*)(pg + kv_k_index(tau, d1)) = tfm_e4m3x8(fa);
+      *(uint2*)(pg + kv_k_index(tau, d2)) = tfm_e4m3x8(fb);
+    } else {
+      const uint2 qa = tfm_e4m3x8(fa), qb = tfm_e4m3x8(fb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pg[kv_v_index(tau, d1 + e)] = (unsigned char)(((e < 4 ? qa.x : qa.y) >> (8 * (e & 3))) & 0xff);
+        pg[kv_v_index(tau, d2 + e)] = (unsigned char)(((e < 4 ? qb.x : qb.y) >> (8 * (e & 3))) & 0xff);
+      }
+    }
+  } else {
+    unsigned short* pg = (unsigned short*)cache + region;
+    if (!isv) {
+      *(bf16x8*)(pg + kv_k_index(tau, d1)) = a;
+      *(bf16x8*)(pg + kv_k_index(tau, d2)) = b;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        pg[kv_v_index(tau, d1 + e)] = (unsigned short)a[e];
+        pg[kv_v_index(tau, d2 + e)] = (unsigned short)b[e];
+      }
+    }
+  }
+}
+
 // qkv row t: [H q heads | HKV k heads | HKV v heads] x 128. Thread = (token,
 // head among H + 2 HKV, chunk c < 8): q/k heads rotate dims (8c.., 64+8c..) in
 // place; k and v heads are also written into page slot[t] (skipped when < 0).
@@ -583,43 +627,7 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
   }
   if (h < H) return;
   if (sl < 0) return;
-  const int page = sl / PAGE, tau = sl - page * PAGE;
-  const bool isv = h >= H + HKV;
-  const int kvh = isv ? h - H - HKV : h - H;
-  const long region = (((long)page * HKV + kvh) * 2 + (isv ? 1 : 0)) * PAGE_ELEMS;
-  const int d1 = 8 * c, d2 = HD / 2 + 8 * c;
-  if constexpr (KV8) {
-    unsigned char* pg = (unsigned char*)cache + region;
-    float fa[8], fb[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      fa[e] = bf2f((unsigned short)a[e]);
-      fb[e] = bf2f((unsigned short)b[e]);
-    }
-    if (!isv) {
-      *(uint2*)(pg + kv_k_index(tau, d1)) = tfm_e4m3x8(fa);
-      *(uint2*)(pg + kv_k_index(tau, d2)) = tfm_e4m3x8(fb);
-    } else {
-      const uint2 qa = tfm_e4m3x8(fa), qb = tfm_e4m3x8(fb);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        pg[kv_v_index(tau, d1 + e)] = (unsigned char)(((e < 4 ? qa.x : qa.y) >> (8 * (e & 3))) & 0xff);
-        pg[kv_v_index(tau, d2 + e)] = (unsigned char)(((e < 4 ? qb.x : qb.y) >> (8 * (e & 3))) & 0xff);
-      }
-    }
-  } else {
-    unsigned short* pg = (unsigned short*)cache + region;
-    if (!isv) {
-      *(bf16x8*)(pg + kv_k_index(tau, d1)) = a;
-      *(bf16x8*)(pg + kv_k_index(tau, d2)) = b;
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        pg[kv_v_index(tau, d1 + e)] = (unsigned short)a[e];
-        pg[kv_v_index(tau, d2 + e)] = (unsigned short)b[e];
-      }
-    }
-  }
+  kv_write<KV8>(cache, sl, h, H, HKV, c, a, b);
 }
 
 // ---------------------------------------------------------------------------
@@ -638,6 +646,16 @@ struct AttnArgs {
   int B, H, HKV, max_pages, pages_per_split, nsplit;
   int merge;                    // nsplit > 1: 1 = last split merges in-launch, 0 = paged_reduce follows
   float sl2;                    // scale * log2(e)
+  // RP (rope prologue): q / k / v arrive as nslice fp32 split-K partials of the
+  // fused qkv projection, P[s][B][(H + 2 HKV) * 128]; the wave reduces, rotates
+  // and caches its own (sequence, KV head) rows -- rope_cache folded in
+  const float* P;
+  int nslice;
+  const float* cosv;            // [max_pos, 64]
+  const float* sinv;
+  const int* pos;               // [B]
+  const int* slot;              // [B] cache slot of the new token (< 0: no write)
+  void* cache_w;                // the same layer base as cache, writable
 };
 
 // store O^T[dim 16dt + 4g + i][head] * inv for the lane's head
@@ -657,7 +675,16 @@ __device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, f
 // PIPE (small grids, e.g. batch 1-16): the next page's loads are issued before
 // the current page is computed. With a few dozen waves on the chip no other wave
 // hides a page's HBM latency, so a split otherwise pays it once per page.
-template <bool KV8, bool PIPE = false>
+//
+// RP: the rope_cache work of this (sequence, KV head) runs first, in the wave:
+// lane (hs = lane / 8, c = lane % 8) takes head slot hs (G q heads, then the k
+// and the v head) and dims (8c.., 64+8c..), reduces the nslice partials in
+// slice order, rounds to bf16 and rotates exactly as rope_cache does. The q
+// heads go to LDS (the q fragments below are read from there), k and v to the
+// cache slot -- written by the split whose pages hold the new token, which
+// reads them back after its own stores have drained (vmcnt(0); nothing on
+// this CU has that line in L1). Every split rotates q for itself.
+template <bool KV8, bool PIPE = false, bool RP = false>
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int lane = threadIdx.x;
   const int G = a.H / a.HKV;
@@ -670,6 +697,54 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int npages = (ctx + PAGE - 1) / PAGE;
   const int p0 = sp * a.pages_per_split, p1 = min(npages, p0 + a.pages_per_split);
   const int h = kvh * G + n;
+  __shared__ __attribute__((aligned(16))) unsigned short qs[RP ? 6 * HD : 8];  // RP: G <= 6 (host check)
+
+  if constexpr (RP) {
+    const int hs = lane >> 3, c = lane & 7;
+    if (p0 < p1 && hs < G + 2) {
+      const int nh = a.H + 2 * a.HKV;
+      const int hh = hs < G ? kvh * G + hs : (hs == G ? a.H + kvh : a.H + a.HKV + kvh);
+      const int p = a.pos[b];
+      const int sl = a.slot[b];
+      const long MN = (long)a.B * nh * HD, e = (long)b * nh * HD + (long)hh * HD + 8 * c;
+      f32x4 s4[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s4[q] = *(const f32x4*)(a.P + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+      for (int si = 1; si < a.nslice; ++si)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s4[q] += *(const f32x4*)(a.P + si * MN + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+      bf16x8 ra, rb;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        ra[k] = (short)f2bf(s4[k >> 2][k & 3]);
+        rb[k] = (short)f2bf(s4[2 + (k >> 2)][k & 3]);
+      }
+      if (hs <= G) {  // q and k heads: rotate-half RoPE at position p
+        const f32x4* cp = (const f32x4*)(a.cosv + (long)p * (HD / 2) + 8 * c);
+        const f32x4* spp = (const f32x4*)(a.sinv + (long)p * (HD / 2) + 8 * c);
+        const f32x4 c0 = cp[0], c1 = cp[1], s0 = spp[0], s1 = spp[1];
+        bf16x8 o1, o2;
+#pragma unroll
+        for (int e2 = 0; e2 < 8; ++e2) {
+          const float cs = e2 < 4 ? c0[e2] : c1[e2 - 4];
+          const float sn = e2 < 4 ? s0[e2] : s1[e2 - 4];
+          const float x1 = bf2f((unsigned short)ra[e2]), x2 = bf2f((unsigned short)rb[e2]);
+          o1[e2] = (short)f2bf(x1 * cs - x2 * sn);
+          o2[e2] = (short)f2bf(x2 * cs + x1 * sn);
+        }
+        ra = o1;
+        rb = o2;
+      }
+      if (hs < G) {
+        *(bf16x8*)(qs + hs * HD + 8 * c) = ra;
+        *(bf16x8*)(qs + hs * HD + HD / 2 + 8 * c) = rb;
+      } else if (sl >= 0 && (ctx - 1) / PAGE >= p0 && (ctx - 1) / PAGE < p1) {
+        kv_write<KV8>(a.cache_w, sl, hh, a.H, a.HKV, c, ra, rb);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // cache stores landed, q in LDS
+    __syncthreads();
+  }
 
   float m = -INFINITY, lsum = 0.f;
   f32x4v acc[8];
@@ -678,9 +753,14 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
 
   if (p0 < p1) {
     bf16x8 qf[4];
-    const unsigned short* qp = a.q + (long)b * a.ldq + (long)h * HD + 8 * g;
+    if constexpr (RP) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qp + 32 * ks) : bf16x8{};
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qs + n * HD + 8 * g + 32 * ks) : bf16x8{};
+    } else {
+      const unsigned short* qp = a.q + (long)b * a.ldq + (long)h * HD + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) qf[ks] = n < G ? *(const bf16x8*)(qp + 32 * ks) : bf16x8{};
+    }
     const int* bt = a.block_tables + (long)b * a.max_pages;
     auto load_page = [&](bf16x8 (&kf)[8], bf16x8 (&vf)[8], int pi) {
       const long region = ((long)bt[pi] * a.HKV + kvh) * 2 * PAGE_ELEMS;  // elements of the K region
@@ -1151,7 +1231,8 @@ KGS_EXPORT int kgs_paged_decode_bf16_ex(const void* q, const void* cache, const 
   // the reduce launch but costs each group's last split an acquire
   const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
   AttnArgs a{(const unsigned short*)q, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po,
-             pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f};
+             pml, cnt, ldq, ldo, B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f,
+             nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr};
   // up to 4 waves per CU (1024 on the chip) other waves cannot hide a page's
   // latency: pipeline inside the wave there. Round 3 measured the pipeline at
   // 1.2-1.9x for 512-1024-wave grids (batch 64-128 at 528-2000 cached
@@ -1163,6 +1244,46 @@ KGS_EXPORT int kgs_paged_decode_bf16_ex(const void* q, const void* cache, const 
   } else {
     if (pipe) hipLaunchKernelGGL((paged_decode<false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
     else hipLaunchKernelGGL((paged_decode<false, false>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+  }
+  if (nsplit > 1 && !merge)
+    hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
+                       ldo);
+  return (int)hipGetLastError();
+}
+
+// rope_cache + paged decode attention in one launch: the fused qkv projection
+// arrives as nslice fp32 split-K partials P [nslice][B][(H + 2 HKV) * 128]
+// (gemm_nt_w4x_partials); each attention wave reduces, rotates and caches its
+// own (sequence, KV head) rows (paged_decode RP) -- the same bits as
+// kgs_rope_cache_bf16(P) followed by kgs_paged_decode_bf16 on the rotated q.
+// slot[b]: the new token's cache slot; its page must be the last one of
+// ctx_lens[b] in block_tables (as the engine assigns it).
+KGS_EXPORT int kgs_paged_decode_rope_bf16(const float* P, int nslice, const float* cosv, const float* sinv,
+                                         const int* pos, const int* slot, void* cache, const int* block_tables,
+                                         const int* ctx_lens, void* o, float* po, float* pml, int* cnt, int B, int H,
+                                         int HKV, int hd, int max_pages, int pages_per_split, int nsplit, long ldo,
+                                         float scale, int kv8, int pipe_mode, hipStream_t s) {
+  using namespace kgs::dec;
+  if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 6 || hd != HD) return KGS_ERR_SHAPE;
+  if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0 || nslice <= 0) return KGS_ERR_SHAPE;
+  if ((long)pages_per_split * nsplit < max_pages) return KGS_ERR_ARG;
+  if (ldo < (long)H * HD || ldo % 8) return KGS_ERR_SHAPE;
+  if (P == nullptr || pos == nullptr || slot == nullptr) return KGS_ERR_ARG;
+  if (!al16(P) || !al16(cosv) || !al16(sinv) || !al16(cache) || !al16(o)) return KGS_ERR_ALIGN;
+  if (nsplit > 1 && (po == nullptr || pml == nullptr || !al16(po))) return KGS_ERR_ARG;
+  const long nwg = (long)B * HKV * nsplit;
+  if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
+  const int merge = nsplit > 1 && cnt != nullptr && (long)B * HKV <= 32;
+  AttnArgs a{nullptr, (const unsigned short*)cache, block_tables, ctx_lens, (unsigned short*)o, po, pml, cnt, 0, ldo,
+             B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f,
+             P, nslice, cosv, sinv, pos, slot, cache};
+  const bool pipe = pipe_mode < 0 ? nwg <= 1024 : pipe_mode != 0;
+  if (kv8) {
+    if (pipe) hipLaunchKernelGGL((paged_decode<true, true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((paged_decode<true, false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+  } else {
+    if (pipe) hipLaunchKernelGGL((paged_decode<false, true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((paged_decode<false, false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
   }
   if (nsplit > 1 && !merge)
     hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,

@@ -139,14 +139,14 @@ step() {
                     --variants pw4x_bm256_bn128_s8,pw4x_bm256_bn128_s4,pw4x_bm128_bn128_s8,pw4x_bm128_bn128_s4,pw4x_bm128_bn128_s4_t4,pw4x_bm128_bn128_s2,pw4x_bm128_bn128_s2_t4 \
                     --out "$O/rt_$P.json" || return 1
             done && step serve_ab ;;
-        serve_ab)  # batch-256 serving A/B/A: production table, $ROUTES (KGS_W4X_ROUTES), production; trace of B
-            run serve_a1 300 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
-                --max-batch 256 --max-model-len 2048 &&
-            (export KGS_W4X_ROUTES="$ROUTES"; run serve_b 300 python -u -m kgs.serve bench --requests 256 \
-                --input-len 512 --output-len 256 --max-batch 256 --max-model-len 2048) &&
-            run serve_a2 300 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \
-                --max-batch 256 --max-model-len 2048 &&
-            (export KGS_W4X_ROUTES="$ROUTES"; run dtrace_b 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        serve_ab)  # batch-256 serving A/B/A: $AENV (e.g. KGS_ROPE_ATTN=0) vs $BENV / $ROUTES (KGS_W4X_ROUTES);
+            # kernel trace of B. AENV / BENV: one VAR=value each (optional)
+            local SA="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 --max-batch 256 --max-model-len 2048"
+            (export ${AENV:-KGS_AB=a}; run serve_a1 300 $SA) &&
+            (export ${BENV:-KGS_AB=b}; [ -n "$ROUTES" ] && export KGS_W4X_ROUTES="$ROUTES"; run serve_b 300 $SA) &&
+            (export ${AENV:-KGS_AB=a}; run serve_a2 300 $SA) &&
+            (export ${BENV:-KGS_AB=b}; [ -n "$ROUTES" ] && export KGS_W4X_ROUTES="$ROUTES"
+             run dtrace_b 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$O/dtrace_b" -o d -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 \
                 --max-batch 256 --max-model-len 2048) ;;
         stages_probe)  # LDS stages (t2/t3/t4) x tiles on all four decode projections, HBM-streamed weights

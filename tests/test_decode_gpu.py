@@ -337,6 +337,47 @@ def test_rope_cache_from_splitk_partials(kv_dtype):
     assert torch.equal(caches[0].layer(0).view(torch.uint8), caches[1].layer(0).view(torch.uint8))
 
 
+@pytest.mark.parametrize("b,kv_dtype,pps", [(4, "bf16", 2), (64, "bf16", None), (256, "bf16", None),
+                                             (256, "fp8", None), (20, "fp8", 3)])
+def test_rope_paged_decode_matches_two_launches(b, kv_dtype, pps):
+    """rope_cache (split-K partials) + paged decode attention folded into one
+    launch (kgs_paged_decode_rope_bf16): the same KV cache bytes and the same
+    attention output as the two launches, across one-split / split-with-merge /
+    split-with-reduce grids, the pipelined and the large-grid kernel, bf16 and
+    e4m3 caches, ragged contexts and scattered pages."""
+    from kgs.ops.decode import (PAGE, PagedKVCache, paged_decode_attention, rope_cache_,
+                                rope_paged_decode_attention)
+    from kgs.ops.transformer import rope_tables
+
+    heads, hkv, hd, nslice = 32, 8, 128, 4
+    nh = heads + 2 * hkv
+    g = torch.Generator(device=DEV).manual_seed(b)
+    ctxs = torch.randint(1, 300, (b,), generator=g, device=DEV).int()
+    max_pages = int((ctxs.max().item() + PAGE - 1) // PAGE)
+    npages = b * max_pages + 4
+    perm = torch.randperm(npages, generator=g, device=DEV).int()
+    bt = perm[: b * max_pages].view(b, max_pages).contiguous()
+    last = ctxs.long() - 1
+    slots = (bt.gather(1, (last // PAGE).view(-1, 1)).view(-1).long() * PAGE + last % PAGE).int().contiguous()
+    pos = last.int().contiguous()
+    cos, sin = rope_tables(4096, hd, 500000.0, DEV)
+    parts = (torch.randn(nslice, b, nh * hd, generator=g, device=DEV) * 0.5).contiguous()
+    caches = [PagedKVCache(1, npages, hkv, DEV, dtype=kv_dtype) for _ in range(2)]
+    fill = (torch.randn(caches[0].layer(0).shape, generator=g, device=DEV) * 0.5).to(caches[0].layer(0).dtype)
+    for c in caches:
+        c.layer(0).copy_(fill)
+    qkv = torch.empty((b, nh * hd), dtype=torch.bfloat16, device=DEV)
+    rope_cache_(qkv, cos, sin, pos, slots, caches[0].layer(0), heads, hkv, partials=parts)
+    ref = paged_decode_attention(qkv, caches[0].layer(0), bt, ctxs, heads, hkv, pages_per_split=pps)
+    out = rope_paged_decode_attention(parts, cos, sin, pos, slots, caches[1].layer(0), bt, ctxs, heads, hkv,
+                                      pages_per_split=pps)
+    torch.cuda.synchronize()
+    c0, c1 = caches[0].layer(0).view(torch.uint8), caches[1].layer(0).view(torch.uint8)
+    assert torch.equal(c0, c1), int((c0 != c1).sum())
+    err = ((out.float() - ref.float()).abs().max() / ref.float().abs().max()).item()
+    assert torch.equal(out, ref) or err < 1e-2, err
+
+
 @pytest.mark.parametrize("m,cols,nslice", [(256, 4096, 8), (200, 4096, 4), (130, 8192, 2)])
 def test_splitk_add_rmsnorm_matches_unfused(m, cols, nslice):
     """o / down projection partials reduced inside the residual add + RMSNorm:
