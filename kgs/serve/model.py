@@ -60,8 +60,11 @@ class ServingModel:
         # qkv, residual add + RMSNorm after o and down) instead of a reduce
         # launch, and an unsplit gate|up applies SwiGLU in its epilogue
         self.fuse_splitk = fuse_splitk and backend == "kgs"
-        # split-K qkv decode layers: reduce + RoPE + KV write inside the attention launch
-        self.rope_attn = os.environ.get("KGS_ROPE_ATTN", "1") != "0"
+        # split-K qkv decode layers: reduce + RoPE + KV write inside the attention
+        # launch (KGS_ROPE_ATTN=1). Off by default: measured 2.9 % slower at batch
+        # 256 (attention 86 -> 105 us against the 10 us rope_cache it replaces;
+        # profiles/r3/decode/README.md, run r3r)
+        self.rope_attn = os.environ.get("KGS_ROPE_ATTN", "0") == "1"
         base = LlamaModel(cfg, device=device, backend="torch" if backend == "ref" else "kgs", seed=seed)
         self.oracle = base  # same weights, full-recompute forward (tests)
         self.embed, self.norm = base.embed, base.norm
@@ -423,8 +426,8 @@ class ServingModel:
         if rq or ro or rd or rg:
             from kgs.ops.gemm import gemm_nt_w4x_partials, gemm_nt_w4x_swiglu
             from kgs.ops.transformer import splitk_add_rmsnorm
-        # split-K qkv: its reduce + RoPE + KV write run inside the attention
-        # launch (one launch per layer fewer) unless KGS_ROPE_ATTN=0
+        # split-K qkv with KGS_ROPE_ATTN=1: its reduce + RoPE + KV write run
+        # inside the attention launch (one launch per layer fewer)
         fused_attn = bool(rq) and self.backend == "kgs" and self.rope_attn and c.heads // c.kv_heads <= 6
         for i in range(c.layers):
             if fused_attn:
