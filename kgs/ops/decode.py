@@ -601,6 +601,8 @@ def rope_paged_decode_attention(partials: torch.Tensor, cos: torch.Tensor, sin: 
             partials.shape[2] != nh * HEAD_DIM or not partials.is_cuda:
         raise ValueError("partials must be contiguous fp32 GPU [nslice, B, (H + 2 HKV) * 128]")
     b = partials.shape[1]
+    if partials.shape[0] not in (2, 4, 8):
+        raise ValueError("rope_paged_decode_attention: 2, 4 or 8 K slices (compile-time in the kernel)")
     if heads % kv_heads or heads // kv_heads > 6:
         raise ValueError("rope_paged_decode_attention: GQA group of at most 6 q heads per KV head")
     for v, name in ((positions, "positions"), (slots, "slots"), (ctx_lens, "ctx_lens")):

@@ -428,7 +428,8 @@ class ServingModel:
             from kgs.ops.transformer import splitk_add_rmsnorm
         # split-K qkv with KGS_ROPE_ATTN=1: its reduce + RoPE + KV write run
         # inside the attention launch (one launch per layer fewer)
-        fused_attn = bool(rq) and self.backend == "kgs" and self.rope_attn and c.heads // c.kv_heads <= 6
+        fused_attn = bool(rq) and rq[1] in (2, 4, 8) and self.backend == "kgs" and self.rope_attn and \
+            c.heads // c.kv_heads <= 6
         for i in range(c.layers):
             if fused_attn:
                 part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)

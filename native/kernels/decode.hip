@@ -682,9 +682,11 @@ __device__ __forceinline__ void store_o(unsigned short* op, const f32x4v* acc, f
 // slice order, rounds to bf16 and rotates exactly as rope_cache does. The q
 // heads go to LDS (the q fragments below are read from there), k and v to the
 // cache slot -- written by the split whose pages hold the new token, which
-// reads them back after its own stores have drained (vmcnt(0); nothing on
-// this CU has that line in L1). Every split rotates q for itself.
-template <bool KV8, bool PIPE = false, bool RP = false>
+// reads them back after its own stores have drained (vmcnt(0) before that
+// page's loads only; nothing on this CU has that line in L1). Every split
+// rotates q for itself. RP = the slice count (2, 4 or 8): all partial loads
+// are issued before the first add, next to the position / slot loads.
+template <bool KV8, bool PIPE = false, int RP = 0>
 __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
   const int lane = threadIdx.x;
   const int G = a.H / a.HKV;
@@ -707,12 +709,18 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
       const int p = a.pos[b];
       const int sl = a.slot[b];
       const long MN = (long)a.B * nh * HD, e = (long)b * nh * HD + (long)hh * HD + 8 * c;
+      f32x4 ps[RP][4];
+#pragma unroll
+      for (int si = 0; si < RP; ++si)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ps[si][q] = *(const f32x4*)(a.P + si * MN + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
       f32x4 s4[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) s4[q] = *(const f32x4*)(a.P + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
-      for (int si = 1; si < a.nslice; ++si)
+      for (int q = 0; q < 4; ++q) {
+        s4[q] = ps[0][q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s4[q] += *(const f32x4*)(a.P + si * MN + e + (q >> 1) * (HD / 2) + (q & 1) * 4);
+        for (int si = 1; si < RP; ++si) s4[q] += ps[si][q];
+      }
       bf16x8 ra, rb;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -742,9 +750,9 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
         kv_write<KV8>(a.cache_w, sl, hh, a.H, a.HKV, c, ra, rb);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // cache stores landed, q in LDS
-    __syncthreads();
+    __syncthreads();  // q in LDS (the cache stores drain before the last page's loads)
   }
+  const int last_page = (ctx - 1) / PAGE;  // RP: the page that holds the new token
 
   float m = -INFINITY, lsum = 0.f;
   f32x4v acc[8];
@@ -763,6 +771,8 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
     }
     const int* bt = a.block_tables + (long)b * a.max_pages;
     auto load_page = [&](bf16x8 (&kf)[8], bf16x8 (&vf)[8], int pi) {
+      if constexpr (RP != 0)
+        if (pi == last_page) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // own k / v stores landed
       const long region = ((long)bt[pi] * a.HKV + kvh) * 2 * PAGE_ELEMS;  // elements of the K region
       if constexpr (KV8) {  // e4m3 pages: 8 B per lane per fragment, dequantised in registers
         const u32x2* kp = (const u32x2*)((const unsigned char*)a.cache + region) + lane;
@@ -1265,7 +1275,8 @@ KGS_EXPORT int kgs_paged_decode_rope_bf16(const float* P, int nslice, const floa
                                          float scale, int kv8, int pipe_mode, hipStream_t s) {
   using namespace kgs::dec;
   if (B <= 0 || H <= 0 || HKV <= 0 || H % HKV || H / HKV > 6 || hd != HD) return KGS_ERR_SHAPE;
-  if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0 || nslice <= 0) return KGS_ERR_SHAPE;
+  if (max_pages <= 0 || pages_per_split <= 0 || nsplit <= 0) return KGS_ERR_SHAPE;
+  if (nslice != 2 && nslice != 4 && nslice != 8) return KGS_ERR_ARG;  // compile-time slice counts
   if ((long)pages_per_split * nsplit < max_pages) return KGS_ERR_ARG;
   if (ldo < (long)H * HD || ldo % 8) return KGS_ERR_SHAPE;
   if (P == nullptr || pos == nullptr || slot == nullptr) return KGS_ERR_ARG;
@@ -1278,13 +1289,20 @@ KGS_EXPORT int kgs_paged_decode_rope_bf16(const float* P, int nslice, const floa
              B, H, HKV, max_pages, pages_per_split, nsplit, merge, scale * 1.4426950408889634f,
              P, nslice, cosv, sinv, pos, slot, cache};
   const bool pipe = pipe_mode < 0 ? nwg <= 1024 : pipe_mode != 0;
-  if (kv8) {
-    if (pipe) hipLaunchKernelGGL((paged_decode<true, true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((paged_decode<true, false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
-  } else {
-    if (pipe) hipLaunchKernelGGL((paged_decode<false, true, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
-    else hipLaunchKernelGGL((paged_decode<false, false, true>), dim3((unsigned)nwg), dim3(64), 0, s, a);
+#define KGS_PDR(KV, PP, NS) hipLaunchKernelGGL((paged_decode<KV, PP, NS>), dim3((unsigned)nwg), dim3(64), 0, s, a)
+#define KGS_PDR_NS(KV, PP)         \
+  switch (nslice) {                \
+    case 2: KGS_PDR(KV, PP, 2); break; \
+    case 4: KGS_PDR(KV, PP, 4); break; \
+    default: KGS_PDR(KV, PP, 8); break; \
   }
+  if (kv8) {
+    if (pipe) { KGS_PDR_NS(true, true); } else { KGS_PDR_NS(true, false); }
+  } else {
+    if (pipe) { KGS_PDR_NS(false, true); } else { KGS_PDR_NS(false, false); }
+  }
+#undef KGS_PDR_NS
+#undef KGS_PDR
   if (nsplit > 1 && !merge)
     hipLaunchKernelGGL(paged_reduce, dim3((unsigned)(B * H)), dim3(64), 0, s, po, pml, (unsigned short*)o, H, nsplit,
                        ldo);
