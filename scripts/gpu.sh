@@ -149,6 +149,14 @@ step() {
              run dtrace_b 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$O/dtrace_b" -o d -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 \
                 --max-batch 256 --max-model-len 2048) ;;
+        rope_attn_probe)  # two launches vs the fused rope+attention launch vs attention alone, then counters
+            run rap 200 python bench/rope_attn_probe.py &&
+            run rap_pmc_two 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
+                SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_two" -o rap \
+                -- python3 bench/rope_attn_probe.py --variants two --iters 10 &&
+            run rap_pmc_fused 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_BUSY_CYCLES \
+                SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc_fused" -o rap \
+                -- python3 bench/rope_attn_probe.py --variants fused --iters 10 ;;
         stages_probe)  # LDS stages (t2/t3/t4) x tiles on all four decode projections, HBM-streamed weights
             run st_gateup 300 python bench/decode_gateup_probe.py --batches ${BATCHES:-128,256} \
                 --variants swiglu_bm256_bn128,swiglu_bm256_bn128_t3,pswiglu_bm256_bn128,pswiglu_bm256_bn128_t3,swiglu_bm128_bn128,swiglu_bm128_bn128_t3,swiglu_bm128_bn128_t4,swiglu_bm128_bn256_t3 \
