@@ -272,6 +272,16 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm(const float* __restric
   __shared__ float red[4];
   const int row = blockIdx.x, t = threadIdx.x;
   bf16x8* xr = (bf16x8*)(x + row * ldx);
+  // the residual chunks and the norm weight are loaded next to the partials:
+  // the weight would otherwise cost a second memory round trip after the
+  // row-sum barrier
+  const bf16x8* wr = (const bf16x8*)w;
+  bf16x8 xin[NJ], wv[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    xin[j] = xr[t + 256 * j];
+    wv[j] = wr[t + 256 * j];
+  }
   float v[NJ][8];
   float ss = 0.f;
 #pragma unroll
@@ -300,7 +310,7 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm(const float* __restric
         b += *(const f32x4*)(P + sl * MN + e + 4);
       }
     }
-    const bf16x8 xv = xr[t + 256 * j];
+    const bf16x8 xv = xin[j];
     bf16x8 o;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -316,14 +326,12 @@ __global__ __launch_bounds__(256) void splitk_add_rmsnorm(const float* __restric
   __syncthreads();
   ss = (red[0] + red[1]) + (red[2] + red[3]);
   const float r = rsqrtf(ss / (float)cols + eps);
-  const bf16x8* wr = (const bf16x8*)w;
   bf16x8* yr = (bf16x8*)(y + row * ldy);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const bf16x8 wv = wr[t + 256 * j];
     bf16x8 o;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) o[k] = (short)f2bf(v[j][k] * r * bf2f((unsigned short)wv[k]));
+    for (int k = 0; k < 8; ++k) o[k] = (short)f2bf(v[j][k] * r * bf2f((unsigned short)wv[j][k]));
     yr[t + 256 * j] = o;
   }
 }
