@@ -59,6 +59,7 @@ step() {
         smoke) run smoke 300 python __graft_entry__.py smoke ;;
         bench) run bench 300 python bench.py ;;
         bench_long) run bench_long 300 python bench.py --steps 4000 --warmup 20 ;;
+        bench_fp8) run bench_fp8 300 python bench.py --dtype fp8 ;;
         gemm_sweep) run gemm_sweep 600 python bench/gemm_sweep.py --shapes 4096,8192,16384x16384x8192 \
             --variants fast --rounds 7 --out "$O/gemm_sweep.json" ;;
         gemm_trace) run gemm_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o gemm \
