@@ -33,6 +33,11 @@
 #   serve_b16    batch-16 serving; skinny_tune: skinny GEMM variant x split-K tune at batches $MS
 #   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
 #   serve_sweep  offline serving at batch 1 / 64 / 128 / 256 / 512, fp8 KV, fp8 prefill + fp8 KV (256 and 512)
+#   bench_fp8    bench.py --dtype fp8 (e4m3 operands, extra)
+#   stages_probe LDS stages x tiles on the four decode projections
+#   route_ab     128-row decode tiles probe, then serve_ab; serve_ab: batch-256 serving A/B/A with
+#                $AENV / $BENV (one VAR=value each) and $ROUTES (KGS_W4X_ROUTES), trace of B
+#   rope_attn_probe  rope_cache + attention vs the fused launch vs attention alone, with counters
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${1:?usage: gpu.sh OUT step...}
