@@ -10,8 +10,10 @@ Lifecycle (kubelet device-plugin protocol v1beta1):
    health flips (device nodes present + KFD node alive, plus amd-smi
    uncorrectable-ECC count and xGMI link status against a baseline; polled);
 5. on ``Allocate`` hand the container ``/dev/kfd`` and the allocated
-   ``/dev/dri/renderD<minor>`` nodes (ROCr only enumerates GPUs whose render node
-   it can open, so the pod sees exactly its GPUs);
+   ``/dev/dri/renderD<minor>`` nodes, plus ``ROCR_VISIBLE_DEVICES=GPU-<uuid>,...``
+   for exactly those GPUs. The device nodes isolate an unprivileged container
+   (ROCr only enumerates GPUs whose render node it can open); the UUIDs also pin
+   a privileged one, which sees every render node of its worker;
 6. ``GetPreferredAllocation`` keeps multi-GPU pods on one xGMI island / NUMA
    node (:mod:`kgs.deviceplugin.allocator`);
 7. if the kubelet restarts (it wipes the plugin directory) the plugin notices
@@ -88,7 +90,7 @@ class RealSource:
                 render_minor=g.render_minor, healthy=g.healthy, reason=g.health_reason,
                 xgmi_peers=frozenset(g.xgmi_peers()),
                 meta={"gfx": g.gfx_arch, "cus": g.cu_count, "vram_gib": round(g.vram_bytes / 2**30, 1),
-                      "uuid": g.uuid, "bdf": g.bdf},
+                      "uuid": g.uuid, "bdf": g.bdf, "rocr_uuid": g.rocr_uuid},
             ))
         self._devs = devs
 
@@ -261,6 +263,9 @@ class AmdGpuDevicePlugin:
             sick = [i for i in ids if not devs[i].healthy]
             if sick:
                 context.abort(grpc.StatusCode.FAILED_PRECONDITION, f"unhealthy devices {sick}")
+            # HIP device i of the container is the i-th GPU by KFD order, in
+            # every list below (render minors, ROCr UUIDs)
+            ids.sort(key=lambda i: devs[i].index)
             car = resp.container_responses.add()
             car.devices.extend(self.source.common_specs)
             minors = []
@@ -272,6 +277,17 @@ class AmdGpuDevicePlugin:
                 car.envs["KGS_FAKE_GPUS"] = ",".join(ids)
             else:
                 car.envs["KGS_RENDER_MINORS"] = ",".join(minors)
+                # Pin ROCr to exactly these GPUs by UUID. The device nodes
+                # alone isolate an unprivileged container, but a privileged one
+                # gets every /dev/dri node of its kind worker; an index list
+                # would name other GPUs there, a UUID cannot.
+                uuids = [devs[i].meta.get("rocr_uuid", "") for i in ids]
+                if all(uuids):
+                    car.envs["ROCR_VISIBLE_DEVICES"] = ",".join(uuids)
+                else:
+                    log.warning("Allocate %s: no KFD unique_id for %s; ROCR_VISIBLE_DEVICES not set, "
+                                "only the device nodes isolate this container", ids,
+                                [i for i, u in zip(ids, uuids) if not u])
             car.annotations["kgs.amd.com/gpus"] = ",".join(ids)
             self.allocations += 1
             log.info("Allocate: %s -> %s", ids, [d.host_path for d in car.devices])

@@ -15,8 +15,8 @@ with the kubelet's device-plugin side played by the in-tree fake kubelet
   allocate              GetPreferredAllocation + Allocate of N devices (the
                         pod-admission RPCs)
   pod-first-gemm        start the pod entrypoint as a child with exactly the
-                        Allocate response's envs, the GPUs restricted to the
-                        allocated render minors (ROCR_VISIBLE_DEVICES), until its
+                        Allocate response's envs (which pin ROCr to the
+                        allocated GPUs by UUID: ROCR_VISIBLE_DEVICES), until its
                         first checked 8192^3 GEMM result line (``KGS_FIRST_GEMM``
                         from the native probe, or the worker's result when the
                         probe is not built)
@@ -156,7 +156,8 @@ def nokind_once(gpus: int = 1, dev_root: str = "/", fake_gpus: int = 0, gemm_siz
             rec.update(device_ids=ids, device_paths=[s.host_path for s in resp.devices])
         env = dict(env_base, **envs)
         minors = [int(x) for x in envs.get("KGS_RENDER_MINORS", "").split(",") if x]
-        if minors:
+        if minors and "ROCR_VISIBLE_DEVICES" not in envs:
+            # GPUs without a KFD unique_id: Allocate could not pin by UUID
             env["ROCR_VISIBLE_DEVICES"] = visible_devices_for(minors, dev_root)
         res_path = os.path.join(d, "pod_result.json")
         cmd = [py, "-m", "kgs.workload.entrypoint", "--gemm-size", str(gemm_size), "--gemm-iters", "10",

@@ -83,6 +83,18 @@ class Gpu:
     def render_path(self) -> str:
         return f"/dev/dri/renderD{self.render_minor}"
 
+    @property
+    def rocr_uuid(self) -> str:
+        """The agent UUID ROCr reports and matches in ``ROCR_VISIBLE_DEVICES``:
+        ``GPU-`` + the KFD ``unique_id`` as 16 hex digits ("" when the kernel
+        exposes no unique_id). Unlike an index, it names the same GPU whatever
+        else the process can see (privileged or not, any enumeration order)."""
+        try:
+            uid = int(self.unique_id)
+        except (TypeError, ValueError):
+            return ""
+        return f"GPU-{uid:016x}" if uid else ""
+
     def xgmi_peers(self) -> set:
         return {lk.to_node for lk in self.links if lk.is_xgmi}
 
@@ -160,6 +172,28 @@ def discover_json(root: str = "/", use_amdsmi: bool = True) -> str:
 
 def discover(root: str | os.PathLike = "/", use_amdsmi: bool = True) -> Topology:
     return _parse(discover_json(str(root), use_amdsmi))
+
+
+def rocr_visible_devices(gpus) -> str:
+    """``ROCR_VISIBLE_DEVICES`` value pinning a process to exactly ``gpus`` (in
+    that order: HIP device i is ``gpus[i]``). Raises if a GPU has no UUID --
+    an index list would silently mean other GPUs in a privileged container."""
+    ids = [g.rocr_uuid for g in gpus]
+    missing = [g.render_minor for g, u in zip(gpus, ids) if not u]
+    if missing:
+        raise GpuInfoUnavailable(f"no KFD unique_id for renderD{missing}: cannot pin by UUID")
+    return ",".join(ids)
+
+
+def parse_rocr_uuids(value: str | None) -> list | None:
+    """The ``GPU-<hex>`` entries of a ``ROCR_VISIBLE_DEVICES`` value, lower-case;
+    None when it is unset or holds anything but UUIDs (indices)."""
+    if not value:
+        return None
+    items = [x.strip() for x in value.split(",") if x.strip()]
+    if not items or not all(x.upper().startswith("GPU-") for x in items):
+        return None
+    return ["GPU-" + x[4:].lower() for x in items]
 
 
 def health(root: str, node_id: int, render_minor: int) -> tuple:

@@ -234,8 +234,12 @@ def vllm_rocm_pod(image: str = C.VLLM_ROCM_IMAGE) -> list:
     ``config.json`` plus the serving Pod that mounts it at ``/models/llama3-8b``.
 
     Mirrors /root/reference/pods/vllm-cpu-pod.yaml:1-38 (name pattern, port
-    8000, /dev/shm memory emptyDir, privileged, GPU nodeSelector/toleration with
-    the value quoted -- Q12) with a real ``amd.com/gpu: 1``. Offline by
+    8000, /dev/shm memory emptyDir, GPU nodeSelector/toleration with the value
+    quoted -- Q12) with a real ``amd.com/gpu: 1``. NOT privileged, unlike the
+    reference's CPU pod (:24-25): a privileged container gets every render node
+    of its kind worker, so a 1-GPU pod could run on another pod's GPU. The
+    device plugin's Allocate passes /dev/kfd, the one render node and
+    ``ROCR_VISIBLE_DEVICES=GPU-<uuid>``, which is all vLLM needs. Offline by
     construction: the model is a local path (no hub id), weights are
     ``--load-format=dummy`` and ``--skip-tokenizer-init`` means no tokenizer is
     needed (requests send token ids)."""
@@ -277,7 +281,6 @@ def vllm_rocm_pod(image: str = C.VLLM_ROCM_IMAGE) -> list:
                     {"name": "dshm", "mountPath": "/dev/shm"},
                     {"name": "model-config", "mountPath": VLLM_MODEL_DIR, "readOnly": True},
                 ],
-                "securityContext": {"privileged": True},
             }],
             "nodeSelector": {C.LABEL_HARDWARE[0]: C.LABEL_HARDWARE[1]},
             "tolerations": [{"key": C.TAINT[0], "operator": "Equal", "value": C.TAINT[1], "effect": C.TAINT[2]}],

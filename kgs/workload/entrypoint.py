@@ -43,28 +43,51 @@ def _free_port() -> int:
     return port
 
 
-def allocated_gpus() -> list:
-    """GPUs visible in this container (the device plugin only passes the
-    allocated render nodes, so this is exactly the pod's allocation)."""
-    if os.environ.get("KGS_FAKE_GPUS"):
+def allocated_gpus(root: str = "/", environ=None) -> list:
+    """The pod's allocation, in HIP device order.
+
+    What the container can see is NOT assumed to be the allocation: a
+    privileged container sees every render node of its kind worker. The
+    device plugin's Allocate names the GPUs twice -- ``ROCR_VISIBLE_DEVICES``
+    (``GPU-<uuid>`` list, the order HIP numbers them) and ``KGS_RENDER_MINORS``
+    -- and both filters apply when present."""
+    env = os.environ if environ is None else environ
+    if env.get("KGS_FAKE_GPUS"):
         return []
-    if not os.path.exists("/dev/kfd"):
+    if not os.path.exists(os.path.join(root, "dev/kfd")):
         return []
     try:
         from kgs import gpuinfo
 
-        topo = gpuinfo.discover("/", use_amdsmi=False)
+        topo = gpuinfo.discover(root, use_amdsmi=False)
         gpus = [g for g in topo.gpus if g.render_node_present and g.healthy]
     except Exception:
         return []
-    # the device plugin's Allocate names the render minors (KGS_RENDER_MINORS):
-    # inside a pod they are all that is visible anyway; outside one (kgs bench
-    # --no-kind) they are what the pod would see
-    alloc = os.environ.get("KGS_RENDER_MINORS")
+    alloc = env.get("KGS_RENDER_MINORS")
     if alloc:
         want = {int(x) for x in alloc.split(",") if x.strip()}
         gpus = [g for g in gpus if g.render_minor in want]
+    uuids = gpuinfo.parse_rocr_uuids(env.get("ROCR_VISIBLE_DEVICES"))
+    if uuids is not None:
+        by_uuid = {g.rocr_uuid: g for g in gpus}
+        gpus = [by_uuid[u] for u in uuids if u in by_uuid]
     return gpus
+
+
+def pinned_env(gpus: list, environ=None) -> dict:
+    """The environment for this pod's GPU children (probe, torch workers):
+    ``ROCR_VISIBLE_DEVICES`` pinned to ``gpus`` by UUID unless Allocate already
+    pinned it. Without it a child of a privileged pod would enumerate every GPU
+    of the worker and take HIP device 0, whichever GPU that is."""
+    from kgs import gpuinfo
+
+    env = dict(os.environ if environ is None else environ)
+    if gpus and gpuinfo.parse_rocr_uuids(env.get("ROCR_VISIBLE_DEVICES")) is None:
+        try:
+            env["ROCR_VISIBLE_DEVICES"] = gpuinfo.rocr_visible_devices(gpus)
+        except gpuinfo.GpuInfoUnavailable as e:  # old kernel: only the device nodes isolate the pod
+            print(f"kgs workload: WARNING: {e}", file=sys.stderr, flush=True)
+    return env
 
 
 def probe_binary() -> str | None:
@@ -72,7 +95,7 @@ def probe_binary() -> str | None:
     return exe if os.access(exe, os.X_OK) else None
 
 
-def run_probe(size: int, timeout: int = 300) -> dict:
+def run_probe(size: int, timeout: int = 300, env: dict | None = None) -> dict:
     """Native first-GEMM probe over every GPU this process sees.
 
     The probe prints ``KGS_FIRST_GEMM {...}`` as soon as every device passed
@@ -87,21 +110,28 @@ def run_probe(size: int, timeout: int = 300) -> dict:
         return {"skipped": "kgs-gpuprobe not built (python -m kgs.utils.build)"}
     import threading
 
-    proc = subprocess.Popen([exe, "--size", str(size)], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
-    timer = threading.Timer(timeout, proc.kill)
-    timer.start()
-    res: dict | None = None
-    try:
-        for line in proc.stdout:
-            if line.startswith("KGS_FIRST_GEMM "):
-                print(line.rstrip("\n"), flush=True)
-                res = json.loads(line[len("KGS_FIRST_GEMM "):])
-            elif line.startswith("KGS_PROBE_TPUT ") and res is not None:
-                res["throughput"] = json.loads(line[len("KGS_PROBE_TPUT "):])
-        err = proc.stderr.read()
-        rc = proc.wait()
-    finally:
-        timer.cancel()
+    import tempfile
+
+    # stderr goes to a file, not a second pipe: a pipe read only after stdout's
+    # EOF fills at ~64 KiB (AMD_LOG_LEVEL output) and blocks the probe
+    with tempfile.TemporaryFile(mode="w+") as errf:
+        proc = subprocess.Popen([exe, "--size", str(size)], stdout=subprocess.PIPE, stderr=errf, text=True,
+                                env=env)
+        timer = threading.Timer(timeout, proc.kill)
+        timer.start()
+        res: dict | None = None
+        try:
+            for line in proc.stdout:
+                if line.startswith("KGS_FIRST_GEMM "):
+                    print(line.rstrip("\n"), flush=True)
+                    res = json.loads(line[len("KGS_FIRST_GEMM "):])
+                elif line.startswith("KGS_PROBE_TPUT ") and res is not None:
+                    res["throughput"] = json.loads(line[len("KGS_PROBE_TPUT "):])
+            rc = proc.wait()
+        finally:
+            timer.cancel()
+        errf.seek(0)
+        err = errf.read()
     if res is None:
         sys.stderr.write(err[-2000:])
         why = f"kgs-gpuprobe killed after {timeout}s" if rc < 0 else "no KGS_FIRST_GEMM line"
@@ -110,14 +140,14 @@ def run_probe(size: int, timeout: int = 300) -> dict:
     return res
 
 
-def rocminfo_agents(timeout: int = 60) -> dict:
+def rocminfo_agents(timeout: int = 60, env: dict | None = None) -> dict:
     """GPU agents reported by ``rocminfo`` (run as a child process: the parent
     never initialises the GPU itself)."""
     exe = shutil.which("rocminfo") or shutil.which("rocminfo", path="/opt/rocm/bin")
     if exe is None:
         return {"ok": False, "error": "rocminfo not found"}
     try:
-        r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run([exe], capture_output=True, text=True, timeout=timeout, env=env)
     except subprocess.TimeoutExpired:
         return {"ok": False, "error": "rocminfo timed out"}
     names = [ln.split(":", 1)[1].strip() for ln in r.stdout.splitlines()
@@ -179,18 +209,19 @@ def main(argv=None) -> int:
         for g in gpus:
             print(f"  renderD{g.render_minor} {g.bdf} {g.gfx_arch} {g.cu_count} CUs {g.num_xcc} XCDs "
                   f"{g.vram_bytes / 2**30:.0f} GiB numa{g.numa_node}", flush=True)
+        env = pinned_env(gpus)
+        result["rocr_visible_devices"] = env.get("ROCR_VISIBLE_DEVICES")
         if a.smoke:
-            result["rocminfo"] = rocminfo_agents()
+            result["rocminfo"] = rocminfo_agents(env=env)
             print(f"rocminfo GPU agents: {result['rocminfo'].get('gpu_agents')}", flush=True)
         if not a.smoke and not a.no_probe and a.gemm_size % 256 == 0:
-            result["first_gemm"] = run_probe(a.gemm_size, a.timeout)
+            result["first_gemm"] = run_probe(a.gemm_size, a.timeout, env)
             # only a probe that ran and failed its check fails the pod
             if "skipped" not in result["first_gemm"] and not result["first_gemm"].get("ok"):
                 result["all_ok"] = False
         if a.probe_only:
             return _finish(a, result, rc=0 if result.get("all_ok", True) else 1)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-        env = dict(os.environ)
         env["PYTHONPATH"] = root + (":" + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         worker = ["-m", "kgs.workload.worker", "--gemm-size", str(a.gemm_size), "--gemm-iters", str(a.gemm_iters)]

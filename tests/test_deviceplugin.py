@@ -78,6 +78,48 @@ def test_allocate_gives_kfd_and_render_nodes(cluster):
         assert os.path.exists(os.path.join(host, h.lstrip("/")))
 
 
+def test_allocate_pins_rocr_to_the_allocated_gpus_by_uuid(cluster):
+    """Allocate of renderD136 returns exactly that GPU's
+    ROCr UUID (GPU-<KFD unique_id as 16 hex digits>), so even a privileged
+    container -- which sees every render node of its worker -- runs on it; an
+    8-GPU allocation lists all eight, in the same order as KGS_RENDER_MINORS."""
+    kub, plug, src, host = cluster
+    d136 = next(d for d in src.devices() if d.render_minor == 136)
+    c = kub.allocate([d136.id]).container_responses[0]
+    assert c.envs["KGS_RENDER_MINORS"] == "136"
+    # fake tree: unique_id = 0xA6FF75A300000000 + index (kgs/gpuinfo/fake.py)
+    assert c.envs["ROCR_VISIBLE_DEVICES"] == f"GPU-{0xA6FF75A300000000 + d136.index:016x}" == "GPU-a6ff75a300000001"
+    ids = [d.id for d in src.devices()]
+    c8 = kub.allocate(list(reversed(ids))).container_responses[0]  # kubelet order does not matter
+    uu = c8.envs["ROCR_VISIBLE_DEVICES"].split(",")
+    assert uu == [f"GPU-{0xA6FF75A300000000 + i:016x}" for i in range(8)]
+    assert c8.envs["KGS_RENDER_MINORS"] == ",".join(str(128 + 8 * i) for i in range(8))
+    assert len(set(uu)) == 8
+
+
+def test_allocate_without_unique_id_sets_no_index_pin(short_tmp):
+    """A GPU without a KFD unique_id cannot be pinned by UUID; Allocate then
+    sets no ROCR_VISIBLE_DEVICES at all rather than an index list (which would
+    name other GPUs in a privileged container)."""
+    host = make_fake_mi355x(os.path.join(short_tmp, "h0"), n_gpus=2)
+    for p in (host / "sys/class/kfd/kfd/topology/nodes").glob("*/properties"):
+        p.write_text("".join(ln if not ln.startswith("unique_id ") else "unique_id 0\n"
+                             for ln in p.read_text().splitlines(keepends=True)))
+    dpdir = os.path.join(short_tmp, "dp0")
+    kub = FakeKubelet(dpdir)
+    kub.start()
+    src = RealSource(str(host), use_amdsmi=False)
+    plug = AmdGpuDevicePlugin(src, plugin_dir=dpdir)
+    plug.start()
+    plug.register()
+    try:
+        c = kub.allocate([src.devices()[0].id]).container_responses[0]
+        assert "ROCR_VISIBLE_DEVICES" not in c.envs and c.envs["KGS_RENDER_MINORS"] == "128"
+    finally:
+        plug.stop()
+        kub.stop()
+
+
 def test_allocate_unknown_device_rejected(cluster):
     kub, *_ = cluster
     with pytest.raises(grpc.RpcError) as ei:
@@ -261,3 +303,27 @@ def test_prometheus_metrics(cluster):
     assert "kgs_deviceplugin_registrations_total 1.0" in text
     assert "kgs_deviceplugin_health_flips_total 1.0" in text
     assert 'render_minor="136"' in text
+
+
+def test_entrypoint_does_not_assume_isolation(host8):
+    """The pod entrypoint on a privileged worker view (all 8 render nodes
+    visible): its allocation is what Allocate named, and the children it starts
+    are pinned to exactly those GPUs by UUID, in HIP device order."""
+    from kgs.workload.entrypoint import allocated_gpus, pinned_env
+
+    everything = allocated_gpus(host8, environ={})
+    assert len(everything) == 8  # no allocation envs: what is visible
+    env = {"KGS_RENDER_MINORS": "144,136"}
+    got = allocated_gpus(host8, environ=env)
+    assert sorted(g.render_minor for g in got) == [136, 144]
+    pin = pinned_env(got, environ=env)["ROCR_VISIBLE_DEVICES"]
+    assert pin == ",".join(g.rocr_uuid for g in got) and pin.count("GPU-") == 2
+    # Allocate's own pin (upper-case hex is the same UUID) wins and sets the order
+    env = {"ROCR_VISIBLE_DEVICES": "GPU-A6FF75A300000007,GPU-a6ff75a300000002"}
+    got = allocated_gpus(host8, environ=env)
+    assert [g.render_minor for g in got] == [184, 144]
+    assert pinned_env(got, environ=env)["ROCR_VISIBLE_DEVICES"] == env["ROCR_VISIBLE_DEVICES"]
+    # an index list is not a pin: replaced by the UUIDs
+    assert pinned_env(got, environ={"ROCR_VISIBLE_DEVICES": "0,1"})["ROCR_VISIBLE_DEVICES"] == \
+        "GPU-a6ff75a300000007,GPU-a6ff75a300000002"
+    assert allocated_gpus(host8, environ={"KGS_FAKE_GPUS": "fake-amdgpu-0"}) == []

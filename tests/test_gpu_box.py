@@ -212,3 +212,41 @@ def test_device_identity_is_informative():
     dom, bus, dev = bus_part.split(":")
     assert bus not in ("None", "-1"), ident
     assert uuid and uuid.strip("0-") != "", ident
+
+
+def _count_in_child(rocr: str) -> dict:
+    """A fresh child (started like the bench's ranks: a new interpreter, not an
+    exec) with ROCR_VISIBLE_DEVICES=<rocr>; reports what HIP enumerates."""
+    code = ("import json, torch; n = torch.cuda.device_count(); "
+            "print(json.dumps({'n': n, 'uuid': [str(torch.cuda.get_device_properties(i).uuid) for i in range(n)]}))")
+    env = dict(ENV, ROCR_VISIBLE_DEVICES=rocr)
+    env.pop("HIP_VISIBLE_DEVICES", None)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return _last_json(r.stdout)
+
+
+def test_rocr_uuid_pin_selects_exactly_the_allocated_gpu():
+    """VERDICT r3 next-step 1, on the MI355X: the UUID form the device plugin's
+    Allocate puts into ROCR_VISIBLE_DEVICES (GPU-<KFD unique_id hex>) names the
+    box's GPU -- with it the child sees exactly 1 device, with a UUID that
+    matches no GPU it sees 0. The plugin's own Allocate on this box returns
+    that same value."""
+    from kgs import gpuinfo
+
+    gpus = [g for g in gpuinfo.discover("/", use_amdsmi=False).gpus if g.render_minor >= 0]
+    assert gpus and all(g.rocr_uuid for g in gpus), [g.unique_id for g in gpus]
+    mine = _count_in_child(gpus[0].rocr_uuid)
+    assert mine["n"] == 1, mine
+    none = _count_in_child("GPU-00000000deadbeef")
+    assert none["n"] == 0, none
+    upper = _count_in_child("GPU-" + gpus[0].rocr_uuid[4:].upper())  # ROCr parses the hex either case
+    assert upper["n"] == 1, upper
+    r = subprocess.run([sys.executable, "-m", "kgs.deviceplugin", "--self-test",
+                        "--partition-file", "/nonexistent/gpus.json"],
+                       env=ENV, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rep = json.loads(r.stdout)
+    assert rep["allocate"]["envs"]["ROCR_VISIBLE_DEVICES"] == gpus[0].rocr_uuid, rep["allocate"]
+    print(json.dumps({"rocr_uuid": gpus[0].rocr_uuid, "visible_with_uuid": mine, "visible_with_other": none}))

@@ -61,7 +61,7 @@ def test_vllm_pod():
     args = " ".join(ctr["args"])
     assert "--dtype=bfloat16" in args and "--tensor-parallel-size=1" in args
     assert ctr["resources"]["limits"] == {"amd.com/gpu": 1}
-    assert ctr["securityContext"]["privileged"] is True
+    assert not ctr.get("securityContext", {}).get("privileged")
     assert doc["spec"]["restartPolicy"] == "Never"
     assert {"containerPort": 8000} in ctr["ports"]
 
@@ -155,8 +155,8 @@ def test_kgs_serve_pod():
     assert ctr["command"] == ["python3", "-m", "kgs.serve", "serve"]
     assert "--port=8000" in ctr["args"] and {"containerPort": 8000} in ctr["ports"]
     # same layout as the vLLM pod it stands in for
-    for key in ("resources", "securityContext"):
-        assert ctr[key] == vctr[key]
+    assert ctr["resources"] == vctr["resources"]
+    assert ctr.get("securityContext") == vctr.get("securityContext")
     assert ctr["volumeMounts"][0] == vctr["volumeMounts"][0]  # /dev/shm
     for key in ("nodeSelector", "tolerations", "restartPolicy"):
         assert doc["spec"][key] == vllm["spec"][key]
@@ -173,3 +173,23 @@ def test_kgs_serve_8gpu_pod():
     assert c8["command"] == c1["command"] and {"containerPort": 8000} in c8["ports"]
     for key in ("nodeSelector", "tolerations", "restartPolicy"):
         assert eight["spec"][key] == one["spec"][key]
+
+
+def test_no_gpu_pod_is_privileged_without_a_stated_reason():
+    """a privileged container gets every /dev/dri node
+    of its kind worker, so a GPU pod that is privileged could run on GPUs the
+    device plugin gave to another pod (or never advertised). Only the device
+    plugin's ROCR_VISIBLE_DEVICES pin would stop it; the pods must not rely on
+    that alone. A pod that really needs privilege must say why in a
+    ``# privileged because: ...`` comment."""
+    for f in sorted(glob.glob(os.path.join(PODS, "*.yaml"))):
+        with open(f) as fh:
+            text = fh.read()
+        pod = _docs(f)[-1]
+        for ctr in pod["spec"]["containers"]:
+            if ctr.get("resources", {}).get("limits", {}).get("amd.com/gpu") and \
+                    ctr.get("securityContext", {}).get("privileged"):
+                assert "# privileged because:" in text, f"{os.path.basename(f)}: privileged GPU pod, no reason"
+    # the renderers agree
+    for doc in [manifests.gpu_test_pod("x", gpus=1), manifests.vllm_rocm_pod()[-1]]:
+        assert not doc["spec"]["containers"][0].get("securityContext", {}).get("privileged")
