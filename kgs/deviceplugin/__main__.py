@@ -48,6 +48,19 @@ def make_source(a):
     return RealSource(a.dev_root, allowed, use_amdsmi=not a.no_amdsmi)
 
 
+def _loaded(name: str) -> str:
+    """Path of the first mapped shared object whose file name contains ``name``."""
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                path = line.split(None, 5)[-1].strip()
+                if name in os.path.basename(path):
+                    return path
+    except OSError:
+        pass
+    return ""
+
+
 def self_test(a) -> int:
     """Serve on a private dir with the fake kubelet; Allocate every device."""
     from .fake_kubelet import FakeKubelet
@@ -64,7 +77,12 @@ def self_test(a) -> int:
         ok = kub.wait(lambda: bool(kub.device_lists), timeout=10)
         report = {"devices": [dv.__dict__ | {"xgmi_peers": sorted(dv.xgmi_peers)} for dv in devs],
                   "kubelet_saw": kub.latest_devices(), "capacity": kub.capacity(), "allocate": None,
-                  "paths_exist": None}
+                  "paths_exist": None,
+                  # which amd-smi answered (the shipped image's lib/ or the host's)
+                  "amdsmi_used": bool(getattr(src, "amdsmi_used", False)),
+                  "amdsmi_library": getattr(src, "amdsmi_library", ""),
+                  "amdsmi_loaded_from": _loaded("libamd_smi"),
+                  "gpuinfo_loaded_from": _loaded("kgs_gpuinfo") or _loaded("_gpuinfo")}
         if ok and devs:
             resp = kub.allocate([dv.id for dv in devs])
             specs = [(s.container_path, s.host_path, s.permissions) for s in resp.container_responses[0].devices]

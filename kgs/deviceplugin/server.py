@@ -79,6 +79,8 @@ class RealSource:
         from kgs import gpuinfo
 
         topo = gpuinfo.discover(self.root, use_amdsmi=self.use_amdsmi)
+        self.amdsmi_used = topo.amdsmi_used
+        self.amdsmi_library = topo.amdsmi_library
         devs = []
         for g in topo.gpus:
             if g.render_minor < 0:

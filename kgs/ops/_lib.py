@@ -36,6 +36,7 @@ _c_long = ctypes.c_long
 
 _SIGS = {
     "kgs_gemm_bf16_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_tile_queue_stats": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
     "kgs_gemm_bf16_nt_fast_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_bounded_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
@@ -154,3 +155,12 @@ def stream_handle(device=None) -> int:
     import torch
 
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def tile_queue_stats(device: int = 0) -> dict:
+    """The persistent GEMMs' ticket-slot pool on ``device`` (tile_queue.h):
+    slots allocated, owned by streams, owned by captured launches, and the
+    launches that found no slot (they ran the one-shot grid)."""
+    out = (_c_long * 4)()
+    check(lib().kgs_tile_queue_stats(int(device), out), "kgs_tile_queue_stats")
+    return {"slots": out[0], "stream_slots": out[1], "capture_slots": out[2], "fallbacks": out[3]}

@@ -217,6 +217,17 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
 
 }  // namespace kgs
 
+// Ticket-slot pool of the persistent GEMMs on device `dev` (tile_queue.h):
+// out = {slots allocated, stream-owned, capture-owned, nullptr fallbacks}.
+KGS_EXPORT int kgs_tile_queue_stats(int dev, long* out) {
+  const kgs::TileQueueStats st = kgs::tile_queue_stats(dev);
+  out[0] = st.slots;
+  out[1] = st.stream_slots;
+  out[2] = st.capture_slots;
+  out[3] = st.fallbacks;
+  return 0;
+}
+
 // Can the 256x256 pipelined kernel take this problem?
 KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
                                         int ldb, int ldc) {

@@ -1,5 +1,5 @@
 // Launcher of the persistent four-wave bf16 GEMM (gemm_w4p.h) for the aligned
-// fast path of kgs_gemm_bf16_nt (gemm_bf16.hip, variant 3 with K >= 256 and
+// fast path of kgs_gemm_bf16_nt (gemm_bf16.hip, variant 3 with K >= 384 and
 // more 256x256 tiles than CUs). A separate translation unit so that it and
 // gemm_bf16.hip compile in parallel.
 //

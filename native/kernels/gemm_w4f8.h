@@ -155,7 +155,7 @@ __device__ __forceinline__ void fepi(const Ctx& c, unsigned short* __restrict__ 
 // words: the ticket read needs a barrier between K-step 1 and the last pair).
 // Kw / ldaw / ldbw are in 16-bit words (fp8 elements / 2); ldc in bf16
 // elements. alpha *= *alpha_ptr when alpha_ptr is given (dynamic activation
-// scale). q: this stream's ticket slot (tile_queue.h). Grid <= tiles.
+// scale). q: this launch's ticket slot (tile_queue.h). Grid <= tiles.
 template <int EPI, int X = 0, class KN = FKnobs>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_fp8_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,

@@ -31,7 +31,8 @@
 // K-step, stored to LDS after barrier 2 of the second, read by every wave
 // before the last two K-steps, which load the next tile). The last
 // workgroup to leave (exit counter q[8]) zeroes q[0..8] for the next launch on
-// the stream (tile_queue.h hands every stream its own slot).
+// the stream (tile_queue.h: every stream, and every launch captured into a
+// hipGraph, owns its slot; no two concurrent launches share one).
 //
 // K-step schedule, LDS image, DMA placement, barriers and MFMA order are
 // gemm_w4.h's (Knobs<256, 256>: B1 24, R 20, P 1, growing-square order), so the
@@ -170,7 +171,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 
 // Aligned shapes only (M, N % 256, K % 128 with K >= 384; 16-B operands); the
 // grid is at most the tile count. X: gemm_w4.h's knob bag (tile map, DMA order).
-// q: this stream's zeroed ticket slot (tile_queue.h), zero again on return.
+// q: this launch's zeroed ticket slot (tile_queue.h), zero again on return.
 // DYN = false: the static walk v, v + G, v + 2G (q unused), for measurements.
 template <int EPI, int X = 0, bool DYN = true>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(

@@ -60,7 +60,8 @@ PMC_GEMM="python3 bench/gemm_profile.py --iters 5 --torch --mnk ${MNK:-8192} --v
 
 step() {
     case "$1" in
-        tests) run tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread ;;
+        tests) KGS_EVIDENCE_DIR="$O" run tests 1100 python -u -m pytest tests -x -v -m gpu --timeout 120 \
+            --timeout-method thread ;;
         smoke) run smoke 300 python __graft_entry__.py smoke ;;
         bench) run bench 300 python bench.py ;;
         bench_long) run bench_long 300 python bench.py --steps 4000 --warmup 20 ;;

@@ -451,6 +451,7 @@ def test_entrypoint_missing_probe_does_not_fail_the_pod(tmp_path, monkeypatch):
     class G:
         render_minor, bdf, gfx_arch, cu_count, num_xcc, vram_bytes, numa_node = 128, "0000:05:00.0", "gfx950", \
             256, 8, 288 << 30, 0
+        rocr_uuid = "GPU-a6ff75a300000000"
 
     monkeypatch.setattr(entrypoint, "allocated_gpus", lambda: [G()])
     monkeypatch.setattr(entrypoint, "probe_binary", lambda: None)

@@ -217,8 +217,12 @@ def test_device_identity_is_informative():
 def _count_in_child(rocr: str) -> dict:
     """A fresh child (started like the bench's ranks: a new interpreter, not an
     exec) with ROCR_VISIBLE_DEVICES=<rocr>; reports what HIP enumerates."""
-    code = ("import json, torch; n = torch.cuda.device_count(); "
-            "print(json.dumps({'n': n, 'uuid': [str(torch.cuda.get_device_properties(i).uuid) for i in range(n)]}))")
+    # hipGetDeviceCount itself (torch.cuda.device_count() counts without
+    # initialising HIP, so it does not see the ROCr filter)
+    code = ("import ctypes, json, torch; "
+            "lib = [l.split()[-1] for l in open('/proc/self/maps') if 'libamdhip64' in l][0]; "
+            "n = ctypes.c_int(0); rc = ctypes.CDLL(lib).hipGetDeviceCount(ctypes.byref(n)); "
+            "print(json.dumps({'rc': rc, 'n': n.value if rc == 0 else 0}))")
     env = dict(ENV, ROCR_VISIBLE_DEVICES=rocr)
     env.pop("HIP_VISIBLE_DEVICES", None)
     env.pop("CUDA_VISIBLE_DEVICES", None)

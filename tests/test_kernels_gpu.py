@@ -761,3 +761,152 @@ def test_gemm_fp8_four_wave_persistent_equals_eight_wave(M, N, K, act):
     dev_scale = torch.tensor([sa], device=DEV, dtype=torch.float32)
     assert torch.equal(gemm_fp8_nt(qa, qb, dev_scale, sb, variant="w4p", **kw),
                        gemm_fp8_nt(qa, qb, dev_scale, sb, variant="fast", **kw))
+
+
+# --- ticket-queue ownership under any stream / graph use
+_QM, _QN, _QK = 4608, 4096, 1024  # 18 x 16 = 288 tiles > 256 CUs: the persistent grid
+
+
+def _queue_operands(n, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    b = (torch.rand(_QN, _QK, device=DEV, generator=g) * 2 - 1).bfloat16()
+    As = [(torch.rand(_QM, _QK, device=DEV, generator=g) * 2 - 1).bfloat16() for _ in range(n)]
+    return As, b
+
+
+def _hip_streams(n):
+    """n distinct HIP streams (torch's pool recycles 32 per priority), as
+    torch ExternalStreams, plus a destroyer."""
+    import ctypes
+
+    # the HIP runtime torch already loaded (one runtime per process)
+    hip = ctypes.CDLL([ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln][0])
+    handles = []
+    for _ in range(n):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), ctypes.c_uint(1)) == 0  # non-blocking
+        handles.append(s)
+
+    def destroy():
+        for s in handles:
+            hip.hipStreamDestroy(s)
+
+    return [torch.cuda.ExternalStream(s.value, device=DEV) for s in handles], destroy
+
+
+def test_persistent_graph_replayed_on_another_stream_while_eager_gemms_run_on_the_capture_stream():
+    """A graph captured on stream S replayed on S2 at the same time as eager
+    persistent GEMMs on S: the graph's kernel owns a slot of its own (not S's),
+    so every output is bitwise the one-shot kernel's."""
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_stats
+
+    As, b = _queue_operands(4, seed=11)
+    refs = [gemm_nt(a, b, variant="w4_oneshot") for a in As]
+    S, S2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV, priority=-1)
+    gout = torch.empty_like(refs[0])
+    with torch.cuda.stream(S):
+        gemm_nt(As[0], b, out=gout)  # eager on S first: S owns a slot, the pool exists
+    torch.cuda.synchronize()
+    st0 = tile_queue_stats()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=S):
+        gemm_nt(As[0], b, out=gout)
+    st1 = tile_queue_stats()
+    assert st1["capture_slots"] == st0["capture_slots"] + 1 and st1["fallbacks"] == st0["fallbacks"], (st0, st1)
+    eager = [torch.empty_like(refs[0]) for _ in range(3)]
+    for it in range(10):
+        gout.zero_()
+        for e in eager:
+            e.zero_()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(S2):
+            g.replay()
+        with torch.cuda.stream(S):
+            for i, e in enumerate(eager):
+                gemm_nt(As[1 + i], b, out=e)
+        torch.cuda.synchronize()
+        assert torch.equal(gout, refs[0]), it
+        for i, e in enumerate(eager):
+            assert torch.equal(e, refs[1 + i]), (it, i)
+
+
+def test_two_persistent_graphs_from_one_capture_stream_replayed_concurrently():
+    """Two graphs captured on the same stream (each with its own persistent GEMM)
+    replayed at the same time on two streams, and one graph replayed
+    concurrently with itself: outputs bitwise the one-shot kernel's, every
+    time."""
+    from kgs.ops import gemm_nt
+
+    As, b = _queue_operands(2, seed=12)
+    refs = [gemm_nt(a, b, variant="w4_oneshot") for a in As]
+    S = torch.cuda.Stream(device=DEV)
+    outs = [torch.empty_like(refs[0]) for _ in range(2)]
+    with torch.cuda.stream(S):
+        gemm_nt(As[0], b, out=outs[0])
+    torch.cuda.synchronize()
+    graphs = []
+    for i in range(2):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=S):
+            for _ in range(3):  # three launches per replay: longer overlap window
+                gemm_nt(As[i], b, out=outs[i])
+        graphs.append(g)
+    S1, S2 = torch.cuda.Stream(device=DEV), torch.cuda.Stream(device=DEV)
+    for it in range(10):
+        for o in outs:
+            o.zero_()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(S1):
+            graphs[0].replay()
+        with torch.cuda.stream(S2):
+            graphs[1].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], refs[0]) and torch.equal(outs[1], refs[1]), it
+    for it in range(5):  # one exec on two streams at once: the same product, never a skipped tile
+        outs[0].zero_()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(S1):
+            graphs[0].replay()
+        with torch.cuda.stream(S2):
+            graphs[0].replay()
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], refs[0]), it
+    # and an eager launch on each stream afterwards still starts from a zero queue
+    for s in (S, S1, S2):
+        with torch.cuda.stream(s):
+            o = gemm_nt(As[1], b)
+        torch.cuda.synchronize()
+        assert torch.equal(o, refs[1])
+
+
+def test_eighty_streams_each_launch_a_persistent_gemm():
+    """80 distinct HIP streams (more than the old pool's 64 slots, which wrapped
+    onto live ones), each launching one persistent GEMM at the same time: each
+    stream gets a slot of its own (the pool grows) and every output is bitwise
+    the one-shot kernel's."""
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_stats
+
+    As, b = _queue_operands(8, seed=13)
+    refs = [gemm_nt(a, b, variant="w4_oneshot") for a in As]
+    streams, destroy = _hip_streams(80)
+    try:
+        st0 = tile_queue_stats()
+        outs = [torch.empty_like(refs[0]) for _ in streams]
+        for rnd in range(2):
+            for o in outs:
+                o.zero_()
+            torch.cuda.synchronize()
+            for i, s in enumerate(streams):
+                with torch.cuda.stream(s):
+                    gemm_nt(As[i % len(As)], b, out=outs[i])
+            torch.cuda.synchronize()
+            bad = [i for i, o in enumerate(outs) if not torch.equal(o, refs[i % len(As)])]
+            assert not bad, (rnd, bad)
+        st1 = tile_queue_stats()
+        assert st1["stream_slots"] == st0["stream_slots"] + 80, (st0, st1)
+        assert st1["fallbacks"] == st0["fallbacks"] and st1["slots"] >= st1["stream_slots"] + st1["capture_slots"]
+    finally:
+        torch.cuda.synchronize()
+        destroy()
