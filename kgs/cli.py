@@ -9,7 +9,7 @@
   kgs bench  [--gpus=N] [--pod-gpus=M] create --gpus N -> gpu-rocm-test (M GPUs, default N) Running,
              [--sweep=1,2,4,8]        per-phase JSON; --sweep repeats it per advertised count
              [--no-kind]              the docker-free chained tail instead (plugin -> pod -> GEMM)
-  kgs images [--workload] [--plugin] build the in-tree images
+  kgs images [--workload] [--plugin] [--amdsmi-lib]  build the in-tree images
   kgs pod NAME [--registry-port=N]   print pods/NAME.yaml with the image on the
                                      configured local registry (| kubectl create -f -)
 
@@ -56,6 +56,12 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
     ap.add_argument("--base-mirror", default=C.BASE_MIRROR,
                     help="registry prefix for library base images (python, registry); reference: patch_dockerfile")
     ap.add_argument("--rocm-base-image", default=C.ROCM_BASE_IMAGE, help="PyTorch-ROCm base of the workload image")
+    ap.add_argument("--rocm-dev-image", default=C.ROCM_DEV_IMAGE,
+                    help="ROCm image the device-plugin build copies the amd-smi header and libraries from "
+                         "(docs/deviceplugin.md: pull size, lighter sources)")
+    ap.add_argument("--rocm-mirror", default=None,
+                    help=f"registry prefix replacing {C.ROCM_REGISTRY} in the ROCm image references "
+                         "(plugin amd-smi stage, workload base), e.g. a pull-through cache")
     ap.add_argument("--plugin-image", default=None, help="use a prebuilt device-plugin image")
     ap.add_argument("--skip-build", action="store_true")
     ap.add_argument("--ready-timeout", type=int, default=C.PLUGIN_READY_TIMEOUT_S)
@@ -84,6 +90,9 @@ def build_parser(prog: str = "kgs") -> argparse.ArgumentParser:
     ap.add_argument("--workload-image", default=None)
     ap.add_argument("--workload", action="store_true")
     ap.add_argument("--plugin", action="store_true")
+    ap.add_argument("--amdsmi-lib", action="store_true",
+                    help="images: build the small amd-smi source image (images/Dockerfile.amdsmi-lib) for "
+                         "--rocm-dev-image")
     ap.add_argument("-v", "--verbose", action="store_true")
     return ap
 
@@ -95,7 +104,8 @@ def settings_from(a) -> C.Settings:
         registry_bind=a.registry_bind, kind_node_image=a.kind_node_image, dry_run=a.dry_run,
         keep_on_fail=a.keep_on_fail, skip_build=a.skip_build, timings_json=a.timings_json,
         plugin_image=a.plugin_image, ready_timeout_s=a.ready_timeout, dev_root=a.dev_root,
-        base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image, extra={"serial": a.serial},
+        base_mirror=a.base_mirror, rocm_base_image=a.rocm_base_image, rocm_dev_image=a.rocm_dev_image,
+        rocm_mirror=a.rocm_mirror, extra={"serial": a.serial},
     )
 
 
@@ -177,7 +187,9 @@ def main(argv=None, prog: str = "kgs") -> int:
         if a.verb == "images":
             from .images import build_images
 
-            return build_images(p, workload=a.workload or not a.plugin, plugin=a.plugin or not a.workload)
+            only_lib = a.amdsmi_lib and not (a.workload or a.plugin)
+            return build_images(p, workload=not only_lib and (a.workload or not a.plugin),
+                                plugin=not only_lib and (a.plugin or not a.workload), amdsmi_lib=a.amdsmi_lib)
     except (ProvisionError, RuntimeNotFound) as e:
         print(str(e), file=sys.stderr)
         return 1

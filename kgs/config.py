@@ -18,6 +18,10 @@ REGISTRY_IMAGE = f"{BASE_MIRROR}/registry:2"
 # Pinned bases (the reference pins nothing for ROCm, Q6). gfx950 needs ROCm >= 7.0.
 ROCM_BASE_IMAGE = "docker.io/rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.8.0"
 ROCM_DEV_IMAGE = "docker.io/rocm/dev-ubuntu-22.04:7.0"          # amd-smi source of the plugin image
+# The ROCm release images above live on Docker Hub under this prefix;
+# --rocm-mirror=<registry>/<path> swaps it (the C13 mirror rewrite, applied to
+# the ROCm images: the reference rewrites only its library bases, :144-178).
+ROCM_REGISTRY = "docker.io/rocm"
 PY_BUILD_IMAGE = "python:3.12.8-bookworm"
 PY_SLIM_IMAGE = "python:3.12.8-slim-bookworm"
 VLLM_ROCM_IMAGE = "docker.io/rocm/vllm:rocm7.0.0_vllm_0.10.2_20251006"
@@ -94,6 +98,7 @@ class Settings:
     base_mirror: str = BASE_MIRROR       # C13: registry prefix for library base images
     rocm_base_image: str = ROCM_BASE_IMAGE
     rocm_dev_image: str = ROCM_DEV_IMAGE
+    rocm_mirror: str | None = None       # replaces ROCM_REGISTRY in the ROCm image references
     kind_node_image: str | None = None
     config_file: str = CONFIG_FILE
     dry_run: bool = False
@@ -109,6 +114,13 @@ class Settings:
         """``name`` (e.g. ``python:3.12.8-slim-bookworm``) from the configured library mirror."""
         return f"{self.base_mirror.rstrip('/')}/{name}"
 
+    def rocm_image(self, ref: str) -> str:
+        """A ROCm release image (``docker.io/rocm/<name>:<tag>``) from the
+        ``--rocm-mirror`` registry when one is set; other references as given."""
+        if self.rocm_mirror and ref.startswith(ROCM_REGISTRY + "/"):
+            return self.rocm_mirror.rstrip("/") + ref[len(ROCM_REGISTRY):]
+        return ref
+
     @property
     def registry_container_image(self) -> str:
         return self.registry_image or self.library_image("registry:2")
@@ -117,7 +129,7 @@ class Settings:
         """``--build-arg`` list for images/Dockerfile.deviceplugin."""
         return ["--build-arg", f"PY_IMAGE={self.library_image(PY_SLIM_IMAGE)}",
                 "--build-arg", f"BUILD_IMAGE={self.library_image(PY_BUILD_IMAGE)}",
-                "--build-arg", f"ROCM_IMAGE={self.rocm_dev_image}"]
+                "--build-arg", f"ROCM_IMAGE={self.rocm_image(self.rocm_dev_image)}"]
 
     @property
     def registry_host(self) -> str:

@@ -14,9 +14,21 @@ from . import config as C
 from .cluster import REPO_ROOT
 
 
-def build_images(p, workload: bool = True, plugin: bool = True) -> int:
+AMDSMI_LIB_REPO = "kgs-amdsmi-lib"
+AMDSMI_LIB_TAG = "7.0"
+
+
+def build_images(p, workload: bool = True, plugin: bool = True, amdsmi_lib: bool = False) -> int:
     rt = p.ensure_runtime()
     p.start_registry()
+    if amdsmi_lib:
+        # the light source of the plugin's amd-smi stage (images/Dockerfile.amdsmi-lib)
+        tag = f"{p.s.registry_host}/{AMDSMI_LIB_REPO}:{AMDSMI_LIB_TAG}"
+        rt.cr("build", "-t", tag, "--build-arg", f"UBUNTU_IMAGE={p.s.library_image('ubuntu:22.04')}",
+              "-f", str(REPO_ROOT / "images" / "Dockerfile.amdsmi-lib"), str(REPO_ROOT))
+        if rt.name == "docker":
+            rt.cr("push", tag)
+        print(f"amd-smi stage image: {tag}  (use: --rocm-dev-image={tag})")
     if plugin:
         tag = f"{p.s.registry_host}/{C.PLUGIN_IMAGE_REPO}:{C.PLUGIN_IMAGE_TAG}"
         rt.cr("build", "-t", tag, *p.s.plugin_build_args(),
@@ -26,7 +38,7 @@ def build_images(p, workload: bool = True, plugin: bool = True) -> int:
     if workload:
         if p.topology is None and p.s.fake_gpus is None:
             p.discover()
-        base = p.s.library_image(C.PY_SLIM_IMAGE) if p.fake else p.s.rocm_base_image
+        base = p.s.library_image(C.PY_SLIM_IMAGE) if p.fake else p.s.rocm_image(p.s.rocm_base_image)
         tag = f"{p.s.registry_host}/{C.WORKLOAD_IMAGE_REPO}:{C.WORKLOAD_IMAGE_TAG}"
         rt.cr("build", "-t", tag, "--build-arg", f"BASE_IMAGE={base}",
               "--build-arg", f"BUILD_NATIVE={'0' if p.fake else '1'}",

@@ -52,6 +52,7 @@ _SIGS = {
     "kgs_gemm_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 9 + [_c_void_p], _c_int),
     "kgs_gemm_bf16_layout_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8, _c_int),
     "kgs_vector_add_f32": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
+    "kgs_cu_hold": ([_c_int, ctypes.c_double, _c_int, _c_void_p], _c_int),
     "kgs_comm_standin_f32": ([_c_void_p, _c_void_p, _c_long, _c_int, _c_int, _c_int, _c_void_p], _c_int),
     "kgs_vector_add_bf16": ([_c_void_p, _c_void_p, _c_void_p, _c_long, _c_void_p], _c_int),
     "kgs_transpose_bf16": ([_c_void_p, _c_void_p, _c_int, _c_int, _c_int, _c_int, _c_void_p], _c_int),

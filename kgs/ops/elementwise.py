@@ -51,6 +51,15 @@ def comm_standin(dst: torch.Tensor, src: torch.Tensor, blocks: int = 32, passes:
     return dst
 
 
+def cu_hold(blocks: int, usec: float, lds_kb: int = 64, device=None) -> None:
+    """A collective's CU footprint by time: ``blocks`` workgroups (RCCL
+    channels), each holding a CU for ``usec`` microseconds from when it starts,
+    on the current stream. ``lds_kb`` > 32: no 128 KiB GEMM workgroup fits on
+    the same CU (bench/overlap_rccl.py)."""
+    _lib.check(_lib.lib().kgs_cu_hold(int(blocks), float(usec), int(lds_kb) * 1024, _lib.stream_handle(device)),
+               "cu_hold")
+
+
 def transpose_bf16(x: torch.Tensor, variant: int = 0) -> torch.Tensor:
     """Materialised ``x.T`` (variant 0 = auto: 16-B path when shapes allow,
     1 = element-wise tile, 2 = force the 16-B path)."""

@@ -94,6 +94,8 @@ def lib() -> ctypes.CDLL:
     so.kgs_gemm_stamp_n.restype = i
     so.kgs_exp_gemm_w4h.argtypes = [vp] * 3 + [i] * 7 + [vp]
     so.kgs_exp_gemm_w4h.restype = i
+    so.kgs_exp_gemm_w4p_grid.argtypes = [vp] * 3 + [i] * 8 + [vp]
+    so.kgs_exp_gemm_w4p_grid.restype = i
     so.kgs_exp_gemm_fp8_w4f8.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
     so.kgs_exp_gemm_fp8_w4f8.restype = i
     return so
@@ -154,3 +156,14 @@ def gemm_fp8_nt(a: torch.Tensor, b: torch.Tensor, scale_a: float, scale_b: float
                                    _lib.stream_handle(a.device))
     _lib.check(rc, f"fp8 experiment {variant}[{M}x{N}x{K}]")
     return out
+
+
+def gemm_w4p_grid(a, b, out, mode: int = 1, grid: int = 0) -> None:
+    """The persistent GEMM (default map) with first-ticket ``mode`` (1 = static,
+    2 = from the queue) on ``grid`` workgroups (0 = one per CU), on the current
+    stream. ``a`` [M, K], ``b`` [N, K], ``out`` [M, N], bf16 row-major."""
+    M, K = a.shape
+    N = b.shape[0]
+    _lib.check(lib().kgs_exp_gemm_w4p_grid(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
+                                           b.stride(0), out.stride(0), int(mode), int(grid),
+                                           _lib.stream_handle(a.device)), "kgs_exp_gemm_w4p_grid")

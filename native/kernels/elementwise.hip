@@ -185,6 +185,16 @@ __global__ __launch_bounds__(EW_THREADS) void comm_standin_f32(f32x4* __restrict
     for (long i = lo + threadIdx.x; i < hi; i += EW_THREADS) dst[i] += src[i];
 }
 
+// Collective stand-in by TIME (bench/overlap_rccl.py): each workgroup holds its
+// CU for `ticks` of the constant wall clock from the moment it starts, the way
+// an RCCL channel's workgroup sits on a CU for the length of the collective.
+// With dynamic LDS > 32 KiB (launch argument) no 128 KiB GEMM workgroup fits
+// beside it, and the GEMM waves need a whole SIMD's registers anyway.
+__global__ __launch_bounds__(256) void cu_hold(long ticks) {
+  const long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(4);
+}
+
 static int blocks_for(long n) {
   long b = (n + EW_THREADS - 1) / EW_THREADS;
   if (b < 1) b = 1;
@@ -272,6 +282,22 @@ KGS_EXPORT int kgs_comm_standin_f32(void* dst, const void* src, long n, int nblo
   if ((uintptr_t)dst % 16 || (uintptr_t)src % 16) return KGS_ERR_ALIGN;
   hipLaunchKernelGGL(kgs::comm_standin_f32, dim3(nblocks), dim3(kgs::EW_THREADS), lds_bytes, s, (f32x4*)dst,
                      (const f32x4*)src, n / 4, passes);
+  return (int)hipGetLastError();
+}
+
+// nblocks workgroups of 256 threads, each holding a CU for `usec` microseconds
+// (kgs::cu_hold). lds_bytes of dynamic LDS per workgroup (<= 160 KiB).
+KGS_EXPORT int kgs_cu_hold(int nblocks, double usec, int lds_bytes, hipStream_t s) {
+  if (nblocks <= 0 || usec < 0 || usec > 1e7) return KGS_ERR_SHAPE;
+  if (lds_bytes < 0 || lds_bytes > 160 * 1024) return KGS_ERR_ARG;
+  static int khz[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return KGS_ERR_ARG;
+  if (!khz[dev] && (hipDeviceGetAttribute(&khz[dev], hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+                    khz[dev] <= 0))
+    khz[dev] = 100000;  // gfx9 constant clock: 100 MHz
+  const long ticks = (long)(usec * 1e-3 * khz[dev]);
+  hipLaunchKernelGGL(kgs::cu_hold, dim3(nblocks), dim3(256), lds_bytes, s, ticks);
   return (int)hipGetLastError();
 }
 

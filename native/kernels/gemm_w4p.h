@@ -172,8 +172,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 // Aligned shapes only (M, N % 256, K % 128 with K >= 384; 16-B operands); the
 // grid is at most the tile count. X: gemm_w4.h's knob bag (tile map, DMA order).
 // q: this launch's zeroed ticket slot (tile_queue.h), zero again on return.
-// DYN = false: the static walk v, v + G, v + 2G (q unused), for measurements.
-template <int EPI, int X = 0, bool DYN = true>
+// DYN: 1 = per-XCD ticket queue, first ticket static (the workgroup's rank in
+// its label: no atomic before the first DMA); 2 = every ticket from the queue,
+// the first one too (a workgroup that starts late -- its CU held by a
+// collective launched just before -- takes only the tiles still left);
+// 0 = the static walk v, v + G, v + 2G (q unused), for measurements.
+template <int EPI, int X = 0, int DYN = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
@@ -214,8 +218,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // from nwx on. Static walk: t = v.
   const int nwx = ((int)gridDim.x - x + 7) >> 3;  // workgroups of label x
   const int lim = DYN ? ntx : ntiles;
-  int t = DYN ? (int)blockIdx.x >> 3 : (int)blockIdx.x;
-  if (t >= lim) {  // (never with the host's grid <= tiles)
+  const int base = DYN == 1 ? nwx : 0;  // queue tickets are numbered from here
+  int t;
+  if constexpr (DYN == 2) {
+    if (threadIdx.x == 0) tslot = atomicAdd(q + x, 1);
+    __syncthreads();
+    t = __builtin_amdgcn_readfirstlane(tslot);
+  } else {
+    t = DYN ? (int)blockIdx.x >> 3 : (int)blockIdx.x;
+  }
+  if (t >= lim) {  // (DYN 2: queue empty when this workgroup started; DYN 0/1: never with grid <= tiles)
     if (DYN && threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
       for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
     return;
@@ -261,7 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       pstep<0, X, false>(c, c, f0, f1, t + 2, tq);
       pstep<1, X, false>(c, c, f0, f1, t + 3, tq);
     }
-    const int tnx = DYN ? nwx + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
+    const int tnx = DYN ? base + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
     const bool more = tnx < lim;
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
@@ -296,7 +308,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.rb = cn.rb;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
-  if constexpr (DYN) {
+  if constexpr (DYN != 0) {
     if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)  // last one out resets the queue
       for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
   }

@@ -17,6 +17,10 @@
 #   gemm_pmc     two counter passes over the GEMM (stall / MFMA busy)
 #   overlap      GEMM vs comm-kernel overlap measurement (bench/overlap.py)
 #   overlap_trace  kernel trace of the overlap run
+#   counters_list  rocprofv3 -L (the counter names this box offers)
+#   step_ab      the bench step under the persistent / one-shot / hipBLASLt paths, interleaved ($MNK);
+#                step_ab_long: 3-second blocks (sustained clocks)
+#   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
 #   e2e          kgs bench --no-kind chained tail (plugin -> pod -> first GEMM)
@@ -75,6 +79,13 @@ step() {
             run pmc_mfma 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU \
             GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc2" -o gemm -- $PMC_GEMM ;;
         overlap) run overlap 300 python bench/overlap.py --out "$O/overlap.json" ;;
+        counters_list) run counters_list 120 rocprofv3 -L ;;
+        step_ab) run step_ab 400 python bench/step_ab.py --mnk ${MNK:-8192} --out "$O/step_ab_${MNK:-8192}.json" ;;
+        step_ab_long) run step_ab_long 600 python bench/step_ab.py --mnk ${MNK:-8192} --seconds 3 --rounds 5 \
+            --out "$O/step_ab_long_${MNK:-8192}.json" ;;
+        overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
+            run overlap_rccl_hi 300 python bench/overlap_rccl.py --side-priority high \
+                --out "$O/overlap_rccl_shape_hiprio.json" ;;
         overlap_trace) run overlap_trace 300 rocprofv3 --kernel-trace --output-format csv -d "$O/otrace" -o ov \
             -- python3 bench/overlap.py --iters 3 ;;
         serve) run serve 400 python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 \

@@ -487,6 +487,29 @@ def test_base_mirror_rewrites_base_images(world):
     assert reg["image"] == "mirror.example:5001/library/registry:2"
 
 
+def test_rocm_images_are_mirrorable_and_overridable(world, tmp_path):
+    """the plugin image's ROCm stage (a multi-GB
+    Docker Hub pull made for one header directory and three .so files) takes
+    --rocm-mirror (the C13 rewrite, kind-gpu-sim.sh:144-178) and --rocm-dev-image,
+    and both reach the `docker build` argv."""
+    assert run("create", "--dev-root", world.nogpu, "--rocm-mirror=mirror.example:5001/rocm") == 0
+    build = world.calls("docker", "build")[0]
+    assert "ROCM_IMAGE=mirror.example:5001/rocm/dev-ubuntu-22.04:7.0" in build
+    assert not any("docker.io/rocm" in x for x in build), build
+    assert run("delete") == 0
+    n = len(world.calls("docker", "build"))
+    assert run("create", "--dev-root", world.nogpu, "--rocm-dev-image=registry.local/amdsmi-lib:7.0.0",
+               "--rocm-mirror=mirror.example:5001/rocm") == 0
+    build = world.calls("docker", "build")[n]
+    assert "ROCM_IMAGE=registry.local/amdsmi-lib:7.0.0" in build  # not a docker.io/rocm ref: left alone
+    # the workload image's PyTorch-ROCm base takes the same mirror
+    from kgs import config as Cfg
+
+    s = Cfg.Settings(rocm_mirror="mirror.example:5001/rocm")
+    assert s.rocm_image(Cfg.ROCM_BASE_IMAGE) == "mirror.example:5001/rocm/" + Cfg.ROCM_BASE_IMAGE.split("/", 2)[2]
+    assert Cfg.Settings().rocm_image(Cfg.ROCM_BASE_IMAGE) == Cfg.ROCM_BASE_IMAGE
+
+
 def test_default_base_images_use_public_mirror(world):
     assert run("create", "--dev-root", world.nogpu) == 0
     build = world.calls("docker", "build")[0]
@@ -737,3 +760,11 @@ def test_bench_sweep_keeps_the_registry_between_points(world, tmp_path):
     pushes = [a for a in world.calls("docker", "push") if a[1].endswith("kgs-rocm-test:dev")]
     assert len(pushes) == 3  # built + pushed once, re-pushed (cached) by the next two points
     assert "kind-registry" not in world.state()["containers"]
+
+
+def test_images_amdsmi_lib_builds_the_light_source(world, capsys):
+    assert run("images", "--amdsmi-lib", "--dev-root", world.nogpu) == 0
+    builds = world.calls("docker", "build")
+    assert len(builds) == 1 and any("Dockerfile.amdsmi-lib" in x for x in builds[0])
+    assert "UBUNTU_IMAGE=public.ecr.aws/docker/library/ubuntu:22.04" in builds[0]
+    assert "--rocm-dev-image=localhost:5000/kgs-amdsmi-lib:7.0" in capsys.readouterr().out

@@ -114,7 +114,7 @@ def test_missing_source_in_build_stage_fails(tmp_path):
         ex.run_stage("build")
 
 
-@pytest.mark.parametrize("path", [DP, WL])
+@pytest.mark.parametrize("path", [DP, WL, os.path.join(ROOT, "images", "Dockerfile.amdsmi-lib")])
 def test_images_pin_every_base_and_requirement(path):
     gargs, stages = parse(path)
     for st in stages:
@@ -138,3 +138,18 @@ def test_ci_builds_the_plugin_image_the_same_way():
     wf = open(os.path.join(ROOT, ".github", "workflows", "rocm-ci.yaml")).read()
     assert "kgs.utils.build --only gpuinfo" in wf
     assert "Dockerfile.deviceplugin" in wf or "images --plugin" in wf
+
+
+def test_light_amdsmi_image_provides_what_the_plugin_build_copies():
+    """images/Dockerfile.amdsmi-lib (the small --rocm-dev-image source) ends
+    with the same existence check as the plugin Dockerfile's rocm stage, for
+    every path that stage's COPY --from=rocm lines read."""
+    lite = open(os.path.join(ROOT, "images", "Dockerfile.amdsmi-lib")).read()
+    _, stages = parse(DP)
+    copies = [a for st in stages for op, a in st.instrs if op == "COPY" and a.startswith("--from=rocm")]
+    assert copies
+    for a in copies:
+        for src in a.split()[1:-1]:
+            head = src.split("*")[0].rstrip(".")
+            assert head.rsplit("/", 1)[0] in lite, (src, "not checked by Dockerfile.amdsmi-lib")
+    assert "repo.radeon.com/rocm/apt/7.0" in lite and "amd-smi-lib" in lite

@@ -910,3 +910,30 @@ def test_eighty_streams_each_launch_a_persistent_gemm():
     finally:
         torch.cuda.synchronize()
         destroy()
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("grid", [0, 224, 100])
+def test_persistent_first_ticket_modes_and_reserved_grids_are_exact(mode, grid):
+    """The persistent kernel with the static first ticket (1, production) and
+    with every ticket from the queue (2), on one workgroup per CU and on fewer
+    (CUs left to a collective): bitwise the one-shot kernel, and a CU held by
+    another kernel while it starts does not change that."""
+    from kgs.ops import gemm_nt
+    from kgs.ops.elementwise import cu_hold
+    from kgs.ops.experiments import gemm_w4p_grid
+
+    a = (torch.rand(4608, 2048, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(4096, 2048, device=DEV) * 2 - 1).bfloat16()
+    ref = gemm_nt(a, b, variant="w4_oneshot")
+    side = torch.cuda.Stream(device=DEV)
+    for held in (0, 48):
+        out = torch.zeros_like(ref)
+        if held:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                cu_hold(held, 200.0, lds_kb=64)
+        gemm_w4p_grid(a, b, out, mode=mode, grid=grid)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), (mode, grid, held)
