@@ -11,7 +11,8 @@ the weight-streaming floor):
   hipblaslt           torch.matmul + silu_mul
   p<any of the above> the same on weights packed tile-panel major
                       (kgs.ops.gemm.pack_w4x_weight, PACKB), e.g. pswiglu_bm256_bn128
-A ``_tT`` suffix runs the four-wave kernel with T LDS stages (3 or 4).
+A ``_tT`` suffix runs the four-wave kernel with T LDS stages (3 or 4); ``_nt``
+streams the weights non-temporally (B loads only; two stages).
 With ``--proj down`` (x [M, 14336] . W [4096, 14336]^T, no SwiGLU), ``qkv``
 ([6144, 4096]) or ``o`` ([4096, 4096]) the candidates are w4x_bmXXX_bnYYY[_sS][_tT],
 pw4x_... and hipblaslt.
@@ -70,6 +71,8 @@ def main():
         pk = v.startswith("p")
         v = v[1:] if pk else v
         f = v.split("_")
+        nt = "nt" in f
+        f = [t for t in f if t != "nt"]
         opt = {t[0]: int(t[1:]) for t in f[1:] if t[0] in "st"}  # sS: K slices, tT: LDS stages
         s, st = opt.get("s", 1), opt.get("t", 2)
         if f[0] in ("swiglu", "w4x"):
@@ -79,11 +82,11 @@ def main():
         sw = f[0] == "swiglu"
         w = (lambda i: ring_of(bn, sw)[i]) if pk else (lambda i: ws[i])
         if sw:
-            return lambda i: gemm_nt_w4x_swiglu(x, w(i), bn=bn, bm=bm, stages=st)
+            return lambda i: gemm_nt_w4x_swiglu(x, w(i), bn=bn, bm=bm, stages=st, nt_weights=nt)
         if f[0] == "skf":  # split-K partials + fused reduce-and-SwiGLU
             return lambda i: gemm_nt_w4x_splitk_swiglu(x, w(i), bn=bn, nslice=s)
         if down:
-            return lambda i: gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm, stages=st)
+            return lambda i: gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm, stages=st, nt_weights=nt)
         return lambda i: silu_mul(gemm_nt_w4x(x, w(i), bn=bn, nslice=s, bm=bm, stages=st))
 
     res = []

@@ -258,6 +258,19 @@ def w4x_stages(route) -> int:
     return route[3] if len(route) > 3 else 2
 
 
+# Decode weights are read once per step by one CU each: their loads go
+# non-temporal (gemm_w4.h AUX 52, B's loads only; the activations, re-read by
+# every workgroup from L2, keep the default policy). gate|up at batch 256:
+# 69.1 -> 68.0 us row-major, 67.5 -> 64.9 us tile-panel packed
+# (profiles/r4/decode/README.md). KGS_NT_WEIGHTS=0 turns it off.
+NT_WEIGHTS = os.environ.get("KGS_NT_WEIGHTS", "1") != "0"
+
+
+def w4x_nt(route) -> bool:
+    """Stream this route's weights non-temporally (two-stage routes only)."""
+    return NT_WEIGHTS and w4x_stages(route) == 2
+
+
 def w4x_split_bns(n: int, k: int) -> set:
     """Tile widths the split-K four-wave routes use for an ``[n, k]`` weight
     (the bn a tile-panel copy must be packed with)."""

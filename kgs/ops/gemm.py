@@ -174,10 +174,12 @@ def pack_w4x_weight(w: torch.Tensor, bn: int, swiglu: bool = False) -> PanelWeig
     return PanelWeight(data, N, K, bn, swiglu)
 
 
-def _w4x_flags(packed: int, stages: int) -> int:
+def _w4x_flags(packed: int, stages: int, nt_weights: bool = False) -> int:
     if stages not in (2, 3, 4):
         raise ValueError(f"stages must be 2, 3 or 4, got {stages}")
-    return packed | (stages - 2) << 4
+    if nt_weights and stages != 2:
+        raise ValueError("nt_weights runs with two LDS stages only")
+    return packed | (2 if nt_weights else 0) | (stages - 2) << 4
 
 
 def _packed_operand(b, bn, swiglu):
@@ -189,13 +191,16 @@ def _packed_operand(b, bn, swiglu):
 
 
 def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
-                out: torch.Tensor | None = None, bm: int = 256, stages: int = 2) -> torch.Tensor:
+                out: torch.Tensor | None = None, bm: int = 256, stages: int = 2,
+                nt_weights: bool = False) -> torch.Tensor:
     """``a @ b.T`` on the four-wave kernel with ``bm`` x ``bn`` tiles (256 or 128
     each), any M (rows past M read as zeros), over ``nslice`` K-slices (fp32
     partials + reduce when > 1): the decode-batch GEMM path.
     ``N % bn == 0`` and ``(K / nslice) % 128 == 0``. ``b`` is a ``[N, K]`` tensor
     or a :class:`PanelWeight` packed with the same ``bn``. ``stages``: LDS
-    stages (3 / 4 keep more K-tiles in flight; only where they fit in 160 KiB)."""
+    stages (3 / 4 keep more K-tiles in flight; only where they fit in 160 KiB).
+    ``nt_weights``: ``b``'s loads non-temporal (decode weights each CU streams
+    once), ``a``'s loads default (two stages only)."""
     _check_operand(a, "a")
     b, bshape, ldb, packed = _packed_operand(b, bn, False)
     if not packed:
@@ -219,12 +224,13 @@ def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
         ws_ptr = ws.data_ptr()
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x_ex(a.data_ptr(), b.data_ptr(), out.data_ptr(), ws_ptr, M, N, K, a.stride(0),
                                             ldb, out.stride(0), int(bn), int(nslice), int(bm),
-                                            _w4x_flags(packed, stages), _lib.stream_handle(a.device))
+                                            _w4x_flags(packed, stages, nt_weights), _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return out
 
 
-def gemm_nt_w4x_partials(a: torch.Tensor, b, bn: int, nslice: int, bm: int = 256, stages: int = 2) -> torch.Tensor:
+def gemm_nt_w4x_partials(a: torch.Tensor, b, bn: int, nslice: int, bm: int = 256, stages: int = 2,
+                         nt_weights: bool = False) -> torch.Tensor:
     """The split-K four-wave GEMM WITHOUT its reduce: returns the fp32 partial
     products ``[nslice, M, N]`` (a view of the per-GPU split-K workspace, valid
     until the next split-K call on the stream) for a fused consumer --
@@ -248,14 +254,16 @@ def gemm_nt_w4x_partials(a: torch.Tensor, b, bn: int, nslice: int, bm: int = 256
             raise RuntimeError("gemm_nt_w4x_partials: reserve_splitk_workspace() before hipGraph capture")
         ws = reserve_splitk_workspace(a.device, need)
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x_ex(a.data_ptr(), b.data_ptr(), None, ws.data_ptr(), M, N, K, a.stride(0),
-                                            ldb, N, int(bn), int(nslice), int(bm), _w4x_flags(packed, stages),
+                                            ldb, N, int(bn), int(nslice), int(bm),
+                                            _w4x_flags(packed, stages, nt_weights),
                                             _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x_partials[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return ws[:need].view(nslice, M, N)
 
 
 def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up, bn: int = 128,
-                       out: torch.Tensor | None = None, bm: int = 256, stages: int = 2) -> torch.Tensor:
+                       out: torch.Tensor | None = None, bm: int = 256, stages: int = 2,
+                       nt_weights: bool = False) -> torch.Tensor:
     """``silu(a @ gate.T) * (a @ up.T)`` for a fused gate|up weight ``[2I, K]``
     (gate rows first) on the four-wave kernel, the SwiGLU applied in the GEMM
     epilogue: returns ``[M, I]`` (both products rounded to bf16 first, as
@@ -274,7 +282,8 @@ def gemm_nt_w4x_swiglu(a: torch.Tensor, w_gate_up, bn: int = 128,
         out = torch.empty((M, N // 2), dtype=torch.bfloat16, device=a.device)
     rc = _lib.lib().kgs_gemm_bf16_nt_w4x_swiglu_ex(a.data_ptr(), w.data_ptr(), out.data_ptr(), M, N, K,
                                                    a.stride(0), ldb, out.stride(0), int(bn), int(bm),
-                                                   _w4x_flags(packed, stages), _lib.stream_handle(a.device))
+                                                   _w4x_flags(packed, stages, nt_weights),
+                                                   _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x_swiglu[{M}x{N}x{K} {bm}x{bn}]")
     return out
 

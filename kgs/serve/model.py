@@ -112,6 +112,18 @@ class ServingModel:
             bns = {n: D.w4x_split_bns(*self.w[0][n].shape) for n in ("qkv", "o", "down")}
             self.w4x_panels = [{(n, bn): pack_w4x_weight(lw[n], bn) for n in bns for bn in bns[n]}
                                for lw in self.w]
+        # SwiGLU tile-panel copies of gate|up (235 MB per layer and tile width)
+        # for the unsplit decode routes: with non-temporal weight loads they
+        # read 4 % faster than row-major at batch 256 (64.9 vs 68.0 us,
+        # profiles/r4/decode/README.md). Opt-in: KGS_GATEUP_PANELS=1.
+        self.gate_up_panels = None
+        if self.fuse_splitk and packed_decode and os.environ.get("KGS_GATEUP_PANELS", "0") == "1":
+            from kgs.ops.gemm import pack_w4x_weight
+
+            gbns = {r[0] for (_, n, k), r in D.W4X_TUNED.items()
+                    if (n, k) == tuple(self.w[0]["gate_up"].shape) and r[1] == 1}
+            self.gate_up_panels = [{bn: pack_w4x_weight(lw["gate_up"], bn, swiglu=True) for bn in gbns}
+                                   for lw in self.w]
         if prefill_weights not in ("bf16", "fp8"):
             raise ValueError(f"prefill_weights must be bf16 or fp8, got {prefill_weights!r}")
         self.prefill_f8 = None
@@ -143,7 +155,8 @@ class ServingModel:
             if route is not None:
                 from kgs.ops.gemm import gemm_nt_w4x
 
-                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1], bm=route[2], stages=D.w4x_stages(route))
+                return gemm_nt_w4x(x, w, bn=route[0], nslice=route[1], bm=route[2], stages=D.w4x_stages(route),
+                                   nt_weights=D.w4x_nt(route))
         if decode:
             ns = D.splitk_slices(m, w.shape[0], w.shape[1])
             if ns == 1:
@@ -187,6 +200,13 @@ class ServingModel:
             if p is not None:
                 return p
         return self.w[layer][name]
+
+    def _gate_up_weight(self, layer: int, bn: int):
+        """gate|up as the SwiGLU four-wave kernel reads it: the SwiGLU tile-panel
+        copy for ``bn`` when ``gate_up_panels`` made one, else row-major."""
+        if self.gate_up_panels is not None and bn in self.gate_up_panels[layer]:
+            return self.gate_up_panels[layer][bn]
+        return self.w[layer]["gate_up"]
 
     def _swiglu_route(self, m: int):
         """(bn, 1) when the decode gate|up projection runs unsplit on the
@@ -432,12 +452,12 @@ class ServingModel:
             c.heads // c.kv_heads <= 6
         for i in range(c.layers):
             if fused_attn:
-                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)
+                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq, nt_weights=D.w4x_nt(rq))
                 a = D.rope_paged_decode_attention(part, self.cos, self.sin, positions, slots, self.cache.layer(i),
                                                   block_tables, ctx_lens, c.heads, c.kv_heads,
                                                   pages_per_split=pages_per_split)
             elif rq:
-                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq)
+                part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq, nt_weights=D.w4x_nt(rq))
                 qkv = torch.empty((m, part.shape[2]), dtype=torch.bfloat16, device=x.device)
                 D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(i), c.heads, c.kv_heads,
                               partials=part)
@@ -453,18 +473,19 @@ class ServingModel:
                 a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                              pages_per_split=pages_per_split)
             if ro:
-                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self._w4x_weight(i, "o", ro[0]), *ro), x, self.ln2[i],
-                                       c.eps)
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self._w4x_weight(i, "o", ro[0]), *ro,
+                                                            nt_weights=D.w4x_nt(ro)), x, self.ln2[i], c.eps)
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
             if rg:
-                act = gemm_nt_w4x_swiglu(y, self.w[i]["gate_up"], bn=rg[0], bm=rg[2], stages=D.w4x_stages(rg))
+                act = gemm_nt_w4x_swiglu(y, self._gate_up_weight(i, rg[0]), bn=rg[0], bm=rg[2],
+                                         stages=D.w4x_stages(rg), nt_weights=D.w4x_nt(rg))
             else:
                 act = self._silu_mul(self._proj(y, i, "gate_up", True))
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             if rd:
-                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self._w4x_weight(i, "down", rd[0]), *rd), x, nxt,
-                                       c.eps)
+                y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self._w4x_weight(i, "down", rd[0]), *rd,
+                                                            nt_weights=D.w4x_nt(rd)), x, nxt, c.eps)
             else:
                 y = self._norm(x, self._proj(act, i, "down", True), nxt)
         return self._proj(y, None, "lm", True)

@@ -652,6 +652,12 @@ int launch_w4x(dim3 grid, hipStream_t s, const unsigned short* a, const unsigned
                int M, int N, int ks, int lda, int ldb, int ld, int mode, int flags) {
   constexpr int BM = kgs::w4::tile_m<TM>();
   const bool packed = flags & 1;
+  if (flags & 2) {  // weights (B) non-temporal: two LDS stages only
+    if (flags & 0x30) return KGS_ERR_ARG;
+    if (packed) launch_w4x_x<BN, TM, 1000005200>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    else launch_w4x_x<BN, TM, 5200>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
+    return 0;
+  }
   switch (flags & 0x30) {
     case 0x00:
       if (packed) launch_w4x_x<BN, TM, 1000000000>(grid, s, a, b, out, M, N, ks, lda, ldb, ld, mode);
@@ -694,6 +700,12 @@ int launch_w4sw(dim3 grid, hipStream_t s, const unsigned short* a, const unsigne
                 int N, int K, int lda, int ldb, int ldc, bool aligned_m, int flags) {
   constexpr int BM = kgs::w4::tile_m<TM>();
   const bool packed = flags & 1;
+  if (flags & 2) {  // weights (B) non-temporal: two LDS stages only
+    if (flags & 0x30) return KGS_ERR_ARG;
+    if (packed) launch_w4sw_x<BN, TM, 1001005200>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    else launch_w4sw_x<BN, TM, 1005200>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
+    return 0;
+  }
   switch (flags & 0x30) {
     case 0x00:
       if (packed) launch_w4sw_x<BN, TM, 1001000000>(grid, s, a, b, c, M, N, K, lda, ldb, ldc, aligned_m);
@@ -729,12 +741,13 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x(const void* A, const void* B, void* C, float
 
 // flags bit 0: B is the tile-panel-major copy of a [N, K] weight
 // ([N / bn][K / 64][bn][64], kgs.ops.gemm.pack_w4x_weight) and ldb must be K;
-// bits 4-5: LDS stages - 2 (0..2, where they fit in 160 KiB)
+// bit 1: B's loads non-temporal (two stages only); bits 4-5: LDS stages - 2
+// (0..2, where they fit in 160 KiB)
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, float* ws, int M, int N, int K,
                                        int lda, int ldb, int ldc, int bn, int nslice, int bm, int flags,
                                        hipStream_t stream) {
   using namespace kgs;
-  if (flags & ~0x31 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
+  if (flags & ~0x33 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
   if ((flags & 1) && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || nslice <= 0 || K % nslice) return KGS_ERR_SHAPE;
   if (lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
@@ -785,7 +798,7 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu(const void* A, const void* B, void* C
 KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void* C, int M, int N, int K, int lda,
                                               int ldb, int ldc, int bn, int bm, int flags, hipStream_t stream) {
   using namespace kgs;
-  if (flags & ~0x31 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
+  if (flags & ~0x33 || (flags & 0x30) == 0x30) return KGS_ERR_ARG;
   if ((flags & 1) && ldb != K) return KGS_ERR_SHAPE;
   if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N / 2) return KGS_ERR_SHAPE;
   if ((bn != 128 && bn != 256) || (bm != 128 && bm != 256)) return KGS_ERR_ARG;

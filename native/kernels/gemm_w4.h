@@ -140,20 +140,25 @@ __device__ __forceinline__ void dma(const Ctx& c, int st, int j, int k0) {
 
 // X: the knob bag of the kernel template (GROUP_M = X % 100, AUX = X / 100 % 100,
 // DMA window = X / 10^4 % 100, SW = X / 10^6 % 10, MAP = X / 10^7 % 10,
-// DMA operand order = X / 10^8 % 10, packed B = X / 10^9 == 1)
+// DMA operand order = X / 10^8 % 10, packed B = X / 10^9 == 1). AUX < 50: the
+// cache-policy bits of both operands' loads; AUX >= 50: AUX - 50 on B's loads
+// only (52: B non-temporal -- decode weights that one CU streams once -- while
+// A, re-read by every workgroup, keeps the default policy).
 template <int BM, int BN, int X>
 __device__ __forceinline__ void dma_any(const Ctx& c, int st, int j, int k0) {
-  constexpr int AUX = (X / 100) % 100;
+  constexpr int AUXX = (X / 100) % 100;
+  constexpr int AUX = AUXX >= 50 ? AUXX - 50 : AUXX;   // B
+  constexpr int AUXA = AUXX >= 50 ? 0 : AUXX;          // A
   constexpr bool SW = (X / 1000000) % 10 != 0;
   constexpr int ORDB = (X / 100000000) % 10;  // 1: the B operand's DMAs first, 2: A and B interleaved
   constexpr bool PK = (X / 1000000000) == 1;  // B packed by K-tile (PACKB)
   constexpr int JA = BM / 32, JB = BN / 32;
   if constexpr (ORDB == 1) {
-    if (j < JB) dma<BM, BN, 1, AUX, SW, PK>(c, st, j, k0); else dma<BM, BN, 0, AUX>(c, st, j - JB, k0);
+    if (j < JB) dma<BM, BN, 1, AUX, SW, PK>(c, st, j, k0); else dma<BM, BN, 0, AUXA>(c, st, j - JB, k0);
   } else if constexpr (ORDB == 2 && JA == JB) {
-    if (j & 1) dma<BM, BN, 1, AUX, SW, PK>(c, st, j >> 1, k0); else dma<BM, BN, 0, AUX>(c, st, j >> 1, k0);
+    if (j & 1) dma<BM, BN, 1, AUX, SW, PK>(c, st, j >> 1, k0); else dma<BM, BN, 0, AUXA>(c, st, j >> 1, k0);
   } else {
-    if (j < JA) dma<BM, BN, 0, AUX>(c, st, j, k0); else dma<BM, BN, 1, AUX, SW, PK>(c, st, j - JA, k0);
+    if (j < JA) dma<BM, BN, 0, AUXA>(c, st, j, k0); else dma<BM, BN, 1, AUX, SW, PK>(c, st, j - JA, k0);
   }
 }
 

@@ -20,6 +20,9 @@
 #   counters_list  rocprofv3 -L (the counter names this box offers)
 #   step_ab      the bench step under the persistent / one-shot / hipBLASLt paths, interleaved ($MNK);
 #                step_ab_long: 3-second blocks (sustained clocks)
+#   gateup_pmc   counter passes (SQ waits, FETCH_SIZE, TCC hit/miss, TA/TCP/TD stalls) + trace of the batch-256
+#                gate|up kernel, default vs nt weight loads
+#   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
 #   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
@@ -83,6 +86,29 @@ step() {
         step_ab) run step_ab 400 python bench/step_ab.py --mnk ${MNK:-8192} --out "$O/step_ab_${MNK:-8192}.json" ;;
         step_ab_long) run step_ab_long 600 python bench/step_ab.py --mnk ${MNK:-8192} --seconds 3 --rounds 5 \
             --out "$O/step_ab_long_${MNK:-8192}.json" ;;
+        gateup_pmc)  # counter passes over the batch-256 gate|up + SwiGLU kernel (default vs nt weight loads)
+            local GU="python3 bench/decode_gateup_probe.py --batches 256 --iters 30"
+            GU="$GU --variants ${VARIANTS:-swiglu_bm256_bn128,swiglu_bm256_bn128_nt}"
+            run gu_pmc_sq 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_INST_LEVEL_VMEM SQ_INSTS_MFMA GRBM_GUI_ACTIVE \
+                GRBM_COUNT --output-format csv -d "$O/gu_pmc_sq" -o gu -- $GU &&
+            run gu_pmc_fetch 120 timeout -s KILL 100 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum GRBM_GUI_ACTIVE \
+                --output-format csv -d "$O/gu_pmc_fetch" -o gu -- $GU &&
+            run gu_pmc_tcc 120 timeout -s KILL 100 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum \
+                TCC_EA0_RDREQ_DRAM_sum GRBM_GUI_ACTIVE --output-format csv -d "$O/gu_pmc_tcc" -o gu -- $GU &&
+            run gu_pmc_ta 120 timeout -s KILL 100 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum \
+                TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum \
+                TCP_TCR_TCP_STALL_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE \
+                --output-format csv -d "$O/gu_pmc_ta" -o gu -- $GU &&
+            run gu_trace 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/gu_trace" -o gu -- $GU ;;
+        serve_nt_ab)  # batch-$B serving: nt weight loads off / on / on + gate|up panels, A B C A B C
+            local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
+            SB="$SB --max-batch ${B:-256} --max-model-len 2048"
+            for r in 1 2; do
+                (export KGS_NT_WEIGHTS=0; run serve_nt0_$r 300 $SB) &&
+                (export KGS_NT_WEIGHTS=1; run serve_nt1_$r 300 $SB) &&
+                (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=1; run serve_nt1gp_$r 300 $SB) || return 1
+            done ;;
         overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
             run overlap_rccl_hi 300 python bench/overlap_rccl.py --side-priority high \
                 --out "$O/overlap_rccl_shape_hiprio.json" ;;

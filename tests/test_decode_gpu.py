@@ -526,3 +526,17 @@ def test_skinny_kin_variants(m, v):
     torch.cuda.synchronize()
     assert torch.equal(q1, q2)
     assert torch.equal(caches[0].layer(0), caches[1].layer(0))
+
+
+@pytest.mark.parametrize("M", [256, 200])
+def test_nt_weight_loads_are_bitwise_the_default_policy(M):
+    """Non-temporal weight loads (gemm_w4.h AUX >= 50: the policy on B's loads
+    only) change where the bytes are cached, never the result: the SwiGLU,
+    plain and split-K decode GEMMs are bitwise those of the default policy."""
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu
+
+    x = torch.randn(M, 4096, device=DEV).bfloat16()
+    w = (torch.randn(2 * 1024, 4096, device=DEV) * 0.02).bfloat16()
+    assert torch.equal(gemm_nt_w4x_swiglu(x, w, bn=128, nt_weights=True), gemm_nt_w4x_swiglu(x, w, bn=128))
+    assert torch.equal(gemm_nt_w4x(x, w, bn=128, nt_weights=True), gemm_nt_w4x(x, w, bn=128))
+    assert torch.equal(gemm_nt_w4x(x, w, bn=128, nslice=4, nt_weights=True), gemm_nt_w4x(x, w, bn=128, nslice=4))
