@@ -249,7 +249,9 @@ def run(args, wd) -> int:
             **extra,
         }
         launch.report_once(out)  # the one JSON line (a later signal cannot add an error line)
-    wd.set_phase("shutdown")
+    # the measurement is done on every rank: from here only the teardown is bounded
+    # (its store exit barrier waits up to 60 s for a lagging peer)
+    wd.shutdown_bound(90.0)
     kdist.shutdown(ctx)
     return 0
 

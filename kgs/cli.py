@@ -130,6 +130,7 @@ def main(argv=None, prog: str = "kgs") -> int:
     from .cluster import Provisioner, ProvisionError
     from .runtime import RuntimeNotFound
     from .utils.proc import CommandError
+    from .e2e import result_timeout
 
     s = settings_from(a)
     p = Provisioner(s)
@@ -157,7 +158,7 @@ def main(argv=None, prog: str = "kgs") -> int:
             counts = _parse_counts(a.sweep)
             if a.no_kind:
                 kw = dict(dev_root=a.dev_root, fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
-                          timeout=max(60, a.pod_timeout * 10))
+                          timeout=result_timeout(a.pod_timeout))
                 return run_sweep(None, counts, pod_gpus=a.pod_gpus, sweep_json=a.sweep_json, out=p.out,
                                  no_kind=True, **kw)
 
@@ -174,7 +175,7 @@ def main(argv=None, prog: str = "kgs") -> int:
 
             return run_nokind(gpus=a.pod_gpus or a.gpus or 1, advertise=a.gpus, dev_root=a.dev_root,
                               fake_gpus=a.fake_gpus or 0, gemm_size=a.gemm_size,
-                              timeout=max(60, a.pod_timeout * 10), timings_json=a.timings_json)
+                              timeout=result_timeout(a.pod_timeout), timings_json=a.timings_json)
         if a.verb == "bench":
             from .e2e import run_e2e
 
@@ -192,6 +193,9 @@ def main(argv=None, prog: str = "kgs") -> int:
                                 plugin=not only_lib and (a.plugin or not a.workload), amdsmi_lib=a.amdsmi_lib)
     except (ProvisionError, RuntimeNotFound) as e:
         print(str(e), file=sys.stderr)
+        return 1
+    except TimeoutError as e:  # a bench wait ran out (pod result, plugin capacity, ...)
+        print(f"ERROR: {e}", file=sys.stderr)
         return 1
     except CommandError as e:
         print(f"ERROR: {e}", file=sys.stderr)

@@ -41,6 +41,11 @@ def run_e2e(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, kee
     return 0
 
 
+def result_timeout(pod_timeout: float) -> float:
+    """Seconds to wait for the test pod's result line once it is Ready."""
+    return max(1.0, pod_timeout * 10.0)
+
+
 def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, keep: bool = False,
              workload_image: str | None = None, pod_command: list | None = None,
              keep_registry: bool = False) -> dict:
@@ -77,7 +82,7 @@ def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, ke
     if p.ensure_runtime().name == "podman" and not workload_image:
         with t.phase("workload-image-load"):
             p.rt.load_into_kind(image, p.s.cluster_name)
-    pod =manifests.gpu_test_pod(image, gpus=gpus, command=pod_command)
+    pod = manifests.gpu_test_pod(image, gpus=gpus, command=pod_command)
     name = pod["metadata"]["name"]
     result = {}
     try:
@@ -89,7 +94,11 @@ def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, ke
         with t.phase("pod-ready"):
             p.kubectl("wait", "--for=condition=Ready", f"pod/{name}", f"--timeout={pod_timeout}s")
         with t.phase("pod-logs"):
-            deadline = time.monotonic() + (600 if not p.runner.dry_run else 0)
+            # the pod's result line comes after its workload (GEMM sweep,
+            # all-reduce), well after Ready: the same bound as the --no-kind
+            # chain, scaled by --pod-timeout (600 s at the default 60 s)
+            wait_s = result_timeout(pod_timeout)
+            deadline = time.monotonic() + (wait_s if not p.runner.dry_run else 0)
             while True:
                 r = p.kubectl("logs", f"pod/{name}", check=False, mutating=False)
                 for line in r.stdout.splitlines():
@@ -98,6 +107,9 @@ def e2e_once(p, gpus: int = 1, pod_timeout: int = C.TEST_POD_READY_TIMEOUT_S, ke
                 if result or time.monotonic() > deadline:
                     break
                 time.sleep(2)
+            if not result and not p.runner.dry_run:
+                raise TimeoutError(f"pod/{name}: no result line in its logs within {wait_s:.0f}s "
+                                   f"(--pod-timeout {pod_timeout}s x 10)")
         t.meta.update(create_to_running_s=round(running_s, 4), gpus_requested=gpus, pod_result=result)
     finally:
         t.write(p.s.timings_json)

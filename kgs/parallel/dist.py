@@ -31,6 +31,21 @@ class DistContext:
         return self.world_size > 1
 
 
+def pick_device_index(local_rank: int, ndev: int, allow_shared_device: bool = False) -> int:
+    """This rank's GPU. One visible GPU per rank (SLURM --gpus-per-task=1, one
+    k8s container per rank with its own ROCR_VISIBLE_DEVICES pin): device 0
+    whatever LOCAL_RANK says -- two ranks on one physical GPU are caught by
+    check_distinct_devices. With several visible GPUs LOCAL_RANK must index one
+    of them (unless the ranks deliberately share, the 1-GPU test mode)."""
+    if ndev < 1:
+        raise DeviceConflict("no GPU visible to this process")
+    if ndev == 1:
+        return 0
+    if local_rank >= ndev and not allow_shared_device:
+        raise DeviceConflict(f"LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible to this process")
+    return local_rank % ndev
+
+
 def _env_int(name: str, default: int) -> int:
     v = os.environ.get(name)
     return int(v) if v not in (None, "") else default
@@ -116,10 +131,7 @@ def init_from_env(expected_world: int | None = None, backend: str | None = None,
 
     use_gpu = torch.cuda.is_available() if device_type is None else device_type == "cuda"
     if use_gpu:
-        ndev = torch.cuda.device_count()
-        if local_rank >= ndev and not allow_shared_device:
-            raise DeviceConflict(f"LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible to this process")
-        dev_index = local_rank % max(1, ndev)
+        dev_index = pick_device_index(local_rank, torch.cuda.device_count(), allow_shared_device)
         torch.cuda.set_device(dev_index)
         device = torch.device("cuda", dev_index)
     else:

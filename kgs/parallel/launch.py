@@ -283,6 +283,22 @@ class Watchdog:
         if self._t is not None:
             self._t.cancel()
 
+    def shutdown_bound(self, timeout_s: float) -> None:
+        """Switch to a bound on the shutdown alone, once the run's result is
+        out: a peer that lags in the process-group teardown must not
+        turn a reported result into exit 124. If the teardown runs out, the
+        rank leaves with status 0 -- the result line already stands."""
+        self.cancel()
+        self.set_phase("shutdown")
+        self._t = threading.Timer(timeout_s, self._fire_shutdown, args=(timeout_s,))
+        self._t.daemon = True
+        self._t.start()
+
+    def _fire_shutdown(self, timeout_s: float) -> None:
+        print(f"[kgs] rank {self.rank}: process-group shutdown not done after {timeout_s:.0f}s; leaving "
+              "(the result was already reported)", file=sys.stderr, flush=True)
+        os._exit(0)
+
 
 def _kill_group(p: subprocess.Popen, sig) -> None:
     try:

@@ -2,6 +2,10 @@
 #
 #   gpurun --timeout 1200 -- 'bash scripts/gpu.sh OUT step [step ...]'
 #
+# Parameters go in as environment variables (KT, SHAPES, VARIANTS, MNK, BATCHES, B, ...), e.g.
+#   gpurun -- 'SHAPES=8192,4096 VARIANTS=fast,w4_oneshot bash scripts/gpu.sh r4x gemm_llm bench'
+# -- one command line per experiment, no per-run wrapper scripts.
+#
 # Every step runs under its own `timeout -k 10`, logs to gpurun_out/OUT/<step>.log
 # and the chain stops at the first failure (no retries, nothing after a fault).
 # Counter passes (pmc_*) are separate rocprofv3 runs with --pmc only; they are
@@ -23,6 +27,8 @@
 #   gateup_pmc   counter passes (SQ waits, FETCH_SIZE, TCC hit/miss, TA/TCP/TD stalls) + trace of the batch-256
 #                gate|up kernel, default vs nt weight loads
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
+#   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
+#   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
 #   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
@@ -109,6 +115,14 @@ step() {
                 (export KGS_NT_WEIGHTS=1; run serve_nt1_$r 300 $SB) &&
                 (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=1; run serve_nt1gp_$r 300 $SB) || return 1
             done ;;
+        fp8_sweep) run fp8_sweep 600 python bench/gemm_sweep.py --dtype fp8 --data normal \
+            --shapes ${SHAPES:-8192,16384x16384x8192,8192x28672x4096,8192x6144x4096,4096x8192x14336,8192x4096x14336} \
+            --variants ${VARIANTS:-fast,w4p} --rounds 7 --out "$O/fp8_sweep.json" ;;
+        overlap_variants)  # persistent vs one-shot GEMM against the comm stand-in, without / with 64 KiB LDS
+            for v in auto w4_oneshot; do for l in 0 64; do
+                run overlap_${v}_lds$l 200 python bench/overlap.py --variant $v --standin-lds-kb $l \
+                    --out "$O/overlap_${v}_lds$l.json" || return 1
+            done; done ;;
         overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
             run overlap_rccl_hi 300 python bench/overlap_rccl.py --side-priority high \
                 --out "$O/overlap_rccl_shape_hiprio.json" ;;

@@ -9,7 +9,7 @@ orchestrator's control flow: error strings for "already connected", exit codes
 for missing containers, kind node naming, kubelet-managed capacity once the
 device-plugin DaemonSet is applied (from the bind-mounted partition file), etc.
 Fault injection: $KGS_FAKE_FAIL = comma list of {plugin-ready, kind-create,
-push, pod-running, network-connect}. Node lists come back sorted by name, as
+push, pod-running, pod-no-result, network-connect}. Node lists come back sorted by name, as
 the real kubectl prints them (worker, worker10, worker2, ...).
 """
 import fcntl
@@ -281,7 +281,9 @@ def kubectl_tool():
         out("condition met\n")
     elif verb == "logs":
         if any("gpu-rocm-test" in x for x in a):
-            out("Hello from fake ROCm GPU node\n" + json.dumps({"mode": "fake", "n_gpus": 0}) + "\n")
+            out("Hello from fake ROCm GPU node\n")
+            if "pod-no-result" not in FAIL:
+                out(json.dumps({"mode": "fake", "n_gpus": 0}) + "\n")
         else:
             out("plugin log line\n")
     elif verb == "delete":

@@ -342,6 +342,23 @@ def test_bench_e2e(world, tmp_path, capsys):
     assert any(p["phase"] == "prepull-wait" for p in t["phases"])
 
 
+def test_bench_result_wait_follows_pod_timeout(world, tmp_path, monkeypatch, capsys):
+    """VERDICT r3 item 8: the wait for the pod's result line is --pod-timeout
+    x 10 (not a fixed 600 s), and a pod that never prints one fails the bench
+    (exit 1) instead of reporting an empty result."""
+    import time
+
+    from kgs.e2e import result_timeout
+
+    assert result_timeout(60) == 600 and result_timeout(1) == 10
+    monkeypatch.setenv("KGS_FAKE_FAIL", "pod-no-result")
+    t0 = time.monotonic()
+    assert run("bench", "--dev-root", world.nogpu, "--pod-timeout", "1") == 1
+    assert 9 <= time.monotonic() - t0 < 60
+    assert "no result line" in capsys.readouterr().err
+    assert world.state()["clusters"] == {}  # still cleaned up
+
+
 def test_bench_uses_cached_workload_image_and_registry_port(world, tmp_path, capsys):
     """An image already present is not rebuilt; --registry-port flows into the
     pod's image reference (VERDICT r1 weak #8, #9)."""

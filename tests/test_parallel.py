@@ -10,6 +10,8 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _port():
     s = socket.socket()
@@ -430,3 +432,37 @@ def test_bench_under_torchrun_failing_rank_reports():
     assert p.returncode != 0
     j = _error_line(p.stdout)
     assert j["status"] == "error" and j["value"] is None
+
+
+def test_pick_device_index_one_gpu_per_rank_launchers():
+    """a rank that sees exactly one GPU (SLURM --gpus-per-task=1,
+    one container per rank) uses it whatever its LOCAL_RANK; with several
+    visible GPUs LOCAL_RANK must index one."""
+    from kgs.parallel.dist import DeviceConflict, pick_device_index
+
+    assert pick_device_index(5, 1) == 0
+    assert pick_device_index(3, 8) == 3
+    with pytest.raises(DeviceConflict):
+        pick_device_index(9, 8)
+    assert pick_device_index(9, 8, allow_shared_device=True) == 1
+    with pytest.raises(DeviceConflict):
+        pick_device_index(0, 0)
+
+
+def test_watchdog_shutdown_bound_keeps_a_reported_result(tmp_path):
+    """after the result line, a lagging teardown ends the rank with
+    status 0 (the shutdown-only bound), not the run watchdog's 124."""
+    import subprocess
+    import sys
+    import time
+
+    code = ("import time, sys; sys.path.insert(0, %r)\n"
+            "from kgs.parallel.launch import Watchdog\n"
+            "wd = Watchdog(1.0, 0, 1, {'metric': 'x'})\n"
+            "wd.shutdown_bound(0.5)\n"
+            "time.sleep(5)\n") % ROOT
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, (r.returncode, r.stderr)
+    assert time.monotonic() - t0 < 4.5
+    assert "shutdown not done" in r.stderr and "watchdog: no completion" not in r.stderr
