@@ -124,3 +124,35 @@ def test_persistent_gemm_k_loop_has_no_full_vmcnt_drain(gemm_build):
         full = [i for i, ln in enumerate(lines)
                 if re.search(r"s_waitcnt vmcnt\(0\)", ln) and "ASMSTART" not in lines[i - 1]]
         assert len(full) <= 3, (name, full)
+
+
+def test_named_agpr_kernels_never_touch_agprs_outside_asm(gemm_build):
+    """KGS_ACC_RESERVE clobbers a0..a255 only at kernel entry, so
+    after it the allocator could legally put an AV-class value, a spill or a
+    direct AGPR load/store in an accumulator register and corrupt it. In the
+    named-accumulator kernels (the persistent bf16 / fp8 GEMMs) no instruction
+    outside an inline-asm block may name an a-register at all -- stricter than
+    the mov/write check above, which misses compiler-emitted global_load /
+    ds_read / VALU forms with AGPR operands."""
+    _, asm = gemm_build
+    funcs = _functions(asm, r"gemm_nt_w4pI|gemm_fp8_w4pI")
+    assert len(funcs) >= 2 * 5 * 4, len(funcs)
+    for name, body in funcs.items():
+        inside, stray, seen = False, [], 0
+        for ln in body.splitlines():
+            if "ASMSTART" in ln:
+                inside = True
+                continue
+            if "ASMEND" in ln:
+                inside = False
+                continue
+            code = ln.split(";")[0].strip()
+            if not code or code.startswith("."):
+                continue
+            if re.search(r"(?<![\w.])a\[?\d+", code):
+                if inside:
+                    seen += 1
+                else:
+                    stray.append(code)
+        assert seen >= 256, (name, seen)  # the accumulators are there, through asm
+        assert not stray, (name, stray[:5])
