@@ -29,6 +29,7 @@
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
+#   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
 #   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
@@ -123,6 +124,16 @@ step() {
                 run overlap_${v}_lds$l 200 python bench/overlap.py --variant $v --standin-lds-kb $l \
                     --out "$O/overlap_${v}_lds$l.json" || return 1
             done; done ;;
+        gemm_pmc2)  # kgs vs hipBLASLt at $MNK: SQ waits + MFMA, L2 hit/miss + DRAM requests, L1 latency / stalls
+            local G="python3 bench/gemm_profile.py --iters 10 --torch --mnk ${MNK:-8192} --variant ${VAR:-auto}"
+            run g2_sq 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+                GRBM_COUNT --output-format csv -d "$O/g2_sq_${MNK:-8192}" -o g -- $G &&
+            run g2_tcc 120 timeout -s KILL 100 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum \
+                TCC_EA0_RDREQ_DRAM_sum GRBM_GUI_ACTIVE --output-format csv -d "$O/g2_tcc_${MNK:-8192}" -o g -- $G &&
+            run g2_tcp 120 timeout -s KILL 100 rocprofv3 --pmc TA_BUSY_avr TCP_TCC_READ_REQ_sum \
+                TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE \
+                --output-format csv -d "$O/g2_tcp_${MNK:-8192}" -o g -- $G ;;
         overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
             run overlap_rccl_hi 300 python bench/overlap_rccl.py --side-priority high \
                 --out "$O/overlap_rccl_shape_hiprio.json" ;;
