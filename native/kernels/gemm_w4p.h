@@ -215,7 +215,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // DYN: t is a ticket of label x (tile v = x + 8 t, t < ntx). The first one is
   // static, the workgroup's rank in its label (no atomic + barrier before the
   // first DMA: that cost 1.2 % at 3 tiles per CU); the queue numbers the rest
-  // from nwx on. Static walk: t = v.
+  // from nwx on. Against an RCCL-shaped collective holding 16-64 CUs for
+  // 0.1-0.7 ms the static first ticket was faster than DYN 2 in all 18 cells
+  // with the collective issued before the GEMMs (the bench step's order) and
+  // within 2.3 % either way when issued after the first GEMM
+  // (profiles/r4/overlap_rccl_README.md). Static walk: t = v.
   const int nwx = ((int)gridDim.x - x + 7) >> 3;  // workgroups of label x
   const int lim = DYN ? ntx : ntiles;
   const int base = DYN == 1 ? nwx : 0;  // queue tickets are numbered from here
