@@ -1,0 +1,75 @@
+// Slot-ownership rules of native/kernels/tile_queue.h, on the host (fake HIP):
+// distinct streams -> distinct slots (no wrap at any count), per-thread
+// default stream keyed by thread, captured launches get a fresh slot each plus
+// a memset node, never reused, reserve exhaustion during capture -> nullptr
+// (the one-shot grid), a slot per (device, stream).
+#include <cstdio>
+#include <set>
+#include <thread>
+
+#include "../../native/kernels/tile_queue.h"
+
+#define CHECK(c)                                                         \
+  do {                                                                   \
+    if (!(c)) {                                                          \
+      std::printf("FAIL line %d: %s\n", __LINE__, #c);                   \
+      return 1;                                                          \
+    }                                                                    \
+  } while (0)
+
+static hipStream_t S(long i) { return (hipStream_t)(0x10000 + 16 * i); }
+
+int main() {
+  using namespace kgs;
+  // 1. 300 distinct streams: 300 distinct, zeroed slots; the same stream again -> the same slot
+  std::set<int*> seen;
+  for (int i = 0; i < 300; ++i) {
+    int* q = tile_queue(S(i));
+    CHECK(q != nullptr);
+    for (int j = 0; j < TQ_INTS; ++j) CHECK(q[j] == 0);
+    CHECK(seen.insert(q).second);
+  }
+  CHECK(tile_queue(S(7)) == tile_queue(S(7)));
+  CHECK(tile_queue_stats(0).stream_slots == 300);
+  // free slots kept for captures: more than the reserve after the growth
+  CHECK(tile_queue_stats(0).slots - 300 > TQ_RESERVE);
+  // 2. hipStreamPerThread: one slot per thread
+  int* mine = tile_queue(hipStreamPerThread);
+  int* theirs = nullptr;
+  std::thread t([&] { theirs = tile_queue(hipStreamPerThread); });
+  t.join();
+  CHECK(mine && theirs && mine != theirs && !seen.count(mine) && !seen.count(theirs));
+  CHECK(tile_queue(hipStreamPerThread) == mine);
+  // 3. captures: each a fresh slot with a memset recorded on the capture stream, never S(0)'s
+  fakehip::capturing()[S(0)] = true;
+  const size_t m0 = fakehip::memsets().size();
+  int* c1 = tile_queue(S(0));
+  int* c2 = tile_queue(S(0));
+  CHECK(c1 && c2 && c1 != c2 && c1 != tile_queue(S(1)));
+  CHECK(!seen.count(c1) && !seen.count(c2) && c1 != mine && c2 != mine);
+  CHECK(fakehip::memsets().size() == m0 + 2);
+  CHECK(fakehip::memsets()[m0].p == c1 && fakehip::memsets()[m0].captured && fakehip::memsets()[m0].n == 64);
+  // 4. no allocation during a capture: exhaust the reserve -> nullptr, counted
+  const int mallocs = fakehip::mallocs();
+  int got = 0;
+  while (tile_queue(S(0)) != nullptr) ++got;
+  CHECK(got > 0 && fakehip::mallocs() == mallocs);
+  CHECK(tile_queue_stats(0).fallbacks == 1);
+  fakehip::capturing()[S(0)] = false;
+  // eager S(0) keeps its own slot (taken before the capture) ...
+  CHECK(seen.count(tile_queue(S(0))));
+  // ... and a new stream outside the capture grows the pool again
+  int* fresh = tile_queue(S(1000));
+  CHECK(fresh != nullptr && fakehip::mallocs() == mallocs + 1);
+  // 5. a stream on device 1 gets device 1's pool (its own slot)
+  fakehip::stream_dev()[S(2000)] = 1;
+  int* d1 = tile_queue(S(2000));
+  CHECK(d1 && tile_queue_stats(1).stream_slots == 1 && tile_queue_stats(0).stream_slots == 303);
+  CHECK(fakehip::cur_dev() == 0);  // restored after allocating on device 1
+  // 6. allocation failure on a fresh pool -> nullptr, not a crash
+  fakehip::malloc_budget() = 0;
+  fakehip::stream_dev()[S(3000)] = 2;
+  CHECK(tile_queue(S(3000)) == nullptr && tile_queue_stats(2).fallbacks == 1);
+  std::printf("tile_queue host test: OK (%ld slots on device 0)\n", tile_queue_stats(0).slots);
+  return 0;
+}
