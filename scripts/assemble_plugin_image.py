@@ -27,6 +27,24 @@ DOCKERFILE = os.path.join(ROOT, "images", "Dockerfile.deviceplugin")
 DEFAULT_OUT = os.path.join(ROOT, "images", "_assembled", "deviceplugin")
 
 
+def _relink_sonames(lib: str) -> None:
+    """COPY follows symlinks, so libX.so, libX.so.N and libX.so.N.M arrive as
+    three identical files; put the ROCm install's links back (the tree is
+    pushed to the GPU box on every call: 5.6 MB less)."""
+    by_digest: dict = {}
+    for name in sorted(os.listdir(lib), key=len, reverse=True):  # the full version first
+        path = os.path.join(lib, name)
+        if os.path.islink(path) or not os.path.isfile(path):
+            continue
+        with open(path, "rb") as f:
+            d = hashlib.sha256(f.read()).hexdigest()
+        if d in by_digest:
+            os.unlink(path)
+            os.symlink(by_digest[d], path)
+        else:
+            by_digest[d] = name
+
+
 def assemble(out: str = DEFAULT_OUT, python: str = sys.executable) -> dict:
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from dockerfile_exec import Executor  # noqa: E402
@@ -42,6 +60,7 @@ def assemble(out: str = DEFAULT_OUT, python: str = sys.executable) -> dict:
         shutil.copytree(final, out, symlinks=True)
     finally:
         shutil.rmtree(work, ignore_errors=True)
+    _relink_sonames(os.path.join(out, "opt", "kgs", "lib"))
     with open(DOCKERFILE, "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()
     info = {"dockerfile": os.path.relpath(DOCKERFILE, ROOT), "dockerfile_sha256": sha, "assembled_at": time.time(),
