@@ -30,6 +30,7 @@
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
 #   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
+#   bench_trace  kernel trace of bench.py (GEMM durations and the gaps between them)
 #   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
 #   serve        kgs.serve batch-256 serving bench (serve_nofuse: split-K reduces unfused)
 #   decode_trace kernel trace of batch-256 decode (decode_trace_b1: batch 1; serve_b1: batch-1 serving)
@@ -134,6 +135,8 @@ step() {
             run g2_tcp 120 timeout -s KILL 100 rocprofv3 --pmc TA_BUSY_avr TCP_TCC_READ_REQ_sum \
                 TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE \
                 --output-format csv -d "$O/g2_tcp_${MNK:-8192}" -o g -- $G ;;
+        bench_trace) run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/btrace" -o b \
+            -- python3 bench.py --steps 20 --warmup 5 ;;
         overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
             run overlap_rccl_hi 300 python bench/overlap_rccl.py --side-priority high \
                 --out "$O/overlap_rccl_shape_hiprio.json" ;;
