@@ -45,9 +45,31 @@ def main(argv=None) -> int:
     C = [torch.empty((M, N), device=dev, dtype=torch.bfloat16) for _ in range(2)]
     ref = A.float()[:256] @ B.float().T
 
+    side = torch.cuda.Stream(device=dev)
+    main = torch.cuda.current_stream(dev)
+
+    def two_streams(v):
+        """The step's independent GEMMs alternated over two streams (odd ones
+        on a side stream that joins at the end of the step), so one GEMM's
+        tail and the next one's ramp overlap instead of queueing behind the
+        stream's kernel barrier. Experiment only: bench.py keeps one stream."""
+        def f(i):
+            if i == 0:
+                side.wait_stream(main)  # before GEMM 0 is queued: GEMM 1 may start on CUs GEMM 0 frees
+            if i & 1:
+                with torch.cuda.stream(side):
+                    gemm_nt(A, B, out=C[i & 1], variant=v)
+            else:
+                gemm_nt(A, B, out=C[i & 1], variant=v)
+            if i == a.gemms - 1:
+                main.wait_stream(side)
+        return f
+
     def path(p):
         if p == "hipblaslt":
             return lambda i: torch.matmul(A, B.T, out=C[i & 1])
+        if p.endswith("_2s"):
+            return two_streams(p[:-3])
         return lambda i: gemm_nt(A, B, out=C[i & 1], variant=p)
 
     paths = {p: path(p) for p in a.paths.split(",")}
