@@ -91,7 +91,8 @@ step() {
             GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc2" -o gemm -- $PMC_GEMM ;;
         overlap) run overlap 300 python bench/overlap.py --out "$O/overlap.json" ;;
         counters_list) run counters_list 120 rocprofv3 -L ;;
-        step_ab) run step_ab 400 python bench/step_ab.py --mnk ${MNK:-8192} --out "$O/step_ab_${MNK:-8192}.json" ;;
+        step_ab) run step_ab 400 python bench/step_ab.py --mnk ${MNK:-8192} --paths ${PATHS:-fast,w4_oneshot,hipblaslt} \
+            --out "$O/step_ab_${MNK:-8192}.json" ;;
         step_ab_long) run step_ab_long 600 python bench/step_ab.py --mnk ${MNK:-8192} --seconds 3 --rounds 5 \
             --out "$O/step_ab_long_${MNK:-8192}.json" ;;
         gateup_pmc)  # counter passes over the batch-256 gate|up + SwiGLU kernel (default vs nt weight loads)
