@@ -60,6 +60,15 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
       KGS_W4P(107, 100000000, true)
       KGS_W4P(108, 200000000, true)
       KGS_W4P(109, 140000002, true)
+      // C stored non-temporally: default / mirror G8 maps
+      case 131:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, true>), pg, dim3(256), 0, s, a, b, c, nullptr, M,
+                           N, K, lda, ldb, ldc, tq);
+        break;
+      case 132:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, true>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)

@@ -140,7 +140,7 @@ __device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>&
 // Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
 // bias + activation, pack to bf16, pair n-tiles with v_permlane16_swap -> one
 // 16-B store per lane (the one-shot kernel's epilogue, reading named AGPRs).
-template <int EPI, int Q>
+template <int EPI, int Q, bool NTST = false>
 __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn,
                                      const float (&bv)[NB][4]) {
   if constexpr (Q < MA * NB) {
@@ -157,8 +157,15 @@ __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ 
     const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
     const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
     const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
-    *(uint4*)(C + (long)row * ldc + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
-    pepi<EPI, Q + 2>(c, C, ldc, tm, tn, bv);
+    uint4* dst = (uint4*)(C + (long)row * ldc + col0 + (fq & 1) * 16 + (fq >> 1) * 8);
+    if constexpr (NTST) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 v = {qv.x, qv.y, qv.z, qv.w};
+      __builtin_nontemporal_store(v, (u32x4*)dst);
+    } else {
+      *dst = qv;
+    }
+    pepi<EPI, Q + 2, NTST>(c, C, ldc, tm, tn, bv);
   }
 }
 
@@ -177,7 +184,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 // the first one too (a workgroup that starts late -- its CU held by a
 // collective launched just before -- takes only the tiles still left);
 // 0 = the static walk v, v + G, v + 2G (q unused), for measurements.
-template <int EPI, int X = 0, int DYN = 1>
+// NTST: C stored non-temporally (measurement knob: the output is not re-read
+// by this launch, so it need not displace A / B lines in L2 / MALL).
+template <int EPI, int X = 0, int DYN = 1, bool NTST = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
@@ -303,7 +312,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
     }
-    pepi<EPI, 0>(c, C, ldc, tm, tn, bv);
+    pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
     if (!more) break;
     t = tnx;
     tm = tmn;

@@ -649,7 +649,8 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 384, "w4p_0"), (4608, 4096, 384, "w4p_0"),
-                                           (8192, 2304, 512, "w4p_140000000"), (1024, 768, 1024, "w4p_0")])
+                                           (8192, 2304, 512, "w4p_140000000"), (1024, 768, 1024, "w4p_0"),
+                                           (4608, 4096, 384, "w4pn_0"), (8192, 2304, 9216, "w4pn_140000008")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
     tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
