@@ -77,7 +77,7 @@ W4H.update({f"w4p_{x}": 101 + i for i, x in enumerate(_W4P_X)})
 # the same with the static tile walk (no ticket queue): w4ps_X -> 121..
 W4H.update({f"w4ps_{x}": 121 + i for i, x in enumerate((0, 140000000, 8, 140000008))})
 # round 4: C stored non-temporally (gemm_w4p.h NTST): w4pn_X -> 131..
-W4H.update({"w4pn_0": 131, "w4pn_140000008": 132})
+W4H.update({"w4pn_0": 131, "w4pn_140000008": 132, "w4pn_8": 133, "w4pn_140000000": 134})
 
 
 @lru_cache(maxsize=1)

@@ -69,6 +69,14 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
         hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, true>), pg, dim3(256), 0, s, a, b, c,
                            nullptr, M, N, K, lda, ldb, ldc, tq);
         break;
+      case 133:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 8, 1, true>), pg, dim3(256), 0, s, a, b, c, nullptr, M,
+                           N, K, lda, ldb, ldc, tq);
+        break;
+      case 134:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000000, 1, true>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)
