@@ -70,6 +70,12 @@ def main(argv=None) -> int:
             return lambda i: torch.matmul(A, B.T, out=C[i & 1])
         if p.endswith("_2s"):
             return two_streams(p[:-3])
+        from kgs.ops.gemm import VARIANTS
+
+        if p not in VARIANTS:  # a measured alternative from the experiments library
+            from kgs.ops import experiments
+
+            return lambda i: experiments.gemm_nt(A, B, p, out=C[i & 1])
         return lambda i: gemm_nt(A, B, out=C[i & 1], variant=p)
 
     paths = {p: path(p) for p in a.paths.split(",")}

@@ -94,6 +94,7 @@ step() {
         step_ab) run step_ab 400 python bench/step_ab.py --mnk ${MNK:-8192} --paths ${PATHS:-fast,w4_oneshot,hipblaslt} \
             --out "$O/step_ab_${MNK:-8192}.json" ;;
         step_ab_long) run step_ab_long 600 python bench/step_ab.py --mnk ${MNK:-8192} --seconds 3 --rounds 5 \
+            --paths ${PATHS:-fast,w4_oneshot,hipblaslt} \
             --out "$O/step_ab_long_${MNK:-8192}.json" ;;
         gateup_pmc)  # counter passes over the batch-256 gate|up + SwiGLU kernel (default vs nt weight loads)
             local GU="python3 bench/decode_gateup_probe.py --batches 256 --iters 30"
