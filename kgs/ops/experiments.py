@@ -98,6 +98,8 @@ def lib() -> ctypes.CDLL:
     so.kgs_exp_gemm_w4h.restype = i
     so.kgs_exp_gemm_w4p_grid.argtypes = [vp] * 3 + [i] * 8 + [vp]
     so.kgs_exp_gemm_w4p_grid.restype = i
+    so.kgs_exp_gemm_w4p_stamps.argtypes = [vp] * 3 + [i] * 7 + [vp] * 3
+    so.kgs_exp_gemm_w4p_stamps.restype = i
     so.kgs_exp_gemm_fp8_w4f8.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
     so.kgs_exp_gemm_fp8_w4f8.restype = i
     return so
@@ -169,3 +171,24 @@ def gemm_w4p_grid(a, b, out, mode: int = 1, grid: int = 0) -> None:
     _lib.check(lib().kgs_exp_gemm_w4p_grid(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
                                            b.stride(0), out.stride(0), int(mode), int(grid),
                                            _lib.stream_handle(a.device)), "kgs_exp_gemm_w4p_grid")
+
+
+def gemm_w4p_stamps(a, b, out, stamps: torch.Tensor, map_: int = 0) -> int:
+    """The production persistent GEMM's timing build (gemm_w4p.h TS) on the
+    current stream: ``stamps`` is an int64 [>= grid, 16] device tensor that
+    receives per-workgroup start / per-tile end stamps (s_memrealtime, 100 MHz),
+    HW_ID and XCC_ID. ``map_`` 0 = default tile map, 1 = mirrored G8 (tall,
+    K > 8192). Returns the grid."""
+    M, K = a.shape
+    N = b.shape[0]
+    if stamps.dtype != torch.int64 or stamps.dim() != 2 or stamps.shape[1] != 16 or not stamps.is_contiguous():
+        raise ValueError("stamps must be a contiguous int64 [grid, 16] tensor")
+    grid = ctypes.c_int(0)
+    tiles = (M // 256) * (N // 256)
+    if stamps.shape[0] < min(tiles, torch.cuda.get_device_properties(a.device).multi_processor_count):
+        raise ValueError("stamps has fewer rows than the grid")
+    _lib.check(lib().kgs_exp_gemm_w4p_stamps(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
+                                             b.stride(0), out.stride(0), int(map_), stamps.data_ptr(),
+                                             ctypes.byref(grid), _lib.stream_handle(a.device)),
+               "kgs_exp_gemm_w4p_stamps")
+    return grid.value

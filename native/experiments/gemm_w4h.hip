@@ -143,6 +143,35 @@ KGS_EXPORT int kgs_exp_gemm_w4p_grid(const void* A, const void* B, void* C, int 
   return (int)hipGetLastError();
 }
 
+// The production persistent kernel's timing build (gemm_w4p.h TS): map 0 =
+// the default tile map (square / wide problems), 1 = mirrored G8 (tall, long
+// K). `stamps`: long long[grid][16], grid = min(tiles, CUs) (returned in *grid_out).
+KGS_EXPORT int kgs_exp_gemm_w4p_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                       int ldc, int map, void* stamps, int* grid_out, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K < 384 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (M % 256 || N % 256 || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16 || !stamps) return KGS_ERR_ALIGN;
+  if ((long)lda * 256 * 2 >= (1L << 31) || (long)ldb * 256 * 2 >= (1L << 31)) return KGS_ERR_SHAPE;
+  const int ntiles = (M / 256) * (N / 256);
+  const int grid = ntiles < cu_count() ? ntiles : cu_count();
+  if (grid_out) *grid_out = grid;
+  int* tq = kgs::tile_queue(s);
+  if (!tq) return KGS_ERR_ARG;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto ts = (const unsigned short*)stamps;
+  if (map == 0)
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, true>), dim3(grid), dim3(256), 0, s, a, b, c,
+                       ts, M, N, K, lda, ldb, ldc, tq);
+  else if (map == 1)
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, true>), dim3(grid), dim3(256), 0, s,
+                       a, b, c, ts, M, N, K, lda, ldb, ldc, tq);
+  else
+    return KGS_ERR_ARG;
+  return (int)hipGetLastError();
+}
+
 // fp8 four-wave persistent kernel (gemm_w4f8.h) with schedule knobs B1 / R / P
 // and tile-map X; ids 40.. (kgs/ops/experiments.py W4F8). Aligned shapes,
 // K (fp8) >= 768 and % 256; lengths in fp8 elements.

@@ -186,7 +186,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 // 0 = the static walk v, v + G, v + 2G (q unused), for measurements.
 // NTST: C stored non-temporally (measurement knob: the output is not re-read
 // by this launch, so it need not displace A / B lines in L2 / MALL).
-template <int EPI, int X = 0, int DYN = 1, bool NTST = false>
+// TS: timing build (experiments only, EPI_NONE): `bias` is a long long[grid][16]
+// buffer; workgroup b writes [0] its start (s_memrealtime, 100 MHz), [1] HW_ID |
+// XCC_ID << 32, [2 + j] the end of its j-th tile's epilogue (j < 14), [15] tiles.
+template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
@@ -201,6 +204,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntm = M / BM, ntn = N / BN, ntiles = ntm * ntn;
+  static_assert(!TS || EPI == EPI_NONE, "timing build: bias carries the stamp buffer");
+  long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
+  int ntile_done = 0;
+  if constexpr (TS) {
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_ID, all 32 bits
+    const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (3 << 11));  // XCC_ID[3:0]
+    if (threadIdx.x == 0) {
+      ts[0] = t0;
+      ts[1] = (long long)hw | ((long long)xcc << 32);
+    }
+  }
 
   Ctx c;
   c.smem = smem;
@@ -313,6 +328,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
     pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
+    if constexpr (TS) {
+      const long long te = (long long)__builtin_amdgcn_s_memrealtime();
+      if (threadIdx.x == 0 && ntile_done < 14) ts[2 + ntile_done] = te;
+      ++ntile_done;
+      if (threadIdx.x == 0) ts[15] = ntile_done;
+    }
     if (!more) break;
     t = tnx;
     tm = tmn;

@@ -42,6 +42,7 @@
 #   gemm_llm     kgs vs hipBLASLt on the Llama-shaped GEMMs ($SHAPES overrides)
 #   prefill      Llama-3-8B prefill, batch 4 x 2048 (kgs / torch / fp8); prefill_trace: its kernel trace
 #   gpuinfo      kgs-gpuinfo --json (amd-smi + KFD views)
+#   gemm_tail    per-workgroup start / per-tile end stamps of the persistent GEMM (head, tail, XCD spread)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
 #   attn_bench   flash-attention forward vs SDPA
@@ -205,6 +206,8 @@ step() {
         gemm_llm) run gemm_llm 600 python bench/gemm_sweep.py \
             --shapes ${SHAPES:-8192x4096x14336,4096,8192x28672x4096,8192x6144x4096,8192} \
             --variants ${VARIANTS:-fast} --rounds 7 --out "$O/gemm_llm.json" ;;
+        gemm_tail) run gemm_tail 300 python bench/gemm_tail.py --shapes ${SHAPES:-8192,8192x4096x14336,16384x16384x8192} \
+            --launches ${L:-20} --out "$O/gemm_tail.json" ;;
         gpuinfo) run gpuinfo 60 kgs/_native/kgs-gpuinfo --json ;;
         route_ab)  # 128-row tiles for the split-K decode projections at 192-384 rows, then serving A/B/A
             # with $ROUTES (KGS_W4X_ROUTES syntax) and a kernel trace of the B routes
