@@ -39,36 +39,39 @@ def analyse(st_all, grid: int) -> dict:
     for li in range(st_all.shape[0]):
         s = st_all[li, :grid]
         start = s[:, 0].double()
+        last = s[:, 14].double()
         ntl = s[:, 15].long()
-        ends = []
-        for b in range(grid):
-            n = int(min(ntl[b].item(), 14))
-            ends.append(s[b, 2:2 + n].double())
-        last = torch.stack([e[-1] for e in ends])
         t0, t1 = start.min().item(), last.max().item()
         span = (t1 - t0) * tick_us
-        head = ((start - t0) * tick_us)
-        tail = ((t1 - last) * tick_us)
+        head = (start - t0) * tick_us
+        tail = (t1 - last) * tick_us
         xcc = (s[:, 1] >> 32).long() & 0xF
-        per_x = {}
+        # mean tile time per workgroup after its first tile (tiles 1 .. n-1), and per XCD
+        per_tile = ((last - s[:, 2].double()) * tick_us) / (ntl - 1).clamp(min=1).double()
+        per_x_fin, per_x_tile = {}, {}
         for x in sorted(set(xcc.tolist())):
             m = xcc == x
-            per_x[int(x)] = round(((t1 - last[m].max().item()) * tick_us), 2)
-        # tile times by index: first tile from the workgroup's start, later ones end-to-end
+            per_x_fin[int(x)] = round((t1 - last[m].max().item()) * tick_us, 2)
+            per_x_tile[int(x)] = round(per_tile[m].mean().item(), 2)
         by_idx = {}
         for b in range(grid):
-            e = ends[b]
+            n = int(min(ntl[b].item(), 11))
             prev = start[b].item()
-            for j in range(e.shape[0]):
-                by_idx.setdefault(j, []).append((e[j].item() - prev) * tick_us)
-                prev = e[j].item()
+            for j in range(n):
+                e = s[b, 2 + j].item()
+                by_idx.setdefault(j, []).append((e - prev) * tick_us)
+                prev = e
+        exit_ = s[:, 13].double()
         rec = {
             "span_us": round(span, 2),
+            # the last workgroup's exit (queue exit counter + reset) after the launch's last tile end
+            "exit_after_last_tile_us": round((exit_.max().item() - t1) * tick_us, 2),
             "head_mean_us": round(head.mean().item(), 2), "head_max_us": round(head.max().item(), 2),
             "tail_mean_us": round(tail.mean().item(), 2), "tail_max_us": round(tail.max().item(), 2),
             "edge_idle_frac": round((head.mean().item() + tail.mean().item()) / span, 4),
             "tiles_per_wg": sorted(set(ntl.tolist())),
-            "xcd_finish_before_last_us": per_x,
+            "xcd_finish_before_last_us": per_x_fin,
+            "xcd_mean_tile_us": per_x_tile,
             "tile_us_median_by_index": {j: round(st.median(v), 2) for j, v in by_idx.items()},
             "tile_us_p10_p90_by_index": {j: [round(sorted(v)[len(v) // 10], 2), round(sorted(v)[(9 * len(v)) // 10], 2)]
                                          for j, v in by_idx.items()},
@@ -78,18 +81,27 @@ def analyse(st_all, grid: int) -> dict:
         prev_end = t1
         launches.append(rec)
     body = launches[1:] if len(launches) > 2 else launches
-    keys = ("span_us", "head_mean_us", "head_max_us", "tail_mean_us", "tail_max_us", "edge_idle_frac")
+    keys = ("span_us", "exit_after_last_tile_us", "head_mean_us", "head_max_us", "tail_mean_us", "tail_max_us", "edge_idle_frac")
     summary = {k: round(st.median([r[k] for r in body]), 4) for k in keys}
     gaps = [r["gap_from_previous_us"] for r in body if "gap_from_previous_us" in r]
     if gaps:
         summary["gap_from_previous_us"] = round(st.median(gaps), 2)
-    return {"summary": summary, "launches": launches}
+    xs = sorted(body[0]["xcd_mean_tile_us"])
+    summary["xcd_mean_tile_us"] = {x: round(st.median([r["xcd_mean_tile_us"][x] for r in body]), 2) for x in xs}
+    summary["xcd_finish_before_last_us"] = {x: round(st.median([r["xcd_finish_before_last_us"][x] for r in body]), 2)
+                                            for x in xs}
+    mid = st_all[st_all.shape[0] // 2, :grid]
+    raw = {"t0": int(mid[:, 0].min().item()),
+           "rows": [[int(v) for v in mid[b].tolist()] for b in range(grid)]}
+    return {"summary": summary, "launches": launches, "raw_middle_launch": raw}
 
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--shapes", default="8192,8192x4096x14336")
     ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--maps", default="prod",
+                    help="comma list of tile maps (kgs.ops.experiments.STAMP_MAPS names) or 'prod'")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -98,12 +110,9 @@ def main() -> int:
 
     dev = torch.device("cuda", 0)
     res = []
-    for sh in a.shapes.split(","):
+    for sh, mp in [(sh, mp) for sh in a.shapes.split(",") for mp in a.maps.split(",")]:
         M, N, K = parse_shape(sh)
-        map_ = 1 if (M > N and K > 8192) else 0
-        if M > N and K <= 8192 or (M <= N and K > 8192):
-            print(f"{sh}: production uses a map the timing build does not have; skipped", file=sys.stderr)
-            continue
+        map_ = ex.production_map(M, N, K) if mp == "prod" else mp
         g = torch.Generator(device=dev)
         g.manual_seed(0)
         A = (torch.rand((M, K), generator=g, device=dev) * 2 - 1).bfloat16()
@@ -118,7 +127,7 @@ def main() -> int:
         ex.gemm_w4p_stamps(A, B, C2, stamps[0], map_)
         gemm_nt(A, B, out=C)
         torch.cuda.synchronize()
-        same = bool(torch.equal(C, C2))
+        same = bool(torch.equal(C, C2))  # the maps change only the tile order: same bits everywhere
         # timing build vs production, interleaved blocks of L launches
         ev = lambda: torch.cuda.Event(enable_timing=True)  # noqa: E731
         t_prod, t_ts = [], []
@@ -139,10 +148,10 @@ def main() -> int:
             ex.gemm_w4p_stamps(A, B, C2, stamps[i], map_)
         torch.cuda.synchronize()
         an = analyse(stamps.cpu(), grid)
-        r = {"shape": [M, N, K], "grid": grid, "bitwise_production": same,
+        r = {"shape": [M, N, K], "map": map_, "grid": grid, "bitwise_production": same,
              "us_per_launch_production": round(st.median(t_prod), 2),
              "us_per_launch_timing_build": round(st.median(t_ts), 2), **an}
-        print(json.dumps({k: v for k, v in r.items() if k != "launches"}), flush=True)
+        print(json.dumps({k: v for k, v in r.items() if k not in ("launches", "raw_middle_launch")}), flush=True)
         res.append(r)
     if a.out:
         Path(a.out).write_text(json.dumps(res, indent=1))

@@ -173,12 +173,23 @@ def gemm_w4p_grid(a, b, out, mode: int = 1, grid: int = 0) -> None:
                                            _lib.stream_handle(a.device)), "kgs_exp_gemm_w4p_grid")
 
 
-def gemm_w4p_stamps(a, b, out, stamps: torch.Tensor, map_: int = 0) -> int:
-    """The production persistent GEMM's timing build (gemm_w4p.h TS) on the
-    current stream: ``stamps`` is an int64 [>= grid, 16] device tensor that
-    receives per-workgroup start / per-tile end stamps (s_memrealtime, 100 MHz),
-    HW_ID and XCC_ID. ``map_`` 0 = default tile map, 1 = mirrored G8 (tall,
-    K > 8192). Returns the grid."""
+# tile maps of the timing build (gemm_w4h.hip kgs_exp_gemm_w4p_stamps)
+STAMP_MAPS = {"default": 0, "mirror_g8": 1, "g8": 2, "mirror": 3, "blk1": 4, "blk2": 5, "blk3": 6}
+
+
+def production_map(M: int, N: int, K: int) -> str:
+    """The tile map gemm_persistent.hip's launcher uses for an aligned problem."""
+    tall, longk = M > N, K > 8192
+    return "mirror_g8" if tall and longk else "mirror" if tall else "g8" if longk else "default"
+
+
+def gemm_w4p_stamps(a, b, out, stamps: torch.Tensor, map_: int | str = 0) -> int:
+    """The persistent GEMM's timing build (gemm_w4p.h TS) on the current
+    stream: ``stamps`` is an int64 [>= grid, 16] device tensor that receives
+    per-workgroup start / per-tile end stamps (s_memrealtime, 100 MHz), HW_ID
+    and XCC_ID. ``map_``: a STAMP_MAPS name or id. Returns the grid."""
+    if isinstance(map_, str):
+        map_ = STAMP_MAPS[map_]
     M, K = a.shape
     N = b.shape[0]
     if stamps.dtype != torch.int64 or stamps.dim() != 2 or stamps.shape[1] != 16 or not stamps.is_contiguous():

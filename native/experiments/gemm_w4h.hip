@@ -143,9 +143,8 @@ KGS_EXPORT int kgs_exp_gemm_w4p_grid(const void* A, const void* B, void* C, int 
   return (int)hipGetLastError();
 }
 
-// The production persistent kernel's timing build (gemm_w4p.h TS): map 0 =
-// the default tile map (square / wide problems), 1 = mirrored G8 (tall, long
-// K). `stamps`: long long[grid][16], grid = min(tiles, CUs) (returned in *grid_out).
+// The persistent kernel's timing build (gemm_w4p.h TS) with tile map `map`
+// (table below; 0 and 1 are production's for square / tall long-K problems). `stamps`: long long[grid][16], grid = min(tiles, CUs) (returned in *grid_out).
 KGS_EXPORT int kgs_exp_gemm_w4p_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                        int ldc, int map, void* stamps, int* grid_out, hipStream_t s) {
   if (M <= 0 || N <= 0 || K < 384 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
@@ -161,14 +160,23 @@ KGS_EXPORT int kgs_exp_gemm_w4p_stamps(const void* A, const void* B, void* C, in
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
   auto ts = (const unsigned short*)stamps;
-  if (map == 0)
-    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, true>), dim3(grid), dim3(256), 0, s, a, b, c,
-                       ts, M, N, K, lda, ldb, ldc, tq);
-  else if (map == 1)
-    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, true>), dim3(grid), dim3(256), 0, s,
-                       a, b, c, ts, M, N, K, lda, ldb, ldc, tq);
-  else
-    return KGS_ERR_ARG;
+#define KGS_W4PT(ID, X)                                                                                          \
+  case ID:                                                                                                        \
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, X, 1, false, true>), dim3(grid), dim3(256), 0, s, a, b, \
+                       c, ts, M, N, K, lda, ldb, ldc, tq);                                                        \
+    break;
+  // map: 0 default, 1 mirrored G8 (production tall long-K), 2 G8, 3 mirrored, 4..6 XCD-blocked MAP 1..3
+  switch (map) {
+    KGS_W4PT(0, 0)
+    KGS_W4PT(1, 140000008)
+    KGS_W4PT(2, 8)
+    KGS_W4PT(3, 140000000)
+    KGS_W4PT(4, 10000000)
+    KGS_W4PT(5, 20000000)
+    KGS_W4PT(6, 30000000)
+    default: return KGS_ERR_ARG;
+  }
+#undef KGS_W4PT
   return (int)hipGetLastError();
 }
 

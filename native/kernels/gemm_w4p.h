@@ -188,7 +188,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 // by this launch, so it need not displace A / B lines in L2 / MALL).
 // TS: timing build (experiments only, EPI_NONE): `bias` is a long long[grid][16]
 // buffer; workgroup b writes [0] its start (s_memrealtime, 100 MHz), [1] HW_ID |
-// XCC_ID << 32, [2 + j] the end of its j-th tile's epilogue (j < 14), [15] tiles.
+// XCC_ID << 32, [2 + j] the end of its j-th tile's epilogue (j < 11), [13] its
+// exit (after the queue's exit counter / reset), [14] the end of its last tile,
+// [15] tiles.
 template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
@@ -330,9 +332,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
     if constexpr (TS) {
       const long long te = (long long)__builtin_amdgcn_s_memrealtime();
-      if (threadIdx.x == 0 && ntile_done < 14) ts[2 + ntile_done] = te;
+      if (threadIdx.x == 0 && ntile_done < 11) ts[2 + ntile_done] = te;
       ++ntile_done;
-      if (threadIdx.x == 0) ts[15] = ntile_done;
+      if (threadIdx.x == 0) {
+        ts[14] = te;
+        ts[15] = ntile_done;
+      }
     }
     if (!more) break;
     t = tnx;
@@ -345,6 +350,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   if constexpr (DYN != 0) {
     if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)  // last one out resets the queue
       for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
+  }
+  if constexpr (TS) {
+    __syncthreads();
+    const long long tx = (long long)__builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) ts[13] = tx;
   }
 }
 
