@@ -93,7 +93,8 @@ def main():
     ap.add_argument("--cool", type=float, default=2.0)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--period", type=float, default=0.005)
-    ap.add_argument("--backends", default="kgs,hipblaslt")
+    ap.add_argument("--backends", default="kgs,hipblaslt",
+                    help="kgs, hipblaslt and/or kgs.ops.experiments variant names")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from kgs.ops import gemm_nt
@@ -104,6 +105,11 @@ def main():
     B = (torch.rand(N, K, device="cuda") * 2 - 1).bfloat16()
     C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     fns = {"kgs": lambda: gemm_nt(A, B, out=C), "hipblaslt": lambda: torch.matmul(A, B.T, out=C)}
+    for name in a.backends.split(","):  # any other name: a kgs.ops.experiments variant
+        if name not in fns:
+            from kgs.ops import experiments
+
+            fns[name] = (lambda v: lambda: experiments.gemm_nt(A, B, v, out=C))(name)
     fl = 2.0 * M * N * K
     for f in fns.values():
         f()

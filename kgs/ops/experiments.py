@@ -78,6 +78,11 @@ W4H.update({f"w4p_{x}": 101 + i for i, x in enumerate(_W4P_X)})
 W4H.update({f"w4ps_{x}": 121 + i for i, x in enumerate((0, 140000000, 8, 140000008))})
 # round 4: C stored non-temporally (gemm_w4p.h NTST): w4pn_X -> 131..
 W4H.update({"w4pn_0": 131, "w4pn_140000008": 132, "w4pn_8": 133, "w4pn_140000000": 134})
+# round 4: LDS layout 1 (gemm_w4p.h Lay<1>: rows DMA'd by consecutive lanes in address order,
+# placed for conflict-free fragment reads): w4pl_X -> 135..
+W4H.update({"w4pl_0": 135, "w4pl_140000008": 136, "w4pl_8": 137, "w4pl_140000000": 138})
+# round 4: MFMA order inside a k-sub: i-major (w4po0_X) / n-major (w4po2_X) instead of the growing square
+W4H.update({"w4po0_0": 139, "w4po2_0": 140, "w4po0_140000008": 141, "w4po2_140000008": 142})
 
 
 @lru_cache(maxsize=1)

@@ -77,6 +77,40 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
         hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000000, 1, true>), pg, dim3(256), 0, s, a, b, c,
                            nullptr, M, N, K, lda, ldb, ldc, tq);
         break;
+      // round 4: LDS layout 1 (linear rows, conflict-free placement; gemm_w4p.h Lay<1>)
+      case 135:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 1>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 136:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, false, 1>), pg, dim3(256), 0, s,
+                           a, b, c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 137:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 8, 1, false, false, 1>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 138:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000000, 1, false, false, 1>), pg, dim3(256), 0, s,
+                           a, b, c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      // round 4: MFMA order inside a k-sub (gemm_w4p.h ord_of): i-major / n-major, default and mirror G8 maps
+      case 139:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 10>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 140:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 30>), pg, dim3(256), 0, s, a, b, c,
+                           nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 141:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, false, 10>), pg, dim3(256), 0, s,
+                           a, b, c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 142:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, false, 30>), pg, dim3(256), 0, s,
+                           a, b, c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)

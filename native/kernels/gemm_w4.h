@@ -203,7 +203,8 @@ __device__ __forceinline__ void read_row(f32x4 (&v)[NB]) {
 __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 
 // MFMA order inside a k-sub. ORD 0: i-major (a[i] over all n), reads b0..b(NB-1)
-// then a0..a(MA-1). ORD 1: "growing square": reads alternate b0 a0 b1 a1 ...
+// then a0..a(MA-1). ORD 2: n-major (b[n] over all i), reads a0..a(MA-1) then
+// b0..b(NB-1). ORD 1: "growing square": reads alternate b0 a0 b1 a1 ...
 // (then the remaining fragments of the larger side), and each MFMA (i, n) runs
 // right after the read that completes its pair, so the first MFMA of a k-sub
 // waits for 2 reads.
@@ -213,10 +214,14 @@ struct MOrder {
 
 // read r of a k-sub: which fragment (0 = b, 1 = a) and its index
 constexpr int rd_isa(int ord, int ma, int nb, int r) {
-  return ord == 0 ? (r >= nb) : (r < 2 * (ma < nb ? ma : nb) ? (r & 1) : (ma > nb ? 1 : 0));
+  return ord == 0 ? (r >= nb)
+       : ord == 2 ? (r < ma)
+                  : (r < 2 * (ma < nb ? ma : nb) ? (r & 1) : (ma > nb ? 1 : 0));
 }
 constexpr int rd_idx(int ord, int ma, int nb, int r) {
-  return ord == 0 ? (r < nb ? r : r - nb) : (r < 2 * (ma < nb ? ma : nb) ? (r >> 1) : r - (ma < nb ? ma : nb));
+  return ord == 0 ? (r < nb ? r : r - nb)
+       : ord == 2 ? (r < ma ? r : r - ma)
+                  : (r < 2 * (ma < nb ? ma : nb) ? (r >> 1) : r - (ma < nb ? ma : nb));
 }
 
 constexpr MOrder make_order(int ord, int ma, int nb) {
@@ -225,6 +230,11 @@ constexpr MOrder make_order(int ord, int ma, int nb) {
   if (ord == 0) {
     for (int i = 0; i < ma; ++i)
       for (int n = 0; n < nb; ++n) { o.i[k] = i; o.n[k] = n; ++k; }
+    return o;
+  }
+  if (ord == 2) {  // n-major: B fragment n (the MFMA's first operand) held for ma MFMAs
+    for (int n = 0; n < nb; ++n)
+      for (int i = 0; i < ma; ++i) { o.i[k] = i; o.n[k] = n; ++k; }
     return o;
   }
   bool ha[8] = {}, hb[8] = {};

@@ -55,6 +55,93 @@ using S = w4::Shape<BM, BN>;
 using Kn = w4::Knobs<BM, BN>;
 constexpr int MA = S::MA, NB = S::NB;
 
+// LDS image layouts (template parameter L of the kernel).
+//   L 0: gemm_w4.h's. A DMA instruction brings 8 consecutive 128-B rows; the
+//        16-B chunk c of row r lands at c ^ ((r >> 1) & 7), which is done by
+//        permuting the SOURCE address of the lanes of a row.
+//   L 1 (round 4 experiment): every row is read by 8 consecutive lanes in
+//        address order (no permutation inside a row). The rows are placed so
+//        the fragment reads stay conflict-free. A 32-row group is 4 DMA
+//        instructions k = 0..3, 1056 B apart (so instruction k starts at bank
+//        unit 2k), and the group is padded to 4352 B (17 x 256). Instruction
+//        k holds 4 rows of each 16-row fragment f in slots 4f + p:
+//          k0: 0 1 4 5   k1: 2 3 6 7   k2: 12 13 8 9   k3: 14 15 10 11
+//        In ds_read_b128 lane group {0-3, 12-15, 20-27}, rows {0-3, 12-15}
+//        read chunk q at 16-B units 2k + 8 (p & 1) + q (the 8 even units + q),
+//        and rows 4-11 read chunk q + 1 at the 8 odd units + q. The other
+//        three lane groups have the same structure, shifted.
+template <int L>
+struct Lay;
+template <>
+struct Lay<0> {
+  static constexpr int GROUP = 4096;  // bytes per 32-row group
+  static constexpr int OPA = S::OPA, STAGE = S::STAGE;
+  __device__ static constexpr int frag_off(int x) { return x * 2048; }
+  __device__ static int dma_dst(int j, int w) { return (j * 4 + w) * 1024; }
+  // row of the 32-row group and 16-B chunk that lane `lane` of wave `w` DMAs
+  __device__ static void dma_lane(int lane, int w, int& row, int& ch) {
+    row = w * 8 + (lane >> 3);
+    ch = (lane & 7) ^ ((row >> 1) & 7);
+  }
+  __device__ static int read_lane(int fr, int chunk) { return fr * 128 + ((chunk ^ (fr >> 1)) * 16); }
+};
+template <>
+struct Lay<1> {
+  static constexpr int GROUP = 4352, KSTRIDE = 1056;
+  static constexpr int OPA = (BM / 32) * GROUP, STAGE = OPA + (BN / 32) * GROUP;
+  __device__ static constexpr int frag_off(int x) { return (x >> 1) * GROUP + (x & 1) * 512; }
+  __device__ static int dma_dst(int j, int w) { return j * GROUP + w * KSTRIDE; }
+  __device__ static void dma_lane(int lane, int w, int& row, int& ch) {
+    // slot s = lane / 8 = 4 f + p; table row (k = w, p)
+    const int p = (lane >> 3) & 3, f = lane >> 5;
+    const int s1 = (w & 1) * 2 + (w >> 1) * 12;  // first S1 row of instruction k: 0 2 12 14
+    const int s2 = 4 + (w & 1) * 2 + (w >> 1) * 4;  // first S2 row: 4 6 8 10
+    row = 16 * f + ((p < 2) ? s1 + p : s2 + p - 2);
+    ch = lane & 7;
+  }
+  __device__ static int read_lane(int fr, int chunk) {
+    const int k = ((fr >> 1) & 1) + 2 * (fr >> 3);
+    const int p = (fr & 1) + 2 * (((fr >> 2) ^ (fr >> 3)) & 1);
+    return k * KSTRIDE + p * 128 + chunk * 16;
+  }
+};
+
+// L / 10 (experiments): the MFMA order inside a k-sub, L / 10 - 1 (gemm_w4.h
+// make_order: 0 i-major, 1 growing square, 2 n-major); 0 = Knobs (growing square).
+constexpr int ord_of(int L) { return L / 10 ? L / 10 - 1 : Kn::ORD; }
+
+template <int L>
+__device__ __forceinline__ const char* pabase(const Ctx& c, int st, int sub) {
+  return c.smem + st * Lay<L % 10>::STAGE + c.wr * 4 * Lay<L % 10>::GROUP + (sub ? c.ro1 : c.ro0);
+}
+template <int L>
+__device__ __forceinline__ const char* pbbase(const Ctx& c, int st, int sub) {
+  return c.smem + st * Lay<L % 10>::STAGE + Lay<L % 10>::OPA + c.wc * 4 * Lay<L % 10>::GROUP + (sub ? c.ro1 : c.ro0);
+}
+
+// DMA instruction j (A: j < 8, then B) of the K-tile at k0 into stage st, in
+// layout L, with gemm_w4.h's operand order (X / 10^8) and cache bits (X / 100).
+template <int L, int X>
+__device__ __forceinline__ void pdma(const Ctx& c, int st, int j, int k0) {
+  if constexpr (L % 10 == 0) {
+    w4::dma_any<BM, BN, X>(c, st, j, k0);
+  } else {
+    constexpr int AUXX = (X / 100) % 100;
+    constexpr int AUXB = AUXX >= 50 ? AUXX - 50 : AUXX, AUXA = AUXX >= 50 ? 0 : AUXX;
+    constexpr int ORDB = (X / 100000000) % 10;
+    static_assert(ORDB != 2, "layout 1: A-then-B or B-then-A DMA order only");
+    constexpr int JA = BM / 32;
+    const bool isb = ORDB == 1 ? j < JA : j >= JA;
+    const int jj = ORDB == 1 ? (isb ? j : j - JA) : (isb ? j - JA : j);
+    char* dst = c.smem + st * Lay<L % 10>::STAGE + (isb ? Lay<L % 10>::OPA : 0) + Lay<L % 10>::dma_dst(jj, c.w);
+    const int so = jj * (isb ? c.sb32 : c.sa32) + k0 * 2;
+    if (isb)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(c.rb, (KGS_LDS void*)dst, 16, c.vob, so, 0, AUXB);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(c.ra, (KGS_LDS void*)dst, 16, c.voa, so, 0, AUXA);
+  }
+}
+
 template <bool ZERO, int I, int N>
 __device__ __forceinline__ void pmma(const Frag<MA, NB>& f) {
   if constexpr (ZERO) accr::mfma0<I * NB + N>(f.b[N], f.a[I]);
@@ -77,24 +164,24 @@ struct Tick {
 // follows it. The DMA issues use `cd` (this tile's or the next tile's buffer
 // resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`. TK: 1 =
 // issue the ticket atomic after barrier 2, 2 = publish the ticket there.
-template <int ST, int X, bool ZERO, int TK, int K>
+template <int ST, int X, bool ZERO, int TK, int K, int L = 0>
 __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
                                       Frag<MA, NB>& f1, Tick& tq) {
-  constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = Kn::ORD;
+  constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = ord_of(L);
   constexpr int KM = S::KM, HM = S::HM, NR = S::NR, ND = w4::dma_per_stage<BM, BN>();
   if constexpr (K < KM) {
     constexpr int mi = w4::Order<ORD, MA, NB>::o.i[K % HM], mn = w4::Order<ORD, MA, NB>::o.n[K % HM];
     if constexpr (K < HM) pmma<ZERO, mi, mn>(f0); else pmma<false, mi, mn>(f1);
     if constexpr (K < NR) {
       constexpr int x = w4::rd_idx(ORD, MA, NB, K);
-      if constexpr (w4::rd_isa(ORD, MA, NB, K)) f1.a[x] = w4::frag(sp.pa1 + x * 2048);
-      else f1.b[x] = w4::frag(sp.pb1 + x * 2048);
+      if constexpr (w4::rd_isa(ORD, MA, NB, K)) f1.a[x] = w4::frag(sp.pa1 + Lay<L % 10>::frag_off(x));
+      else f1.b[x] = w4::frag(sp.pb1 + Lay<L % 10>::frag_off(x));
     }
     if constexpr (K >= B1 && K < KM - R) {
       constexpr int NW = KM - R - B1;
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        if (B1 + (j * NW) / ND == K) w4::dma_any<BM, BN, X>(cd, ST, j, sp.k0);
+        if (B1 + (j * NW) / ND == K) pdma<L, X>(cd, ST, j, sp.k0);
       }
     }
     if constexpr (K >= KM - R) {
@@ -102,8 +189,8 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
 #pragma unroll
       for (int e = q * P; e < (q + 1) * P && e < NR; ++e) {
         const int x = w4::rd_idx(ORD, MA, NB, e);
-        if (w4::rd_isa(ORD, MA, NB, e)) f0.a[x] = w4::frag(sp.pa0 + x * 2048);
-        else f0.b[x] = w4::frag(sp.pb0 + x * 2048);
+        if (w4::rd_isa(ORD, MA, NB, e)) f0.a[x] = w4::frag(sp.pa0 + Lay<L % 10>::frag_off(x));
+        else f0.b[x] = w4::frag(sp.pb0 + Lay<L % 10>::frag_off(x));
       }
     }
     w4::fence();
@@ -120,21 +207,21 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
         if (threadIdx.x == 0) *tq.slot = tq.tk;
       }
     }
-    pbody<ST, X, ZERO, TK, K + 1>(c, cd, sp, f0, f1, tq);
+    pbody<ST, X, ZERO, TK, K + 1, L>(c, cd, sp, f0, f1, tq);
   }
 }
 
 // One K-step on stage ST; its DMAs bring K-tile kd (of cd's tile) into ST.
-template <int ST, int X, bool ZERO, int TK = 0>
+template <int ST, int X, bool ZERO, int TK = 0, int L = 0>
 __device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd,
                                       Tick& tq) {
   StepPtrs sp;
-  sp.pa1 = w4::abase<BM, BN, 1>(c, ST);
-  sp.pb1 = w4::bbase<BM, BN, 1>(c, ST);
-  sp.pa0 = w4::abase<BM, BN, 0>(c, ST ^ 1);
-  sp.pb0 = w4::bbase<BM, BN, 0>(c, ST ^ 1);
+  sp.pa1 = pabase<L>(c, ST, 1);
+  sp.pb1 = pbbase<L>(c, ST, 1);
+  sp.pa0 = pabase<L>(c, ST ^ 1, 0);
+  sp.pb0 = pbbase<L>(c, ST ^ 1, 0);
   sp.k0 = kd * BK;
-  pbody<ST, X, ZERO, TK, 0>(c, cd, sp, f0, f1, tq);
+  pbody<ST, X, ZERO, TK, 0, L>(c, cd, sp, f0, f1, tq);
 }
 
 // Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
@@ -191,7 +278,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B
 // XCC_ID << 32, [2 + j] the end of its j-th tile's epilogue (j < 11), [13] its
 // exit (after the queue's exit counter / reset), [14] the end of its last tile,
 // [15] tiles.
-template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false>
+// L: LDS image layout (L % 10, Lay above) and MFMA order (L / 10, ord_of); 0 = production.
+template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false, int L = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
@@ -200,8 +288,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // One LDS object, not a second __shared__ variable: with two, hipcc's LDS-DMA
   // alias tracking put an s_waitcnt vmcnt(0) before every K-step's first
   // fragment read (all DMAs in flight drained).
-  __shared__ __attribute__((aligned(1024))) char smem[2 * S::STAGE + 16];
-  int& tslot = *(int*)(smem + 2 * S::STAGE);
+  static_assert(2 * Lay<L % 10>::STAGE + 16 <= 160 * 1024, "LDS image exceeds 160 KiB");
+  __shared__ __attribute__((aligned(1024))) char smem[2 * Lay<L % 10>::STAGE + 16];
+  int& tslot = *(int*)(smem + 2 * Lay<L % 10>::STAGE);
   KGS_ACC_RESERVE();
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -228,13 +317,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   c.sa32 = 32 * lda * 2;
   c.sb32 = 32 * ldb * 2;
   {
-    const int row = w * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    int row, ch;
+    Lay<L % 10>::dma_lane(lane, w, row, ch);
     c.voa = (row * lda + ch * 8) * 2;
     c.vob = (row * ldb + ch * 8) * 2;
-    const int fr = lane & 15, fq = lane >> 4, f = fr >> 1;
-    c.ro0 = fr * 128 + ((fq ^ f) * 16);
-    c.ro1 = fr * 128 + (((4 + fq) ^ f) * 16);
+    const int fr = lane & 15, fq = lane >> 4;
+    c.ro0 = Lay<L % 10>::read_lane(fr, fq);
+    c.ro1 = Lay<L % 10>::read_lane(fr, 4 + fq);
   }
   const int x = blockIdx.x & 7;             // XCD label
   const int ntx = (ntiles - x + 7) >> 3;     // its tiles: v = x + 8 t, t < ntx
@@ -271,18 +360,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
   for (int st = 0; st < 2; ++st)
 #pragma unroll
-    for (int j = 0; j < ND; ++j) w4::dma_any<BM, BN, X>(c, st, j, st * BK);
+    for (int j = 0; j < ND; ++j) pdma<L, X>(c, st, j, st * BK);
   w4::wait_vm<ND>();
   w4::bar();
   Frag<MA, NB> f0, f1;
   {
-    const char* pa = w4::abase<BM, BN, 0>(c, 0);
-    const char* pb = w4::bbase<BM, BN, 0>(c, 0);
+    const char* pa = pabase<L>(c, 0, 0);
+    const char* pb = pbbase<L>(c, 0, 0);
 #pragma unroll
     for (int e = 0; e < S::NR; ++e) {
-      const int x = w4::rd_idx(Kn::ORD, MA, NB, e);
-      if (w4::rd_isa(Kn::ORD, MA, NB, e)) f0.a[x] = w4::frag(pa + x * 2048);
-      else f0.b[x] = w4::frag(pb + x * 2048);
+      const int x = w4::rd_idx(ord_of(L), MA, NB, e);
+      if (w4::rd_isa(ord_of(L), MA, NB, e)) f0.a[x] = w4::frag(pa + Lay<L % 10>::frag_off(x));
+      else f0.b[x] = w4::frag(pb + Lay<L % 10>::frag_off(x));
     }
   }
   __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -297,11 +386,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   Tick tq{q + x + vzero, &tslot, 0};
   for (;;) {
-    pstep<0, X, true, DYN ? 1 : 0>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
-    pstep<1, X, false, DYN ? 2 : 0>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
+    pstep<0, X, true, DYN ? 1 : 0, L>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
+    pstep<1, X, false, DYN ? 2 : 0, L>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
     for (int t = 2; t < nt - 2; t += 2) {
-      pstep<0, X, false>(c, c, f0, f1, t + 2, tq);
-      pstep<1, X, false>(c, c, f0, f1, t + 3, tq);
+      pstep<0, X, false, 0, L>(c, c, f0, f1, t + 2, tq);
+      pstep<1, X, false, 0, L>(c, c, f0, f1, t + 3, tq);
     }
     const int tnx = DYN ? base + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
     const bool more = tnx < lim;
@@ -312,8 +401,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     cn.rb = rsrc_b(B, tnn, ldb);
     // the last two K-steps bring the next tile's K-tiles 0 and 1 (no next tile:
     // harmless re-loads of this tile's last K-tile into the freed stages)
-    pstep<0, X, false>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
-    pstep<1, X, false>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
+    pstep<0, X, false, 0, L>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
+    pstep<1, X, false, 0, L>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read
     float bv[NB][4];
     {
