@@ -650,7 +650,12 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
 
 @pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 384, "w4p_0"), (4608, 4096, 384, "w4p_0"),
                                            (8192, 2304, 512, "w4p_140000000"), (1024, 768, 1024, "w4p_0"),
-                                           (4608, 4096, 384, "w4pn_0"), (8192, 2304, 9216, "w4pn_140000008")])
+                                           (4608, 4096, 384, "w4pn_0"), (8192, 2304, 9216, "w4pn_140000008"),
+                                           # round 4: LDS layout 1 and the MFMA-order knobs
+                                           (4608, 4096, 384, "w4pl_0"), (8192, 2304, 9216, "w4pl_140000008"),
+                                           (8192, 2304, 512, "w4pl_140000000"), (4096, 4608, 8320, "w4pl_8"),
+                                           (4608, 4096, 384, "w4po0_0"), (4608, 4096, 384, "w4po2_0"),
+                                           (8192, 2304, 9216, "w4po2_140000008")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
     tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
@@ -667,6 +672,36 @@ def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     # run twice more on other data: nothing carried over between launches/tiles
     a2 = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     assert torch.equal(_gemm_v(a2, b, variant), _gemm_v(a2, b, "w4h_1_24_20_1_0"))
+
+
+@pytest.mark.parametrize("M,N,K", [(8192, 8192, 512), (8192, 2304, 9216), (1024, 768, 1024)])
+def test_gemm_persistent_timing_build_stamps(M, N, K):
+    """bench/gemm_tail.py's source: the timing build (gemm_w4p.h TS) computes
+    production's bits, every workgroup stamps a start, its tiles' ends in
+    order and an exit after its last tile, and the tile counts add up to the
+    tile grid (the per-XCD queue hands out every tile exactly once)."""
+    from kgs.ops import experiments as ex
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    ref = gemm_nt(a, b)
+    out = torch.empty_like(ref)
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    st = torch.zeros((cus, 16), dtype=torch.int64, device=DEV)
+    grid = ex.gemm_w4p_stamps(a, b, out, st, ex.production_map(M, N, K))
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    s = st[:grid].cpu()
+    tiles = (M // 256) * (N // 256)
+    assert grid == min(tiles, cus)
+    assert int(s[:, 15].sum()) == tiles and int(s[:, 15].min()) >= 1
+    assert bool((s[:, 0] > 0).all()) and bool((s[:, 14] >= s[:, 0]).all()) and bool((s[:, 13] >= s[:, 14]).all())
+    for row in s.tolist():
+        n = min(row[15], 11)
+        ends = [row[0]] + row[2:2 + n]
+        assert ends == sorted(ends), row
+        assert (row[1] >> 32) & 0xF < 8  # XCC id
 
 
 @pytest.mark.parametrize("act", [None, "bias", "gelu", "silu"])
