@@ -47,6 +47,9 @@ def main(argv=None) -> int:
     ap.add_argument("--inter", type=int, default=14336)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="", help="comma list: attn,ops")
+    ap.add_argument("--w4", action="store_true",
+                    help="also time the one-wave-per-SIMD named-register kernel (kgs.ops.experiments, seq % 256 == 0)")
+    ap.add_argument("--rounds", type=int, default=1, help="interleaved timing rounds (medians reported)")
     a = ap.parse_args(argv)
     only = set(a.only.split(",")) if a.only else {"attn", "ops"}
     dev = "cuda"
@@ -60,16 +63,34 @@ def main(argv=None) -> int:
         k = qkv[:, nh * hd:(nh + nkv) * hd].reshape(b, s, nkv, hd).transpose(1, 2).contiguous()
         v = qkv[:, (nh + nkv) * hd:].reshape(b, s, nkv, hd).transpose(1, 2).contiguous()
         for causal in (True, False):
+            import statistics
+
             flops = 4.0 * b * nh * s * s * hd * (0.5 if causal else 1.0)
-            ms = _time(lambda: T.attention_qkv(qkv, b, s, nh, nkv, causal=causal, out=out), a.iters)
-            ms_t = _time(lambda: torch.nn.functional.scaled_dot_product_attention(
-                q, k, v, is_causal=causal, enable_gqa=True), a.iters)
+            fns = {"kgs": lambda: T.attention_qkv(qkv, b, s, nh, nkv, causal=causal, out=out),
+                   "sdpa": lambda: torch.nn.functional.scaled_dot_product_attention(
+                       q, k, v, is_causal=causal, enable_gqa=True)}
+            out4 = torch.empty_like(out)
+            if a.w4:
+                from kgs.ops import experiments
+
+                fns["kgs_w4"] = lambda: experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, out=out4)
+            times = {n: [] for n in fns}
+            for _ in range(a.rounds):
+                for n, f in fns.items():
+                    times[n].append(_time(f, a.iters))
+            ms, ms_t = statistics.median(times["kgs"]), statistics.median(times["sdpa"])
             ref = torch.nn.functional.scaled_dot_product_attention(q, k, v, is_causal=causal, enable_gqa=True)
-            err = (out.float() - ref.transpose(1, 2).reshape(t, nh * hd).float()).abs().max().item()
-            print(json.dumps({"op": "attention_fwd", "causal": causal, "batch": b, "seq": s, "heads": nh,
-                              "kv_heads": nkv, "kgs_ms": round(ms, 4), "kgs_tflops": round(flops / ms / 1e9, 1),
-                              "sdpa_ms": round(ms_t, 4), "sdpa_tflops": round(flops / ms_t / 1e9, 1),
-                              "speedup": round(ms_t / ms, 2), "max_abs_err_vs_sdpa": round(err, 5)}), flush=True)
+            ref = ref.transpose(1, 2).reshape(t, nh * hd).float()
+            err = (out.float() - ref).abs().max().item()
+            rec = {"op": "attention_fwd", "causal": causal, "batch": b, "seq": s, "heads": nh,
+                   "kv_heads": nkv, "kgs_ms": round(ms, 4), "kgs_tflops": round(flops / ms / 1e9, 1),
+                   "sdpa_ms": round(ms_t, 4), "sdpa_tflops": round(flops / ms_t / 1e9, 1),
+                   "speedup": round(ms_t / ms, 2), "max_abs_err_vs_sdpa": round(err, 5)}
+            if a.w4:
+                ms4 = statistics.median(times["kgs_w4"])
+                rec.update(kgs_w4_ms=round(ms4, 4), kgs_w4_tflops=round(flops / ms4 / 1e9, 1),
+                           kgs_w4_max_abs_err_vs_sdpa=round((out4.float() - ref).abs().max().item(), 5))
+            print(json.dumps(rec), flush=True)
         del qkv, q, k, v, out
     if "ops" in only:
         h, inter = a.hidden, a.inter

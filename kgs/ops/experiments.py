@@ -103,6 +103,9 @@ def lib() -> ctypes.CDLL:
     so.kgs_exp_gemm_w4h.restype = i
     so.kgs_exp_gemm_w4p_grid.argtypes = [vp] * 3 + [i] * 8 + [vp]
     so.kgs_exp_gemm_w4p_grid.restype = i
+    L = ctypes.c_long
+    so.kgs_exp_attn4_fwd_bf16.argtypes = [vp] * 4 + [i] * 6 + [L] * 4 + [ctypes.c_float, i, vp]
+    so.kgs_exp_attn4_fwd_bf16.restype = i
     so.kgs_exp_gemm_w4p_stamps.argtypes = [vp] * 3 + [i] * 7 + [vp] * 3
     so.kgs_exp_gemm_w4p_stamps.restype = i
     so.kgs_exp_gemm_fp8_w4f8.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
@@ -208,3 +211,25 @@ def gemm_w4p_stamps(a, b, out, stamps: torch.Tensor, map_: int | str = 0) -> int
                                              ctypes.byref(grid), _lib.stream_handle(a.device)),
                "kgs_exp_gemm_w4p_stamps")
     return grid.value
+
+
+def attention_qkv_w4(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_heads: int, head_dim: int = 128,
+                     causal: bool = True, scale: float | None = None, out: torch.Tensor | None = None) -> torch.Tensor:
+    """:func:`kgs.ops.transformer.attention_qkv` on the one-wave-per-SIMD,
+    named-register kernel (native/kernels/attention_w4.h; ``seq % 256 == 0``)."""
+    import math
+
+    if qkv.dtype != torch.bfloat16 or not qkv.is_cuda or qkv.stride(1) != 1:
+        raise ValueError("qkv must be a row-major bf16 GPU tensor")
+    if qkv.shape[0] != batch * seq or qkv.shape[1] < (heads + 2 * kv_heads) * head_dim:
+        raise ValueError("qkv shape does not match batch/seq/heads")
+    out = torch.empty((batch * seq, heads * head_dim), dtype=torch.bfloat16, device=qkv.device) \
+        if out is None else out
+    scale = 1.0 / math.sqrt(head_dim) if scale is None else scale
+    ld, esz, base = qkv.stride(0), qkv.element_size(), qkv.data_ptr()
+    rc = lib().kgs_exp_attn4_fwd_bf16(base, base + heads * head_dim * esz, base + (heads + kv_heads) * head_dim * esz,
+                                      out.data_ptr(), batch, seq, seq, heads, kv_heads, head_dim, ld, ld, ld,
+                                      out.stride(0), float(scale), 1 if causal else 0,
+                                      _lib.stream_handle(qkv.device))
+    _lib.check(rc, "attention_qkv_w4")
+    return out

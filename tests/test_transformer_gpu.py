@@ -111,6 +111,34 @@ def test_attention_matches_sdpa(b, s, nh, nkv, causal):
     assert err < 2e-2, (err, mag)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+@pytest.mark.parametrize("b,s,nh,nkv,qscale", [(1, 256, 4, 4, 1.0), (2, 512, 8, 2, 1.0), (1, 1024, 32, 8, 1.0),
+                                               (2, 512, 8, 2, 6.0)])
+def test_attention_w4_matches_reference(b, s, nh, nkv, qscale, causal):
+    """The one-wave-per-SIMD named-register kernel (attention_w4.h, via the
+    experiments library) against the fp32 reference, including peaky scores
+    (qscale 6: the deferred rescale of the AGPR-resident O runs), and against
+    the production kernel."""
+    from kgs.ops import experiments
+    from kgs.ops.transformer import attention_qkv, ref_attention_qkv
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    hd = 128
+    qkv = torch.randn(b * s, (nh + 2 * nkv) * hd, device=DEV, generator=g)
+    qkv[:, :nh * hd] *= qscale
+    qkv = qkv.to(torch.bfloat16)
+    got = experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal)
+    ref = ref_attention_qkv(qkv, b, s, nh, nkv, causal=causal)
+    prod = attention_qkv(qkv, b, s, nh, nkv, causal=causal)
+    torch.cuda.synchronize()
+    assert torch.isfinite(got.float()).all()
+    mag = ref.abs().max().item()
+    assert (got.float() - ref).abs().max().item() < 2e-2 * max(1.0, mag)
+    assert (got.float() - prod.float()).abs().max().item() < 2e-2 * max(1.0, mag)
+    # deterministic: a second run gives the same bits
+    assert torch.equal(got, experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal))
+
+
 def test_attention_peaky_softmax_rescales():
     # large scores: the running max moves by a lot between tiles, so the
     # online-softmax rescale of O and l is exercised on every row
