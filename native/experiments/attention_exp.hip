@@ -3,10 +3,11 @@
 // opt-in libkgs_experiments.so; numbers in profiles/r4/attention/.
 #include "attention_w4.h"
 
-// Same operand contract as kgs_attn_fwd_bf16_ex, with S % 256 == 0.
+// Same operand contract as kgs_attn_fwd_bf16_ex, with S % 256 == 0; `stamps`
+// (optional) selects the timing build.
 KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* v, void* o, int B, int S, int Sk,
                                       int H, int HKV, int hd, long ldq, long ldk, long ldv, long ldo, float scale,
-                                      int causal, hipStream_t s) {
+                                      int causal, void* stamps, hipStream_t s) {
   using namespace kgs::attn4;
   if (B <= 0 || S <= 0 || H <= 0 || HKV <= 0 || H % HKV) return KGS_ERR_SHAPE;
   if (hd != HD || S % QB || Sk < S || (Sk - S) % KB) return KGS_ERR_SHAPE;
@@ -16,7 +17,11 @@ KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* 
   const long nwg = (long)B * H * (S / QB);
   if (nwg > 0x7fffffff) return KGS_ERR_SHAPE;
   Args a{(const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o,
-         ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0, Sk, Sk - S};
-  hipLaunchKernelGGL(fwd, dim3((unsigned)nwg), dim3(256), 0, s, a);
+         ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0, Sk, Sk - S,
+         (long long*)stamps};
+  if (stamps)  // timing build: long long[64 workgroups][4 waves][64 tiles][8]
+    hipLaunchKernelGGL(fwd<true>, dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(fwd<false>, dim3((unsigned)nwg), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }

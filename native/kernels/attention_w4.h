@@ -64,6 +64,7 @@ struct Args {
   int causal;
   int Sk;
   int qoff;
+  long long* ts;  // timing build (TS): per (workgroup < 64, wave) s_memtime stamps, else unused
 };
 
 __device__ __forceinline__ int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
@@ -83,6 +84,13 @@ __device__ __forceinline__ void fence() { __builtin_amdgcn_sched_barrier(0); }
 // recognizer cannot insert for an asm MFMA. Tied to s so that nothing reading
 // s is scheduled above it.
 __device__ __forceinline__ void pad_s(f32x16& s) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(s)); }
+
+// An asm MFMA reads its VGPR operands after issue, and hipcc, which cannot
+// see that, would recycle a fragment's registers for VALU temporaries right
+// after the MFMA that last names it (first cut: every P.V whose operands died
+// in its own slot computed garbage). keep() extends the operands' live range
+// into a later slot.
+__device__ __forceinline__ void keep(const bf16x8& x) { asm volatile("" ::"v"(x)); }
 
 __device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
   bf16x8 r;
@@ -153,6 +161,11 @@ __device__ __forceinline__ void mask_diag(f32x16 (&s)[2], int kv0, int hh, int r
     }
 }
 
+// TS: timing build. Workgroups 0..63 stamp s_memtime (shader cycles) at the
+// start of every tile and after each of its sections, per wave: ts[((blk * 4 +
+// w) * 64 + min(j, 63)) * 8 + e], e = 0 tile start, 1 after A, 2 after B, 3
+// after the barrier, 4 after C, 5 after D.
+template <bool TS = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fwd(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
   KGS_ATTN_RESERVE();
@@ -160,6 +173,13 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = a.S / QB;
+  const bool stamp = TS && blockIdx.x < 64;
+  auto ts = [&](int j, int e) {
+    if constexpr (TS) {
+      const long long t = (long long)__builtin_amdgcn_s_memtime();
+      if (stamp && lane == 0) a.ts[(((long)blockIdx.x * 4 + w) * 64 + (j < 63 ? j : 63)) * 8 + e] = t;
+    }
+  };
   const int nwg = gridDim.x;
   int lid = blockIdx.x;
   if ((nwg & 31) == 0) {  // 8 consecutive slots of one XCD: 4 heads of one KV group
@@ -244,6 +264,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     bf16x8 pf0[2][2], pf1[2][2];
     Softmax<0> sm0{s0, m0, l0, pf0, sl2, 0.f, 0.f};
     Softmax<1> sm1{s1, m1, l1, pf1, sl2, 0.f, 0.f};
+    ts(j, 0);
     if (act) {
       const char* Vs = smem[buf][1];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K(j) in its AGPRs
@@ -255,6 +276,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         read_v(Vs, k / 4, (k / 2) % 2, k % 2);
         fence();
       });
+      ts(j, 1);
       // B: QK^T(qb 1) | max, exchange and the t = 0 half of softmax(qb 0)
       static_for<0, 16>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -270,12 +292,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k == 14) sm0.template pack<0, 1>();
         fence();
       });
+      ts(j, 2);
     }
     // tile j's V is in registers and tile j + 1 has landed: after the barrier
     // buffer j is free for tile j + 2 (its DMA is issued in section D)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     __syncthreads();
+    ts(j, 3);
     const bool dnext = j + 2 < ntile;
     if (act) {
       const bool knext = j + 1 < ntile && (!a.causal || kv0 + KB <= wlast);
@@ -284,6 +308,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       static_for<0, 16>([&](auto kc) {
         constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
         atr::pv<0, d>(vf[d][t][sp], pf0[t][sp]);
+        if constexpr (k >= 2) {  // operands of the P.V two slots back
+          constexpr int kk = k - 2;
+          keep(vf[kk % 4][kk / 8][(kk % 8) / 4]);
+          keep(pf0[kk / 8][(kk % 8) / 4]);
+        }
         if constexpr (k == 0) {
           pad_s(s1[1]);
           if (a.causal && kv0 + KB - 1 > qoff + rb1) mask_diag(s1, kv0, hh, qoff + rb1 + l32);
@@ -298,11 +327,21 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k == 15) sm1.template pack<0, 1>();
         fence();
       });
+      ts(j, 4);
       // D: P.V(qb 1) | the t = 1 half of softmax(qb 1), then the K fragments
       //    of tile j + 1 into their AGPRs and the LDS-DMA of tile j + 2
       static_for<0, 16>([&](auto kc) {
         constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
         atr::pv<1, d>(vf[d][t][sp], pf1[t][sp]);
+        if constexpr (k >= 2) {
+          constexpr int kk = k - 2;
+          keep(vf[kk % 4][kk / 8][(kk % 8) / 4]);
+          keep(pf1[kk / 8][(kk % 8) / 4]);
+        } else {  // section C's last two
+          constexpr int kk = 14 + k;
+          keep(vf[kk % 4][kk / 8][(kk % 8) / 4]);
+          keep(pf0[kk / 8][(kk % 8) / 4]);
+        }
         if constexpr (k < 8) sm1.template exps<1, 2 * k, 2>();
         if constexpr (k == 4) sm1.template pack<1, 0>();
         if constexpr (k == 7) sm1.template pack<1, 1>();
@@ -316,6 +355,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         }
         fence();
       });
+      // the last two P.V read their operands after issue: hold them a while
+      asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::"v"(vf[2][1][1]), "v"(vf[3][1][1]), "v"(pf1[1][1]));
+      ts(j, 5);
     } else if (dnext) {
       // a causal wave past its last row still fills its share of the tiles
 #pragma unroll
