@@ -12,8 +12,6 @@ KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* 
   if (B <= 0 || S <= 0 || H <= 0 || HKV <= 0 || H % HKV) return KGS_ERR_SHAPE;
   if (hd != HD || S % QB || Sk < S || (Sk - S) % KB) return KGS_ERR_SHAPE;
   if (ldq < (long)H * HD || ldk < (long)HKV * HD || ldv < (long)HKV * HD || ldo < (long)H * HD) return KGS_ERR_SHAPE;
-  // buffer offsets of K / V rows are 32-bit (bytes from the sequence's first key)
-  if ((long)Sk * (ldk > ldv ? ldk : ldv) * 2 >= 0x7ffffff0L) return KGS_ERR_SHAPE;
   const uintptr_t al = (uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)o;
   if ((al & 15) || (ldq | ldk | ldv | ldo) & 7) return KGS_ERR_ALIGN;
   const long nwg = (long)B * H * (S / QB);

@@ -50,10 +50,6 @@ constexpr int WR = 64;      // query rows per wave
 constexpr int QB = 4 * WR;  // rows per workgroup
 constexpr int KB = 64;      // keys per tile
 constexpr int TILE_BYTES = KB * HD * 2;
-// Three K/V buffers: tile j + 2's LDS-DMA can then be issued anywhere in tile
-// j (its buffer last held tile j - 1), two pieces per section, instead of
-// eight at once after the barrier (stamps: a 2088-cycle section D).
-constexpr int NBUF = 3;
 constexpr float NEG = -1.0e30f;
 constexpr float RESCALE = 8.0f;  // deferred-max threshold (log2 units): P <= 256
 
@@ -171,7 +167,7 @@ __device__ __forceinline__ void mask_diag(f32x16 (&s)[2], int kv0, int hh, int r
 // after the barrier, 4 after C, 5 after D.
 template <bool TS = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fwd(Args a) {
-  __shared__ __attribute__((aligned(16))) char smem[NBUF][2][TILE_BYTES];  // [buf][K, V]
+  __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
   KGS_ATTN_RESERVE();
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -218,27 +214,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const unsigned short* vbase = a.v + ktok0 * a.ldv + (long)kvh * HD;
   // LDS-DMA piece p (0..7) of this wave's share of tile jn: 1 KiB = 4 rows of
   // the K (p even) or V (p odd) tile, into buffer sb
-  // as buffer_load ... lds (SGPR resource + 32-bit lane offset): the issue of a
-  // global_load_lds piece (64-bit lane addresses) measured 150-300 cycles
-  // beside the MFMAs of this one-wave-per-SIMD kernel
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7ffffff0, 0x00020000);
-  int voff_k[4], voff_v[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ch = 4 * w + i;
-    const int r = 4 * ch + (lane >> 4), c = (lane & 15) ^ swz(r);
-    voff_k[i] = (int)((r * a.ldk + 8 * c) * 2);
-    voff_v[i] = (int)((r * a.ldv + 8 * c) * 2);
-  }
   auto dma_piece = [&](int jn, int sb, int p) {
-    const int i = p >> 1, ch = 4 * w + i;
-    if (p & 1)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (KGS_LDS void*)(smem[sb][1] + 1024 * ch), 16, voff_v[i],
-                                               (int)((long)jn * KB * a.ldv * 2), 0, 0);
-    else
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (KGS_LDS void*)(smem[sb][0] + 1024 * ch), 16, voff_k[i],
-                                               (int)((long)jn * KB * a.ldk * 2), 0, 0);
+    const int ch = 4 * w + (p >> 1);
+    const int r = 4 * ch + (lane >> 4), c = (lane & 15) ^ swz(r);
+    const long row = (long)jn * KB + r;
+    if (p & 1) glds16(vbase + row * a.ldv + 8 * c, smem[sb][1] + 1024 * ch);
+    else glds16(kbase + row * a.ldk + 8 * c, smem[sb][0] + 1024 * ch);
   };
   auto dma_tiles = [&](int jn, int sb) {
 #pragma unroll
@@ -251,16 +232,12 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
   const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
   bf16x8 vf[4][2][2];
-  // V fragment reads as asm: hipcc's LDS-DMA alias tracking cannot tell the
-  // buffer being read from the one tile j + 2 is DMA'd into (runtime index) and
-  // put a vmcnt(0) before every builtin transposed read. Their lgkmcnt is ours:
-  // the barrier section waits lgkmcnt(0) before any P.V reads a fragment.
-  auto read_v = [&](unsigned vs_lds, int d, int t, int sp) {
+  auto read_v = [&](const char* Vs, int d, int t, int sp) {
     const int c0 = 4 * d + 2 * (g & 1) + (tp >> 1);
     const int kvb = 32 * t + 16 * sp + 4 * hh + tq;
-    bf16x4s x, y;
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x) : "v"(vs_lds + (unsigned)(off(kvb, c0) + 8 * (tp & 1))));
-    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(y) : "v"(vs_lds + (unsigned)(off(kvb + 8, c0) + 8 * (tp & 1))));
+    const bf16x4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(Vs + off(kvb, c0) + 8 * (tp & 1)));
+    const bf16x4s y =
+        __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(Vs + off(kvb + 8, c0) + 8 * (tp & 1)));
     vf[d][t][sp] = __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
@@ -268,9 +245,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int wlast = qoff + rb1 + 31;  // this wave's last row (causal limit)
 
   dma_tiles(0, 0);
-  if (ntile > 1) dma_tiles(1, 1);
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tiles 0, 1
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tile 0
   __syncthreads();
+  if (ntile > 1) dma_tiles(1, 1);
   static_for<0, 16>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     atr::kread<k / 8, k % 8>(kaddr(0, k / 8, k % 8));
@@ -280,8 +257,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const float sl2 = a.sl2;
 
   for (int j = 0; j < ntile; ++j) {
-    const int buf = j % NBUF, nbuf = (j + 1) % NBUF, dbuf = (j + 2) % NBUF;
-    const bool dnext = j + 2 < ntile;  // this tile issues tile j + 2's DMA: 2 pieces per section
+    const int buf = j & 1;
     const int kv0 = j * KB;
     const bool act = !a.causal || kv0 <= wlast;
     f32x16 s0[2], s1[2];
@@ -290,7 +266,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     Softmax<1> sm1{s1, m1, l1, pf1, sl2, 0.f, 0.f};
     ts(j, 0);
     if (act) {
-      const unsigned Vs = kbase_lds + (unsigned)((2 * buf + 1) * TILE_BYTES);
+      const char* Vs = smem[buf][1];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K(j) in its AGPRs
       fence();
       // A: QK^T(qb 0), one V fragment per MFMA
@@ -298,8 +274,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         constexpr int k = decltype(kc)::value;
         atr::qk<0, k / 8, k % 8, k % 8 == 0>(s0[k / 8]);
         read_v(Vs, k / 4, (k / 2) % 2, k % 2);
-        if constexpr (k % 8 == 7)
-          if (dnext) dma_piece(j + 2, dbuf, k / 8);
         fence();
       });
       ts(j, 1);
@@ -316,26 +290,17 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k >= 5 && k < 13) sm0.template exps<0, 2 * (k - 5), 2>();
         if constexpr (k == 13) sm0.template pack<0, 0>();
         if constexpr (k == 14) sm0.template pack<0, 1>();
-        if constexpr (k % 8 == 7)
-          if (dnext) dma_piece(j + 2, dbuf, 2 + k / 8);
         fence();
       });
       ts(j, 2);
-    } else if (dnext) {
-#pragma unroll
-      for (int p = 0; p < 4; ++p) dma_piece(j + 2, dbuf, p);
     }
     // tile j's V is in registers and tile j + 1 has landed: after the barrier
     // buffer j is free for tile j + 2 (its DMA is issued in section D)
-    // tile j's V is in registers; tile j + 1 has landed once at most the 4
-    // pieces of tile j + 2 issued above are outstanding (vmcnt counts in order)
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    if (dnext) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    fence();
-    asm volatile("s_barrier" ::: "memory");  // raw: __syncthreads() would add its own vmcnt(0)
-    fence();
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+    __syncthreads();
     ts(j, 3);
+    const bool dnext = j + 2 < ntile;
     if (act) {
       const bool knext = j + 1 < ntile && (!a.causal || kv0 + KB <= wlast);
       // C: P.V(qb 0), t = 0 keys first | the t = 1 half of softmax(qb 0), then
@@ -360,8 +325,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k >= 8) sm1.template exps<0, 2 * (k - 8), 2>();
         if constexpr (k == 12) sm1.template pack<0, 0>();
         if constexpr (k == 15) sm1.template pack<0, 1>();
-        if constexpr (k % 8 == 6)
-          if (dnext) dma_piece(j + 2, dbuf, 4 + k / 8);
         fence();
       });
       ts(j, 4);
@@ -385,11 +348,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k >= 8) {
           constexpr int f0 = 2 * (k - 8);
           if (knext) {
-            atr::kread<f0 / 8, f0 % 8>(kaddr(nbuf, f0 / 8, f0 % 8));
-            atr::kread<(f0 + 1) / 8, (f0 + 1) % 8>(kaddr(nbuf, (f0 + 1) / 8, (f0 + 1) % 8));
+            atr::kread<f0 / 8, f0 % 8>(kaddr(buf ^ 1, f0 / 8, f0 % 8));
+            atr::kread<(f0 + 1) / 8, (f0 + 1) % 8>(kaddr(buf ^ 1, (f0 + 1) / 8, (f0 + 1) % 8));
           }
-          if constexpr (k == 9 || k == 13)
-            if (dnext) dma_piece(j + 2, dbuf, 6 + (k - 9) / 4);
+          if (dnext) dma_piece(j + 2, buf, k - 8);
         }
         fence();
       });
@@ -399,7 +361,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     } else if (dnext) {
       // a causal wave past its last row still fills its share of the tiles
 #pragma unroll
-      for (int p = 4; p < 8; ++p) dma_piece(j + 2, dbuf, p);
+      for (int p = 0; p < 8; ++p) dma_piece(j + 2, buf, p);
     }
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last P.V -> v_accvgpr_read
