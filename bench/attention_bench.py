@@ -74,6 +74,8 @@ def main(argv=None) -> int:
                 from kgs.ops import experiments
 
                 fns["kgs_w4"] = lambda: experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, out=out4)
+                fns["kgs_w4rs"] = lambda: experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, out=out4,
+                                                                       staged=True)
             times = {n: [] for n in fns}
             for _ in range(a.rounds):
                 for n, f in fns.items():
@@ -87,9 +89,10 @@ def main(argv=None) -> int:
                    "sdpa_ms": round(ms_t, 4), "sdpa_tflops": round(flops / ms_t / 1e9, 1),
                    "speedup": round(ms_t / ms, 2), "max_abs_err_vs_sdpa": round(err, 5)}
             if a.w4:
-                ms4 = statistics.median(times["kgs_w4"])
-                rec.update(kgs_w4_ms=round(ms4, 4), kgs_w4_tflops=round(flops / ms4 / 1e9, 1),
-                           kgs_w4_max_abs_err_vs_sdpa=round((out4.float() - ref).abs().max().item(), 5))
+                for n in ("kgs_w4", "kgs_w4rs"):
+                    ms4 = statistics.median(times[n])
+                    rec.update({f"{n}_ms": round(ms4, 4), f"{n}_tflops": round(flops / ms4 / 1e9, 1)})
+                rec.update(kgs_w4_max_abs_err_vs_sdpa=round((out4.float() - ref).abs().max().item(), 5))
             print(json.dumps(rec), flush=True)
         del qkv, q, k, v, out
     if "ops" in only:

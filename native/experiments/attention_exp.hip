@@ -7,7 +7,7 @@
 // (optional) selects the timing build.
 KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* v, void* o, int B, int S, int Sk,
                                       int H, int HKV, int hd, long ldq, long ldk, long ldv, long ldo, float scale,
-                                      int causal, void* stamps, hipStream_t s) {
+                                      int causal, void* stamps, int variant, hipStream_t s) {
   using namespace kgs::attn4;
   if (B <= 0 || S <= 0 || H <= 0 || HKV <= 0 || H % HKV) return KGS_ERR_SHAPE;
   if (hd != HD || S % QB || Sk < S || (Sk - S) % KB) return KGS_ERR_SHAPE;
@@ -19,9 +19,17 @@ KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* 
   Args a{(const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o,
          ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0, Sk, Sk - S,
          (long long*)stamps};
-  if (stamps)  // timing build: long long[64 workgroups][4 waves][64 tiles][8]
-    hipLaunchKernelGGL(fwd<true>, dim3((unsigned)nwg), dim3(256), 0, s, a);
+  // variant 0: LDS-DMA K/V tiles, 1: register-staged (attention_w4.h RS);
+  // stamps: the timing build, long long[64 workgroups][4 waves][64 tiles][8]
+  if (variant == 0 && stamps)
+    hipLaunchKernelGGL((fwd<true, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else if (variant == 0)
+    hipLaunchKernelGGL((fwd<false, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else if (variant == 1 && stamps)
+    hipLaunchKernelGGL((fwd<true, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  else if (variant == 1)
+    hipLaunchKernelGGL((fwd<false, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
   else
-    hipLaunchKernelGGL(fwd<false>, dim3((unsigned)nwg), dim3(256), 0, s, a);
+    return KGS_ERR_ARG;
   return (int)hipGetLastError();
 }

@@ -64,17 +64,12 @@ __device__ __forceinline__ bf16x8 tr_frag(const char* lo, const char* hi) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-__device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(s[base + j]);
-  return r;
-}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) { return pack_bf16x8(s, base); }
 
 __global__ __launch_bounds__(256, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) void fwd(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = a.S / QB;
   const int nwg = gridDim.x;

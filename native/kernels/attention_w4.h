@@ -92,12 +92,7 @@ __device__ __forceinline__ void pad_s(f32x16& s) { asm volatile("s_nop 7\n\ts_no
 // into a later slot.
 __device__ __forceinline__ void keep(const bf16x8& x) { asm volatile("" ::"v"(x)); }
 
-__device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(s[base + j]);
-  return r;
-}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& s, int base) { return pack_bf16x8(s, base); }
 
 // Online softmax of one q-block's tile (two 32x32 S^T blocks, lane = one query
 // row), in pieces the MFMA slots place: the row max over 8 scores (maxpart),
@@ -165,12 +160,16 @@ __device__ __forceinline__ void mask_diag(f32x16 (&s)[2], int kv0, int hh, int r
 // start of every tile and after each of its sections, per wave: ts[((blk * 4 +
 // w) * 64 + min(j, 63)) * 8 + e], e = 0 tile start, 1 after A, 2 after B, 3
 // after the barrier, 4 after C, 5 after D.
-template <bool TS = false>
+// RS: K/V tiles register-staged (buffer_load_dwordx4 of tile j + 2 into 8 x 4
+// VGPRs in section D of tile j, ds_write_b128 into the free buffer in section
+// B of tile j + 1) instead of LDS-DMA, whose issue cost stamps put at 150-180
+// cycles per 1 KiB piece beside the MFMAs of a wave alone on its SIMD.
+template <bool TS = false, bool RS = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fwd(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
   KGS_ATTN_RESERVE();
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l32 = lane & 31, hh = lane >> 5;
   const int nqb = a.S / QB;
   const bool stamp = TS && blockIdx.x < 64;
@@ -225,6 +224,25 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
     for (int p = 0; p < 8; ++p) dma_piece(jn, sb, p);
   };
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 stg[8];
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7ffffff0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7ffffff0, 0x00020000);
+  int voff[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int ch = 4 * w + (p >> 1);
+    const int r = 4 * ch + (lane >> 4), c = (lane & 15) ^ swz(r);
+    voff[p] = (int)((r * ((p & 1) ? a.ldv : a.ldk) + 8 * c) * 2);
+  }
+  auto stage_load = [&](int jn, int p) {
+    stg[p] = __builtin_amdgcn_raw_buffer_load_b128((p & 1) ? rv : rk, voff[p],
+                                                   (int)((long)jn * KB * ((p & 1) ? a.ldv : a.ldk) * 2), 0);
+  };
+  auto stage_write = [&](int sb, int p) {
+    const int ch = 4 * w + (p >> 1);
+    *(u32x4*)(smem[sb][p & 1] + 1024 * ch + 16 * lane) = stg[p];
+  };
   // LDS byte address of this lane's K fragment (t, ks) in buffer sb
   const unsigned kbase_lds = (unsigned)(uintptr_t)(KGS_LDS char*)smem[0][0];
   auto kaddr = [&](int sb, int t, int ks) -> unsigned {
@@ -244,10 +262,22 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const int ntile = a.causal ? (qoff + q0 + QB) / KB : a.Sk / KB;
   const int wlast = qoff + rb1 + 31;  // this wave's last row (causal limit)
 
-  dma_tiles(0, 0);
-  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tile 0
-  __syncthreads();
-  if (ntile > 1) dma_tiles(1, 1);
+  if constexpr (RS) {
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage_load(0, p);
+#pragma unroll
+    for (int p = 0; p < 8; ++p) stage_write(0, p);
+    if (ntile > 1) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) stage_load(1, p);
+    }
+    __syncthreads();
+  } else {
+    dma_tiles(0, 0);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tile 0
+    __syncthreads();
+    if (ntile > 1) dma_tiles(1, 1);
+  }
   static_for<0, 16>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     atr::kread<k / 8, k % 8>(kaddr(0, k / 8, k % 8));
@@ -290,9 +320,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k >= 5 && k < 13) sm0.template exps<0, 2 * (k - 5), 2>();
         if constexpr (k == 13) sm0.template pack<0, 0>();
         if constexpr (k == 14) sm0.template pack<0, 1>();
+        if constexpr (RS && k >= 8)
+          if (j + 1 < ntile) stage_write(buf ^ 1, k - 8);
         fence();
       });
       ts(j, 2);
+    } else if (RS && j + 1 < ntile) {
+#pragma unroll
+      for (int p = 0; p < 8; ++p) stage_write(buf ^ 1, p);
     }
     // tile j's V is in registers and tile j + 1 has landed: after the barrier
     // buffer j is free for tile j + 2 (its DMA is issued in section D)
@@ -302,7 +337,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     ts(j, 3);
     const bool dnext = j + 2 < ntile;
     if (act) {
-      const bool knext = j + 1 < ntile && (!a.causal || kv0 + KB <= wlast);
       // C: P.V(qb 0), t = 0 keys first | the t = 1 half of softmax(qb 0), then
       //    max, exchange and the t = 0 half of softmax(qb 1)
       static_for<0, 16>([&](auto kc) {
@@ -330,6 +364,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       ts(j, 4);
       // D: P.V(qb 1) | the t = 1 half of softmax(qb 1), then the K fragments
       //    of tile j + 1 into their AGPRs and the LDS-DMA of tile j + 2
+      // (two copies, with and without the tile j + 2 pieces, so no slot
+      // branches; the K reads run unconditionally -- LDS in bounds -- and are
+      // used only by a wave that has rows in tile j + 1)
+      auto sec_d = [&](auto dnc) {
       static_for<0, 16>([&](auto kc) {
         constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
         atr::pv<1, d>(vf[d][t][sp], pf1[t][sp]);
@@ -347,21 +385,28 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k == 7) sm1.template pack<1, 1>();
         if constexpr (k >= 8) {
           constexpr int f0 = 2 * (k - 8);
-          if (knext) {
-            atr::kread<f0 / 8, f0 % 8>(kaddr(buf ^ 1, f0 / 8, f0 % 8));
-            atr::kread<(f0 + 1) / 8, (f0 + 1) % 8>(kaddr(buf ^ 1, (f0 + 1) / 8, (f0 + 1) % 8));
+          atr::kread<f0 / 8, f0 % 8>(kaddr(buf ^ 1, f0 / 8, f0 % 8));
+          atr::kread<(f0 + 1) / 8, (f0 + 1) % 8>(kaddr(buf ^ 1, (f0 + 1) / 8, (f0 + 1) % 8));
+          if constexpr (decltype(dnc)::value) {
+            if constexpr (RS) stage_load(j + 2, k - 8);
+            else dma_piece(j + 2, buf, k - 8);
           }
-          if (dnext) dma_piece(j + 2, buf, k - 8);
         }
         fence();
       });
+      };
+      if (dnext) sec_d(std::true_type{});
+      else sec_d(std::false_type{});
       // the last two P.V read their operands after issue: hold them a while
       asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::"v"(vf[2][1][1]), "v"(vf[3][1][1]), "v"(pf1[1][1]));
       ts(j, 5);
     } else if (dnext) {
       // a causal wave past its last row still fills its share of the tiles
 #pragma unroll
-      for (int p = 0; p < 8; ++p) dma_piece(j + 2, buf, p);
+      for (int p = 0; p < 8; ++p) {
+        if constexpr (RS) stage_load(j + 2, p);
+        else dma_piece(j + 2, buf, p);
+      }
     }
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last P.V -> v_accvgpr_read

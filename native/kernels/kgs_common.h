@@ -39,8 +39,23 @@ __device__ __forceinline__ float bf2f(unsigned short h) {
   return __builtin_bit_cast(float, ((unsigned)h) << 16);
 }
 
+// Two f32 -> a packed bf16 pair in one v_cvt_pk_bf16_f32. Two f2bf calls
+// compile to two conversions (each with a dummy second source) plus a v_perm:
+// three VALU ops where one does, on every epilogue and P-fragment pack.
 __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
-  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t v = {lo, hi};
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
+}
+
+// s[base .. base + 7] -> a bf16x8 MFMA fragment, four v_cvt_pk_bf16_f32
+template <class V>
+__device__ __forceinline__ bf16x8 pack_bf16x8(const V& s, int base) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  const u32x4_t u = {pack_bf16x2(s[base], s[base + 1]), pack_bf16x2(s[base + 2], s[base + 3]),
+                     pack_bf16x2(s[base + 4], s[base + 5]), pack_bf16x2(s[base + 6], s[base + 7])};
+  return __builtin_bit_cast(bf16x8, u);
 }
 
 // Cross-lane exchanges on gfx950's half-swaps (one VALU op each, no LDS round
