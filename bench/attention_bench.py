@@ -74,8 +74,6 @@ def main(argv=None) -> int:
                 from kgs.ops import experiments
 
                 fns["kgs_w4"] = lambda: experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, out=out4)
-                fns["kgs_w4rs"] = lambda: experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, out=out4,
-                                                                       staged=True)
             times = {n: [] for n in fns}
             for _ in range(a.rounds):
                 for n, f in fns.items():
@@ -89,7 +87,7 @@ def main(argv=None) -> int:
                    "sdpa_ms": round(ms_t, 4), "sdpa_tflops": round(flops / ms_t / 1e9, 1),
                    "speedup": round(ms_t / ms, 2), "max_abs_err_vs_sdpa": round(err, 5)}
             if a.w4:
-                for n in ("kgs_w4", "kgs_w4rs"):
+                for n in ("kgs_w4",):
                     ms4 = statistics.median(times[n])
                     rec.update({f"{n}_ms": round(ms4, 4), f"{n}_tflops": round(flops / ms4 / 1e9, 1)})
                 rec.update(kgs_w4_max_abs_err_vs_sdpa=round((out4.float() - ref).abs().max().item(), 5))

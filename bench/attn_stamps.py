@@ -24,7 +24,6 @@ def main() -> int:
     ap.add_argument("--heads", type=int, default=32)
     ap.add_argument("--kv-heads", type=int, default=8)
     ap.add_argument("--causal", action="store_true")
-    ap.add_argument("--staged", action="store_true", help="register-staged K/V tiles")
     a = ap.parse_args()
     from kgs.ops import experiments as ex
 
@@ -32,8 +31,8 @@ def main() -> int:
     qkv = torch.randn(b * s, (nh + 2 * nkv) * hd, device="cuda").bfloat16()
     st_t = torch.zeros(64, 4, 64, 8, dtype=torch.int64, device="cuda")
     for _ in range(3):
-        ex.attention_qkv_w4(qkv, b, s, nh, nkv, causal=a.causal, staged=a.staged)
-    ex.attention_qkv_w4(qkv, b, s, nh, nkv, causal=a.causal, stamps=st_t, staged=a.staged)
+        ex.attention_qkv_w4(qkv, b, s, nh, nkv, causal=a.causal)
+    ex.attention_qkv_w4(qkv, b, s, nh, nkv, causal=a.causal, stamps=st_t)
     torch.cuda.synchronize()
     x = st_t.cpu()
     names = ["A_qk0", "B_qk1_sm0", "barrier", "C_pv0_sm1", "D_pv1"]

@@ -215,12 +215,12 @@ def gemm_w4p_stamps(a, b, out, stamps: torch.Tensor, map_: int | str = 0) -> int
 
 def attention_qkv_w4(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_heads: int, head_dim: int = 128,
                      causal: bool = True, scale: float | None = None, out: torch.Tensor | None = None,
-                     stamps: torch.Tensor | None = None, staged: bool = False) -> torch.Tensor:
+                     stamps: torch.Tensor | None = None) -> torch.Tensor:
     """:func:`kgs.ops.transformer.attention_qkv` on the one-wave-per-SIMD,
     named-register kernel (native/kernels/attention_w4.h; ``seq % 256 == 0``).
     ``stamps``: an int64 [64, 4, 64, 8] tensor selects the timing build (per
     workgroup < 64, wave and tile: s_memtime at the tile start and after each
-    section). ``staged``: K/V tiles register-staged instead of LDS-DMA."""
+    section)."""
     if stamps is not None and (stamps.dtype != torch.int64 or stamps.numel() < 64 * 4 * 64 * 8):
         raise ValueError("stamps must be an int64 tensor of 64 * 4 * 64 * 8 elements")
     import math
@@ -236,7 +236,7 @@ def attention_qkv_w4(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_hea
     rc = lib().kgs_exp_attn4_fwd_bf16(base, base + heads * head_dim * esz, base + (heads + kv_heads) * head_dim * esz,
                                       out.data_ptr(), batch, seq, seq, heads, kv_heads, head_dim, ld, ld, ld,
                                       out.stride(0), float(scale), 1 if causal else 0,
-                                      stamps.data_ptr() if stamps is not None else None, 1 if staged else 0,
+                                      stamps.data_ptr() if stamps is not None else None, 0,
                                       _lib.stream_handle(qkv.device))
     _lib.check(rc, "attention_qkv_w4")
     return out

@@ -19,17 +19,13 @@ KGS_EXPORT int kgs_exp_attn4_fwd_bf16(const void* q, const void* k, const void* 
   Args a{(const unsigned short*)q, (const unsigned short*)k, (const unsigned short*)v, (unsigned short*)o,
          ldq, ldk, ldv, ldo, B, S, H, HKV, scale * 1.4426950408889634f, causal ? 1 : 0, Sk, Sk - S,
          (long long*)stamps};
-  // variant 0: LDS-DMA K/V tiles, 1: register-staged (attention_w4.h RS);
-  // stamps: the timing build, long long[64 workgroups][4 waves][64 tiles][8]
-  if (variant == 0 && stamps)
-    hipLaunchKernelGGL((fwd<true, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
-  else if (variant == 0)
-    hipLaunchKernelGGL((fwd<false, false>), dim3((unsigned)nwg), dim3(256), 0, s, a);
-  else if (variant == 1 && stamps)
-    hipLaunchKernelGGL((fwd<true, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
-  else if (variant == 1)
-    hipLaunchKernelGGL((fwd<false, true>), dim3((unsigned)nwg), dim3(256), 0, s, a);
+  // variant 0 only (a register-staged K/V variant measured slower and was
+  // removed, profiles/r4/attention); stamps: the timing build,
+  // long long[64 workgroups][4 waves][64 tiles][8]
+  if (variant != 0) return KGS_ERR_ARG;
+  if (stamps)
+    hipLaunchKernelGGL(fwd<true>, dim3((unsigned)nwg), dim3(256), 0, s, a);
   else
-    return KGS_ERR_ARG;
+    hipLaunchKernelGGL(fwd<false>, dim3((unsigned)nwg), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -160,11 +160,7 @@ __device__ __forceinline__ void mask_diag(f32x16 (&s)[2], int kv0, int hh, int r
 // start of every tile and after each of its sections, per wave: ts[((blk * 4 +
 // w) * 64 + min(j, 63)) * 8 + e], e = 0 tile start, 1 after A, 2 after B, 3
 // after the barrier, 4 after C, 5 after D.
-// RS: K/V tiles register-staged (buffer_load_dwordx4 of tile j + 2 into 8 x 4
-// VGPRs in section D of tile j, ds_write_b128 into the free buffer in section
-// B of tile j + 1) instead of LDS-DMA, whose issue cost stamps put at 150-180
-// cycles per 1 KiB piece beside the MFMAs of a wave alone on its SIMD.
-template <bool TS = false, bool RS = false>
+template <bool TS = false>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void fwd(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[2][2][TILE_BYTES];  // [buf][K, V]
   KGS_ATTN_RESERVE();
@@ -224,25 +220,6 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
 #pragma unroll
     for (int p = 0; p < 8; ++p) dma_piece(jn, sb, p);
   };
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  u32x4 stg[8];
-  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)kbase, 0, 0x7ffffff0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)vbase, 0, 0x7ffffff0, 0x00020000);
-  int voff[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int ch = 4 * w + (p >> 1);
-    const int r = 4 * ch + (lane >> 4), c = (lane & 15) ^ swz(r);
-    voff[p] = (int)((r * ((p & 1) ? a.ldv : a.ldk) + 8 * c) * 2);
-  }
-  auto stage_load = [&](int jn, int p) {
-    stg[p] = __builtin_amdgcn_raw_buffer_load_b128((p & 1) ? rv : rk, voff[p],
-                                                   (int)((long)jn * KB * ((p & 1) ? a.ldv : a.ldk) * 2), 0);
-  };
-  auto stage_write = [&](int sb, int p) {
-    const int ch = 4 * w + (p >> 1);
-    *(u32x4*)(smem[sb][p & 1] + 1024 * ch + 16 * lane) = stg[p];
-  };
   // LDS byte address of this lane's K fragment (t, ks) in buffer sb
   const unsigned kbase_lds = (unsigned)(uintptr_t)(KGS_LDS char*)smem[0][0];
   auto kaddr = [&](int sb, int t, int ks) -> unsigned {
@@ -250,34 +227,28 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   };
   const int g = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
   bf16x8 vf[4][2][2];
+  // V fragment reads as asm: with the builtin, hipcc's LDS-DMA alias check
+  // cannot tell buffer j from the buffer the DMA of tile j + 1 fills and puts
+  // a vmcnt(0) at the top of section A (a full wait for the DMA issued one
+  // section earlier). The fragments are used after the barrier's lgkmcnt(0)
+  // only, and nothing between reads their registers (checked in the ISA).
   auto read_v = [&](const char* Vs, int d, int t, int sp) {
     const int c0 = 4 * d + 2 * (g & 1) + (tp >> 1);
     const int kvb = 32 * t + 16 * sp + 4 * hh + tq;
-    const bf16x4s x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(Vs + off(kvb, c0) + 8 * (tp & 1)));
-    const bf16x4s y =
-        __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(Vs + off(kvb + 8, c0) + 8 * (tp & 1)));
+    const unsigned vl = (unsigned)(uintptr_t)(const KGS_LDS char*)Vs + 8 * (tp & 1);
+    bf16x4s x, y;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(x) : "v"(vl + (unsigned)off(kvb, c0)));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(y) : "v"(vl + (unsigned)off(kvb + 8, c0)));
     vf[d][t][sp] = __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
   };
 
   const int ntile = a.causal ? (qoff + q0 + QB) / KB : a.Sk / KB;
   const int wlast = qoff + rb1 + 31;  // this wave's last row (causal limit)
 
-  if constexpr (RS) {
-#pragma unroll
-    for (int p = 0; p < 8; ++p) stage_load(0, p);
-#pragma unroll
-    for (int p = 0; p < 8; ++p) stage_write(0, p);
-    if (ntile > 1) {
-#pragma unroll
-      for (int p = 0; p < 8; ++p) stage_load(1, p);
-    }
-    __syncthreads();
-  } else {
-    dma_tiles(0, 0);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tile 0
-    __syncthreads();
-    if (ntile > 1) dma_tiles(1, 1);
-  }
+  dma_tiles(0, 0);
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): Q and tile 0
+  __syncthreads();
+  if (ntile > 1) dma_tiles(1, 1);
   static_for<0, 16>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
     atr::kread<k / 8, k % 8>(kaddr(0, k / 8, k % 8));
@@ -290,6 +261,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     const int buf = j & 1;
     const int kv0 = j * KB;
     const bool act = !a.causal || kv0 <= wlast;
+    const bool act0 = !a.causal || kv0 <= qoff + rb0 + 31;  // q-block 0 has rows in tile j
     f32x16 s0[2], s1[2];
     bf16x8 pf0[2][2], pf1[2][2];
     Softmax<0> sm0{s0, m0, l0, pf0, sl2, 0.f, 0.f};
@@ -299,35 +271,39 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       const char* Vs = smem[buf][1];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K(j) in its AGPRs
       fence();
-      // A: QK^T(qb 0), one V fragment per MFMA
-      static_for<0, 16>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        atr::qk<0, k / 8, k % 8, k % 8 == 0>(s0[k / 8]);
-        read_v(Vs, k / 4, (k / 2) % 2, k % 2);
-        fence();
-      });
-      ts(j, 1);
-      // B: QK^T(qb 1) | max, exchange and the t = 0 half of softmax(qb 0)
-      static_for<0, 16>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        atr::qk<1, k / 8, k % 8, k % 8 == 0>(s1[k / 8]);
-        if constexpr (k == 0) {
-          pad_s(s0[1]);  // (s0[0]'s last MFMA is 8 MFMAs back)
-          if (a.causal && kv0 + KB - 1 > qoff + rb0) mask_diag(s0, kv0, hh, qoff + rb0 + l32);
-        }
-        if constexpr (k < 4) sm0.template maxpart<k>();
-        if constexpr (k == 4) sm0.xchg();
-        if constexpr (k >= 5 && k < 13) sm0.template exps<0, 2 * (k - 5), 2>();
-        if constexpr (k == 13) sm0.template pack<0, 0>();
-        if constexpr (k == 14) sm0.template pack<0, 1>();
-        if constexpr (RS && k >= 8)
-          if (j + 1 < ntile) stage_write(buf ^ 1, k - 8);
-        fence();
-      });
+      // (sections A-C in two copies: a causal diagonal tile past all of
+      //  q-block 0's rows runs q-block 1 only)
+      auto sec_ab = [&](auto q0c) {
+        constexpr bool Q0 = decltype(q0c)::value;
+        // A: QK^T(qb 0), one V fragment per MFMA
+        static_for<0, 16>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          if constexpr (Q0) atr::qk<0, k / 8, k % 8, k % 8 == 0>(s0[k / 8]);
+          read_v(Vs, k / 4, (k / 2) % 2, k % 2);
+          fence();
+        });
+        ts(j, 1);
+        // B: QK^T(qb 1) | max, exchange and the t = 0 half of softmax(qb 0)
+        static_for<0, 16>([&](auto kc) {
+          constexpr int k = decltype(kc)::value;
+          atr::qk<1, k / 8, k % 8, k % 8 == 0>(s1[k / 8]);
+          if constexpr (Q0) {
+            if constexpr (k == 0) {
+              pad_s(s0[1]);  // (s0[0]'s last MFMA is 8 MFMAs back)
+              if (a.causal && kv0 + KB - 1 > qoff + rb0) mask_diag(s0, kv0, hh, qoff + rb0 + l32);
+            }
+            if constexpr (k < 4) sm0.template maxpart<k>();
+            if constexpr (k == 4) sm0.xchg();
+            if constexpr (k >= 5 && k < 13) sm0.template exps<0, 2 * (k - 5), 2>();
+            if constexpr (k == 13) sm0.template pack<0, 0>();
+            if constexpr (k == 14) sm0.template pack<0, 1>();
+          }
+          fence();
+        });
+      };
+      if (act0) sec_ab(std::true_type{});
+      else sec_ab(std::false_type{});
       ts(j, 2);
-    } else if (RS && j + 1 < ntile) {
-#pragma unroll
-      for (int p = 0; p < 8; ++p) stage_write(buf ^ 1, p);
     }
     // tile j's V is in registers and tile j + 1 has landed: after the barrier
     // buffer j is free for tile j + 2 (its DMA is issued in section D)
@@ -339,34 +315,40 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     if (act) {
       // C: P.V(qb 0), t = 0 keys first | the t = 1 half of softmax(qb 0), then
       //    max, exchange and the t = 0 half of softmax(qb 1)
-      static_for<0, 16>([&](auto kc) {
-        constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
-        atr::pv<0, d>(vf[d][t][sp], pf0[t][sp]);
-        if constexpr (k >= 2) {  // operands of the P.V two slots back
-          constexpr int kk = k - 2;
-          keep(vf[kk % 4][kk / 8][(kk % 8) / 4]);
-          keep(pf0[kk / 8][(kk % 8) / 4]);
-        }
-        if constexpr (k == 0) {
-          pad_s(s1[1]);
-          if (a.causal && kv0 + KB - 1 > qoff + rb1) mask_diag(s1, kv0, hh, qoff + rb1 + l32);
-        }
-        if constexpr (k < 8) sm0.template exps<1, 2 * k, 2>();
-        if constexpr (k < 4) sm1.template maxpart<k>();
-        if constexpr (k == 4) sm0.template pack<1, 0>();
-        if constexpr (k == 5) sm1.xchg();
-        if constexpr (k == 7) sm0.template pack<1, 1>();
-        if constexpr (k >= 8) sm1.template exps<0, 2 * (k - 8), 2>();
-        if constexpr (k == 12) sm1.template pack<0, 0>();
-        if constexpr (k == 15) sm1.template pack<0, 1>();
-        fence();
-      });
+      auto sec_c = [&](auto q0c) {
+        constexpr bool Q0 = decltype(q0c)::value;
+        static_for<0, 16>([&](auto kc) {
+          constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
+          if constexpr (Q0) {
+            atr::pv<0, d>(vf[d][t][sp], pf0[t][sp]);
+            if constexpr (k >= 2) {  // operands of the P.V two slots back
+              constexpr int kk = k - 2;
+              keep(vf[kk % 4][kk / 8][(kk % 8) / 4]);
+              keep(pf0[kk / 8][(kk % 8) / 4]);
+            }
+          }
+          if constexpr (k == 0) {
+            pad_s(s1[1]);
+            if (a.causal && kv0 + KB - 1 > qoff + rb1) mask_diag(s1, kv0, hh, qoff + rb1 + l32);
+          }
+          if constexpr (Q0 && k < 8) sm0.template exps<1, 2 * k, 2>();
+          if constexpr (k < 4) sm1.template maxpart<k>();
+          if constexpr (Q0 && k == 4) sm0.template pack<1, 0>();
+          if constexpr (k == 5) sm1.xchg();
+          if constexpr (Q0 && k == 7) sm0.template pack<1, 1>();
+          if constexpr (k >= 8) sm1.template exps<0, 2 * (k - 8), 2>();
+          if constexpr (k == 12) sm1.template pack<0, 0>();
+          if constexpr (k == 15) sm1.template pack<0, 1>();
+          fence();
+        });
+      };
+      if (act0) sec_c(std::true_type{});
+      else sec_c(std::false_type{});
       ts(j, 4);
       // D: P.V(qb 1) | the t = 1 half of softmax(qb 1), then the K fragments
       //    of tile j + 1 into their AGPRs and the LDS-DMA of tile j + 2
       // (two copies, with and without the tile j + 2 pieces, so no slot
-      // branches; the K reads run unconditionally -- LDS in bounds -- and are
-      // used only by a wave that has rows in tile j + 1)
+      // branches)
       auto sec_d = [&](auto dnc) {
       static_for<0, 16>([&](auto kc) {
         constexpr int k = decltype(kc)::value, t = k / 8, sp = (k % 8) / 4, d = k % 4;
@@ -384,13 +366,14 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if constexpr (k == 4) sm1.template pack<1, 0>();
         if constexpr (k == 7) sm1.template pack<1, 1>();
         if constexpr (k >= 8) {
+          // K(j + 1) fragments (in LDS since the barrier) into the K AGPRs,
+          // unconditionally -- LDS in bounds -- and used only by a wave that
+          // has rows in tile j + 1 (in section C they cost ~150 cycles there
+          // against ~40 here, profiles/r4/attention)
           constexpr int f0 = 2 * (k - 8);
           atr::kread<f0 / 8, f0 % 8>(kaddr(buf ^ 1, f0 / 8, f0 % 8));
           atr::kread<(f0 + 1) / 8, (f0 + 1) % 8>(kaddr(buf ^ 1, (f0 + 1) / 8, (f0 + 1) % 8));
-          if constexpr (decltype(dnc)::value) {
-            if constexpr (RS) stage_load(j + 2, k - 8);
-            else dma_piece(j + 2, buf, k - 8);
-          }
+          if constexpr (decltype(dnc)::value) dma_piece(j + 2, buf, k - 8);
         }
         fence();
       });
@@ -403,10 +386,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     } else if (dnext) {
       // a causal wave past its last row still fills its share of the tiles
 #pragma unroll
-      for (int p = 0; p < 8; ++p) {
-        if constexpr (RS) stage_load(j + 2, p);
-        else dma_piece(j + 2, buf, p);
-      }
+      for (int p = 0; p < 8; ++p) dma_piece(j + 2, buf, p);
     }
   }
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");  // last P.V -> v_accvgpr_read

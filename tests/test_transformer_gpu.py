@@ -137,8 +137,6 @@ def test_attention_w4_matches_reference(b, s, nh, nkv, qscale, causal):
     assert (got.float() - prod.float()).abs().max().item() < 2e-2 * max(1.0, mag)
     # deterministic: a second run gives the same bits
     assert torch.equal(got, experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal))
-    # register-staged K/V tiles: same arithmetic, same bits
-    assert torch.equal(got, experiments.attention_qkv_w4(qkv, b, s, nh, nkv, causal=causal, staged=True))
 
 
 def test_attention_peaky_softmax_rescales():
