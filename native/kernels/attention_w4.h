@@ -26,12 +26,24 @@
 //
 //   Causal: the wave's q-blocks are row blocks w and 7 - w of the workgroup's
 //   256 rows, so the four waves (one per SIMD) run nearly the same number of
-//   tiles.
+//   tiles; a diagonal tile past all of q-block 0's rows runs sections A-C
+//   without q-block 0 (a second copy of the code, no per-slot branches).
 //
-// Hazards hipcc does not see (asm MFMAs): S is read by VALU only after a tied
-// s_nop pad that follows the next section's first MFMA; O is read (rescale,
-// epilogue) at least one section after the last P.V into it, and after a pad
-// at the end; K AGPRs are rewritten in C, a barrier after the last QK^T.
+// With one wave per SIMD nothing hides a stall, and three cost most of the
+// time found by the timing build (profiles/r4/attention):
+//   - a branch per MFMA slot (~40 cycles each): the wave index is made
+//     wave-uniform (readfirstlane) and section D exists in two copies, with and
+//     without the DMA of tile j + 2, instead of guarding each slot;
+//   - the vmcnt(0) hipcc puts before a builtin ds_read_tr when an LDS-DMA is in
+//     flight (its alias check cannot separate the two buffers): V reads are asm;
+//   - three VALU ops per bf16 pair (kgs_common.h pack_bf16x2 now uses one).
+//
+// Hazards hipcc does not see (asm MFMAs, asm LDS reads): S is read by VALU only
+// after a tied s_nop pad that follows the next section's first MFMA; O is read
+// (rescale, epilogue) at least one section after the last P.V into it, and
+// after a pad at the end; K AGPRs are rewritten in D, a barrier after the last
+// QK^T; V fragment registers are read only after the barrier's lgkmcnt(0) (the
+// ISA is checked for any earlier use of them, see docs/architecture.md).
 #pragma once
 
 #include <type_traits>
