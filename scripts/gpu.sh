@@ -54,6 +54,8 @@
 #   route_ab     128-row decode tiles probe, then serve_ab; serve_ab: batch-256 serving A/B/A with
 #                $AENV / $BENV (one VAR=value each) and $ROUTES (KGS_W4X_ROUTES), trace of B
 #   rope_attn_probe  rope_cache + attention vs the fused launch vs attention alone, with counters
+#   attn_pmc     two counter passes over production attention and the w4 experiment (VALU / MFMA
+#                busy and co-issue, waits; instruction mix, LDS)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 OUT=${1:?usage: gpu.sh OUT step...}
@@ -86,6 +88,12 @@ step() {
             --variants fast --rounds 7 --out "$O/gemm_sweep.json" ;;
         gemm_trace) run gemm_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o gemm \
             -- python3 bench/gemm_profile.py --iters 20 --torch ;;
+        attn_pmc) run attn_pmc1 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
+            SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE \
+            --output-format csv -d "$O/apmc1" -o attn -- python3 bench/attn_pmc_driver.py &&
+            run attn_pmc2 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VALU_TRANS_F SQ_INSTS_LDS \
+            SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE \
+            --output-format csv -d "$O/apmc2" -o attn -- python3 bench/attn_pmc_driver.py ;;
         gemm_pmc) run pmc_stall 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
             SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d "$O/pmc1" -o gemm -- $PMC_GEMM &&
             run pmc_mfma 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU \
