@@ -281,7 +281,10 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     ts(j, 0);
     if (act) {
       const char* Vs = smem[buf][1];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // K(j) in its AGPRs
+      // K(j) in its AGPRs, in two steps: the t = 0 fragments (the first 8 of
+      // the 16 reads) now, the rest before the first t = 1 MFMA (slot 8, after
+      // 16 V reads: lgkmcnt(15), the counter's ceiling, over-waits by one)
+      asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
       fence();
       // (sections A-C in two copies: a causal diagonal tile past all of
       //  q-block 0's rows runs q-block 1 only)
@@ -290,6 +293,7 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         // A: QK^T(qb 0), one V fragment per MFMA
         static_for<0, 16>([&](auto kc) {
           constexpr int k = decltype(kc)::value;
+          if constexpr (k == 8) asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
           if constexpr (Q0) atr::qk<0, k / 8, k % 8, k % 8 == 0>(s0[k / 8]);
           read_v(Vs, k / 4, (k / 2) % 2, k % 2);
           fence();
