@@ -15,9 +15,10 @@
 //   of other work (pinned with sched_barrier, the GEMM's kbody technique; at
 //   most two v_exp_f32 per MFMA gap):
 //     A  QK^T(qb 0)  | one V fragment read (2 x ds_read_b64_tr_b16) per MFMA
-//     B  QK^T(qb 1)  | softmax(qb 0): row max, exchange, the t = 0 keys
+//     B  QK^T(qb 1)  | softmax(qb 0): row max, exchange, the t = 0 keys, the
+//                      first 6 t = 1 keys
 //        lgkm / vm waits, barrier
-//     C  P.V(qb 0), t = 0 keys first | softmax(qb 0) t = 1 keys; softmax(qb 1):
+//     C  P.V(qb 0), t = 0 keys first | softmax(qb 0) other t = 1 keys; softmax(qb 1):
 //                      row max, exchange, t = 0 keys
 //     D  P.V(qb 1)   | softmax(qb 1) t = 1 keys; then the K fragments of tile
 //                      j + 1 into the K AGPRs and the LDS-DMA of tile j + 2
@@ -313,6 +314,9 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             if constexpr (k >= 5 && k < 13) sm0.template exps<0, 2 * (k - 5), 2>();
             if constexpr (k == 13) sm0.template pack<0, 0>();
             if constexpr (k == 14) sm0.template pack<0, 1>();
+            // the first 6 t = 1 scores here: section C carries the q-block 1
+            // max and exchange as well and ran ~600 cycles longer than B
+            if constexpr (k >= 13) sm0.template exps<1, 2 * (k - 13), 2>();
           }
           fence();
         });
@@ -347,11 +351,11 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             pad_s(s1[1]);
             if (a.causal && kv0 + KB - 1 > qoff + rb1) mask_diag(s1, kv0, hh, qoff + rb1 + l32);
           }
-          if constexpr (Q0 && k < 8) sm0.template exps<1, 2 * k, 2>();
+          if constexpr (Q0 && k < 5) sm0.template exps<1, 6 + 2 * k, 2>();
           if constexpr (k < 4) sm1.template maxpart<k>();
-          if constexpr (Q0 && k == 4) sm0.template pack<1, 0>();
+          if constexpr (Q0 && k == 1) sm0.template pack<1, 0>();
           if constexpr (k == 5) sm1.xchg();
-          if constexpr (Q0 && k == 7) sm0.template pack<1, 1>();
+          if constexpr (Q0 && k == 5) sm0.template pack<1, 1>();
           if constexpr (k >= 8) sm1.template exps<0, 2 * (k - 8), 2>();
           if constexpr (k == 12) sm1.template pack<0, 0>();
           if constexpr (k == 15) sm1.template pack<0, 1>();
