@@ -194,9 +194,17 @@ __device__ __forceinline__ void read_b(const CtxT& c, Regs& R, const char* half)
 // values, so the 16 chunks read land on 16 distinct bank groups: no conflicts.
 typedef short bf16x4s __attribute__((ext_vector_type(4)));
 
+// As inline asm: with the builtin, hipcc's LDS-DMA alias check cannot tell
+// the half-tile being read from the ones the look-ahead DMAs fill, and puts a
+// vmcnt(0) before every group of these reads -- draining the 5-deep DMA
+// pipeline each phase. The pipeline's own vmcnt + barrier order the DMA before
+// the read, and phase() waits lgkmcnt(0) behind a sched_barrier before the
+// MFMAs that use the fragments.
 __device__ __forceinline__ bf16x8 tr_frag(const char* p) {
-  const bf16x4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)p);
-  const bf16x4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((KGS_LDS bf16x4s*)(p + 4 * 256));
+  const unsigned a = (unsigned)(uintptr_t)(const KGS_LDS char*)p;
+  bf16x4s lo, hi;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:1024" : "=v"(hi) : "v"(a));
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
