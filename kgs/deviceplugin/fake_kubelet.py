@@ -115,6 +115,19 @@ class FakeKubelet:
         d = self.latest_devices() or []
         return sum(1 for _, h, _ in d if h == api.HEALTHY)
 
+    def health(self) -> dict:
+        """{device id: health} of the latest list ({} before the first)."""
+        return {i: h for i, h, _ in (self.latest_devices() or [])}
+
+    # Waits key on the STATE the latest list shows, never on how many lists
+    # arrived: the plugin's register() / notify() lists can land after a test
+    # took a count, and a stale "Healthy" list then satisfies "one more list".
+    def wait_health(self, dev_id: str, state: str, timeout: float = 10.0) -> bool:
+        return self.wait(lambda: self.health().get(dev_id) == state, timeout=timeout)
+
+    def wait_capacity(self, n: int, timeout: float = 10.0) -> bool:
+        return self.wait(lambda: bool(self.device_lists) and self.capacity() == n, timeout=timeout)
+
     def _endpoint_channel(self):
         reg = self.registrations[-1]
         return grpc.insecure_channel(f"unix://{os.path.join(self.dir, reg.endpoint)}")

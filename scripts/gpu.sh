@@ -27,6 +27,7 @@
 #   gateup_pmc   counter passes (SQ waits, FETCH_SIZE, TCC hit/miss, TA/TCP/TD stalls) + trace of the batch-256
 #                gate|up kernel, default vs nt weight loads
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
+#   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
 #   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
@@ -128,6 +129,16 @@ step() {
                 (export KGS_NT_WEIGHTS=1; run serve_nt1_$r 300 $SB) &&
                 (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=1; run serve_nt1gp_$r 300 $SB) || return 1
             done ;;
+        serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
+            # then nt on under a kernel trace (the last dispatches name a faulting kernel)
+            local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
+            SB="$SB --max-batch ${B:-256} --max-model-len 2048"
+            (export KGS_NT_WEIGHTS=1; run serve_nt1_a 300 $SB) &&
+            (export KGS_NT_WEIGHTS=1; run serve_nt1_b 300 $SB) &&
+            (export KGS_NT_WEIGHTS=0; run serve_nt0_a 300 $SB) &&
+            (export KGS_NT_WEIGHTS=1; run serve_nt1_trace 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$O/nt1_trace" -o d -- python3 -m kgs.serve bench --requests ${B:-256} --input-len 512 \
+                --output-len 256 --max-batch ${B:-256} --max-model-len 2048) ;;
         fp8_sweep) run fp8_sweep 600 python bench/gemm_sweep.py --dtype fp8 --data normal \
             --shapes ${SHAPES:-8192,16384x16384x8192,8192x28672x4096,8192x6144x4096,4096x8192x14336,8192x4096x14336} \
             --variants ${VARIANTS:-fast,w4p} --rounds 7 --out "$O/fp8_sweep.json" ;;

@@ -58,3 +58,20 @@ def test_rocm_ci_steps_run_against_the_fakes(world, tmp_path):  # noqa: F811
     assert (work / "create-timings.json").exists()
     assert world.state()["clusters"] == {}
     assert len(ran) >= 6 and len(skipped) == 2
+
+
+def test_tests_workflow_fails_on_native_build_and_pins_rocm():
+    """the CPU tier's native build must not be masked
+    (``|| true`` let it run on the Python fallback), and the gfx950 build job
+    must use a pinned ROCm image, not a moving ``:latest`` (the reference's
+    unpinned-upstream drift, Q6)."""
+    from kgs import config
+
+    wf = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "tests.yaml")))
+    runs = [s["run"] for job in wf["jobs"].values() for s in job["steps"] if "run" in s]
+    assert not any("|| true" in r or "|| :" in r for r in runs), runs
+    build = [r for r in runs if "kgs.utils.build" in r]
+    assert build and all("--only gpuinfo" in r for r in build)
+    images = [job["container"] for job in wf["jobs"].values() if "container" in job]
+    assert images == [config.ROCM_DEV_IMAGE]
+    assert all(not i.endswith(":latest") and ":" in i.rsplit("/", 1)[-1] for i in images)

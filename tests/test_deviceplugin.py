@@ -41,7 +41,7 @@ def cluster(short_tmp, host8):
     plug.start()
     plug.register()
     plug.notify()
-    assert kub.wait(lambda: bool(kub.device_lists))
+    assert kub.wait_capacity(8)
     yield kub, plug, src, host8
     plug.stop()
     kub.stop()
@@ -129,20 +129,17 @@ def test_allocate_unknown_device_rejected(cluster):
 
 def test_health_flip_streams_unhealthy_then_recovers(cluster):
     kub, plug, src, host = cluster
-    n0 = len(kub.device_lists)
+    sick = [d.id for d in src.devices() if d.render_minor == 144][0]
     remove_gpu_device(host, 144)
     assert plug.health_tick()
-    assert kub.wait(lambda: len(kub.device_lists) > n0)
-    devs = dict((i, h) for i, h, _ in kub.latest_devices())
-    sick = [d.id for d in src.devices() if d.render_minor == 144][0]
-    assert devs[sick] == "Unhealthy" and kub.capacity() == 7
+    assert kub.wait_health(sick, "Unhealthy")
+    assert kub.capacity() == 7
     with pytest.raises(grpc.RpcError) as ei:
         kub.allocate([sick])
     assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
-    n1 = len(kub.device_lists)
     restore_gpu_device(host, 144)
     assert plug.health_tick()
-    assert kub.wait(lambda: len(kub.device_lists) > n1)
+    assert kub.wait_health(sick, "Healthy")
     assert kub.capacity() == 8
     assert not plug.health_tick()  # no change -> no update
 
@@ -150,10 +147,8 @@ def test_health_flip_streams_unhealthy_then_recovers(cluster):
 def test_kfd_loss_marks_all_unhealthy(cluster):
     kub, plug, src, host = cluster
     os.unlink(os.path.join(host, "dev/kfd"))
-    n0 = len(kub.device_lists)
     assert plug.health_tick()
-    assert kub.wait(lambda: len(kub.device_lists) > n0)
-    assert kub.capacity() == 0
+    assert kub.wait_capacity(0)
 
 
 def test_preferred_allocation_packs_numa(cluster):
@@ -181,7 +176,7 @@ def test_kubelet_restart_reregisters(short_tmp, host8):
         assert kub.wait(lambda: len(kub.registrations) == 1 and bool(kub.device_lists), timeout=15)
         kub.restart()
         assert kub.wait(lambda: len(kub.registrations) >= 2, timeout=15)
-        assert kub.wait(lambda: kub.capacity() == 8, timeout=15)
+        assert kub.wait_capacity(8, timeout=15)
         deadline = time.monotonic() + 10
         while plug.registrations < 2 and time.monotonic() < deadline:
             time.sleep(0.05)
@@ -233,14 +228,13 @@ def test_fake_source_plugin(short_tmp):
     plug.register()
     plug.notify()
     try:
-        assert kub.wait(lambda: kub.capacity() == 2)
+        assert kub.wait_capacity(2)
         r = kub.allocate(["fake-amdgpu-0"])
         assert len(r.container_responses[0].devices) == 0
         assert r.container_responses[0].envs["KGS_FAKE_GPUS"] == "fake-amdgpu-0"
-        n = len(kub.device_lists)
         src.set_unhealthy("fake-amdgpu-1")
         assert plug.health_tick()
-        assert kub.wait(lambda: len(kub.device_lists) > n)
+        assert kub.wait_health("fake-amdgpu-1", "Unhealthy")
         assert kub.capacity() == 1
     finally:
         plug.stop()
@@ -327,3 +321,30 @@ def test_entrypoint_does_not_assume_isolation(host8):
     assert pinned_env(got, environ={"ROCR_VISIBLE_DEVICES": "0,1"})["ROCR_VISIBLE_DEVICES"] == \
         "GPU-a6ff75a300000007,GPU-a6ff75a300000002"
     assert allocated_gpus(host8, environ={"KGS_FAKE_GPUS": "fake-amdgpu-0"}) == []
+
+
+def test_fake_kubelet_waits_on_state_not_list_count(short_tmp):
+    """a wait keyed on "one more list than before" returned
+    on the plugin's own late register()/notify() list (still Healthy). The
+    state waits only return once the latest list shows the state."""
+    kub = FakeKubelet(os.path.join(short_tmp, "dpw"))
+    healthy = [("gpu-0", "Healthy", [0]), ("gpu-1", "Healthy", [0])]
+    kub.device_lists.append(healthy)
+
+    def feed():
+        time.sleep(0.1)
+        with kub._cv:  # the stale list lands first ...
+            kub.device_lists.append(list(healthy))
+            kub._cv.notify_all()
+        time.sleep(0.2)
+        with kub._cv:  # ... then the flip
+            kub.device_lists.append([("gpu-0", "Healthy", [0]), ("gpu-1", "Unhealthy", [0])])
+            kub._cv.notify_all()
+
+    t = threading.Thread(target=feed)
+    t0 = time.monotonic()
+    t.start()
+    assert kub.wait_health("gpu-1", "Unhealthy", timeout=5)
+    assert time.monotonic() - t0 >= 0.25 and kub.capacity() == 1
+    assert kub.wait_capacity(1, timeout=0.1) and not kub.wait_capacity(2, timeout=0.1)
+    t.join()

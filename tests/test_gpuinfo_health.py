@@ -148,16 +148,14 @@ def test_list_and_watch_flips_on_ecc_and_recovers(smi_host):
         plug.start()
         plug.register()
         plug.notify()
-        assert kub.wait(lambda: bool(kub.device_lists))
-        assert kub.capacity() == 4
+        assert kub.wait_capacity(4)
         assert not plug.health_tick()  # first tick takes the baselines: nothing flips
         dev = [x for x in src.devices() if x.render_minor == 144][0]
-        n0 = len(kub.device_lists)
         stub.gpus[144]["uncorr"] = 1
         stub.write()
         assert plug.health_tick()
-        assert kub.wait(lambda: len(kub.device_lists) > n0)
-        assert dict((i, h) for i, h, _ in kub.latest_devices())[dev.id] == "Unhealthy" and kub.capacity() == 3
+        assert kub.wait_health(dev.id, "Unhealthy")
+        assert kub.capacity() == 3
         with pytest.raises(grpc.RpcError):
             kub.allocate([dev.id])
         from prometheus_client import generate_latest
@@ -167,11 +165,10 @@ def test_list_and_watch_flips_on_ecc_and_recovers(smi_host):
         text = generate_latest(make_registry(plug)).decode()
         assert f'kgs_gpu_ecc_errors{{id="{dev.id}",kind="uncorrectable"}} 1.0' in text
         assert f'kgs_gpu_xgmi_links{{id="{dev.id}",state="up"}} 7.0' in text
-        n1 = len(kub.device_lists)
         stub.gpus[144]["uncorr"] = 0  # reset
         stub.write()
         assert plug.health_tick()
-        assert kub.wait(lambda: len(kub.device_lists) > n1)
+        assert kub.wait_health(dev.id, "Healthy")
         assert kub.capacity() == 4
     finally:
         plug.stop()
