@@ -217,7 +217,7 @@ def attention_qkv_w4(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_hea
                      causal: bool = True, scale: float | None = None, out: torch.Tensor | None = None,
                      stamps: torch.Tensor | None = None) -> torch.Tensor:
     """:func:`kgs.ops.transformer.attention_qkv` on the one-wave-per-SIMD,
-    named-register kernel (native/kernels/attention_w4.h; ``seq % 256 == 0``).
+    named-register kernel (native/experiments/attention_w4.h; ``seq % 256 == 0``).
     ``stamps``: an int64 [64, 4, 64, 8] tensor selects the timing build (per
     workgroup < 64, wave and tile: s_memtime at the tile start and after each
     section)."""

@@ -161,7 +161,7 @@ def targets(out: Path | None = None) -> list[Target]:
             sorted((NATIVE / "experiments").glob("*.hip")),
             HIPCC,
             flags=HIP_FLAGS + ["-fvisibility=hidden", f"-I{kdir}"],
-            headers=k_headers,
+            headers=k_headers + sorted((NATIVE / "experiments").glob("*.h")),
         ),
         Target(
             "gpuinfo-lib",

@@ -41,3 +41,28 @@ def test_graft_entry_build_imports():
     import __graft_entry__
 
     __graft_entry__.build()
+
+
+def test_kernel_dir_holds_only_production_sources():
+    """``native/kernels/`` (the production library)
+    holds only code the production library compiles: every header there is
+    reached from a production ``.hip`` file, and nothing there includes an
+    experiments-only header. Measured alternatives live in ``native/experiments/``."""
+    import re
+    from pathlib import Path
+
+    kdir = Path(ROOT) / "native" / "kernels"
+    inc = re.compile(r'#include\s+"([^"]+)"')
+    reached, todo = set(), [p.name for p in kdir.glob("*.hip")]
+    while todo:
+        name = todo.pop()
+        if name in reached:
+            continue
+        reached.add(name)
+        for dep in inc.findall((kdir / name).read_text()):
+            assert (kdir / dep).exists(), f"{name} includes {dep}, which is not in native/kernels"
+            todo.append(dep)
+    headers = {p.name for p in kdir.glob("*.h")}
+    assert headers <= reached, sorted(headers - reached)
+    gens = {p.name for p in kdir.glob("gen_*.py")}
+    assert gens == {"gen_acc_regs.py"}, gens  # acc_regs.h's generator (the persistent GEMM's AGPR map)
