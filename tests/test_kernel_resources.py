@@ -156,3 +156,52 @@ def test_named_agpr_kernels_never_touch_agprs_outside_asm(gemm_build):
                     stray.append(code)
         assert seen >= 256, (name, seen)  # the accumulators are there, through asm
         assert not stray, (name, stray[:5])
+
+
+def _vregs(text: str) -> set:
+    out = set()
+    for a, b in re.findall(r"(?<![\w.])v\[(\d+):(\d+)\]", text):
+        out |= set(range(int(a), int(b) + 1))
+    out |= {int(a) for a in re.findall(r"(?<![\w.\[])v(\d+)\b", text)}
+    return out
+
+
+def _tr_read_hazards(body: str) -> list:
+    """Instructions that name a VGPR an inline-asm ``ds_read_b64_tr_b16`` is
+    still filling, i.e. before the next ``s_waitcnt`` with ``lgkmcnt(0)``
+    (textual order; only lgkmcnt(0) retires the reads)."""
+    pending, bad = set(), []
+    for ln in body.splitlines():
+        code = ln.split(";")[0].strip()
+        if not code or code.startswith(".") or code.endswith(":"):
+            continue
+        if code.startswith("s_waitcnt") and "lgkmcnt(0)" in code:
+            pending = set()
+        elif code.startswith("ds_read_b64_tr_b16"):
+            dst, addr = code.split(None, 1)[1].split(",", 1)
+            if _vregs(addr) & pending:
+                bad.append(code)
+            pending |= _vregs(dst)
+        elif _vregs(code) & pending:
+            bad.append(code)
+    return bad
+
+
+def test_tr_read_hazard_check_catches_an_early_use():
+    body = ("\tds_read_b64_tr_b16 v[10:11], v5\n\ts_waitcnt lgkmcnt(0)\n\tv_mov_b32 v20, v10\n"
+            "\tds_read_b64_tr_b16 v[12:13], v5 offset:1024\n\tv_mov_b32 v21, v13\n\ts_waitcnt lgkmcnt(0)\n")
+    assert _tr_read_hazards(body) == ["v_mov_b32 v21, v13"]
+
+
+def test_transposed_layout_tr_reads_are_waited_before_use(gemm_build):
+    """the transposed-layout GEMMs issue ds_read_b64_tr_b16 as inline
+    asm (gemm_pipeline.h tr_frag), so hipcc's waitcnt pass does not know those
+    VGPRs arrive asynchronously. Results are right only while no instruction
+    touches a destination before phase()'s s_waitcnt lgkmcnt(0): a register
+    copy of the shufflevector result, or an MFMA scheduled above the wait,
+    would read a stale fragment. Checked on every build, every such kernel."""
+    _, asm = gemm_build
+    funcs = {n: b for n, b in _functions(asm, r".").items() if "ds_read_b64_tr_b16" in b}
+    assert len(funcs) >= 8, len(funcs)  # A-, B- and AB-transposed layouts x epilogues
+    for name, body in funcs.items():
+        assert _tr_read_hazards(body) == [], name
