@@ -24,15 +24,22 @@
 //  * no slot (reserve empty during a capture, allocation failure): nullptr and
 //    the caller runs the one-shot grid, which needs no counters.
 //
-// Pool memory is allocated and zeroed outside any capture (hipMalloc +
-// stream-ordered memset + sync of the calling stream) and never freed: 64 B
-// per stream or captured launch.
+// Pool memory is allocated and zeroed outside any capture and outside the pool
+// lock, and never freed: 64 B per stream or captured launch. A new chunk is
+// zeroed on the pool's own non-blocking stream and only THAT stream is
+// synchronised (one 16 KiB memset is all it ever holds): the caller's stream
+// -- possibly queued behind a long kernel -- is never waited on, and no other
+// thread's tile_queue() call waits behind the growth.
+// Owners are found through a hash map keyed by (stream, thread).
 #pragma once
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 namespace kgs {
@@ -51,15 +58,25 @@ struct TileQueueStats {
 
 namespace tq_detail {
 
-struct Owner {
+struct OwnerKey {
   hipStream_t stream;
   std::thread::id thread;  // only for hipStreamPerThread
-  int* slot;
+  bool operator==(const OwnerKey& o) const { return stream == o.stream && thread == o.thread; }
+};
+
+struct OwnerHash {
+  size_t operator()(const OwnerKey& k) const {
+    return std::hash<const void*>()((const void*)k.stream) ^
+           (std::hash<std::thread::id>()(k.thread) * 0x9e3779b97f4a7c15ull);
+  }
 };
 
 struct DevicePool {
   std::vector<int*> free_slots;
-  std::vector<Owner> owners;
+  std::unordered_map<OwnerKey, int*, OwnerHash> owners;
+  hipStream_t zero_stream = nullptr;  // private, non-blocking; touched only by the growing thread
+  bool growing = false;               // one growth at a time per device
+  bool warned = false;                // capture fallback reported once
   long slots = 0, capture_slots = 0, fallbacks = 0;
 };
 
@@ -72,20 +89,38 @@ inline DevicePool* pools() {
   return p;
 }
 
-// one more chunk of zeroed slots for device `dev` (caller holds mu, not capturing)
-inline bool grow(DevicePool& P, int dev, hipStream_t stream) {
+// One chunk of zeroed slots for device `dev`, made WITHOUT the pool lock by
+// the one thread that set P.growing: hipMalloc, a memset on the pool's private
+// stream, a sync of that stream. nullptr on failure.
+inline int* new_chunk(DevicePool& P, int dev) {
   int cur = 0;
-  if (hipGetDevice(&cur) != hipSuccess) return false;
-  if (cur != dev && hipSetDevice(dev) != hipSuccess) return false;
+  if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
   int* p = nullptr;
-  bool ok = hipMalloc(&p, sizeof(int) * TQ_INTS * TQ_CHUNK) == hipSuccess;
-  ok = ok && hipMemsetAsync(p, 0, sizeof(int) * TQ_INTS * TQ_CHUNK, stream) == hipSuccess &&
-       hipStreamSynchronize(stream) == hipSuccess;
+  bool ok = P.zero_stream != nullptr ||
+            hipStreamCreateWithFlags(&P.zero_stream, hipStreamNonBlocking) == hipSuccess;
+  ok = ok && hipMalloc(&p, sizeof(int) * TQ_INTS * TQ_CHUNK) == hipSuccess;
+  ok = ok && hipMemsetAsync(p, 0, sizeof(int) * TQ_INTS * TQ_CHUNK, P.zero_stream) == hipSuccess &&
+       hipStreamSynchronize(P.zero_stream) == hipSuccess;
   if (cur != dev) (void)hipSetDevice(cur);
-  if (!ok) {
-    if (p) (void)hipFree(p);
-    return false;
+  if (!ok && p) {
+    (void)hipFree(p);
+    p = nullptr;
   }
+  return p;
+}
+
+// Grow device `dev`'s pool by one chunk; called with `lock` held, releases it
+// around the allocation. Returns false if another thread is already growing
+// the pool or the allocation failed.
+inline bool grow(DevicePool& P, int dev, std::unique_lock<std::mutex>& lock) {
+  if (P.growing) return false;
+  P.growing = true;
+  lock.unlock();
+  int* p = new_chunk(P, dev);
+  lock.lock();
+  P.growing = false;
+  if (!p) return false;
   for (int i = TQ_CHUNK - 1; i >= 0; --i) P.free_slots.push_back(p + i * TQ_INTS);
   P.slots += TQ_CHUNK;
   return true;
@@ -100,17 +135,18 @@ inline int* tile_queue(hipStream_t stream) {
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return nullptr;
   const bool capturing = cs != hipStreamCaptureStatusNone;
-  std::lock_guard<std::mutex> lock(mu());
+  std::unique_lock<std::mutex> lock(mu());
   DevicePool& P = pools()[dev];
   if (capturing) {
     // no allocation or sync inside a capture: a reserved slot, or the one-shot grid
-    if (P.free_slots.empty()) {
+    int* s = P.free_slots.empty() ? nullptr : P.free_slots.back();
+    if (s == nullptr || hipMemsetAsync(s, 0, sizeof(int) * TQ_INTS, stream) != hipSuccess) {
       ++P.fallbacks;
-      return nullptr;
-    }
-    int* s = P.free_slots.back();
-    if (hipMemsetAsync(s, 0, sizeof(int) * TQ_INTS, stream) != hipSuccess) {
-      ++P.fallbacks;
+      if (!P.warned) {
+        P.warned = true;
+        std::fprintf(stderr, "[kgs] tile_queue: no reserved ticket slot for a captured persistent GEMM on device "
+                             "%d; the capture runs the one-shot grid (an eager launch refills the reserve)\n", dev);
+      }
       return nullptr;
     }
     P.free_slots.pop_back();  // owned by this graph node for the life of the process
@@ -118,16 +154,20 @@ inline int* tile_queue(hipStream_t stream) {
     return s;
   }
   const bool per_thread = stream == hipStreamPerThread;
-  const std::thread::id me = per_thread ? std::this_thread::get_id() : std::thread::id();
-  for (const Owner& o : P.owners)
-    if (o.stream == stream && o.thread == me) return o.slot;
-  if ((int)P.free_slots.size() <= TQ_RESERVE && !grow(P, dev, stream) && P.free_slots.empty()) {
+  const OwnerKey key{stream, per_thread ? std::this_thread::get_id() : std::thread::id()};
+  auto it = P.owners.find(key);
+  int* s = it == P.owners.end() ? nullptr : it->second;
+  // keep the capture reserve filled: captures cannot allocate, eager calls can
+  // (a known stream's calls refill it too)
+  if ((int)P.free_slots.size() <= TQ_RESERVE) grow(P, dev, lock);
+  if (s != nullptr) return s;
+  if (P.free_slots.empty()) {
     ++P.fallbacks;
     return nullptr;
   }
-  int* s = P.free_slots.back();
+  s = P.free_slots.back();
   P.free_slots.pop_back();
-  P.owners.push_back(Owner{stream, me, s});
+  P.owners.emplace(key, s);
   return s;
 }
 

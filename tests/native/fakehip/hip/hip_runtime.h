@@ -14,6 +14,7 @@ typedef int hipDevice_t;
 enum { hipSuccess = 0, hipErrorOutOfMemory = 2 };
 typedef enum { hipStreamCaptureStatusNone = 0, hipStreamCaptureStatusActive = 1 } hipStreamCaptureStatus;
 #define hipStreamPerThread ((hipStream_t)2)
+enum { hipStreamDefault = 0, hipStreamNonBlocking = 1 };
 
 namespace fakehip {
 inline int& cur_dev() { static int d = 0; return d; }
@@ -23,6 +24,8 @@ inline int& mallocs() { static int n = 0; return n; }
 inline int& malloc_budget() { static int n = 1 << 30; return n; }
 struct Memset { void* p; size_t n; hipStream_t s; bool captured; };
 inline std::vector<Memset>& memsets() { static std::vector<Memset> v; return v; }
+inline std::vector<hipStream_t>& syncs() { static std::vector<hipStream_t> v; return v; }
+inline std::vector<hipStream_t>& created() { static std::vector<hipStream_t> v; return v; }
 }  // namespace fakehip
 
 inline hipError_t hipGetDevice(int* d) { *d = fakehip::cur_dev(); return hipSuccess; }
@@ -50,4 +53,14 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t s) {
   if (!fakehip::capturing()[s]) std::memset(p, v, n);
   return hipSuccess;
 }
-inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipStreamSynchronize(hipStream_t s) {
+  fakehip::syncs().push_back(s);
+  return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned flags) {
+  static long next = 0x7000000;
+  *s = (hipStream_t)(next += 16);
+  fakehip::stream_dev()[*s] = fakehip::cur_dev();
+  fakehip::created().push_back(*s);
+  return flags == hipStreamNonBlocking ? hipSuccess : 1;
+}

@@ -70,6 +70,28 @@ int main() {
   fakehip::malloc_budget() = 0;
   fakehip::stream_dev()[S(3000)] = 2;
   CHECK(tile_queue(S(3000)) == nullptr && tile_queue_stats(2).fallbacks == 1);
+  // 7. growth never touches a caller's stream: every chunk memset and every
+  // sync went to a pool-private stream
+  std::set<hipStream_t> priv(fakehip::created().begin(), fakehip::created().end());
+  CHECK(priv.size() == 3);  // one per device that tried to grow (device 2: allocation then failed)
+  for (const auto& m : fakehip::memsets())
+    CHECK(m.n == 64 ? !priv.count(m.s) : (priv.count(m.s) && !m.captured));
+  CHECK(!fakehip::syncs().empty());
+  for (hipStream_t s : fakehip::syncs()) CHECK(priv.count(s));
+  // 8. captures that drain the reserve are refilled by the next eager call of
+  // an already-known stream, not only by a new stream
+  fakehip::malloc_budget() = 1 << 30;
+  fakehip::capturing()[S(5)] = true;
+  while (tile_queue(S(5)) != nullptr) {
+  }
+  const long fb = tile_queue_stats(0).fallbacks;
+  fakehip::capturing()[S(5)] = false;
+  const int mallocs2 = fakehip::mallocs();
+  CHECK(seen.count(tile_queue(S(5))));  // its own slot, and the pool grew
+  CHECK(fakehip::mallocs() == mallocs2 + 1);
+  fakehip::capturing()[S(5)] = true;
+  CHECK(tile_queue(S(5)) != nullptr && tile_queue_stats(0).fallbacks == fb);
+  fakehip::capturing()[S(5)] = false;
   std::printf("tile_queue host test: OK (%ld slots on device 0)\n", tile_queue_stats(0).slots);
   return 0;
 }

@@ -948,6 +948,53 @@ def test_eighty_streams_each_launch_a_persistent_gemm():
         destroy()
 
 
+def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
+    """the ticket pool used to grow with a
+    hipStreamSynchronize of the CALLER's stream, so the first persistent GEMM
+    on a new stream blocked the host until everything already queued there had
+    run. Now a stream holding a ~50 ms kernel gets its first persistent GEMM --
+    with the pool at its capture reserve, so the call itself grows the pool --
+    in under 5 ms of host time, and the product is bitwise the one-shot one."""
+    import time
+
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_stats
+    from kgs.ops.elementwise import cu_hold
+
+    As, b = _queue_operands(1, seed=14)
+    ref = gemm_nt(As[0], b, variant="w4_oneshot")
+    st = tile_queue_stats()
+    free = st["slots"] - st["stream_slots"] - st["capture_slots"]
+    reserve = 64  # tile_queue.h TQ_RESERVE
+    fill = max(0, free - reserve)  # new streams that bring the pool down to its reserve
+    streams, destroy = _hip_streams(fill + 1)
+    try:
+        junk = torch.empty_like(ref)
+        for s in streams[:fill]:
+            with torch.cuda.stream(s):
+                gemm_nt(As[0], b, out=junk)
+        torch.cuda.synchronize()
+        st0 = tile_queue_stats()
+        assert st0["slots"] == 0 or st0["slots"] - st0["stream_slots"] - st0["capture_slots"] <= reserve, st0
+        busy = streams[-1]
+        out = torch.zeros_like(ref)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(busy):
+            cu_hold(256, 50000.0, lds_kb=0)
+            t0 = time.perf_counter()
+            gemm_nt(As[0], b, out=out)
+            host_ms = (time.perf_counter() - t0) * 1e3
+        st1 = tile_queue_stats()
+        assert st1["slots"] > st0["slots"] and st1["stream_slots"] == st0["stream_slots"] + 1, (st0, st1)
+        assert st1["fallbacks"] == st0["fallbacks"]
+        assert host_ms < 5.0, host_ms
+        busy.synchronize()
+        assert torch.equal(out, ref)
+    finally:
+        torch.cuda.synchronize()
+        destroy()
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("grid", [0, 224, 100])
 def test_persistent_first_ticket_modes_and_reserved_grids_are_exact(mode, grid):
