@@ -160,17 +160,33 @@ def test_workload_entrypoint_smoke_mode():
     assert all("gemm" not in r for r in res["ranks"])
 
 
-def test_workload_entrypoint_counters(tmp_path):
-    """BASELINE config 3: the pod's GEMM re-run under rocprofv3 (--pmc passes only,
-    never combined with tracing), summarised to MFMA busy / LDS conflicts / L2 hit."""
-    env = dict(ENV, TMPDIR="/tmp")
-    r = subprocess.run([sys.executable, "-m", "kgs.workload.entrypoint", "--nproc", "1", "--gemm-size", "4096",
+def test_workload_entrypoint_counters_with_the_plugin_allocation(tmp_path):
+    """BASELINE config 3 as pods/rocm-gpu-counters-pod.yaml runs it: the
+    entrypoint with --counters and EXACTLY the environment the device plugin's
+    Allocate returns on this box (its --self-test: ROCR_VISIBLE_DEVICES
+    GPU-<uuid>, KGS_RENDER_MINORS, KGS_GPU_IDS), no --nproc override, as the
+    box's ordinary (non-root) user with only the device nodes: the GEMM re-run
+    under rocprofv3 --pmc (passes only, never combined with tracing) and
+    summarised to MFMA busy / LDS conflict / L2 hit lines."""
+    r = subprocess.run([sys.executable, "-m", "kgs.deviceplugin", "--self-test",
+                        "--partition-file", "/nonexistent/gpus.json"],
+                       env=ENV, capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    alloc = json.loads(r.stdout)["allocate"]["envs"]
+    assert alloc["ROCR_VISIBLE_DEVICES"].startswith("GPU-") and alloc["KGS_RENDER_MINORS"], alloc
+    env = dict(ENV, TMPDIR="/tmp", **alloc)
+    for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "kgs.workload.entrypoint", "--gemm-size", "4096",
                         "--gemm-iters", "3", "--counters", "--counters-dir", str(tmp_path / "prof")],
                        env=env, capture_output=True, text=True, timeout=900, cwd="/tmp")
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = _last_json(r.stdout)
+    assert res["n_gpus"] == 1 and res["rocr_visible_devices"] == alloc["ROCR_VISIBLE_DEVICES"], res
     assert all(v is True for v in res["counters"]["passes"].values()), res["counters"]
-    assert "MFMA busy" in r.stdout and "L2 hit" in r.stdout
+    for want in ("MFMA busy", "LDS conflict", "L2 hit"):
+        assert want in r.stdout, (want, r.stdout[-3000:])
+    print(json.dumps({"uid": os.getuid(), "alloc": alloc, "passes": res["counters"]["passes"]}))
 
 
 def test_doctor_device_checks_on_the_box():

@@ -193,3 +193,20 @@ def test_no_gpu_pod_is_privileged_without_a_stated_reason():
     # the renderers agree
     for doc in [manifests.gpu_test_pod("x", gpus=1), manifests.vllm_rocm_pod()[-1]]:
         assert not doc["spec"]["containers"][0].get("securityContext", {}).get("privileged")
+
+
+def test_counters_pod():
+    """BASELINE config 3 (VERDICT r4 missing 3): a gpu-rocm-test-shaped pod with
+    one GPU whose entrypoint re-runs the GEMM under rocprofv3 counters;
+    unprivileged, and its manifest states the permission --pmc needs."""
+    doc = _load("rocm-gpu-counters-pod.yaml")
+    assert doc == manifests.gpu_test_pod("localhost:5000/kgs-rocm-test:dev", gpus=1, name="gpu-rocm-counters",
+                                         command=["python3", "-m", "kgs.workload.entrypoint", "--counters", "--pod"])
+    assert not doc["spec"]["containers"][0].get("securityContext")
+    with open(os.path.join(PODS, "rocm-gpu-counters-pod.yaml")) as f:
+        text = f.read()
+    assert "# Permissions: NOT privileged" in text and "/dev/kfd" in text and "renderD" in text
+    assert "test_workload_entrypoint_counters_with_the_plugin_allocation" in text
+    rendered = manifests.render_static_pod("rocm-gpu-counters-pod", "localhost:5001")
+    assert "image: localhost:5001/kgs-rocm-test:dev" in rendered
+    assert yaml.safe_load(manifests.render_static_pod("rocm-gpu-counters", "localhost:5000")) == doc
