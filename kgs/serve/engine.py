@@ -25,6 +25,7 @@ from kgs.models.llama import LlamaConfig
 from kgs.ops.decode import PAGE, PagedKVCache
 
 from .model import ServingModel
+from .trace import TRACE
 
 
 @dataclass
@@ -113,7 +114,10 @@ class LLMEngine:
         self._gen = torch.Generator(device=self.device).manual_seed(cfg.seed)
         self.stats = {"prefill_steps": 0, "decode_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "mixed_steps": 0, "preemptions": 0, "graph_replays": 0, "graph_captures": 0}
-        self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs"
+        # per-op synchronisation (fault attribution, kgs.serve.trace) cannot run inside a capture
+        self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs" and not TRACE.sync_ops
+        self.vocab = model_cfg.vocab
+        self.validate = True  # host-side range checks of every step's device inputs (_check_plan)
         self._want_lp: set = set()
         self._want_pen: set = set()
         self._seeded: set = set()
@@ -171,6 +175,10 @@ class LLMEngine:
             return []
         self.stats["preemptions"] += len(plan.preempted)
         ids = plan.seq_ids
+        if self.validate:
+            self._check_plan(plan)
+        nstep = sum(self.stats[k] for k in ("prefill_steps", "decode_steps", "mixed_steps"))
+        TRACE.mark(f"step {nstep} kind={plan.kind} seqs={len(ids)} rows={len(plan.tokens)} begin")
         if plan.kind == 3:
             logits = self._run_mixed(plan)
             npf = plan.n_prefill
@@ -192,6 +200,7 @@ class LLMEngine:
         toks_dev = self._sample(ids, logits)
         lps = self._logprobs(ids, logits, toks_dev)
         toks = toks_dev.cpu().numpy().astype(np.int32)
+        TRACE.mark(f"step {nstep} end")
         eos = np.zeros(len(ids), dtype=np.uint8)
         now = time.perf_counter()
         for j, rid in enumerate(ids):
@@ -227,6 +236,42 @@ class LLMEngine:
         while self.has_work():
             self.step()
         return [self.requests.pop(r) for r in rids]
+
+    # -------------------------------------------------------------- checks
+    def _check_plan(self, plan) -> None:
+        """Every index a step's kernels turn into an address, checked on the host
+        before it reaches the GPU (microseconds of numpy per step): token ids
+        (embedding rows), positions (RoPE table rows), cache slots and block-table
+        pages (KV-cache pages) and context lengths. A scheduler bug then raises
+        here with the offending values instead of surfacing as an asynchronous
+        GPU memory fault with no kernel named."""
+        npg, maxpos = self.num_pages, self.cfg.max_model_len
+        bad = []
+
+        def rng(name, a, lo, hi):
+            a = np.asarray(a)
+            if a.size and (a.min() < lo or a.max() >= hi):
+                bad.append(f"{name} outside [{lo}, {hi}): min {a.min()} max {a.max()}")
+
+        rng("tokens", plan.tokens, 0, self.vocab)
+        rng("positions", plan.positions, 0, maxpos)
+        rng("slots", plan.slots, -1, npg * PAGE)
+        if plan.kind in (2, 3) and len(plan.ctx_lens):
+            bt = np.asarray(plan.block_tables)
+            ctx = np.asarray(plan.ctx_lens)
+            rng("block_tables", bt, 0, npg)
+            rng("ctx_lens", ctx, 1, bt.shape[1] * PAGE + 1)
+            if not bad and plan.kind == 2:
+                # decode: the new token's slot lies in the last page of its context
+                last = bt[np.arange(len(ctx)), (ctx - 1) // PAGE]
+                sl = np.asarray(plan.slots)
+                if np.any((sl >= 0) & (sl // PAGE != last)):
+                    bad.append("decode slot not in the last page of its context")
+        if plan.kind == 3 and plan.n_prefill:
+            rng("pf_block_tables", plan.pf_block_tables, 0, npg)
+        if bad:
+            raise RuntimeError(f"scheduler plan (kind {plan.kind}, {len(plan.seq_ids)} seqs) failed its checks: "
+                               + "; ".join(bad))
 
     # -------------------------------------------------------------- runners
     def _dev(self, a, dtype=torch.int32):

@@ -45,6 +45,7 @@ import torch
 from kgs.models.llama import LlamaConfig, LlamaModel, _rms_norm
 from kgs.ops import decode as D
 
+from .trace import TRACE as T
 
 
 class ServingModel:
@@ -266,17 +267,26 @@ class ServingModel:
             return self._prefill_fp8(tokens, positions, slots, seq_starts, seq_lens, padded_lens)
         x = self.embed[tokens.long()].reshape(-1, h).contiguous()
         y = self._norm(x, None, self.ln1[0])
+        T.op("prefill embed+norm")
         for i in range(c.layers):
             qkv = self._proj(y, i, "qkv", False)
+            T.op(f"prefill L{i} qkv")
             self._rope_cache(qkv, i, positions, slots)
+            T.op(f"prefill L{i} rope_cache")
             a = self._prefill_attention(qkv, seq_starts, seq_lens, padded_lens)
+            T.op(f"prefill L{i} attention")
             y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
+            T.op(f"prefill L{i} o+norm")
             act = self._gate_up_act(y, i)
+            T.op(f"prefill L{i} gate_up")
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             y = self._norm(x, self._proj(act, i, "down", False), nxt)
+            T.op(f"prefill L{i} down+norm")
         last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
         yl = y[last].contiguous()
-        return self._proj(yl, None, "lm", True)
+        out = self._proj(yl, None, "lm", True)
+        T.op("prefill lm_head")
+        return out
 
     def _prefill_fp8(self, tokens, positions, slots, seq_starts, seq_lens, padded_lens) -> torch.Tensor:
         """W8A8 prompt pass: every GEMM input is e4m3 rows with per-row scales from
@@ -456,14 +466,17 @@ class ServingModel:
                 a = D.rope_paged_decode_attention(part, self.cos, self.sin, positions, slots, self.cache.layer(i),
                                                   block_tables, ctx_lens, c.heads, c.kv_heads,
                                                   pages_per_split=pages_per_split)
+                T.op(f"decode L{i} qkv+rope+attention")
             elif rq:
                 part = gemm_nt_w4x_partials(y, self._w4x_weight(i, "qkv", rq[0]), *rq, nt_weights=D.w4x_nt(rq))
                 qkv = torch.empty((m, part.shape[2]), dtype=torch.bfloat16, device=x.device)
                 D.rope_cache_(qkv, self.cos, self.sin, positions, slots, self.cache.layer(i), c.heads, c.kv_heads,
                               partials=part)
+                T.op(f"decode L{i} qkv+rope_cache")
             else:
                 qkv = self._proj(y, i, "qkv", True)
                 self._rope_cache(qkv, i, positions, slots)
+                T.op(f"decode L{i} qkv+rope_cache")
             if fused_attn:
                 pass
             elif self.backend == "ref":
@@ -472,23 +485,29 @@ class ServingModel:
             else:
                 a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                              pages_per_split=pages_per_split)
+                T.op(f"decode L{i} attention")
             if ro:
                 y = splitk_add_rmsnorm(gemm_nt_w4x_partials(a, self._w4x_weight(i, "o", ro[0]), *ro,
                                                             nt_weights=D.w4x_nt(ro)), x, self.ln2[i], c.eps)
             else:
                 y = self._norm(x, self._proj(a, i, "o", True), self.ln2[i])
+            T.op(f"decode L{i} o+norm")
             if rg:
                 act = gemm_nt_w4x_swiglu(y, self._gate_up_weight(i, rg[0]), bn=rg[0], bm=rg[2],
                                          stages=D.w4x_stages(rg), nt_weights=D.w4x_nt(rg))
             else:
                 act = self._silu_mul(self._proj(y, i, "gate_up", True))
+            T.op(f"decode L{i} gate_up")
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
             if rd:
                 y = splitk_add_rmsnorm(gemm_nt_w4x_partials(act, self._w4x_weight(i, "down", rd[0]), *rd,
                                                             nt_weights=D.w4x_nt(rd)), x, nxt, c.eps)
             else:
                 y = self._norm(x, self._proj(act, i, "down", True), nxt)
-        return self._proj(y, None, "lm", True)
+            T.op(f"decode L{i} down+norm")
+        out = self._proj(y, None, "lm", True)
+        T.op("decode lm_head")
+        return out
 
     def _decode_fused(self, tokens, positions, slots, block_tables, ctx_lens, pages_per_split):
         """Decode with every norm / SwiGLU / residual add inside the skinny GEMMs:
@@ -509,9 +528,14 @@ class ServingModel:
             else:
                 qkv = D.skinny_gemm(x, P["qkv"], rms=ss_b, eps=eps)
                 self._rope_cache(qkv, i, positions, slots)
+            T.op(f"decode-fused L{i} qkv+rope")
             a = D.paged_decode_attention(qkv, self.cache.layer(i), block_tables, ctx_lens, c.heads, c.kv_heads,
                                          pages_per_split=pages_per_split)
+            T.op(f"decode-fused L{i} attention")
             D.skinny_gemm(a, P["o"], out=x, resid_ss=ss_a, zero=ss_b)
             act = D.skinny_gemm(x, P["gate_up"], rms=ss_a, eps=eps)
             D.skinny_gemm(act, P["down"], out=x, resid_ss=ss_b, zero=ss_a)
-        return D.skinny_gemm(x, self.packed_lm, rms=ss_b, eps=eps)
+            T.op(f"decode-fused L{i} o+mlp")
+        out = D.skinny_gemm(x, self.packed_lm, rms=ss_b, eps=eps)
+        T.op("decode-fused lm_head")
+        return out

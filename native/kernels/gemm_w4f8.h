@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       fstep<1, X, false, 0, KN>(c, c, f, k + 3, tq);
     }
     const int tnx = nwx + __builtin_amdgcn_readfirstlane(tslot);
-    const bool more = tnx < ntx;
+    const bool more = (unsigned)tnx < (unsigned)ntx;  // a ticket outside [0, ntx) never becomes a tile index
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(x + 8 * tnx, ntiles, ntm, ntn, sl, tmn, tnn);
     Ctx cn = c;

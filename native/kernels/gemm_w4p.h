@@ -346,7 +346,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   } else {
     t = DYN ? (int)blockIdx.x >> 3 : (int)blockIdx.x;
   }
-  if (t >= lim) {  // (DYN 2: queue empty when this workgroup started; DYN 0/1: never with grid <= tiles)
+  // unsigned: a ticket outside [0, lim) -- a corrupted slot -- ends the
+  // workgroup instead of becoming a tile index (no address from it, ever)
+  if ((unsigned)t >= (unsigned)lim) {  // (DYN 2: queue empty when this workgroup started; DYN 0/1: never with grid <= tiles)
     if (DYN && threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
       for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
     return;
@@ -393,7 +395,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       pstep<1, X, false, 0, L>(c, c, f0, f1, t + 3, tq);
     }
     const int tnx = DYN ? base + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
-    const bool more = tnx < lim;
+    const bool more = (unsigned)tnx < (unsigned)lim;  // see the first ticket's check
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
     Ctx cn = c;

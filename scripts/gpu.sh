@@ -28,6 +28,8 @@
 #                gate|up kernel, default vs nt weight loads
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
 #   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
+#   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
+#   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
 #   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
@@ -139,6 +141,17 @@ step() {
             (export KGS_NT_WEIGHTS=1; run serve_nt1_trace 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$O/nt1_trace" -o d -- python3 -m kgs.serve bench --requests ${B:-256} --input-len 512 \
                 --output-len 256 --max-batch ${B:-256} --max-model-len 2048) ;;
+        uninit_probe)  # serving under two allocator fill patterns (bench/uninit_probe.py): must agree bitwise
+            (export KGS_STEP_TRACE="$O/steps_u0.log"; run uninit_0 300 python bench/uninit_probe.py --pattern 0 \
+                --out "$O/uninit_0.json") &&
+            (export KGS_STEP_TRACE="$O/steps_u400.log"; run uninit_400 300 python bench/uninit_probe.py \
+                --pattern 0x400 --out "$O/uninit_400.json") ;;
+        serve_rep)  # the batch-256 serving bench $N times back to back (default policy), step breadcrumbs on
+            local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256"
+            SB="$SB --max-batch 256 --max-model-len 2048"
+            for r in $(seq 1 ${N:-3}); do
+                (export KGS_STEP_TRACE="$O/steps_serve_$r.log"; run serve_rep_$r 300 $SB) || return 1
+            done ;;
         fp8_sweep) run fp8_sweep 600 python bench/gemm_sweep.py --dtype fp8 --data normal \
             --shapes ${SHAPES:-8192,16384x16384x8192,8192x28672x4096,8192x6144x4096,4096x8192x14336,8192x4096x14336} \
             --variants ${VARIANTS:-fast,w4p} --rounds 7 --out "$O/fp8_sweep.json" ;;

@@ -963,19 +963,31 @@ def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
 
     As, b = _queue_operands(1, seed=14)
     ref = gemm_nt(As[0], b, variant="w4_oneshot")
-    st = tile_queue_stats()
-    free = st["slots"] - st["stream_slots"] - st["capture_slots"]
     reserve = 64  # tile_queue.h TQ_RESERVE
-    fill = max(0, free - reserve)  # new streams that bring the pool down to its reserve
-    streams, destroy = _hip_streams(fill + 1)
-    try:
-        junk = torch.empty_like(ref)
-        for s in streams[:fill]:
+
+    def free():
+        st = tile_queue_stats()
+        return st["slots"] - st["stream_slots"] - st["capture_slots"]
+
+    # new streams (each taking one slot) until the pool is down to its reserve;
+    # HIP recycles destroyed stream handles, which keep their old slot, so count
+    # by the pool's own statistics, not by streams made
+    streams, destroys = [], []
+    junk = torch.empty_like(ref)
+    while free() > reserve and len(streams) < 1024:
+        more, d = _hip_streams(max(1, free() - reserve))
+        streams += more
+        destroys.append(d)
+        for s in more:
             with torch.cuda.stream(s):
                 gemm_nt(As[0], b, out=junk)
         torch.cuda.synchronize()
+    more, d = _hip_streams(1)
+    destroys.append(d)
+    streams += more
+    try:
         st0 = tile_queue_stats()
-        assert st0["slots"] == 0 or st0["slots"] - st0["stream_slots"] - st0["capture_slots"] <= reserve, st0
+        assert st0["slots"] == 0 or free() <= reserve, st0
         busy = streams[-1]
         out = torch.zeros_like(ref)
         torch.cuda.synchronize()
@@ -992,7 +1004,8 @@ def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
         assert torch.equal(out, ref)
     finally:
         torch.cuda.synchronize()
-        destroy()
+        for d in destroys:
+            d()
 
 
 @pytest.mark.parametrize("mode", [1, 2])

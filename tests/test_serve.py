@@ -770,3 +770,59 @@ def test_w4x_route_override_cpu():
     finally:
         D.W4X_TUNED.clear()
         D.W4X_TUNED.update(saved)
+
+
+def test_engine_checks_every_index_before_the_gpu_sees_it():
+    """A corrupted scheduler plan (out-of-range page, position, slot, token or
+    a decode slot outside its last page) raises on the host with the values,
+    instead of reaching a kernel as an address."""
+    import types
+
+    from kgs.serve import EngineConfig, LLMEngine
+
+    eng = LLMEngine(_tiny(), EngineConfig(num_pages=16, max_batch=4, max_model_len=256, cuda_graphs=False),
+                    device="cpu", backend="ref")
+
+    def plan(**kw):
+        p = dict(kind=2, seq_ids=np.arange(2), tokens=np.array([5, 6]), positions=np.array([40, 7]),
+                 slots=np.array([1 * 32 + 8, 3 * 32 + 7]), ctx_lens=np.array([41, 8]),
+                 block_tables=np.array([[2, 1], [3, 0]]), n_prefill=0)
+        p.update(kw)
+        return types.SimpleNamespace(**p)
+
+    eng._check_plan(plan())  # a consistent decode plan passes
+    for kw, msg in ((dict(block_tables=np.array([[2, 16], [3, 0]])), "block_tables outside [0, 16)"),
+                    (dict(positions=np.array([40, 256])), "positions outside"),
+                    (dict(slots=np.array([40, 16 * 32])), "slots outside"),
+                    (dict(tokens=np.array([5, 512])), "tokens outside"),
+                    (dict(ctx_lens=np.array([41, 0])), "ctx_lens outside"),
+                    (dict(slots=np.array([2 * 32 + 8, 3 * 32 + 7])), "not in the last page")):
+        with pytest.raises(RuntimeError, match=msg.replace("[", r"\[").replace("(", r"\(").replace(")", r"\)")):
+            eng._check_plan(plan(**kw))
+
+
+def test_step_trace_breadcrumbs(tmp_path):
+    """kgs.serve.trace: one begin / end line per engine step, unbuffered, and
+    an op line per op with KGS_SYNC_DEBUG (the first op without a line after a
+    GPU fault is the faulting one)."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+    from kgs.serve import trace
+
+    path = tmp_path / "steps.log"
+    t = trace.StepTrace(str(path))
+    old = trace.TRACE
+    import kgs.serve.engine as E
+
+    E.TRACE = t
+    try:
+        eng = LLMEngine(_tiny(), EngineConfig(num_pages=32, max_batch=4, max_model_len=256, cuda_graphs=False),
+                        device="cpu", backend="ref")
+        eng.generate([[5, 6, 7], [9, 10]], SamplingParams(max_tokens=3, ignore_eos=True))
+    finally:
+        E.TRACE = old
+    lines = path.read_text().splitlines()
+    begins = [ln for ln in lines if ln.endswith(" begin")]
+    ends = [ln for ln in lines if ln.endswith(" end")]
+    assert len(begins) == len(ends) == eng.stats["prefill_steps"] + eng.stats["decode_steps"] >= 3
+    assert "kind=1" in begins[0] and "kind=2" in begins[-1]
+    assert not trace.StepTrace(None).on and not trace.StepTrace(None, sync_ops=True).sync_ops
