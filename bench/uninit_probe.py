@@ -96,7 +96,10 @@ def main(argv=None) -> int:
     # per-layer sums of the cache's 32-bit words (every page, used or not)
     sums = [int(cache[i].view(torch.int32).sum(dtype=torch.int64).item()) for i in range(cache.shape[0])]
     ck = hashlib.sha256(np.array(sums, dtype=np.int64).tobytes()).hexdigest()
-    res = {"pattern": hex(pattern), "fill": fill, "graphs": not a.no_graphs, "requests": a.requests,
+    from kgs.ops._lib import tile_queue_check
+
+    tq = tile_queue_check(0)
+    res = {"tile_queue": tq, "pattern": hex(pattern), "fill": fill, "graphs": not a.no_graphs, "requests": a.requests,
            "tokens_sha": hashlib.sha256(toks.tobytes()).hexdigest(), "logits_abs_sum": last.get("logits"),
            "logit_nans": last.get("nan"), "cache_sha": ck, "stats": dict(eng.stats),
            "seconds": round(time.perf_counter() - t0, 1)}

@@ -37,6 +37,7 @@ _c_long = ctypes.c_long
 _SIGS = {
     "kgs_gemm_bf16_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8 + [_c_void_p], _c_int),
     "kgs_tile_queue_stats": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
+    "kgs_tile_queue_check": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
     "kgs_gemm_bf16_nt_fast_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_bounded_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
@@ -165,3 +166,17 @@ def tile_queue_stats(device: int = 0) -> dict:
     out = (_c_long * 4)()
     check(lib().kgs_tile_queue_stats(int(device), out), "kgs_tile_queue_stats")
     return {"slots": out[0], "stream_slots": out[1], "capture_slots": out[2], "fallbacks": out[3]}
+
+
+def tile_queue_check(device: int = 0) -> dict:
+    """The ticket-slot pool's quiescent invariant (tile_queue.h): with no
+    persistent GEMM in flight every word of every slot is zero. Synchronises
+    the device first. ``dirty_slots`` > 0 means a launch left its tickets
+    behind or something wrote into the pool (the next eager launch on that
+    slot would take wrong tickets)."""
+    import torch
+
+    torch.cuda.synchronize(device)
+    out = (_c_long * 4)()
+    check(lib().kgs_tile_queue_check(int(device), out), "kgs_tile_queue_check")
+    return {"dirty_slots": out[0], "dirty_words": out[1], "first_value": out[2], "first_word": out[3]}

@@ -68,6 +68,9 @@ def run_engine(a) -> dict:
     dt = time.perf_counter() - t0
     n_out = sum(len(r.output) for r in outs)
     n_in = a.requests * a.input_len
+    from kgs.ops._lib import tile_queue_check
+
+    tq = tile_queue_check(0)  # the persistent GEMMs' ticket pool must be all zero again
     ttft = sorted(r.t_first - r.t_arrival for r in outs)
     tpot = sorted((r.t_done - r.t_first) / max(1, len(r.output) - 1) for r in outs)
     return {
@@ -84,6 +87,7 @@ def run_engine(a) -> dict:
         "total_tok_per_s": round((n_out + n_in) / dt, 1), "requests_per_s": round(a.requests / dt, 3),
         "ttft_p50_ms": round(1e3 * ttft[len(ttft) // 2], 1), "tpot_p50_ms": round(1e3 * tpot[len(tpot) // 2], 2),
         "load_s": round(t_load, 1), "warmup_s": round(t_warm, 1), "stats": dict(eng.stats),
+        "tile_queue_dirty_slots": tq["dirty_slots"],
     }
 
 

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -118,6 +119,8 @@ class LLMEngine:
         self.use_graphs = cfg.cuda_graphs and self.device.type == "cuda" and backend == "kgs" and not TRACE.sync_ops
         self.vocab = model_cfg.vocab
         self.validate = True  # host-side range checks of every step's device inputs (_check_plan)
+        # KGS_TQ_CHECK=1: the persistent GEMMs' ticket pool checked after every step (kgs.ops._lib.tile_queue_check)
+        self.tq_check = os.environ.get("KGS_TQ_CHECK", "0") == "1" and self.device.type == "cuda"
         self._want_lp: set = set()
         self._want_pen: set = set()
         self._seeded: set = set()
@@ -201,6 +204,13 @@ class LLMEngine:
         lps = self._logprobs(ids, logits, toks_dev)
         toks = toks_dev.cpu().numpy().astype(np.int32)
         TRACE.mark(f"step {nstep} end")
+        if self.tq_check:
+            from kgs.ops._lib import tile_queue_check
+
+            tq = tile_queue_check(self.device.index or 0)
+            if tq["dirty_slots"]:
+                TRACE.mark(f"step {nstep} tile queue dirty {tq}")
+                raise RuntimeError(f"step {nstep} (kind {plan.kind}): persistent-GEMM ticket pool not clean: {tq}")
         eos = np.zeros(len(ids), dtype=np.uint8)
         now = time.perf_counter()
         for j, rid in enumerate(ids):

@@ -228,6 +228,10 @@ KGS_EXPORT int kgs_tile_queue_stats(int dev, long* out) {
   return 0;
 }
 
+// The quiescent-pool invariant (tile_queue.h tile_queue_check): out = {dirty
+// slots, dirty words, first dirty value, its word index}. No GEMM may be in flight.
+KGS_EXPORT int kgs_tile_queue_check(int dev, long* out) { return kgs::tile_queue_check(dev, out); }
+
 // Can the 256x256 pipelined kernel take this problem?
 KGS_EXPORT int kgs_gemm_bf16_nt_fast_ok(const void* A, const void* B, const void* C, int M, int N, int K, int lda,
                                         int ldb, int ldc) {

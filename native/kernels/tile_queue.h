@@ -72,6 +72,7 @@ struct OwnerHash {
 };
 
 struct DevicePool {
+  std::vector<int*> chunks;  // every allocation, for tile_queue_check
   std::vector<int*> free_slots;
   std::unordered_map<OwnerKey, int*, OwnerHash> owners;
   hipStream_t zero_stream = nullptr;  // private, non-blocking; touched only by the growing thread
@@ -122,6 +123,7 @@ inline bool grow(DevicePool& P, int dev, std::unique_lock<std::mutex>& lock) {
   P.growing = false;
   if (!p) return false;
   for (int i = TQ_CHUNK - 1; i >= 0; --i) P.free_slots.push_back(p + i * TQ_INTS);
+  P.chunks.push_back(p);
   P.slots += TQ_CHUNK;
   return true;
 }
@@ -169,6 +171,44 @@ inline int* tile_queue(hipStream_t stream) {
   P.free_slots.pop_back();
   P.owners.emplace(key, s);
   return s;
+}
+
+// The pool invariant, checked from the host: with no persistent GEMM running on
+// device `dev`, every int of every slot is zero -- tickets and exit counter
+// (each launch's last workgroup resets them) and the padding (nothing writes
+// it). A nonzero word means a launch did not finish its reset or something
+// wrote into the pool; the next eager launch on that slot would take wrong
+// tickets. Copies the pool to the host (synchronous): the caller makes sure no
+// GEMM is in flight. out = {dirty slots, dirty words, first dirty value, its
+// word index in the pool}; returns 0 or a hipError_t.
+inline int tile_queue_check(int dev, long* out) {
+  using namespace tq_detail;
+  out[0] = out[1] = out[2] = 0;
+  out[3] = -1;
+  if (dev < 0 || dev >= TQ_DEVICES) return 0;
+  std::lock_guard<std::mutex> lock(mu());
+  const DevicePool& P = pools()[dev];
+  std::vector<int> h(TQ_INTS * TQ_CHUNK);
+  long base = 0;
+  for (int* c : P.chunks) {
+    const hipError_t e = hipMemcpy(h.data(), c, sizeof(int) * h.size(), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return (int)e;
+    for (int sl = 0; sl < TQ_CHUNK; ++sl) {
+      bool dirty = false;
+      for (int i = 0; i < TQ_INTS; ++i) {
+        const int v = h[sl * TQ_INTS + i];
+        if (v == 0) continue;
+        dirty = true;
+        if (out[1]++ == 0) {
+          out[2] = v;
+          out[3] = base + sl * TQ_INTS + i;
+        }
+      }
+      out[0] += dirty;
+    }
+    base += TQ_INTS * TQ_CHUNK;
+  }
+  return 0;
 }
 
 inline TileQueueStats tile_queue_stats(int dev) {

@@ -150,7 +150,7 @@ step() {
             local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256"
             SB="$SB --max-batch 256 --max-model-len 2048"
             for r in $(seq 1 ${N:-3}); do
-                (export KGS_STEP_TRACE="$O/steps_serve_$r.log"; run serve_rep_$r 300 $SB) || return 1
+                (export KGS_STEP_TRACE="$O/steps_serve_$r.log" KGS_TQ_CHECK=1; run serve_rep_$r 300 $SB) || return 1
             done ;;
         fp8_sweep) run fp8_sweep 600 python bench/gemm_sweep.py --dtype fp8 --data normal \
             --shapes ${SHAPES:-8192,16384x16384x8192,8192x28672x4096,8192x6144x4096,4096x8192x14336,8192x4096x14336} \

@@ -92,6 +92,16 @@ int main() {
   fakehip::capturing()[S(5)] = true;
   CHECK(tile_queue(S(5)) != nullptr && tile_queue_stats(0).fallbacks == fb);
   fakehip::capturing()[S(5)] = false;
+  // 9. the quiescent-pool invariant: all zero; a stray word anywhere (here the
+  // padding of a stream's slot) is found, with its value
+  long chk[4];
+  CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 0 && chk[1] == 0 && chk[3] == -1);
+  int* victim = tile_queue(S(7));
+  victim[12] = -792735554;  // 0xd0bed0be
+  victim[3] = 5;
+  CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 1 && chk[1] == 2 && chk[2] == 5);
+  victim[12] = victim[3] = 0;
+  CHECK(tile_queue_check(0, chk) == 0 && chk[1] == 0);
   std::printf("tile_queue host test: OK (%ld slots on device 0)\n", tile_queue_stats(0).slots);
   return 0;
 }

@@ -1008,6 +1008,16 @@ def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
             d()
 
 
+def test_tile_queue_pool_is_clean_after_the_concurrency_tests():
+    """The pool's quiescent invariant (tile_queue.h tile_queue_check) after the
+    graph / multi-stream / busy-stream tests above: every ticket, exit counter
+    and padding word back at zero."""
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
+
+    assert tile_queue_stats()["slots"] > 0
+    assert tile_queue_check() == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1}
+
+
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("grid", [0, 224, 100])
 def test_persistent_first_ticket_modes_and_reserved_grids_are_exact(mode, grid):
