@@ -30,6 +30,7 @@
 #   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
 #   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
 #   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
+#   lib_ab       this tree's kernel library vs another build ($LIB_B), interleaved, five sweep shapes
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
 #   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
@@ -152,6 +153,9 @@ step() {
             for r in $(seq 1 ${N:-3}); do
                 (export KGS_STEP_TRACE="$O/steps_serve_$r.log" KGS_TQ_CHECK=1; run serve_rep_$r 300 $SB) || return 1
             done ;;
+        lib_ab)  # two builds of libkgs_kernels.so interleaved in one process ($LIB_B, default the pre-pack build)
+            run lib_ab 600 python bench/lib_ab.py --lib-b ${LIB_B:-gpurun_ab/prepack/libkgs_kernels.so} \
+                --out "$O/lib_ab.json" ;;
         fp8_sweep) run fp8_sweep 600 python bench/gemm_sweep.py --dtype fp8 --data normal \
             --shapes ${SHAPES:-8192,16384x16384x8192,8192x28672x4096,8192x6144x4096,4096x8192x14336,8192x4096x14336} \
             --variants ${VARIANTS:-fast,w4p} --rounds 7 --out "$O/fp8_sweep.json" ;;
