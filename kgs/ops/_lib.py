@@ -173,10 +173,33 @@ def tile_queue_check(device: int = 0) -> dict:
     persistent GEMM in flight every word of every slot is zero. Synchronises
     the device first. ``dirty_slots`` > 0 means a launch left its tickets
     behind or something wrote into the pool (the next eager launch on that
-    slot would take wrong tickets)."""
+    slot would take wrong tickets); ``slot_addr`` / ``words`` are the first
+    dirty slot's device address and its 16 words."""
     import torch
 
     torch.cuda.synchronize(device)
-    out = (_c_long * 4)()
+    out = (_c_long * 21)()
     check(lib().kgs_tile_queue_check(int(device), out), "kgs_tile_queue_check")
-    return {"dirty_slots": out[0], "dirty_words": out[1], "first_value": out[2], "first_word": out[3]}
+    r = {"dirty_slots": out[0], "dirty_words": out[1], "first_value": out[2], "first_word": out[3]}
+    if out[0]:
+        r["slot_addr"] = hex(out[4])
+        r["words"] = [f"{w & 0xffffffff:08x}" for w in out[5:21]]
+    return r
+
+
+def neighbours(addr: int, device: int = 0, span: int = 256 << 20) -> list:
+    """The caching allocator's segments (and their last active blocks) within
+    ``span`` bytes of a device address: what sits next to a corrupted word."""
+    import torch
+
+    out = []
+    for seg in torch.cuda.memory_snapshot():
+        if seg.get("device", 0) != device:
+            continue
+        lo, size = seg["address"], seg["total_size"]
+        if lo - span <= addr <= lo + size + span:
+            blocks = [(hex(b["address"]), b["size"], b["state"]) for b in seg.get("blocks", [])
+                      if b["state"] == "active_allocated"]
+            out.append({"segment": hex(lo), "end": hex(lo + size), "bytes_to_addr": addr - (lo + size),
+                        "pool": seg.get("segment_pool_id"), "stream": seg.get("stream"), "blocks": blocks[-4:]})
+    return sorted(out, key=lambda d: abs(d["bytes_to_addr"]))[:6]

@@ -209,8 +209,12 @@ class LLMEngine:
 
             tq = tile_queue_check(self.device.index or 0)
             if tq["dirty_slots"]:
-                TRACE.mark(f"step {nstep} tile queue dirty {tq}")
-                raise RuntimeError(f"step {nstep} (kind {plan.kind}): persistent-GEMM ticket pool not clean: {tq}")
+                from kgs.ops._lib import neighbours
+
+                near = neighbours(int(tq["slot_addr"], 16), self.device.index or 0)
+                TRACE.mark(f"step {nstep} tile queue dirty {tq} near {near}")
+                raise RuntimeError(f"step {nstep} (kind {plan.kind}): persistent-GEMM ticket pool not clean: {tq}; "
+                                   f"nearest allocator segments: {near}")
         eos = np.zeros(len(ids), dtype=np.uint8)
         now = time.perf_counter()
         for j, rid in enumerate(ids):
@@ -366,6 +370,13 @@ class LLMEngine:
             for wb in widths or [w for w in (8, 16, 32, 64, 128, 256) if w <= maxw]:
                 if (bb, wb) not in self._graphs:
                     self._capture(bb, wb)
+        if self.tq_check:  # the captures' eager warm-up runs used the pool too
+            from kgs.ops._lib import tile_queue_check
+
+            tq = tile_queue_check(self.device.index or 0)
+            TRACE.mark(f"warmup captures done, tile queue {tq}")
+            if tq["dirty_slots"]:
+                raise RuntimeError(f"after the graph captures: persistent-GEMM ticket pool not clean: {tq}")
 
     # -------------------------------------------------------------- sampling
     def _logprobs(self, ids, logits: torch.Tensor, toks: torch.Tensor):

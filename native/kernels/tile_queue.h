@@ -179,11 +179,14 @@ inline int* tile_queue(hipStream_t stream) {
 // it). A nonzero word means a launch did not finish its reset or something
 // wrote into the pool; the next eager launch on that slot would take wrong
 // tickets. Copies the pool to the host (synchronous): the caller makes sure no
-// GEMM is in flight. out = {dirty slots, dirty words, first dirty value, its
-// word index in the pool}; returns 0 or a hipError_t.
+// GEMM is in flight. out[0..3] = {dirty slots, dirty words, first dirty value,
+// its word index in the pool}; out[4] = the first dirty slot's device address,
+// out[5..20] its 16 words (what overwrote it names the writer). Returns 0 or a
+// hipError_t.
+constexpr int TQ_CHECK_OUT = 5 + TQ_INTS;
 inline int tile_queue_check(int dev, long* out) {
   using namespace tq_detail;
-  out[0] = out[1] = out[2] = 0;
+  for (int i = 0; i < TQ_CHECK_OUT; ++i) out[i] = 0;
   out[3] = -1;
   if (dev < 0 || dev >= TQ_DEVICES) return 0;
   std::lock_guard<std::mutex> lock(mu());
@@ -202,6 +205,8 @@ inline int tile_queue_check(int dev, long* out) {
         if (out[1]++ == 0) {
           out[2] = v;
           out[3] = base + sl * TQ_INTS + i;
+          out[4] = (long)(uintptr_t)(c + sl * TQ_INTS);
+          for (int j = 0; j < TQ_INTS; ++j) out[5 + j] = h[sl * TQ_INTS + j];
         }
       }
       out[0] += dirty;

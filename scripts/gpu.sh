@@ -30,6 +30,7 @@
 #   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
 #   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
 #   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
+#   serve_tq     batch-256 serving, ticket pool checked after every step, with and without hipGraphs
 #   lib_ab       this tree's kernel library vs another build ($LIB_B), interleaved, five sweep shapes
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
@@ -153,6 +154,13 @@ step() {
             for r in $(seq 1 ${N:-3}); do
                 (export KGS_STEP_TRACE="$O/steps_serve_$r.log" KGS_TQ_CHECK=1; run serve_rep_$r 300 $SB) || return 1
             done ;;
+        serve_tq)  # batch-256 serving with the ticket pool checked after every step: graphs on, then off
+            local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 32"
+            SB="$SB --max-batch 256 --max-model-len 2048"
+            # a Python error (rc 1: the pool check raised) still runs the eager leg; a fault or kill does not
+            (export KGS_STEP_TRACE="$O/steps_tq_graphs.log" KGS_TQ_CHECK=1; run serve_tq_graphs 300 $SB)
+            [ $? -le 1 ] &&
+            (export KGS_STEP_TRACE="$O/steps_tq_eager.log" KGS_TQ_CHECK=1; run serve_tq_eager 300 $SB --no-graphs) ;;
         lib_ab)  # two builds of libkgs_kernels.so interleaved in one process ($LIB_B, default the pre-pack build)
             run lib_ab 600 python bench/lib_ab.py --lib-b ${LIB_B:-gpurun_ab/prepack/libkgs_kernels.so} \
                 --out "$O/lib_ab.json" ;;

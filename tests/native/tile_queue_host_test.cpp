@@ -94,12 +94,13 @@ int main() {
   fakehip::capturing()[S(5)] = false;
   // 9. the quiescent-pool invariant: all zero; a stray word anywhere (here the
   // padding of a stream's slot) is found, with its value
-  long chk[4];
+  long chk[TQ_CHECK_OUT];
   CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 0 && chk[1] == 0 && chk[3] == -1);
   int* victim = tile_queue(S(7));
   victim[12] = -792735554;  // 0xd0bed0be
   victim[3] = 5;
   CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 1 && chk[1] == 2 && chk[2] == 5);
+  CHECK(chk[4] == (long)(uintptr_t)victim && chk[5 + 3] == 5 && chk[5 + 12] == -792735554 && chk[5] == 0);
   victim[12] = victim[3] = 0;
   CHECK(tile_queue_check(0, chk) == 0 && chk[1] == 0);
   std::printf("tile_queue host test: OK (%ld slots on device 0)\n", tile_queue_stats(0).slots);

@@ -908,6 +908,14 @@ def test_two_persistent_graphs_from_one_capture_stream_replayed_concurrently():
             graphs[0].replay()
         torch.cuda.synchronize()
         assert torch.equal(outs[0], refs[0]), it
+    # the self-concurrent replays shared their capture slots, so those may be
+    # left with counts (tile_queue.h: the memset node in front of each captured
+    # launch is what makes every replay start from zero); one solo replay
+    # leaves them clean again (test_tile_queue_pool_is_clean_after_the_concurrency_tests)
+    with torch.cuda.stream(S1):
+        graphs[0].replay()
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], refs[0])
     # and an eager launch on each stream afterwards still starts from a zero queue
     for s in (S, S1, S2):
         with torch.cuda.stream(s):
@@ -1015,7 +1023,8 @@ def test_tile_queue_pool_is_clean_after_the_concurrency_tests():
     from kgs.ops._lib import tile_queue_check, tile_queue_stats
 
     assert tile_queue_stats()["slots"] > 0
-    assert tile_queue_check() == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1}
+    tq = tile_queue_check()
+    assert tq == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1}, tq
 
 
 @pytest.mark.parametrize("mode", [1, 2])
