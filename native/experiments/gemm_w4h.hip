@@ -6,6 +6,7 @@
 #include "gemm_w4f8.h"
 #include "gemm_w4p.h"
 #include "tile_queue.h"
+#include "tile_queue_zero.h"
 
 static int cu_count() {
   static int n = 0;

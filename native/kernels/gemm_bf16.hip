@@ -62,6 +62,7 @@
 #include "gemm_pipeline.h"
 #include "gemm_w4.h"
 #include "tile_queue.h"
+#include "tile_queue_zero.h"
 
 namespace kgs {
 

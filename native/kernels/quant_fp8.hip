@@ -80,6 +80,13 @@ __global__ __launch_bounds__(THREADS) void quantize_kernel(const void* __restric
   if (blockIdx.x == 0 && threadIdx.x == 0) out2[1] = scale;
 }
 
+// the amax accumulator's reset, as a kernel: inside a hipGraph capture a
+// hipMemsetAsync becomes a memset node, which on this ROCm wrote garbage instead
+// of zeros (tile_queue.h tq_zero_slot, profiles/r5/fault/README.md)
+__global__ __launch_bounds__(64) void zero_amax(unsigned* __restrict__ out2) {
+  if (threadIdx.x == 0) out2[0] = 0u;
+}
+
 }  // namespace q8
 }  // namespace kgs
 
@@ -92,8 +99,7 @@ KGS_EXPORT int kgs_quantize_fp8(const void* x, long n, int dtype, void* y, void*
   const long n8 = n / 8;
   long blocks = (n8 + kgs::q8::THREADS - 1) / kgs::q8::THREADS;
   const int grid = (int)(blocks < 2048 ? blocks : 2048);
-  hipError_t e = hipMemsetAsync(out2, 0, sizeof(float), s);
-  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(kgs::q8::zero_amax, dim3(1), dim3(64), 0, s, (unsigned*)out2);
   if (dtype == 1) {
     hipLaunchKernelGGL(kgs::q8::amax_kernel<true>, dim3(grid), dim3(kgs::q8::THREADS), 0, s, x, n8, (unsigned*)out2);
     hipLaunchKernelGGL(kgs::q8::quantize_kernel<true>, dim3(grid), dim3(kgs::q8::THREADS), 0, s, x, n8,

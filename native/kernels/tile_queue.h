@@ -16,8 +16,9 @@
 //    allocated before the capture and never given to anything else. A graph
 //    exec replayed on any stream, while eager GEMMs run on the capture stream or
 //    while another graph from the same stream replays, therefore uses its own
-//    counters. The capture also records a 64-byte memset of the slot in front
-//    of the kernel node, so every replay starts from zero whatever an earlier
+//    counters. The capture also records a zeroing kernel node for the slot
+//    (tq_zero_slot, not a memset node: see below) in front of the GEMM's node,
+//    so every replay starts from zero whatever an earlier
 //    replay left (one exec replayed concurrently with itself -- HIP does not
 //    document that it serialises those -- can then only compute a tile twice,
 //    with identical inputs and output, never skip one).
@@ -55,6 +56,16 @@ struct TileQueueStats {
   long capture_slots;  // owned by a captured launch
   long fallbacks;      // calls that returned nullptr
 };
+
+// Zero one 64-byte slot on `stream` with a KERNEL (tile_queue_zero.h; one
+// definition per library). In a hipGraph capture it becomes a kernel node like
+// every other node. A captured hipMemsetAsync -- a memset node -- did not
+// zero the slot on this ROCm: after the decode graph's first replay the slot
+// held 64 bytes of host-pointer-like words (0x00005639_00004020,
+// 0x000073fd_988f2020, ...), i.e. garbage tickets; with a word whose high bit
+// was set the persistent GEMM turned it into a negative tile index and the
+// serving run died with hipErrorIllegalAddress (profiles/r5/fault/README.md).
+hipError_t tq_zero_slot(int* slot, hipStream_t stream);
 
 namespace tq_detail {
 
@@ -142,7 +153,7 @@ inline int* tile_queue(hipStream_t stream) {
   if (capturing) {
     // no allocation or sync inside a capture: a reserved slot, or the one-shot grid
     int* s = P.free_slots.empty() ? nullptr : P.free_slots.back();
-    if (s == nullptr || hipMemsetAsync(s, 0, sizeof(int) * TQ_INTS, stream) != hipSuccess) {
+    if (s == nullptr || tq_zero_slot(s, stream) != hipSuccess) {
       ++P.fallbacks;
       if (!P.warned) {
         P.warned = true;

@@ -9,6 +9,12 @@
 
 #include "../../native/kernels/tile_queue.h"
 
+// the zeroing kernel of tile_queue_zero.h, on the host: recorded like a memset
+// (captured when the stream is capturing, applied otherwise)
+namespace kgs {
+hipError_t tq_zero_slot(int* slot, hipStream_t stream) { return hipMemsetAsync(slot, 0, sizeof(int) * TQ_INTS, stream); }
+}  // namespace kgs
+
 #define CHECK(c)                                                         \
   do {                                                                   \
     if (!(c)) {                                                          \

@@ -1016,6 +1016,40 @@ def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
             d()
 
 
+def test_captured_persistent_gemm_slot_is_zero_after_every_replay():
+    """Regression (round 5, profiles/r5/fault/README.md): a persistent GEMM
+    captured into a hipGraph zeroes its ticket slot in front of the GEMM node.
+    With a captured hipMemsetAsync (a memset node) the slot held 64 bytes of
+    host-pointer-like garbage after the serving decode graph's first replay --
+    garbage tickets, and with a negative one an illegal-address fault. The
+    zeroing is now a kernel node: after every replay the whole pool is zero
+    again and the product is bitwise the one-shot kernel's."""
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
+
+    As, b = _queue_operands(2, seed=21)
+    refs = [gemm_nt(a, b, variant="w4_oneshot") for a in As]
+    S = torch.cuda.Stream(device=DEV)
+    outs = [torch.empty_like(refs[0]) for _ in range(2)]
+    with torch.cuda.stream(S):
+        gemm_nt(As[0], b, out=outs[0])
+    torch.cuda.synchronize()
+    st0 = tile_queue_stats()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=S):
+        for i in range(2):
+            gemm_nt(As[i], b, out=outs[i])
+    assert tile_queue_stats()["capture_slots"] == st0["capture_slots"] + 2
+    assert tile_queue_check()["dirty_slots"] == 0
+    for it in range(8):
+        for o in outs:
+            o.zero_()
+        g.replay()  # on the current stream, alone: nothing shares its slots
+        tq = tile_queue_check()
+        assert tq["dirty_slots"] == 0, (it, tq)
+        assert torch.equal(outs[0], refs[0]) and torch.equal(outs[1], refs[1]), it
+
+
 def test_tile_queue_pool_is_clean_after_the_concurrency_tests():
     """The pool's quiescent invariant (tile_queue.h tile_queue_check) after the
     graph / multi-stream / busy-stream tests above: every ticket, exit counter
