@@ -31,6 +31,8 @@
 #   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
 #   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
 #   serve_tq     batch-256 serving, ticket pool checked after every step, with and without hipGraphs
+#   prefix_regress  the graph-replay regression test against gpurun_ab/prefix (the pre-fix library)
+#   overlap_rccl_ab persistent (static first ticket) vs one-shot grid against the RCCL-shaped CU hold
 #   lib_ab       this tree's kernel library vs another build ($LIB_B), interleaved, five sweep shapes
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
@@ -161,6 +163,13 @@ step() {
             (export KGS_STEP_TRACE="$O/steps_tq_graphs.log" KGS_TQ_CHECK=1; run serve_tq_graphs 300 $SB)
             [ $? -le 1 ] &&
             (export KGS_STEP_TRACE="$O/steps_tq_eager.log" KGS_TQ_CHECK=1; run serve_tq_eager 300 $SB --no-graphs) ;;
+        prefix_regress)  # the replay regression test against the pre-fix library (memset node): expected to fail
+            (export KGS_KERNELS_LIB=gpurun_ab/prefix/libkgs_kernels.so
+             run prefix_regress 300 python -u -m pytest tests/test_kernels_gpu.py -x -v -k captured_persistent \
+                --timeout 120 --timeout-method thread)
+            [ $? -le 1 ] ;;  # 1 = the test failed (the point); a fault / kill still stops the chain
+        overlap_rccl_ab) run overlap_rccl_ab 400 python bench/overlap_rccl.py --policies static,oneshot \
+            --out "$O/overlap_rccl_ab.json" ;;
         lib_ab)  # two builds of libkgs_kernels.so interleaved in one process ($LIB_B, default the pre-pack build)
             run lib_ab 600 python bench/lib_ab.py --lib-b ${LIB_B:-gpurun_ab/prepack/libkgs_kernels.so} \
                 --out "$O/lib_ab.json" ;;
