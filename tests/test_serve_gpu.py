@@ -302,3 +302,31 @@ def test_splitk_fused_decode_llama8b_layer(b):
         assert torch.equal(caches[0], caches[j]), j
         err = ((outs[0] - outs[j]).abs().max() / outs[0].abs().max()).item()
         assert err < 2e-2, (j, err)
+
+
+def test_batch256_graph_decode_equals_eager_with_the_persistent_lm_head():
+    """Regression (round 5, profiles/r5/fault/README.md): at batch 256 the
+    Llama-3 LM head (256 x 128256 x 4096, 501 tiles) runs on the persistent
+    GEMM inside the decode hipGraph. Its ticket slot was reset by a memset node
+    that left garbage behind, so graph-replayed steps could skip LM-head tiles
+    (or fault). Graph-replayed and eager decode must give the same tokens, and
+    the ticket pool must be clean afterwards."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.ops._lib import tile_queue_check
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=1, vocab=128256)
+    rng = np.random.default_rng(7)
+    prompts = [rng.integers(3, cfg.vocab, size=33).tolist() for _ in range(256)]
+    p = SamplingParams(max_tokens=5, ignore_eos=True)
+    toks = {}
+    for graphs in (False, True):
+        eng = LLMEngine(cfg, EngineConfig(num_pages=1024, max_batch=256, max_model_len=256, cuda_graphs=graphs),
+                        device="cuda", backend="kgs")
+        toks[graphs] = [r.output for r in eng.generate(prompts, p)]
+        assert eng.stats["decode_steps"] >= 4 and (eng.stats["graph_replays"] > 0) == graphs
+        tq = tile_queue_check()
+        assert tq["dirty_slots"] == 0, (graphs, tq)
+        del eng
+        torch.cuda.empty_cache()
+    assert toks[True] == toks[False]
