@@ -258,16 +258,17 @@ def w4x_stages(route) -> int:
     return route[3] if len(route) > 3 else 2
 
 
-# Decode weights are read once per step by one CU each: their loads can go
+# Decode weights are read once per step by one CU each: their loads go
 # non-temporal (gemm_w4.h AUX 52, B's loads only; the activations, re-read by
 # every workgroup from L2, keep the default policy). gate|up at batch 256:
 # 69.1 -> 68.0 us row-major, 67.5 -> 64.9 us tile-panel packed
-# (profiles/r4/decode/README.md). OPT-IN (KGS_NT_WEIGHTS=1): the first batch-256
-# serving run with it on ended in an illegal-address fault that a serialized
-# rerun (AMD_SERIALIZE_KERNEL=3) did not show and that is not explained yet
-# (the nt kernels differ from the default ones only in the nt bit of B's
-# buffer loads); until it is, serving keeps the default policy.
-NT_WEIGHTS = os.environ.get("KGS_NT_WEIGHTS", "0") == "1"
+# (profiles/r4/decode/README.md); batch-256 serving, two A/B/A passes on one
+# box: 18 247 -> 18 302 output tok/s (profiles/r5/decode/README.md). On by
+# default since round 5: the fault that kept it opt-in in round 4 was the
+# graph memset node of the persistent GEMM's ticket slot, not these loads
+# (profiles/r5/fault/README.md; the nt kernels differ from the default ones
+# only in the nt bit of B's buffer loads). KGS_NT_WEIGHTS=0 turns it off.
+NT_WEIGHTS = os.environ.get("KGS_NT_WEIGHTS", "1") == "1"
 
 
 def w4x_nt(route) -> bool:

@@ -46,7 +46,8 @@ def run_engine(a) -> dict:
                       decode_weights=a.decode_weights, kv_cache_dtype=a.kv_cache_dtype,
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
                       packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights,
-                      fuse_splitk=not a.no_fuse_splitk, w4x_panels=not a.no_w4x_panels)
+                      fuse_splitk=not a.no_fuse_splitk, w4x_panels=not a.no_w4x_panels,
+                      gate_up_panels=not a.no_gate_up_panels)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -69,6 +70,7 @@ def run_engine(a) -> dict:
     n_out = sum(len(r.output) for r in outs)
     n_in = a.requests * a.input_len
     from kgs.ops._lib import tile_queue_check
+    from kgs.ops.decode import NT_WEIGHTS
 
     tq = tile_queue_check(0)  # the persistent GEMMs' ticket pool must be all zero again
     ttft = sorted(r.t_first - r.t_arrival for r in outs)
@@ -80,6 +82,8 @@ def run_engine(a) -> dict:
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "kv_cache_dtype": a.kv_cache_dtype, "prefill_weights": a.prefill_weights,
         "fuse_splitk": not a.no_fuse_splitk, "w4x_panels": not a.no_w4x_panels,
+        "gate_up_panels": eng.model.gate_up_panels is not None,
+        "nt_weights": NT_WEIGHTS,
         "chunked_prefill": a.chunked_prefill,
         "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
         "prefix_hit_tokens": int(eng.sched.prefix_hit_tokens),
@@ -217,6 +221,8 @@ def main(argv=None) -> int:
                     help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
     ap.add_argument("--no-w4x-panels", action="store_true",
                     help="split-K decode projections read the row-major weights (A/B against the panel copies)")
+    ap.add_argument("--no-gate-up-panels", action="store_true",
+                    help="unsplit SwiGLU decode routes read the row-major gate|up (A/B against the panel copies)")
     ap.add_argument("--fused-max-batch", type=int, default=48,
                     help="decode batches up to this run the fused skinny-GEMM layer (0 = never)")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16",

@@ -25,7 +25,7 @@ import torch
 from kgs.models.llama import LlamaConfig
 from kgs.ops.decode import PAGE, PagedKVCache
 
-from .model import ServingModel
+from .model import ServingModel, gate_up_panel_widths
 from .trace import TRACE
 
 
@@ -79,6 +79,7 @@ class EngineConfig:
     prefill_weights: str = "bf16"     # "fp8": W8A8 prompt pass (e4m3 weight copies, per-row activation scales)
     fuse_splitk: bool = True          # split-K decode partials reduced inside RoPE/KV-write and add+RMSNorm
     w4x_panels: bool = True           # tile-panel copies of the split-K decode projections (qkv, o, down)
+    gate_up_panels: bool = True       # SwiGLU tile-panel copies of gate|up for the unsplit decode routes
     seed: int = 0
 
 
@@ -101,7 +102,8 @@ class LLMEngine:
                                   max_model_len=cfg.max_model_len, fused_max_batch=cfg.fused_max_batch,
                                   decode_weights=cfg.decode_weights, kv_cache_dtype=cfg.kv_cache_dtype,
                                   packed_decode=cfg.packed_decode, prefill_weights=cfg.prefill_weights,
-                                  fuse_splitk=cfg.fuse_splitk, w4x_panels=cfg.w4x_panels)
+                                  fuse_splitk=cfg.fuse_splitk, w4x_panels=cfg.w4x_panels,
+                                  gate_up_panels=cfg.gate_up_panels)
         sc = _serve.SchedulerConfig()
         sc.num_pages, sc.page_size, sc.max_batch = num_pages, PAGE, cfg.max_batch
         sc.max_prefill_tokens, sc.max_model_len, sc.pad_multiple = cfg.max_prefill_tokens, cfg.max_model_len, 128
@@ -138,6 +140,9 @@ class LLMEngine:
         resident = weights * (copies if self.backend == "kgs" else 1)
         if self.backend == "kgs" and self.cfg.packed_decode and self.cfg.fuse_splitk and self.cfg.w4x_panels:
             resident += 2 * mc.layers * (h * (h + 2 * kvd) + h * h + i * h)  # qkv / o / down panel copies
+        if (self.backend == "kgs" and self.cfg.packed_decode and self.cfg.fuse_splitk and self.cfg.gate_up_panels
+                and os.environ.get("KGS_GATEUP_PANELS", "1") == "1"):
+            resident += 2 * mc.layers * 2 * i * h * len(gate_up_panel_widths(2 * i, h))  # gate|up panel copies
         avail = max(0, (free - resident - (8 << 30)) * self.cfg.kv_fraction)
         return int(max(64, avail // PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, self.cfg.kv_cache_dtype)))
 

@@ -48,11 +48,18 @@ from kgs.ops import decode as D
 from .trace import TRACE as T
 
 
+def gate_up_panel_widths(n: int, k: int) -> set:
+    """Tile widths of the unsplit SwiGLU decode routes for a gate|up of shape
+    (n, k) (kgs.ops.decode.W4X_TUNED): one tile-panel copy is made per width."""
+    return {r[0] for (_, rn, rk), r in D.W4X_TUNED.items() if (rn, rk) == (n, k) and r[1] == 1}
+
+
 class ServingModel:
     def __init__(self, cfg: LlamaConfig, device="cuda", backend: str = "kgs", seed: int = 0,
                  num_pages: int = 1024, max_model_len: int = 8192, fused_max_batch: int = 48,
                  decode_weights: str = "bf16", kv_cache_dtype: str = "bf16", packed_decode: bool = True,
-                 prefill_weights: str = "bf16", fuse_splitk: bool = True, w4x_panels: bool = True):
+                 prefill_weights: str = "bf16", fuse_splitk: bool = True, w4x_panels: bool = True,
+                 gate_up_panels: bool = True):
         if cfg.head_dim != D.HEAD_DIM:
             raise ValueError(f"head_dim must be {D.HEAD_DIM}")
         self.cfg, self.backend, self.device = cfg, backend, torch.device(device)
@@ -113,16 +120,18 @@ class ServingModel:
             bns = {n: D.w4x_split_bns(*self.w[0][n].shape) for n in ("qkv", "o", "down")}
             self.w4x_panels = [{(n, bn): pack_w4x_weight(lw[n], bn) for n in bns for bn in bns[n]}
                                for lw in self.w]
-        # SwiGLU tile-panel copies of gate|up (235 MB per layer and tile width)
-        # for the unsplit decode routes: with non-temporal weight loads they
-        # read 4 % faster than row-major at batch 256 (64.9 vs 68.0 us,
-        # profiles/r4/decode/README.md). Opt-in: KGS_GATEUP_PANELS=1.
+        # SwiGLU tile-panel copies of gate|up (235 MB per layer and tile width,
+        # 15 GB for Llama-3-8B) for the unsplit decode routes: with non-temporal
+        # weight loads they read 4 % faster than row-major at batch 256 (64.9 vs
+        # 68.0 us, profiles/r4/decode/README.md); batch-256 serving 18 302 ->
+        # 18 442 output tok/s (profiles/r5/decode/README.md). Off:
+        # gate_up_panels=False or KGS_GATEUP_PANELS=0.
         self.gate_up_panels = None
-        if self.fuse_splitk and packed_decode and os.environ.get("KGS_GATEUP_PANELS", "0") == "1":
+        if (self.fuse_splitk and packed_decode and gate_up_panels
+                and os.environ.get("KGS_GATEUP_PANELS", "1") == "1"):
             from kgs.ops.gemm import pack_w4x_weight
 
-            gbns = {r[0] for (_, n, k), r in D.W4X_TUNED.items()
-                    if (n, k) == tuple(self.w[0]["gate_up"].shape) and r[1] == 1}
+            gbns = gate_up_panel_widths(*self.w[0]["gate_up"].shape)
             self.gate_up_panels = [{bn: pack_w4x_weight(lw["gate_up"], bn, swiglu=True) for bn in gbns}
                                    for lw in self.w]
         if prefill_weights not in ("bf16", "fp8"):

@@ -131,8 +131,8 @@ step() {
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
             SB="$SB --max-batch ${B:-256} --max-model-len 2048"
             for r in 1 2; do
-                (export KGS_NT_WEIGHTS=0; run serve_nt0_$r 300 $SB) &&
-                (export KGS_NT_WEIGHTS=1; run serve_nt1_$r 300 $SB) &&
+                (export KGS_NT_WEIGHTS=0 KGS_GATEUP_PANELS=0; run serve_nt0_$r 300 $SB) &&
+                (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=0; run serve_nt1_$r 300 $SB) &&
                 (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=1; run serve_nt1gp_$r 300 $SB) || return 1
             done ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,

@@ -826,3 +826,26 @@ def test_step_trace_breadcrumbs(tmp_path):
     assert len(begins) == len(ends) == eng.stats["prefill_steps"] + eng.stats["decode_steps"] >= 3
     assert "kind=1" in begins[0] and "kind=2" in begins[-1]
     assert not trace.StepTrace(None).on and not trace.StepTrace(None, sync_ops=True).sync_ops
+
+
+def test_kv_page_budget_counts_the_gate_up_panel_copies(monkeypatch):
+    """The SwiGLU gate|up panel copies (one per unsplit decode tile width: 128
+    and 256 for Llama-3-8B, 2 x 32 x 235 MB) come out of the KV-page budget:
+    with them on, the engine sizes 15 GB fewer pages than with them off."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.ops.decode import PagedKVCache
+    from kgs.serve import EngineConfig, LLMEngine
+    from kgs.serve.model import gate_up_panel_widths
+
+    mc = LlamaConfig.named("llama3-8b")
+    assert gate_up_panel_widths(2 * mc.intermediate, mc.hidden) == {128, 256}
+    monkeypatch.setattr(torch.cuda, "mem_get_info", lambda dev=None: (280 << 30, 288 << 30))
+    monkeypatch.delenv("KGS_GATEUP_PANELS", raising=False)
+    pages = {}
+    for on in (True, False):
+        eng = object.__new__(LLMEngine)
+        eng.device, eng.backend, eng.cfg = torch.device("cuda"), "kgs", EngineConfig(gate_up_panels=on)
+        pages[on] = eng._pages_from_memory(mc)
+    extra = 2 * mc.layers * 2 * mc.intermediate * mc.hidden * 2
+    per_page = PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, "bf16")
+    assert abs((pages[False] - pages[True]) - extra * EngineConfig().kv_fraction / per_page) <= 1

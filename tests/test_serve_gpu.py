@@ -330,3 +330,30 @@ def test_batch256_graph_decode_equals_eager_with_the_persistent_lm_head():
         del eng
         torch.cuda.empty_cache()
     assert toks[True] == toks[False]
+
+
+def test_nt_loads_and_gate_up_panels_keep_the_tokens(monkeypatch):
+    """Round 5 made non-temporal decode weight loads and the SwiGLU gate|up
+    tile-panel copies the default (profiles/r5/decode/README.md). Both only
+    change how the weights are read -- the nt bit and the weight layout, not the
+    K order of the sums -- so batch 128 and 256 decode (the unsplit SwiGLU routes
+    of width 128 and 256) must give the same tokens with either switched off."""
+    import kgs.ops.decode as D
+    from kgs.models.llama import LlamaConfig
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=2, vocab=32000)
+    rng = np.random.default_rng(11)
+    p = SamplingParams(max_tokens=4, ignore_eos=True)
+    for nb in (128, 256):
+        prompts = [rng.integers(3, cfg.vocab, size=21).tolist() for _ in range(nb)]
+        toks = {}
+        for nt, panels in ((True, True), (False, True), (True, False)):
+            monkeypatch.setattr(D, "NT_WEIGHTS", nt)
+            eng = LLMEngine(cfg, EngineConfig(num_pages=512, max_batch=nb, max_model_len=128, gate_up_panels=panels),
+                            device="cuda", backend="kgs")
+            assert (eng.model.gate_up_panels is not None) == panels
+            toks[nt, panels] = [r.output for r in eng.generate(prompts, p)]
+            del eng
+            torch.cuda.empty_cache()
+        assert toks[True, True] == toks[False, True] == toks[True, False], nb
