@@ -28,12 +28,20 @@ build is incremental (mtime based) and parallel; ``python -m kgs.utils.build``
 or ``__graft_entry__.build()`` drive it. No JIT cache is used, so the built
 ``.so`` files travel with the repo snapshot to the GPU box.
 
+Every build writes ``kgs/_native/build_manifest.json``: per target, the sha256
+of the output and of every source and header it was built from, the compiler
+line and the toolchain version. ``python -m kgs.utils.build --check`` (and
+``smoke()``) compare it against the tree: a library that no longer matches its
+sources, or a source edited after the last build, is reported by name.
+
 The reference has no native build at all; its only native components are Go
 device plugins cloned and built inside docker (kind-gpu-sim.sh:180-228).
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
+import hashlib
+import json
 import os
 import shutil
 import subprocess
@@ -48,6 +56,7 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = "gfx950"
 
 HIPCC = str(ROCM / "bin" / "hipcc")
+MANIFEST = "build_manifest.json"
 CXX = os.environ.get("CXX", "g++")
 
 HIP_FLAGS = [
@@ -291,7 +300,82 @@ def build_all(jobs: int | None = None, verbose: bool = True, only: list[str] | N
                     print(f"[kgs.build] optional target {t.name} skipped:\n{e}", file=sys.stderr)
             else:
                 raise
+    write_manifest(outdir if outdir is not None else OUT, sel, status)
     return status
+
+
+def _sha256(p: Path) -> str:
+    h = hashlib.sha256()
+    with open(p, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def _rel(p: Path) -> str:
+    try:
+        return str(Path(p).resolve().relative_to(REPO))
+    except ValueError:
+        return str(p)
+
+
+def _toolchain(compiler: str) -> str:
+    try:
+        r = subprocess.run([compiler, "--version"], capture_output=True, text=True, timeout=60)
+        return " | ".join(line for line in r.stdout.splitlines()[:2] if line)
+    except (OSError, subprocess.SubprocessError):
+        return "unknown"
+
+
+def _record(t: Target) -> dict:
+    return {"output": _rel(t.output), "output_sha256": _sha256(t.output),
+            "inputs": {_rel(p): _sha256(p) for p in [*t.sources, *t.headers] if p.exists()},
+            "compile": [Path(t.compiler).name, *t.flags], "link": t.link_flags,
+            "toolchain": _toolchain(t.compiler)}
+
+
+def write_manifest(outdir: Path, sel: list[Target], status: dict[str, str]) -> Path:
+    """Merge the records of the targets built or found fresh into the manifest."""
+    path = outdir / MANIFEST
+    try:
+        man = json.loads(path.read_text())
+    except (OSError, ValueError):
+        man = {}
+    man.setdefault("targets", {})
+    man["arch"], man["mode"] = ARCH, "in-tree (kgs.utils.build), no JIT cache"
+    for t in sel:
+        if t.output.exists() and not status.get(t.name, "").startswith("skipped"):
+            man["targets"][t.name] = _record(t)
+    path.parent.mkdir(parents=True, exist_ok=True)
+    tmp = path.with_name(path.name + ".tmp")
+    tmp.write_text(json.dumps(man, indent=1, sort_keys=True) + "\n")
+    os.replace(tmp, path)
+    return path
+
+
+def check_manifest(out: str | os.PathLike | None = None) -> dict:
+    """Compare the manifest against the tree. Returns {"ok", "targets": {name:
+    "ok" | why}}: a target is not ok when its output is missing or differs from
+    the recorded hash (rebuilt or replaced since), or when one of its inputs
+    changed (the library predates the source)."""
+    outdir = Path(out) if out is not None else OUT
+    try:
+        man = json.loads((outdir / MANIFEST).read_text())
+    except (OSError, ValueError) as e:
+        return {"ok": False, "error": f"no manifest: {e}", "targets": {}}
+    res: dict[str, str] = {}
+    for name, rec in man.get("targets", {}).items():
+        outp = REPO / rec["output"] if not Path(rec["output"]).is_absolute() else Path(rec["output"])
+        if not outp.exists():
+            res[name] = "output missing"
+            continue
+        if _sha256(outp) != rec["output_sha256"]:
+            res[name] = "output differs from the recorded build"
+            continue
+        changed = [k for k, v in rec["inputs"].items()
+                   if not (REPO / k).exists() or _sha256(REPO / k) != v]
+        res[name] = f"inputs changed since the build: {changed}" if changed else "ok"
+    return {"ok": bool(res) and all(v == "ok" for v in res.values()), "targets": res}
 
 
 def clean() -> None:
@@ -314,7 +398,13 @@ def main(argv: list[str] | None = None) -> int:
     ap.add_argument("--out", default=None, help="output directory (default kgs/_native)")
     ap.add_argument("--require-amdsmi", action="store_true",
                     help="fail unless the amd-smi header is found (device-plugin image)")
+    ap.add_argument("--check", action="store_true",
+                    help="build nothing: compare the build manifest against the tree (exit 1 if stale)")
     a = ap.parse_args(argv)
+    if a.check:
+        res = check_manifest(a.out)
+        print(json.dumps(res, indent=1))
+        return 0 if res["ok"] else 1
     if a.clean:
         clean()
     st = build_all(jobs=a.jobs, only=a.only, out=a.out, require_amdsmi=a.require_amdsmi)

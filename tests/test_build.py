@@ -66,3 +66,40 @@ def test_kernel_dir_holds_only_production_sources():
     assert headers <= reached, sorted(headers - reached)
     gens = {p.name for p in kdir.glob("gen_*.py")}
     assert gens == {"gen_acc_regs.py"}, gens  # acc_regs.h's generator (the persistent GEMM's AGPR map)
+
+
+def test_build_manifest_matches_the_tree():
+    """Every build records what each library was built from
+    (``kgs/_native/build_manifest.json``); right after a build the check finds
+    every target's output and inputs unchanged, and the kernels record names
+    the persistent GEMM's headers and the gfx950-only compile line."""
+    import json
+
+    from kgs.utils.build import MANIFEST, check_manifest
+
+    res = check_manifest()
+    assert res["ok"], res
+    man = json.load(open(os.path.join(NATIVE, MANIFEST)))
+    k = man["targets"]["kernels"]
+    assert {"native/kernels/gemm_w4p.h", "native/kernels/tile_queue.h", "native/kernels/gemm_bf16.hip"} <= set(k["inputs"])
+    assert "--offload-arch=gfx950" in k["compile"] and man["arch"] == "gfx950"
+
+
+def test_manifest_check_names_a_stale_library(tmp_path):
+    """A source edited after the build, and a library replaced after it, are
+    both reported by target name."""
+    from pathlib import Path
+
+    from kgs.utils.build import CXX, Target, build_target, check_manifest, write_manifest
+
+    src = tmp_path / "one.cpp"
+    src.write_text("extern \"C\" int one() { return 1; }\n")
+    t = Target("one", tmp_path / "libone.so", [src], CXX, flags=["-O2", "-fPIC"])
+    assert build_target(t, jobs=1, objroot=tmp_path / "obj")
+    write_manifest(tmp_path, [t], {"one": "built"})
+    assert check_manifest(tmp_path) == {"ok": True, "targets": {"one": "ok"}}
+    src.write_text("extern \"C\" int one() { return 2; }\n")
+    r = check_manifest(tmp_path)
+    assert not r["ok"] and "inputs changed" in r["targets"]["one"] and str(src) in r["targets"]["one"]
+    Path(t.output).write_bytes(b"not the recorded library")
+    assert check_manifest(tmp_path)["targets"]["one"] == "output differs from the recorded build"
