@@ -47,7 +47,7 @@ def run_engine(a) -> dict:
                       chunked_prefill=a.chunked_prefill, prefix_caching=a.prefix_caching,
                       packed_decode=not a.no_packed_decode, prefill_weights=a.prefill_weights,
                       fuse_splitk=not a.no_fuse_splitk, w4x_panels=not a.no_w4x_panels,
-                      gate_up_panels=not a.no_gate_up_panels)
+                      gate_up_panels=not a.no_gate_up_panels, overlap=not a.no_overlap)
     t0 = time.perf_counter()
     eng = LLMEngine(mc, ec, device="cuda", backend="kgs")
     t_load = time.perf_counter() - t0
@@ -82,7 +82,7 @@ def run_engine(a) -> dict:
         "fused_max_batch": a.fused_max_batch, "decode_weights": a.decode_weights,
         "kv_cache_dtype": a.kv_cache_dtype, "prefill_weights": a.prefill_weights,
         "fuse_splitk": not a.no_fuse_splitk, "w4x_panels": not a.no_w4x_panels,
-        "gate_up_panels": eng.model.gate_up_panels is not None,
+        "gate_up_panels": eng.model.gate_up_panels is not None, "overlap": eng.overlap,
         "nt_weights": NT_WEIGHTS,
         "chunked_prefill": a.chunked_prefill,
         "prefix_caching": a.prefix_caching, "shared_prefix": a.shared_prefix,
@@ -119,6 +119,7 @@ def run_online(a, mc=None, device="cuda", backend="kgs") -> dict:
                       chunked_prefill=getattr(a, "chunked_prefill", 0),
                       prefix_caching=getattr(a, "prefix_caching", False),
                       packed_decode=not getattr(a, "no_packed_decode", False),
+                      overlap=not getattr(a, "no_overlap", False),
                       **({"num_pages": 256} if device == "cpu" else {}))
     eng = LLMEngine(mc, ec, device=device, backend=backend)
     if not a.no_graphs:
@@ -221,6 +222,8 @@ def main(argv=None) -> int:
                     help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
     ap.add_argument("--no-w4x-panels", action="store_true",
                     help="split-K decode projections read the row-major weights (A/B against the panel copies)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="one step at a time: read each step's tokens back before planning the next (A/B)")
     ap.add_argument("--no-gate-up-panels", action="store_true",
                     help="unsplit SwiGLU decode routes read the row-major gate|up (A/B against the panel copies)")
     ap.add_argument("--fused-max-batch", type=int, default=48,

@@ -80,6 +80,7 @@ class EngineConfig:
     fuse_splitk: bool = True          # split-K decode partials reduced inside RoPE/KV-write and add+RMSNorm
     w4x_panels: bool = True           # tile-panel copies of the split-K decode projections (qkv, o, down)
     gate_up_panels: bool = True       # SwiGLU tile-panel copies of gate|up for the unsplit decode routes
+    overlap: bool = True              # plan/launch step t+1 before step t's tokens are read back (LLMEngine.step)
     seed: int = 0
 
 
@@ -126,6 +127,16 @@ class LLMEngine:
         self._want_lp: set = set()
         self._want_pen: set = set()
         self._seeded: set = set()
+        self._watch_eos: set = set()  # requests whose tokens are checked for EOS / stop ids
+        # Overlapped steps: step t+1 is planned and launched while step t runs,
+        # and step t's tokens are read back after that (see step()). Mixed steps
+        # (chunked prefill, prefix caching) hash pages from token values, and the
+        # debug modes synchronise per step: those run one step at a time.
+        self.overlap = (cfg.overlap and cfg.chunked_prefill == 0 and not cfg.prefix_caching and not self.tq_check
+                        and not TRACE.sync_ops)
+        self._inflight: dict | None = None
+        self._pinned = None  # two host buffers the in-flight tokens are copied into, alternately
+        self._flip = 0
 
     def _pages_from_memory(self, mc: LlamaConfig) -> int:
         if self.device.type != "cuda":
@@ -162,25 +173,54 @@ class LLMEngine:
             self._want_pen.add(rid)
         if params.seed is not None:
             self._seeded.add(rid)
+        if not params.ignore_eos:
+            self._watch_eos.add(rid)
         return rid
 
     def abort(self, rid: int) -> None:
         self._want_lp.discard(rid)
         self._want_pen.discard(rid)
         self._seeded.discard(rid)
+        self._watch_eos.discard(rid)
         if self.sched.abort(rid):
             r = self.requests[rid]
             r.finished, r.finish_reason, r.t_done = True, "abort", time.perf_counter()
             self.sched.release(rid)
 
     def has_work(self) -> bool:
-        return self.sched.num_waiting + self.sched.num_running > 0
+        return self._inflight is not None or self.sched.num_waiting + self.sched.num_running > 0
+
+    def _overlap_now(self) -> bool:
+        """Whether the next step may be planned before the current one's tokens
+        are known: logprobs, penalties and seeded sampling read per-step host
+        state (the output so far, per-request generators), so a batch holding
+        any of them runs one step at a time."""
+        return self.overlap and not (self._want_lp or self._want_pen or self._seeded)
 
     def step(self) -> list[tuple[int, int, bool]]:
-        """Run one scheduler step; returns [(request id, new token, finished)]."""
+        """Run one scheduler step; returns [(request id, new token, finished)].
+
+        Overlapped (EngineConfig.overlap, the default): step t+1 is scheduled
+        and launched while step t still runs on the GPU, and step t's tokens
+        are read back only after that, so the host's share of a step (the
+        scheduler, the result loop, staging the next inputs: 2.9 % of a
+        batch-256 step, profiles/r5/decode/decode_step_period_b256_o128.txt)
+        hides behind the GPU's. The scheduler advances step t's sequences by a
+        pending token (Scheduler.update_pending); step t+1 takes their tokens
+        straight from step t's sampled tokens on the device, and the values are
+        written into the scheduler afterwards (fill_pending). A sequence that
+        stops on EOS is seen one step late: it is finished then, and the token
+        its extra step computed is dropped. Each call then returns the results
+        of the step launched by the call before."""
+        prev = self._inflight
+        if prev is not None and not self._overlap_now():
+            self._inflight = None
+            return self._complete(prev, advanced=None)
+        advanced = self.sched.update_pending(prev["ids"]) if prev is not None else None
         plan = self.sched.schedule()
         if plan.kind == 0:
-            return []
+            self._inflight = None
+            return self._complete(prev, advanced) if prev is not None else []
         self.stats["preemptions"] += len(plan.preempted)
         ids = plan.seq_ids
         if self.validate:
@@ -202,36 +242,98 @@ class LLMEngine:
             self.stats["prefill_steps"] += 1
             self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
         else:
-            logits = self._run_decode(plan)
+            logits = self._run_decode(plan, self._decode_tokens(plan, prev))
             self.stats["decode_steps"] += 1
             self.stats["decode_tokens"] += len(ids)
         toks_dev = self._sample(ids, logits)
+        if self._overlap_now() and plan.kind != 3:
+            self._inflight = self._launch_readback(ids, toks_dev, nstep)
+            return self._complete(prev, advanced) if prev is not None else []
         lps = self._logprobs(ids, logits, toks_dev)
         toks = toks_dev.cpu().numpy().astype(np.int32)
         TRACE.mark(f"step {nstep} end")
-        if self.tq_check:
-            from kgs.ops._lib import tile_queue_check
-
-            tq = tile_queue_check(self.device.index or 0)
-            if tq["dirty_slots"]:
-                from kgs.ops._lib import neighbours
-
-                near = neighbours(int(tq["slot_addr"], 16), self.device.index or 0)
-                TRACE.mark(f"step {nstep} tile queue dirty {tq} near {near}")
-                raise RuntimeError(f"step {nstep} (kind {plan.kind}): persistent-GEMM ticket pool not clean: {tq}; "
-                                   f"nearest allocator segments: {near}")
-        eos = np.zeros(len(ids), dtype=np.uint8)
-        now = time.perf_counter()
-        for j, rid in enumerate(ids):
-            r = self.requests[int(rid)]
-            t = int(toks[j])
-            if not r.params.ignore_eos and (t == self.cfg.eos_token_id or t in r.params.stop_token_ids):
-                eos[j] = 1
+        self._tq_check(nstep, plan.kind)
+        eos = self._eos_mask(ids, toks)
         done = set(int(d) for d in self.sched.update(ids, toks, eos))
+        return self._emit(ids, toks, eos, done, lps)
+
+    # ------------------------------------------------------- step helpers
+    def _launch_readback(self, ids, toks_dev: torch.Tensor, nstep: int) -> dict:
+        """Start the copy of an in-flight step's tokens to the host."""
+        cur = {"ids": ids, "dev": toks_dev, "nstep": nstep, "event": None}
+        if toks_dev.is_cuda:
+            if self._pinned is None:
+                self._pinned = [torch.empty(self.cfg.max_batch, dtype=torch.int64).pin_memory() for _ in range(2)]
+            buf = self._pinned[self._flip][:len(ids)]
+            self._flip ^= 1
+            buf.copy_(toks_dev, non_blocking=True)
+            cur["host"], cur["event"] = buf, torch.cuda.Event()
+            cur["event"].record()
+        else:
+            cur["host"] = toks_dev
+        return cur
+
+    def _complete(self, cur: dict, advanced) -> list[tuple[int, int, bool]]:
+        """Results of an in-flight step. ``advanced``: the ids update_pending
+        finished (the scheduler already moved past this step; its tokens are
+        filled in and EOS stops applied now), or None (a plain update)."""
+        if cur["event"] is not None:
+            cur["event"].synchronize()
+        ids = cur["ids"]
+        toks = cur["host"].numpy().astype(np.int32)
+        TRACE.mark(f"step {cur['nstep']} end")
+        self._tq_check(cur["nstep"], -1)
+        eos = self._eos_mask(ids, toks)
+        if advanced is None:
+            done = set(int(d) for d in self.sched.update(ids, toks, eos))
+        else:
+            self.sched.fill_pending(ids, toks)
+            done = set(int(d) for d in advanced)
+            for j in np.flatnonzero(eos):  # EOS seen one step late: the extra step's token is dropped
+                rid = int(ids[j])
+                if rid not in done and self.sched.abort(rid):
+                    done.add(rid)
+        return self._emit(ids, toks, eos, done, None)
+
+    def _decode_tokens(self, plan, prev) -> torch.Tensor | None:
+        """A decode plan's input tokens on the device when some are still
+        pending in the scheduler: those come from the in-flight step's sampled
+        tokens (same sequence, on the device), the rest from the plan."""
+        pend = plan.tokens == self.sched.PENDING
+        if prev is None or not pend.any():
+            return None
+        pids, sid = prev["ids"], plan.seq_ids
+        order = np.argsort(pids, kind="stable")
+        src = order[np.searchsorted(pids, sid, sorter=order).clip(0, len(pids) - 1)]
+        if not np.array_equal(pids[src][pend], sid[pend]):
+            raise RuntimeError("overlapped decode: a pending sequence was not in the previous step")
+        src = np.where(pend, src, -1)
+        dev = prev["dev"]
+        if pend.all() and np.array_equal(src, np.arange(len(src))):
+            return dev[:len(src)].to(torch.int32)  # steady state: same sequences, same order
+        s = self._dev(src, torch.int64)
+        return torch.where(s >= 0, dev.index_select(0, s.clamp(min=0)).to(torch.int32), self._dev(plan.tokens))
+
+    def _eos_mask(self, ids, toks) -> np.ndarray:
+        eos = np.zeros(len(ids), dtype=np.uint8)
+        if self._watch_eos:
+            for j, rid in enumerate(ids):
+                rid = int(rid)
+                if rid in self._watch_eos:
+                    p = self.requests[rid].params
+                    t = int(toks[j])
+                    if t == self.cfg.eos_token_id or t in p.stop_token_ids:
+                        eos[j] = 1
+        return eos
+
+    def _emit(self, ids, toks, eos, done: set, lps) -> list[tuple[int, int, bool]]:
+        now = time.perf_counter()
         out = []
         for j, rid in enumerate(ids):
             rid = int(rid)
-            r = self.requests[rid]
+            r = self.requests.get(rid)
+            if r is None or r.finished:  # aborted, or finished one step earlier (EOS seen late)
+                continue
             r.output.append(int(toks[j]))
             if lps is not None and j in lps:
                 r.logprobs.append(lps[j])
@@ -243,10 +345,25 @@ class LLMEngine:
                 self._want_lp.discard(rid)
                 self._want_pen.discard(rid)
                 self._seeded.discard(rid)
+                self._watch_eos.discard(rid)
                 r.finish_reason = "stop" if eos[j] else "length"
                 self.sched.release(rid)
             out.append((rid, int(toks[j]), fin))
         return out
+
+    def _tq_check(self, nstep: int, kind: int) -> None:
+        if not self.tq_check:
+            return
+        from kgs.ops._lib import tile_queue_check
+
+        tq = tile_queue_check(self.device.index or 0)
+        if tq["dirty_slots"]:
+            from kgs.ops._lib import neighbours
+
+            near = neighbours(int(tq["slot_addr"], 16), self.device.index or 0)
+            TRACE.mark(f"step {nstep} tile queue dirty {tq} near {near}")
+            raise RuntimeError(f"step {nstep} (kind {kind}): persistent-GEMM ticket pool not clean: {tq}; "
+                               f"nearest allocator segments: {near}")
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list[SamplingParams] | None = None
                  ) -> list[Request]:
@@ -272,7 +389,8 @@ class LLMEngine:
             if a.size and (a.min() < lo or a.max() >= hi):
                 bad.append(f"{name} outside [{lo}, {hi}): min {a.min()} max {a.max()}")
 
-        rng("tokens", plan.tokens, 0, self.vocab)
+        tok = np.asarray(plan.tokens)
+        rng("tokens", tok[tok != self.sched.PENDING], 0, self.vocab)  # pending: the device's own samples
         rng("positions", plan.positions, 0, maxpos)
         rng("slots", plan.slots, -1, npg * PAGE)
         if plan.kind in (2, 3) and len(plan.ctx_lens):
@@ -313,17 +431,21 @@ class LLMEngine:
                                 self._dev(plan.block_tables) if nd else None,
                                 self._dev(plan.ctx_lens) if nd else None)
 
-    def _run_decode(self, plan) -> torch.Tensor:
+    def _run_decode(self, plan, tokens: torch.Tensor | None = None) -> torch.Tensor:
+        """``tokens``: the input tokens on the device (overlapped steps), else the plan's."""
         b = len(plan.seq_ids)
         if not self.use_graphs:
-            return self.model.decode(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots),
+            return self.model.decode(tokens if tokens is not None else self._dev(plan.tokens),
+                                     self._dev(plan.positions), self._dev(plan.slots),
                                      self._dev(plan.block_tables), self._dev(plan.ctx_lens))
         bb = _bucket(b, self.cfg.max_batch)
         wb = _bucket(plan.max_pages, math.ceil(self.cfg.max_model_len / PAGE))
         g = self._graphs.get((bb, wb)) or self._capture(bb, wb)
         io = g["io"]
-        host = g["host"]
-        hn = g["host_np"]  # numpy views of the pinned staging buffers
+        # two sets of pinned staging buffers, alternately: with overlapped steps
+        # the host fills step t+1's while step t's copies may still be queued
+        host, hn = g["host"][g["flip"]], g["host_np"][g["flip"]]  # hn: numpy views of host
+        g["flip"] ^= 1
         hn["tokens"][:] = 0
         hn["tokens"][:b] = plan.tokens
         hn["positions"][:] = 0
@@ -336,6 +458,8 @@ class LLMEngine:
         hn["bt"][:b, :plan.max_pages] = plan.block_tables
         for k in host:
             io[k].copy_(host[k], non_blocking=True)
+        if tokens is not None:
+            io["tokens"][:b].copy_(tokens)
         g["graph"].replay()
         self.stats["graph_replays"] += 1
         return g["logits"][:b]
@@ -360,7 +484,9 @@ class LLMEngine:
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             logits = run()
-        g = {"graph": graph, "io": io, "host": host, "host_np": {k: v.numpy() for k, v in host.items()},
+        host2 = {k: v.clone().pin_memory() for k, v in host.items()}
+        g = {"graph": graph, "io": io, "host": [host, host2], "flip": 0,
+             "host_np": [{k: v.numpy() for k, v in h.items()} for h in (host, host2)],
              "logits": logits}
         self._graphs[(bb, wb)] = g
         self.stats["graph_captures"] += 1

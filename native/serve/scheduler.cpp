@@ -428,6 +428,24 @@ std::vector<int64_t> Scheduler::update(const std::vector<int64_t>& ids, const st
   return done;
 }
 
+std::vector<int64_t> Scheduler::update_pending(const std::vector<int64_t>& ids) {
+  return update(ids, std::vector<int32_t>(ids.size(), kPendingToken), {});
+}
+
+int Scheduler::fill_pending(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks) {
+  int n = 0;
+  for (size_t i = 0; i < ids.size() && i < toks.size(); ++i) {
+    auto it = seqs_.find(ids[i]);
+    if (it == seqs_.end()) continue;  // released meanwhile
+    std::vector<int32_t>& t = it->second.tokens;
+    if (!t.empty() && t.back() == kPendingToken) {
+      t.back() = toks[i];
+      ++n;
+    }
+  }
+  return n;
+}
+
 const Sequence* Scheduler::get(int64_t id) const {
   auto it = seqs_.find(id);
   return it == seqs_.end() ? nullptr : &it->second;

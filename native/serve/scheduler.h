@@ -127,6 +127,18 @@ class Scheduler {
   // finishes sequence i early. Returns the ids that finished.
   std::vector<int64_t> update(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks,
                               const std::vector<uint8_t>& eos);
+  // Two-phase update for an engine that plans step t+1 while step t still runs
+  // on the GPU (kgs/serve/engine.py, EngineConfig.overlap): update_pending()
+  // advances every sequence of step t by one PENDING token (kPendingToken:
+  // lengths, page needs and length stops as update() with no eos), so the next
+  // step can be scheduled before the sampled values are known; fill_pending()
+  // writes the values in once they are (a sequence's pending token is always
+  // its last one: nothing else appends between the two calls). A stop on EOS,
+  // seen one step late, goes through abort(). Returns the ids that finished /
+  // the number of tokens filled.
+  static constexpr int32_t kPendingToken = -1;
+  std::vector<int64_t> update_pending(const std::vector<int64_t>& ids);
+  int fill_pending(const std::vector<int64_t>& ids, const std::vector<int32_t>& toks);
   const Sequence* get(int64_t id) const;
   void release(int64_t id);  // drop a finished sequence's record
   int num_waiting() const { return (int)waiting_.size(); }

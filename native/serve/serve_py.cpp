@@ -88,6 +88,26 @@ PYBIND11_MODULE(_serve, m) {
             return arr(s.update(vi, vt, ve));
           },
           py::arg("ids"), py::arg("tokens"), py::arg("eos"))
+      .def("update_pending",
+           [](Scheduler& s, py::array_t<int64_t> ids) {
+             auto i = ids.unchecked<1>();
+             std::vector<int64_t> vi(i.shape(0));
+             for (py::ssize_t k = 0; k < i.shape(0); ++k) vi[k] = i(k);
+             return arr(s.update_pending(vi));
+           },
+           py::arg("ids"))
+      .def("fill_pending",
+           [](Scheduler& s, py::array_t<int64_t> ids, py::array_t<int32_t> toks) {
+             auto i = ids.unchecked<1>();
+             auto t = toks.unchecked<1>();
+             std::vector<int64_t> vi(i.shape(0));
+             std::vector<int32_t> vt(t.shape(0));
+             for (py::ssize_t k = 0; k < i.shape(0); ++k) vi[k] = i(k);
+             for (py::ssize_t k = 0; k < t.shape(0); ++k) vt[k] = t(k);
+             return s.fill_pending(vi, vt);
+           },
+           py::arg("ids"), py::arg("tokens"))
+      .def_property_readonly_static("PENDING", [](py::object) { return Scheduler::kPendingToken; })
       .def("tokens",
            [](const Scheduler& s, int64_t id) {
              const Sequence* q = s.get(id);

@@ -27,6 +27,7 @@
 #   gateup_pmc   counter passes (SQ waits, FETCH_SIZE, TCC hit/miss, TA/TCP/TD stalls) + trace of the batch-256
 #                gate|up kernel, default vs nt weight loads
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
+#   serve_overlap_ab  batch-$B serving, sequential vs overlapped engine steps, twice
 #   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
 #   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
 #   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
@@ -135,6 +136,13 @@ step() {
                 (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=0; run serve_nt1_$r 300 $SB) &&
                 (export KGS_NT_WEIGHTS=1 KGS_GATEUP_PANELS=1; run serve_nt1gp_$r 300 $SB) || return 1
             done ;;
+        serve_overlap_ab)  # batch-$B serving: one step at a time vs overlapped steps (EngineConfig.overlap), A B A B
+            local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
+            SB="$SB --max-batch ${B:-256} --max-model-len 2048"
+            for r in 1 2; do
+                run serve_seq_b${B:-256}_$r 300 $SB --no-overlap &&
+                run serve_ovl_b${B:-256}_$r 300 $SB || return 1
+            done ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
@@ -203,7 +211,7 @@ step() {
         serve_nofuse) run serve_nofuse 400 python -u -m kgs.serve bench --requests 256 --input-len 512 \
             --output-len 256 --max-batch 256 --max-model-len 2048 --no-fuse-splitk ;;
         decode_trace) run decode_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace" -o d \
-            -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 32 --max-batch 256 \
+            -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len ${OL:-32} --max-batch 256 \
             --max-model-len 2048 ;;
         decode_trace_b1) run decode_trace_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace1" \
             -o d -- python3 -m kgs.serve bench --requests 2 --input-len 512 --output-len 64 --max-batch 1 \

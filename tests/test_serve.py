@@ -849,3 +849,88 @@ def test_kv_page_budget_counts_the_gate_up_panel_copies(monkeypatch):
     extra = 2 * mc.layers * 2 * mc.intermediate * mc.hidden * 2
     per_page = PagedKVCache.bytes_per_page(mc.layers, mc.kv_heads, "bf16")
     assert abs((pages[False] - pages[True]) - extra * EngineConfig().kv_fraction / per_page) <= 1
+
+
+def test_scheduler_two_phase_update():
+    """update_pending advances a step's sequences by a pending token (length
+    stops apply at once), the next step is scheduled before the values are
+    known, and fill_pending writes them in; a late EOS goes through abort."""
+    from kgs._native import _serve
+
+    cfg = _serve.SchedulerConfig()
+    cfg.num_pages, cfg.page_size, cfg.max_batch, cfg.max_model_len, cfg.pad_multiple = 32, 32, 4, 256, 128
+    s = _serve.Scheduler(cfg)
+    P = _serve.Scheduler.PENDING
+    assert s.add(1, [5, 6, 7], 3) and s.add(2, [8, 9], 1)
+    p = s.schedule()
+    assert p.kind == 1 and list(p.seq_ids) == [1, 2]
+    done = s.update_pending(p.seq_ids)
+    assert list(done) == [2]  # max_tokens 1: finished by length before its token is known
+    p2 = s.schedule()  # planned while step 1's tokens are in flight
+    assert p2.kind == 2 and list(p2.seq_ids) == [1] and list(p2.tokens) == [P] and list(p2.positions) == [3]
+    assert s.fill_pending(p.seq_ids, np.array([40, 41], np.int32)) == 2
+    assert list(s.tokens(1)) == [5, 6, 7, 40] and list(s.tokens(2)) == [8, 9, 41]
+    s.release(2)
+    assert list(s.update_pending(p2.seq_ids)) == []
+    assert s.fill_pending(np.array([1, 2]), np.array([42, 0], np.int32)) == 1  # 2 is gone: skipped
+    assert s.abort(1)  # EOS seen one step late
+    assert s.schedule().kind == 0 and s.check_invariants() == ""
+
+
+@pytest.mark.parametrize("case", ["eos", "preempt", "admission"])
+def test_overlapped_steps_generate_what_sequential_steps_do(case):
+    """EngineConfig.overlap plans step t+1 before step t's tokens are read
+    back. With EOS stops (seen one step late), preemption + recompute, and more
+    requests than max_batch (prefill steps between decodes), every request's
+    tokens and finish reason equal those of one-step-at-a-time execution."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    rng = np.random.default_rng({"eos": 3, "preempt": 4, "admission": 5}[case])
+    kw = dict(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False)
+    if case == "preempt":
+        kw.update(num_pages=7, max_batch=3)
+    n = {"eos": 4, "preempt": 3, "admission": 9}[case]
+    prompts = [rng.integers(3, 512, size=int(rng.integers(5, 40))).tolist() for _ in range(n)]
+    params = [SamplingParams(max_tokens=int(rng.integers(2, 14)), ignore_eos=case != "eos") for _ in range(n)]
+    if case == "preempt":  # 5 usable pages for 3 sequences that grow across page boundaries
+        kw.update(num_pages=6)
+        prompts = [rng.integers(3, 512, size=m).tolist() for m in (30, 28, 31)]
+        params = [SamplingParams(max_tokens=m, ignore_eos=True) for m in (12, 9, 12)]
+    eos = -1
+    if case == "eos":  # an EOS id that some request samples early on
+        probe = LLMEngine(_tiny(), EngineConfig(**kw, overlap=False), device="cpu", backend="ref")
+        eos = probe.generate(prompts, [SamplingParams(max_tokens=14, ignore_eos=True)] * n)[1].output[2]
+    outs = {}
+    for ov in (False, True):
+        eng = LLMEngine(_tiny(), EngineConfig(**kw, overlap=ov, eos_token_id=eos), device="cpu", backend="ref")
+        assert eng.overlap == ov
+        outs[ov] = [(r.output, r.finish_reason) for r in eng.generate(prompts, params)]
+        assert eng.sched.check_invariants() == "" and not eng.has_work()
+        if case == "preempt":
+            assert eng.stats["preemptions"] >= 1
+    assert outs[True] == outs[False]
+    if case == "eos":
+        assert any(f == "stop" for _, f in outs[True])
+
+
+def test_overlap_falls_back_for_host_state_sampling():
+    """Logprobs, penalties and seeded sampling read per-step host state: a
+    batch holding one runs one step at a time (the in-flight step is drained
+    first), and its results equal a sequential engine's."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    kw = dict(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False)
+    prompts = [[5, 6, 7], [8, 9, 10, 11]]
+    ps = [SamplingParams(max_tokens=6, ignore_eos=True),
+          SamplingParams(max_tokens=6, ignore_eos=True, logprobs=2, frequency_penalty=0.5)]
+    res = {}
+    for ov in (False, True):
+        eng = LLMEngine(_tiny(), EngineConfig(**kw, overlap=ov), device="cpu", backend="ref")
+        rid0 = eng.add_request(prompts[0], ps[0])
+        eng.step()
+        eng.step()  # overlapped: one step in flight
+        rid1 = eng.add_request(prompts[1], ps[1])
+        while eng.has_work():
+            eng.step()
+        res[ov] = [(eng.requests[r].output, len(eng.requests[r].logprobs)) for r in (rid0, rid1)]
+    assert res[True] == res[False] and res[True][1][1] == 6

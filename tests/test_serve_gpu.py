@@ -357,3 +357,32 @@ def test_nt_loads_and_gate_up_panels_keep_the_tokens(monkeypatch):
             del eng
             torch.cuda.empty_cache()
         assert toks[True, True] == toks[False, True] == toks[True, False], nb
+
+
+def test_overlapped_steps_equal_sequential_steps_on_graphs():
+    """EngineConfig.overlap on the kgs backend with hipGraph decode at batch
+    256 (the serving bench's shape, one layer): step t+1 is replayed with its
+    input tokens gathered on the device from step t's samples, before the host
+    reads them. Tokens equal one-step-at-a-time execution's, with requests of
+    different lengths finishing mid-batch (the batch shrinks and the gather is
+    not the identity), and the ticket pool is clean."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.ops._lib import tile_queue_check
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=1, vocab=128256)
+    rng = np.random.default_rng(13)
+    prompts = [rng.integers(3, cfg.vocab, size=int(rng.integers(20, 60))).tolist() for _ in range(256)]
+    ps = [SamplingParams(max_tokens=int(rng.integers(2, 9)), ignore_eos=True) for _ in range(256)]
+    toks = {}
+    for ov in (False, True):
+        eng = LLMEngine(cfg, EngineConfig(num_pages=1024, max_batch=256, max_model_len=256, overlap=ov),
+                        device="cuda", backend="kgs")
+        assert eng.overlap == ov
+        toks[ov] = [r.output for r in eng.generate(prompts, ps)]
+        assert eng.stats["graph_replays"] >= 7
+        assert tile_queue_check()["dirty_slots"] == 0
+        del eng
+        torch.cuda.empty_cache()
+    assert toks[True] == toks[False]
+    assert [len(t) for t in toks[True]] == [p.max_tokens for p in ps]
