@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
 import time
 
 import numpy as np
@@ -60,6 +61,11 @@ def run_engine(a) -> dict:
     t_warm = time.perf_counter() - t0
     prompts = _prompts(a.requests, a.input_len, mc.vocab, shared=a.shared_prefix)
     params = SamplingParams(max_tokens=a.output_len, ignore_eos=True)
+    if a.gc_freeze:
+        import gc
+
+        gc.collect()
+        gc.freeze()  # the engine's long-lived objects leave the collector's scans
     for k in eng.stats:
         eng.stats[k] = 0
     torch.cuda.synchronize()
@@ -73,6 +79,9 @@ def run_engine(a) -> dict:
     from kgs.ops.decode import NT_WEIGHTS
 
     tq = tile_queue_check(0)  # the persistent GEMMs' ticket pool must be all zero again
+    if os.environ.get("KGS_HOST_PHASES_OUT"):
+        with open(os.environ["KGS_HOST_PHASES_OUT"], "w") as f:
+            json.dump(eng.host_phases(), f)
     ttft = sorted(r.t_first - r.t_arrival for r in outs)
     tpot = sorted((r.t_done - r.t_first) / max(1, len(r.output) - 1) for r in outs)
     return {
@@ -222,6 +231,8 @@ def main(argv=None) -> int:
                     help="reduce split-K decode projections in their own launch (A/B against the fused consumers)")
     ap.add_argument("--no-w4x-panels", action="store_true",
                     help="split-K decode projections read the row-major weights (A/B against the panel copies)")
+    ap.add_argument("--gc-freeze", action="store_true",
+                    help="gc.collect() + gc.freeze() after warm-up (A/B: collector pauses in the step loop)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="one step at a time: read each step's tokens back before planning the next (A/B)")
     ap.add_argument("--no-gate-up-panels", action="store_true",

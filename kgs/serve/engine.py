@@ -135,6 +135,8 @@ class LLMEngine:
         self.overlap = (cfg.overlap and cfg.chunked_prefill == 0 and not cfg.prefix_caching and not self.tq_check
                         and not TRACE.sync_ops)
         self._inflight: dict | None = None
+        # KGS_HOST_PHASES=1: per step, the host time of each phase (host_phases()), to find host stalls
+        self._phases = [] if os.environ.get("KGS_HOST_PHASES", "0") == "1" else None
         self._pinned = None  # two host buffers the in-flight tokens are copied into, alternately
         self._flip = 0
 
@@ -212,12 +214,16 @@ class LLMEngine:
         stops on EOS is seen one step late: it is finished then, and the token
         its extra step computed is dropped. Each call then returns the results
         of the step launched by the call before."""
+        ph = self._phases
+        t = [time.perf_counter()] if ph is not None else None
         prev = self._inflight
         if prev is not None and not self._overlap_now():
             self._inflight = None
             return self._complete(prev, advanced=None)
         advanced = self.sched.update_pending(prev["ids"]) if prev is not None else None
         plan = self.sched.schedule()
+        if t is not None:
+            t.append(time.perf_counter())  # 1: scheduler
         if plan.kind == 0:
             self._inflight = None
             return self._complete(prev, advanced) if prev is not None else []
@@ -242,13 +248,23 @@ class LLMEngine:
             self.stats["prefill_steps"] += 1
             self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
         else:
-            logits = self._run_decode(plan, self._decode_tokens(plan, prev))
+            tok = self._decode_tokens(plan, prev)
+            if t is not None:
+                t.append(time.perf_counter())  # 2: plan checks + input tokens
+            logits = self._run_decode(plan, tok)
             self.stats["decode_steps"] += 1
             self.stats["decode_tokens"] += len(ids)
+        if t is not None:
+            t += [time.perf_counter()] * (4 - len(t))  # 3: launch
         toks_dev = self._sample(ids, logits)
         if self._overlap_now() and plan.kind != 3:
             self._inflight = self._launch_readback(ids, toks_dev, nstep)
-            return self._complete(prev, advanced) if prev is not None else []
+            if t is not None:
+                t.append(time.perf_counter())  # 4: sampler + read-back launch
+            out = self._complete(prev, advanced, t) if prev is not None else []
+            if t is not None:
+                ph.append((plan.kind, *[round((b - a) * 1e6, 1) for a, b in zip(t, t[1:])]))
+            return out
         lps = self._logprobs(ids, logits, toks_dev)
         toks = toks_dev.cpu().numpy().astype(np.int32)
         TRACE.mark(f"step {nstep} end")
@@ -273,12 +289,20 @@ class LLMEngine:
             cur["host"] = toks_dev
         return cur
 
-    def _complete(self, cur: dict, advanced) -> list[tuple[int, int, bool]]:
+    def host_phases(self) -> list:
+        """KGS_HOST_PHASES=1: per overlapped step (kind, us in the scheduler, the
+        plan checks + input tokens, the launch, the sampler + read-back launch,
+        the wait for the previous step's tokens, the result loop)."""
+        return list(self._phases or [])
+
+    def _complete(self, cur: dict, advanced, t=None) -> list[tuple[int, int, bool]]:
         """Results of an in-flight step. ``advanced``: the ids update_pending
         finished (the scheduler already moved past this step; its tokens are
         filled in and EOS stops applied now), or None (a plain update)."""
         if cur["event"] is not None:
             cur["event"].synchronize()
+        if t is not None:
+            t.append(time.perf_counter())  # 5: wait for the previous step's tokens
         ids = cur["ids"]
         toks = cur["host"].numpy().astype(np.int32)
         TRACE.mark(f"step {cur['nstep']} end")
@@ -293,7 +317,10 @@ class LLMEngine:
                 rid = int(ids[j])
                 if rid not in done and self.sched.abort(rid):
                     done.add(rid)
-        return self._emit(ids, toks, eos, done, None)
+        out = self._emit(ids, toks, eos, done, None)
+        if t is not None:
+            t.append(time.perf_counter())  # 6: result loop
+        return out
 
     def _decode_tokens(self, plan, prev) -> torch.Tensor | None:
         """A decode plan's input tokens on the device when some are still

@@ -28,6 +28,7 @@
 #                gate|up kernel, default vs nt weight loads
 #   serve_nt_ab  batch-$B serving with nt weight loads off / on / on + SwiGLU-packed gate|up, twice
 #   serve_overlap_ab  batch-$B serving, sequential vs overlapped engine steps, twice
+#   mall_probe   batch-256 decode projections with weights cold (HBM) vs hot (MALL)
 #   serve_nt_rep the round-4 faulting serving configuration (nt on, output 256) x2, nt off, nt on traced
 #   uninit_probe serving under allocator fill patterns 0 / 0x400 (uninitialised reads show as a difference)
 #   serve_rep    batch-256 serving $N times back to back with step breadcrumbs (KGS_STEP_TRACE)
@@ -143,6 +144,21 @@ step() {
                 run serve_seq_b${B:-256}_$r 300 $SB --no-overlap &&
                 run serve_ovl_b${B:-256}_$r 300 $SB || return 1
             done ;;
+        mall_probe)  # each batch-256 decode projection (production route) with its weights cold (1.5 GB ring,
+            # streamed from HBM) vs hot (two copies: MALL-resident where they fit)
+            local P
+            for P in qkv:pw4x_bm256_bn128_s4_nt o:pw4x_bm128_bn128_s4_nt down:pw4x_bm256_bn128_s8_nt \
+                     gateup:pswiglu_bm256_bn128_nt; do
+                run mall_${P%%:*}_cold 120 python bench/decode_gateup_probe.py --proj ${P%%:*} --batches 256 \
+                    --variants ${P#*:} --iters 60 --ring-gb 1.5 &&
+                run mall_${P%%:*}_hot 120 python bench/decode_gateup_probe.py --proj ${P%%:*} --batches 256 \
+                    --variants ${P#*:} --iters 60 --ring-gb 0.001 || return 1
+            done ;;
+        host_phases)  # batch-256 serving, overlapped, per-step host phase times (KGS_HOST_PHASES); then with gc.freeze
+            local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256"
+            SB="$SB --max-batch 256 --max-model-len 2048"
+            (export KGS_HOST_PHASES=1 KGS_HOST_PHASES_OUT="$O/phases.json"; run host_phases 300 $SB) &&
+            (export KGS_HOST_PHASES=1 KGS_HOST_PHASES_OUT="$O/phases_gcf.json"; run host_phases_gcf 300 $SB --gc-freeze) ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
@@ -212,7 +228,7 @@ step() {
             --output-len 256 --max-batch 256 --max-model-len 2048 --no-fuse-splitk ;;
         decode_trace) run decode_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace" -o d \
             -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len ${OL:-32} --max-batch 256 \
-            --max-model-len 2048 ;;
+            --max-model-len 2048 ${DT_FLAGS:-} ;;
         decode_trace_b1) run decode_trace_b1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/dtrace1" \
             -o d -- python3 -m kgs.serve bench --requests 2 --input-len 512 --output-len 64 --max-batch 1 \
             --max-model-len 2048 ;;
