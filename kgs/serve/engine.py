@@ -334,12 +334,14 @@ class LLMEngine:
         src = order[np.searchsorted(pids, sid, sorter=order).clip(0, len(pids) - 1)]
         if not np.array_equal(pids[src][pend], sid[pend]):
             raise RuntimeError("overlapped decode: a pending sequence was not in the previous step")
-        src = np.where(pend, src, -1)
-        dev = prev["dev"]
-        if pend.all() and np.array_equal(src, np.arange(len(src))):
+        return self._gather_tokens(prev["dev"], np.where(pend, src, -1), plan.tokens)
+
+    def _gather_tokens(self, dev: torch.Tensor, src: np.ndarray, tokens: np.ndarray) -> torch.Tensor:
+        """tokens[j] = dev[src[j]] where src[j] >= 0, else the host's tokens[j]."""
+        if (src >= 0).all() and np.array_equal(src, np.arange(len(src))):
             return dev[:len(src)].to(torch.int32)  # steady state: same sequences, same order
         s = self._dev(src, torch.int64)
-        return torch.where(s >= 0, dev.index_select(0, s.clamp(min=0)).to(torch.int32), self._dev(plan.tokens))
+        return torch.where(s >= 0, dev.index_select(0, s.clamp(min=0)).to(torch.int32), self._dev(tokens))
 
     def _eos_mask(self, ids, toks) -> np.ndarray:
         eos = np.zeros(len(ids), dtype=np.uint8)
@@ -520,7 +522,14 @@ class LLMEngine:
         return g
 
     def warmup(self, batches=None, widths=None) -> None:
-        """Capture decode graphs ahead of traffic (otherwise captured on first use)."""
+        """Capture decode graphs ahead of traffic (otherwise captured on first use),
+        and run the overlapped steps' token gather once: its first use loads the
+        ops' code objects, ~0.1 s the GPU would otherwise spend waiting on the
+        first decode after a prefill (profiles/r5/overlap/README.md)."""
+        if self.overlap and self.device.type == "cuda":
+            dev = torch.zeros(2, dtype=torch.int64, device=self.device)
+            self._gather_tokens(dev, np.array([1, -1], np.int64), np.zeros(2, np.int32))
+            torch.cuda.synchronize(self.device)
         if not self.use_graphs:
             return
         maxw = math.ceil(self.cfg.max_model_len / PAGE)
