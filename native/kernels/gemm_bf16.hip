@@ -165,6 +165,8 @@ static int cu_count() {
 }
 
 // gemm_persistent.hip
+hipError_t launch_w4p_swiglu(const unsigned short* A, const unsigned short* B, unsigned short* C, int M, int N,
+                             int K, int lda, int ldb, int ldc, int cus, int* tq, hipStream_t s);
 template <int EPI>
 hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned short* C, const unsigned short* bias,
                       int M, int N, int K, int lda, int ldb, int ldc, int cus, int* tq, hipStream_t s);
@@ -815,6 +817,14 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_swiglu_ex(const void* A, const void* B, void
   auto c = (unsigned short*)C;
   const dim3 grid(((M + bm - 1) / bm) * (N / bn));
   const bool aligned_m = M % bm == 0;
+  // prompt-pass shapes (256 x 256 tiles, aligned M, more tiles than CUs): the
+  // persistent kernel with the same K-step (bitwise the one-shot result)
+  if (bm == 256 && bn == 256 && aligned_m && flags == 0 && K >= 384 && (long)(M / 256) * (N / 256) > cu_count()) {
+    if (int* tq = tile_queue(stream)) {
+      const hipError_t e = launch_w4p_swiglu(a, b, c, M, N, K, lda, ldb, ldc, cu_count(), tq, stream);
+      return e == hipSuccess ? 0 : (int)e;
+    }
+  }
   int rc;
   if (bm == 256) {
     if (bn == 256) rc = launch_w4sw<256, 0>(grid, stream, a, b, c, M, N, K, lda, ldb, ldc, aligned_m, flags);

@@ -36,6 +36,18 @@ hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned
   return hipGetLastError();
 }
 
+// SwiGLU (B = fused [gate; up] weight, N = 2I rows; C = [M, I]): the prefill
+// gate|up, with the one-shot SwiGLU kernel's K-step and tile order (X 1000000),
+// so the result is bitwise the one-shot kernel's
+hipError_t launch_w4p_swiglu(const unsigned short* A, const unsigned short* B, unsigned short* C, int M, int N,
+                             int K, int lda, int ldb, int ldc, int cus, int* tq, hipStream_t s) {
+  const int tiles = (M / 256) * (N / 256);
+  const dim3 pg(tiles < cus ? tiles : cus);
+  hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI_NONE, 1000000>), pg, dim3(256), 0, s, A, B, C, nullptr, M, N, K, lda, ldb,
+                     ldc, tq);
+  return hipGetLastError();
+}
+
 #define KGS_LAUNCH_W4P(EPI)                                                                                         \
   template hipError_t launch_w4p<EPI>(const unsigned short*, const unsigned short*, unsigned short*,              \
                                       const unsigned short*, int, int, int, int, int, int, int, int*, hipStream_t);

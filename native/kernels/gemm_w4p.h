@@ -256,11 +256,62 @@ __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ 
   }
 }
 
+// SwiGLU epilogue (X's SW digit, gemm_w4.h's one-shot SW epilogue on named
+// accumulators): B's 256 rows of a tile are 128 gate and 128 up rows staged in
+// alternating 32-row DMA groups, so a wave's fragment columns ng = 0, 1, 4, 5
+// are gate and ng + 2 the matching up columns; output fragment pair (QQ, QQ + 1)
+// = silu(gate) * up of fragments ng(QQ), ng(QQ + 1), both products rounded to
+// bf16 first (the roundings of GEMM + silu_mul). C is [M, N / 2].
+template <int Q>
+__device__ __forceinline__ uint2 swiglu4() {
+  constexpr int i = Q / NB, qh = Q % NB, ng = 4 * (qh / 2) + qh % 2;
+  const f32x4 g = accr::read<i * NB + ng>(), u = accr::read<i * NB + ng + 2>();
+  float r[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float gf = bf2f(f2bf(g[e]));
+    r[e] = gf / (1.0f + __expf(-gf)) * bf2f(f2bf(u[e]));
+  }
+  return make_uint2(pack_bf16x2(r[0], r[1]), pack_bf16x2(r[2], r[3]));
+}
+
+template <int I, int QQ>
+__device__ __forceinline__ void pepi_sw(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn) {
+  if constexpr (I < MA) {
+    if constexpr (QQ < NB / 2) {
+      const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+      const uint2 o0 = swiglu4<I * NB + QQ>(), o1 = swiglu4<I * NB + QQ + 1>();
+      auto sx = __builtin_amdgcn_permlane16_swap(o0.x, o1.x, false, false);
+      auto sy = __builtin_amdgcn_permlane16_swap(o0.y, o1.y, false, false);
+      const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      const int row = tm * BM + c.wr * (BM / 2) + I * 16 + fr;
+      const int col0 = tn * (BN / 2) + c.wc * (BN / 4) + QQ * 16;
+      *(uint4*)(C + (long)row * ldc + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
+      pepi_sw<I, QQ + 2>(c, C, ldc, tm, tn);
+    } else {
+      pepi_sw<I + 1, 0>(c, C, ldc, tm, tn);
+    }
+  }
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_a(const unsigned short* A, int tm, int lda) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda), 0, BM * lda * 2, 0x00020000);
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_b(const unsigned short* B, int tn, int ldb) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * BN * ldb), 0, BN * ldb * 2, 0x00020000);
+}
+// B of tile column tn; SwiGLU: its 128 gate rows (rb) and the matching 128 up
+// rows N / 2 further (rb2), as gemm_w4.h's SW staging reads them
+template <bool SW>
+__device__ __forceinline__ void set_b(Ctx& c, const unsigned short* B, int tn, int ldb, int N) {
+  if constexpr (SW) {
+    c.rb = __builtin_amdgcn_make_buffer_rsrc((void*)(B + (long)tn * (BN / 2) * ldb), 0, (BN / 2) * ldb * 2,
+                                             0x00020000);
+    c.rb2 = __builtin_amdgcn_make_buffer_rsrc((void*)(B + ((long)N / 2 + (long)tn * (BN / 2)) * ldb), 0,
+                                              (BN / 2) * ldb * 2, 0x00020000);
+  } else {
+    c.rb = rsrc_b(B, tn, ldb);
+  }
 }
 
 // Aligned shapes only (M, N % 256, K % 128 with K >= 384; 16-B operands); the
@@ -296,6 +347,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ntm = M / BM, ntn = N / BN, ntiles = ntm * ntn;
   static_assert(!TS || EPI == EPI_NONE, "timing build: bias carries the stamp buffer");
+  // X digit 10^6: SwiGLU (B = fused [gate; up], N = 2I rows, C = [M, I]); tiles
+  // are 256 B rows = 128 gate + 128 up, ntn = N / 256
+  constexpr bool SW = (X / 1000000) % 10 != 0;
+  static_assert(!SW || (EPI == EPI_NONE && L == 0 && !NTST), "SwiGLU: no bias, production layout");
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {
@@ -356,7 +411,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int sl, tm, tn;
   w4::tile_of<X, false>(DYN ? x + 8 * t : t, ntiles, ntm, ntn, sl, tm, tn);
   c.ra = rsrc_a(A, tm, lda);
-  c.rb = rsrc_b(B, tn, ldb);
+  set_b<SW>(c, B, tn, ldb, N);
 
   // prologue: K-tiles 0, 1 of the first tile into stages 0, 1; k-sub 0 of K-tile 0 into f0
 #pragma unroll
@@ -400,14 +455,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
     Ctx cn = c;
     cn.ra = rsrc_a(A, tmn, lda);
-    cn.rb = rsrc_b(B, tnn, ldb);
+    set_b<SW>(cn, B, tnn, ldb, N);
     // the last two K-steps bring the next tile's K-tiles 0 and 1 (no next tile:
     // harmless re-loads of this tile's last K-tile into the freed stages)
     pstep<0, X, false, 0, L>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
     pstep<1, X, false, 0, L>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read
+    if constexpr (SW) pepi_sw<0, 0>(c, C, ldc, tm, tn);
     float bv[NB][4];
-    {
+    if constexpr (!SW) {
       const int fq = lane >> 4;
 #pragma unroll
       for (int n = 0; n < NB; ++n) {
@@ -420,7 +476,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         }
       }
     }
-    pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
+    if constexpr (!SW) pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
     if constexpr (TS) {
       const long long te = (long long)__builtin_amdgcn_s_memrealtime();
       if (threadIdx.x == 0 && ntile_done < 11) ts[2 + ntile_done] = te;
@@ -436,6 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     tn = tnn;
     c.ra = cn.ra;
     c.rb = cn.rb;
+    c.rb2 = cn.rb2;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
   if constexpr (DYN != 0) {

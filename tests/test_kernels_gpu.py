@@ -527,6 +527,40 @@ def test_gemm_w4x_swiglu_epilogue(M, I, K, bn, bm):
     assert ((fused.float() - r32).abs().max() / r32.abs().max()).item() < 2e-2
 
 
+@pytest.mark.parametrize("M,I,K", [(2048, 8192, 1024), (1024, 14336, 4096), (4096, 4096, 768)])
+def test_prompt_swiglu_on_the_persistent_kernel(M, I, K):
+    """Round 5: the prompt pass's gate|up (256 x 256 tiles, aligned M, more tiles
+    than CUs) runs on the persistent kernel with the SwiGLU epilogue. It equals
+    the plain GEMM + silu_mul bit for bit, and a captured launch takes a ticket
+    slot of its own (i.e. it IS the persistent kernel), bitwise the eager result."""
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
+    from kgs.ops.gemm import gemm_nt_w4x, gemm_nt_w4x_swiglu
+    from kgs.ops.transformer import silu_mul
+
+    g = torch.Generator(device=DEV).manual_seed(M + I)
+    a = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    w = ((torch.rand(2 * I, K, device=DEV, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
+    fused = gemm_nt_w4x_swiglu(a, w, bn=256, bm=256)
+    ref = silu_mul(gemm_nt_w4x(a, w, bn=256, nslice=1))
+    assert torch.equal(fused, ref)
+    gu = a[:256].float() @ w.float().T
+    r32 = torch.nn.functional.silu(gu[:, :I]) * gu[:, I:]
+    assert ((fused[:256].float() - r32).abs().max() / r32.abs().max()).item() < 2e-2
+    st0 = tile_queue_stats()
+    out = torch.zeros_like(fused)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gemm_nt_w4x_swiglu(a, w, bn=256, bm=256, out=out)
+    st1 = tile_queue_stats()
+    assert st1["capture_slots"] == st0["capture_slots"] + 1 and st1["fallbacks"] == st0["fallbacks"], (st0, st1)
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, fused)
+        assert tile_queue_check()["dirty_slots"] == 0
+    del graph
+
+
 @pytest.mark.parametrize("M,N,K", [(4096, 512, 640), (2048, 256, 1024), (768, 256, 384)])
 def test_gemm_tall_mirrored_schedule_is_bitwise_the_default(M, N, K):
     """M > N runs the mirrored schedule (GROUP_N order, B's DMAs first, round 3):
