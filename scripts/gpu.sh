@@ -159,6 +159,15 @@ step() {
             SB="$SB --max-batch 256 --max-model-len 2048"
             (export KGS_HOST_PHASES=1 KGS_HOST_PHASES_OUT="$O/phases.json"; run host_phases 300 $SB) &&
             (export KGS_HOST_PHASES=1 KGS_HOST_PHASES_OUT="$O/phases_gcf.json"; run host_phases_gcf 300 $SB --gc-freeze) ;;
+        lib_serve_ab)  # batch-256 serving and the Llama prefill bench: this tree's kernels vs $LIB_B, A B A B
+            local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256"
+            SB="$SB --max-batch 256 --max-model-len 2048"
+            for r in 1 2; do
+                run serve_head_$r 300 $SB &&
+                (export KGS_KERNELS_LIB=$LIB_B; run serve_libb_$r 300 $SB) || return 1
+            done
+            run prefill_head 300 python -u -m kgs.models.llama --backends kgs &&
+            (export KGS_KERNELS_LIB=$LIB_B; run prefill_libb 300 python -u -m kgs.models.llama --backends kgs) ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
@@ -261,6 +270,11 @@ step() {
         prefill) run prefill 300 python -u -m kgs.models.llama --backends kgs,torch,fp8 ;;
         prefill_trace) run prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ptrace" \
             -o p -- python3 -m kgs.models.llama --backends kgs --iters 2 ;;
+        serve_prefill_trace)  # kernel trace of the serving bench's prompt pass (256 x 512 tokens, 2 output tokens)
+            run serve_prefill_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/sptrace" -o p \
+                -- python3 -m kgs.serve bench --requests 256 --input-len 512 --output-len 2 --max-batch 256 \
+                --max-model-len 2048 &&
+            python bench/prof_summary.py "$O/sptrace" > "$O/serve_prefill_summary.md" ;;
         e2e) run e2e 300 python -m kgs bench --no-kind --gpus 1 --timings-json "$O/e2e.json" ;;
         gemm_l2) # L2 hit/miss + HBM bytes of kgs vs hipBLASLt at $MNK (two counter passes) + a kernel trace
             local G="python3 bench/gemm_profile.py --mnk ${MNK:-8192x4096x14336} --iters 10 --torch --variant ${VAR:-auto}"
