@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256, (MT * KC_ > 32 || R * MT >= 16) ? 1 : 2) void 
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const float cs = rcs[c][r][i], sn = rsn[c][r][i];
-            o[i] = g < 2 ? vb[i] * cs - pb[i] * sn : vb[i] * cs + pb[i] * sn;
+            o[i] = g < 2 ? rope_lo(vb[i], pb[i], cs, sn) : rope_hi(pb[i], vb[i], cs, sn);
           }
         }
         uint2 pk;
@@ -617,8 +617,8 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
       const float cs = e < 4 ? c0[e] : c1[e - 4];
       const float sn = e < 4 ? s0[e] : s1[e - 4];
       const float x1 = bf2f((unsigned short)a[e]), x2 = bf2f((unsigned short)b[e]);
-      o1[e] = (short)f2bf(x1 * cs - x2 * sn);
-      o2[e] = (short)f2bf(x2 * cs + x1 * sn);
+      o1[e] = (short)f2bf(rope_lo(x1, x2, cs, sn));
+      o2[e] = (short)f2bf(rope_hi(x1, x2, cs, sn));
     }
     *p1 = o1;
     *p2 = o2;
@@ -628,6 +628,57 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
   if (h < H) return;
   if (sl < 0) return;
   kv_write<KV8>(cache, sl, h, H, HKV, c, a, b);
+}
+
+// Prompt-pass form (the projection in qkv, (H + 2 HKV) % 8 == 0): thread =
+// (token, group of 8 heads, chunk c). The cos / sin of (pos[t], c) are loaded
+// once for the 8 heads -- the per-head form above loads them once per head, as
+// many bytes again as the qkv rows, all through L1 -- and the 8 heads' 16 row
+// loads are issued before the first rotation. Same arithmetic per element
+// (bitwise the per-head form's result).
+template <bool KV8>
+__global__ __launch_bounds__(256) void rope_cache_g8(unsigned short* __restrict__ qkv, const float* __restrict__ cosv,
+                                                     const float* __restrict__ sinv, const int* __restrict__ pos,
+                                                     const int* __restrict__ slot, void* __restrict__ cache,
+                                                     long tokens, int H, int HKV, long ld) {
+  const int ng = (H + 2 * HKV) >> 3;
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= tokens * ng * 8) return;
+  const long t = idx / (ng * 8);
+  const int rem = (int)(idx - t * ng * 8);
+  const int g = rem >> 3, c = rem & 7;
+  const int p = pos[t];
+  const int sl = slot[t];
+  unsigned short* base = qkv + t * ld + (long)g * 8 * HD + 8 * c;
+  bf16x8 a[8], b[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = *(const bf16x8*)(base + j * HD);
+    b[j] = *(const bf16x8*)(base + j * HD + HD / 2);
+  }
+  const f32x4* cp = (const f32x4*)(cosv + (long)p * (HD / 2) + 8 * c);
+  const f32x4* sp = (const f32x4*)(sinv + (long)p * (HD / 2) + 8 * c);
+  const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int h = g * 8 + j;
+    if (h < H + HKV) {
+      bf16x8 o1, o2;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float cs = e < 4 ? c0[e] : c1[e - 4];
+        const float sn = e < 4 ? s0[e] : s1[e - 4];
+        const float x1 = bf2f((unsigned short)a[j][e]), x2 = bf2f((unsigned short)b[j][e]);
+        o1[e] = (short)f2bf(rope_lo(x1, x2, cs, sn));
+        o2[e] = (short)f2bf(rope_hi(x1, x2, cs, sn));
+      }
+      *(bf16x8*)(base + j * HD) = o1;
+      *(bf16x8*)(base + j * HD + HD / 2) = o2;
+      a[j] = o1;
+      b[j] = o2;
+    }
+    if (h >= H && sl >= 0) kv_write<KV8>(cache, sl, h, H, HKV, c, a[j], b[j]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -737,8 +788,8 @@ __global__ __launch_bounds__(64) void paged_decode(AttnArgs a) {
           const float cs = e2 < 4 ? c0[e2] : c1[e2 - 4];
           const float sn = e2 < 4 ? s0[e2] : s1[e2 - 4];
           const float x1 = bf2f((unsigned short)ra[e2]), x2 = bf2f((unsigned short)rb[e2]);
-          o1[e2] = (short)f2bf(x1 * cs - x2 * sn);
-          o2[e2] = (short)f2bf(x2 * cs + x1 * sn);
+          o1[e2] = (short)f2bf(rope_lo(x1, x2, cs, sn));
+          o2[e2] = (short)f2bf(rope_hi(x1, x2, cs, sn));
         }
         ra = o1;
         rb = o2;
@@ -1194,6 +1245,14 @@ KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* si
     }
 #undef KGS_RCS_KV
 #undef KGS_RCS
+  } else if ((H + 2 * HKV) % 8 == 0) {
+    const dim3 g8((unsigned)((n / 8 + 255) / 256));
+    if (kv8)
+      hipLaunchKernelGGL(kgs::dec::rope_cache_g8<true>, g8, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, HKV,
+                         ld);
+    else
+      hipLaunchKernelGGL(kgs::dec::rope_cache_g8<false>, g8, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, HKV,
+                         ld);
   } else if (kv8) {
     hipLaunchKernelGGL(kgs::dec::rope_cache<true>, g, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H, HKV, ld,
                        nullptr, 0);

@@ -39,6 +39,19 @@ __device__ __forceinline__ float bf2f(unsigned short h) {
   return __builtin_bit_cast(float, ((unsigned)h) << 16);
 }
 
+// RoPE rotation of the pair (x1, x2) = (d, d + 64): (x1 cos - x2 sin,
+// x2 cos + x1 sin), each as ONE fma on the other element's rounded product.
+// Every kernel that rotates uses these (rope_cache and its split-K / grouped
+// forms, the fused skinny-GEMM and attention prologues, the prompt RoPE): they
+// are compared bit for bit, and hipcc's fp-contract would otherwise choose per
+// call site which product to fuse.
+__device__ __forceinline__ float rope_lo(float x1, float x2, float cs, float sn) {
+  return __builtin_fmaf(x1, cs, -(x2 * sn));
+}
+__device__ __forceinline__ float rope_hi(float x1, float x2, float cs, float sn) {
+  return __builtin_fmaf(x2, cs, x1 * sn);
+}
+
 // Two f32 -> a packed bf16 pair in one v_cvt_pk_bf16_f32. Two f2bf calls
 // compile to two conversions (each with a dummy second source) plus a v_perm:
 // three VALU ops where one does, on every epilogue and P-fragment pack.

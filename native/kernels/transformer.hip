@@ -227,8 +227,8 @@ __global__ __launch_bounds__(256) void rope_qkv(unsigned short* __restrict__ qkv
     const float cs = e < 4 ? c0[e] : c1[e - 4];
     const float sn = e < 4 ? s0[e] : s1[e - 4];
     const float x1 = bf2f((unsigned short)a[e]), x2 = bf2f((unsigned short)b[e]);
-    o1[e] = (short)f2bf(x1 * cs - x2 * sn);
-    o2[e] = (short)f2bf(x2 * cs + x1 * sn);
+    o1[e] = (short)f2bf(rope_lo(x1, x2, cs, sn));
+    o2[e] = (short)f2bf(rope_hi(x1, x2, cs, sn));
   }
   *p1 = o1;
   *p2 = o2;
