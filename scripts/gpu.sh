@@ -168,6 +168,7 @@ step() {
             done
             run prefill_head 300 python -u -m kgs.models.llama --backends kgs &&
             (export KGS_KERNELS_LIB=$LIB_B; run prefill_libb 300 python -u -m kgs.models.llama --backends kgs) ;;
+        mall_prefetch) run mall_prefetch 300 python bench/mall_prefetch_probe.py --out "$O/mall_prefetch.json" ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
