@@ -934,3 +934,29 @@ def test_overlap_falls_back_for_host_state_sampling():
             eng.step()
         res[ov] = [(eng.requests[r].output, len(eng.requests[r].logprobs)) for r in (rid0, rid1)]
     assert res[True] == res[False] and res[True][1][1] == 6
+
+
+def test_abort_while_a_step_is_in_flight():
+    """An abort between overlapped steps (the aborted sequence is in the step
+    on the GPU): the request gets no more tokens, its pages go back, and the
+    other requests generate what a sequential engine gives them."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    kw = dict(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False)
+    prompts = [[5, 6, 7, 8], [9, 10, 11], [12, 13, 14, 15, 16]]
+    p = SamplingParams(max_tokens=8, ignore_eos=True)
+    res = {}
+    for ov in (False, True):
+        eng = LLMEngine(_tiny(), EngineConfig(**kw, overlap=ov), device="cpu", backend="ref")
+        rids = [eng.add_request(q, p) for q in prompts]
+        for _ in range(3):
+            eng.step()
+        n_at_abort = len(eng.requests[rids[1]].output)
+        eng.abort(rids[1])
+        while eng.has_work():
+            eng.step()
+        r = [eng.requests[i] for i in rids]
+        assert r[1].finish_reason == "abort" and len(r[1].output) == n_at_abort
+        assert eng.sched.check_invariants() == "" and eng.sched.num_free_pages == 63
+        res[ov] = [(x.output, x.finish_reason) for x in (r[0], r[2])]
+    assert res[True] == res[False]
