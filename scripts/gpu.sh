@@ -340,6 +340,7 @@ step() {
         serve_sweep)
             local SB="python -u -m kgs.serve bench --input-len 512 --output-len 256 --max-model-len 2048"
             run serve_b1 300 $SB --requests 2 --max-batch 1 &&
+                run serve_b16 300 $SB --requests 16 --max-batch 16 &&
                 run serve_b64 300 $SB --requests 64 --max-batch 64 &&
                 run serve_b128 300 $SB --requests 128 --max-batch 128 &&
                 run serve_b256 300 $SB --requests 256 --max-batch 256 &&
