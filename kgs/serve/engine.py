@@ -129,11 +129,10 @@ class LLMEngine:
         self._seeded: set = set()
         self._watch_eos: set = set()  # requests whose tokens are checked for EOS / stop ids
         # Overlapped steps: step t+1 is planned and launched while step t runs,
-        # and step t's tokens are read back after that (see step()). Mixed steps
-        # (chunked prefill, prefix caching) hash pages from token values, and the
-        # debug modes synchronise per step: those run one step at a time.
-        self.overlap = (cfg.overlap and cfg.chunked_prefill == 0 and not cfg.prefix_caching and not self.tq_check
-                        and not TRACE.sync_ops)
+        # and step t's tokens are read back after that (see step()). Prefix
+        # caching hashes pages from token values, and the debug modes
+        # synchronise per step: those run one step at a time.
+        self.overlap = cfg.overlap and not cfg.prefix_caching and not self.tq_check and not TRACE.sync_ops
         self._inflight: dict | None = None
         # KGS_HOST_PHASES=1: per step, the host time of each phase (host_phases()), to find host stalls
         self._phases = [] if os.environ.get("KGS_HOST_PHASES", "0") == "1" else None
@@ -234,21 +233,22 @@ class LLMEngine:
         nstep = sum(self.stats[k] for k in ("prefill_steps", "decode_steps", "mixed_steps"))
         TRACE.mark(f"step {nstep} kind={plan.kind} seqs={len(ids)} rows={len(plan.tokens)} begin")
         if plan.kind == 3:
-            logits = self._run_mixed(plan)
+            logits = self._run_mixed(plan, self._pending_tokens(plan, prev))
             npf = plan.n_prefill
             # only chunks that complete their prompt produce a token
             ids = np.concatenate([ids[:npf][plan.last_chunk.astype(bool)], ids[npf:]])
             self.stats["mixed_steps"] += 1
             self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
             self.stats["decode_tokens"] += len(plan.seq_ids) - npf
-            if len(ids) == 0:
-                return []
+            if len(ids) == 0:  # nothing sampled: only the step in flight has results
+                self._inflight = None
+                return self._complete(prev, advanced) if prev is not None else []
         elif plan.kind == 1:
-            logits = self._run_prefill(plan)
+            logits = self._run_prefill(plan, self._pending_tokens(plan, prev))
             self.stats["prefill_steps"] += 1
             self.stats["prefill_tokens"] += int(plan.seq_lens.sum())
         else:
-            tok = self._decode_tokens(plan, prev)
+            tok = self._pending_tokens(plan, prev)
             if t is not None:
                 t.append(time.perf_counter())  # 2: plan checks + input tokens
             logits = self._run_decode(plan, tok)
@@ -257,7 +257,7 @@ class LLMEngine:
         if t is not None:
             t += [time.perf_counter()] * (4 - len(t))  # 3: launch
         toks_dev = self._sample(ids, logits)
-        if self._overlap_now() and plan.kind != 3:
+        if self._overlap_now():
             self._inflight = self._launch_readback(ids, toks_dev, nstep)
             if t is not None:
                 t.append(time.perf_counter())  # 4: sampler + read-back launch
@@ -322,19 +322,35 @@ class LLMEngine:
             t.append(time.perf_counter())  # 6: result loop
         return out
 
-    def _decode_tokens(self, plan, prev) -> torch.Tensor | None:
-        """A decode plan's input tokens on the device when some are still
-        pending in the scheduler: those come from the in-flight step's sampled
-        tokens (same sequence, on the device), the rest from the plan."""
+    def _pending_tokens(self, plan, prev) -> torch.Tensor | None:
+        """A plan's input tokens on the device when some are still pending in
+        the scheduler: those come from the in-flight step's sampled tokens
+        (same sequence, on the device), the rest from the plan. A pending token
+        is a sequence's last one: a decode row, or the last row of a prompt
+        chunk that re-computes a preempted sequence."""
         pend = plan.tokens == self.sched.PENDING
         if prev is None or not pend.any():
             return None
-        pids, sid = prev["ids"], plan.seq_ids
+        pids, sid = prev["ids"], self._row_seqs(plan)
         order = np.argsort(pids, kind="stable")
         src = order[np.searchsorted(pids, sid, sorter=order).clip(0, len(pids) - 1)]
         if not np.array_equal(pids[src][pend], sid[pend]):
             raise RuntimeError("overlapped decode: a pending sequence was not in the previous step")
         return self._gather_tokens(prev["dev"], np.where(pend, src, -1), plan.tokens)
+
+    @staticmethod
+    def _row_seqs(plan) -> np.ndarray:
+        """The sequence id of every input row of a plan."""
+        if plan.kind == 2:
+            return np.asarray(plan.seq_ids)
+        rows = np.full(len(plan.tokens), -1, dtype=np.int64)
+        npf = plan.n_prefill if plan.kind == 3 else len(plan.seq_ids)
+        for j in range(npf):
+            rows[plan.seq_starts[j]:plan.seq_starts[j] + plan.padded_lens[j]] = plan.seq_ids[j]
+        nd = len(plan.seq_ids) - npf
+        if nd:
+            rows[len(rows) - nd:] = plan.seq_ids[npf:]
+        return rows
 
     def _gather_tokens(self, dev: torch.Tensor, src: np.ndarray, tokens: np.ndarray) -> torch.Tensor:
         """tokens[j] = dev[src[j]] where src[j] >= 0, else the host's tokens[j]."""
@@ -446,17 +462,20 @@ class LLMEngine:
             t = t.pin_memory().to(self.device, non_blocking=True)
         return t.to(dtype)
 
-    def _run_prefill(self, plan) -> torch.Tensor:
-        return self.model.prefill(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots),
+    def _run_prefill(self, plan, tokens: torch.Tensor | None = None) -> torch.Tensor:
+        return self.model.prefill(tokens if tokens is not None else self._dev(plan.tokens),
+                                  self._dev(plan.positions), self._dev(plan.slots),
                                   plan.seq_starts.tolist(), plan.seq_lens.tolist(), plan.padded_lens.tolist())
 
-    def _run_mixed(self, plan) -> torch.Tensor:
+    def _run_mixed(self, plan, tokens: torch.Tensor | None = None) -> torch.Tensor:
+        """``tokens``: the input tokens on the device (overlapped steps), else the plan's."""
         npf = plan.n_prefill
         pf_bt = self._dev(plan.pf_block_tables) if npf else None
         chunks = [(int(plan.seq_starts[j]), int(plan.seq_lens[j]), int(plan.padded_lens[j]), int(plan.ctx_starts[j]),
                    pf_bt[j], bool(plan.last_chunk[j])) for j in range(npf)]
         nd = len(plan.seq_ids) - npf
-        return self.model.mixed(self._dev(plan.tokens), self._dev(plan.positions), self._dev(plan.slots), chunks,
+        return self.model.mixed(tokens if tokens is not None else self._dev(plan.tokens), self._dev(plan.positions),
+                                self._dev(plan.slots), chunks,
                                 self._dev(plan.block_tables) if nd else None,
                                 self._dev(plan.ctx_lens) if nd else None)
 

@@ -360,6 +360,12 @@ step() {
             run online_r8 300 $OB --request-rate 8 && run online_r16 300 $OB --request-rate 16 &&
                 run online_r32 300 $OB --request-rate 32 && run online_r64 300 $OB --request-rate 64 &&
                 run online_r96 300 $OB --request-rate 96 ;;
+        online_overlap_ab)  # online serving (Poisson 32 req/s, chunked prefill): sequential vs overlapped steps, A B A B
+            local OB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 --max-batch 256"
+            OB="$OB --max-model-len 2048 --chunked-prefill 2048 --request-rate ${RATE:-32}"
+            for r in 1 2; do
+                run online_seq_$r 300 $OB --no-overlap && run online_ovl_$r 300 $OB || return 1
+            done ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac

@@ -877,7 +877,7 @@ def test_scheduler_two_phase_update():
     assert s.schedule().kind == 0 and s.check_invariants() == ""
 
 
-@pytest.mark.parametrize("case", ["eos", "preempt", "admission"])
+@pytest.mark.parametrize("case", ["eos", "preempt", "admission", "chunked", "chunked_preempt"])
 def test_overlapped_steps_generate_what_sequential_steps_do(case):
     """EngineConfig.overlap plans step t+1 before step t's tokens are read
     back. With EOS stops (seen one step late), preemption + recompute, and more
@@ -885,17 +885,19 @@ def test_overlapped_steps_generate_what_sequential_steps_do(case):
     tokens and finish reason equal those of one-step-at-a-time execution."""
     from kgs.serve import EngineConfig, LLMEngine, SamplingParams
 
-    rng = np.random.default_rng({"eos": 3, "preempt": 4, "admission": 5}[case])
+    rng = np.random.default_rng({"eos": 3, "preempt": 4, "admission": 5, "chunked": 6, "chunked_preempt": 7}[case])
     kw = dict(num_pages=64, max_batch=4, max_model_len=256, cuda_graphs=False)
-    if case == "preempt":
-        kw.update(num_pages=7, max_batch=3)
-    n = {"eos": 4, "preempt": 3, "admission": 9}[case]
+    if case.startswith("chunked"):  # mixed steps: prompt chunks of 128 rows beside the decode rows
+        kw.update(chunked_prefill=128, max_model_len=512)
+    n = {"eos": 4, "preempt": 3, "admission": 9, "chunked": 6, "chunked_preempt": 3}[case]
     prompts = [rng.integers(3, 512, size=int(rng.integers(5, 40))).tolist() for _ in range(n)]
     params = [SamplingParams(max_tokens=int(rng.integers(2, 14)), ignore_eos=case != "eos") for _ in range(n)]
-    if case == "preempt":  # 5 usable pages for 3 sequences that grow across page boundaries
-        kw.update(num_pages=6)
+    if case in ("preempt", "chunked_preempt"):  # 5 usable pages, 3 sequences growing across page boundaries
+        kw.update(num_pages=6, max_batch=3)
         prompts = [rng.integers(3, 512, size=m).tolist() for m in (30, 28, 31)]
         params = [SamplingParams(max_tokens=m, ignore_eos=True) for m in (12, 9, 12)]
+    if case == "chunked":  # prompts longer than a chunk
+        prompts = [rng.integers(3, 512, size=int(rng.integers(100, 300))).tolist() for _ in range(n)]
     eos = -1
     if case == "eos":  # an EOS id that some request samples early on
         probe = LLMEngine(_tiny(), EngineConfig(**kw, overlap=False), device="cpu", backend="ref")
@@ -906,8 +908,10 @@ def test_overlapped_steps_generate_what_sequential_steps_do(case):
         assert eng.overlap == ov
         outs[ov] = [(r.output, r.finish_reason) for r in eng.generate(prompts, params)]
         assert eng.sched.check_invariants() == "" and not eng.has_work()
-        if case == "preempt":
+        if case.endswith("preempt"):
             assert eng.stats["preemptions"] >= 1
+        if case.startswith("chunked"):
+            assert eng.stats["mixed_steps"] >= 1
     assert outs[True] == outs[False]
     if case == "eos":
         assert any(f == "stop" for _, f in outs[True])

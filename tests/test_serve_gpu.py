@@ -359,7 +359,8 @@ def test_nt_loads_and_gate_up_panels_keep_the_tokens(monkeypatch):
         assert toks[True, True] == toks[False, True] == toks[True, False], nb
 
 
-def test_overlapped_steps_equal_sequential_steps_on_graphs():
+@pytest.mark.parametrize("chunked", [0, 512])
+def test_overlapped_steps_equal_sequential_steps_on_graphs(chunked):
     """EngineConfig.overlap on the kgs backend with hipGraph decode at batch
     256 (the serving bench's shape, one layer): step t+1 is replayed with its
     input tokens gathered on the device from step t's samples, before the host
@@ -372,15 +373,18 @@ def test_overlapped_steps_equal_sequential_steps_on_graphs():
 
     cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=1, vocab=128256)
     rng = np.random.default_rng(13)
-    prompts = [rng.integers(3, cfg.vocab, size=int(rng.integers(20, 60))).tolist() for _ in range(256)]
-    ps = [SamplingParams(max_tokens=int(rng.integers(2, 9)), ignore_eos=True) for _ in range(256)]
+    # chunked: mixed steps (prompt chunks beside decode rows, eager) between graph-replayed decodes
+    n, lo, hi = (256, 20, 60) if not chunked else (64, 100, 700)
+    prompts = [rng.integers(3, cfg.vocab, size=int(rng.integers(lo, hi))).tolist() for _ in range(n)]
+    ps = [SamplingParams(max_tokens=int(rng.integers(2, 9)), ignore_eos=True) for _ in range(n)]
     toks = {}
     for ov in (False, True):
-        eng = LLMEngine(cfg, EngineConfig(num_pages=1024, max_batch=256, max_model_len=256, overlap=ov),
-                        device="cuda", backend="kgs")
+        eng = LLMEngine(cfg, EngineConfig(num_pages=2048, max_batch=256, max_model_len=1024, overlap=ov,
+                                          chunked_prefill=chunked), device="cuda", backend="kgs")
         assert eng.overlap == ov
         toks[ov] = [r.output for r in eng.generate(prompts, ps)]
-        assert eng.stats["graph_replays"] >= 7
+        assert eng.stats["graph_replays"] >= (7 if not chunked else 1)
+        assert not chunked or eng.stats["mixed_steps"] >= 2
         assert tile_queue_check()["dirty_slots"] == 0
         del eng
         torch.cuda.empty_cache()
