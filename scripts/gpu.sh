@@ -141,7 +141,7 @@ step() {
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"
             SB="$SB --max-batch ${B:-256} --max-model-len 2048"
             for r in 1 2; do
-                run serve_seq_b${B:-256}_$r 300 $SB --no-overlap &&
+                run serve_seq_b${B:-256}_$r 300 $SB --overlap off &&
                 run serve_ovl_b${B:-256}_$r 300 $SB || return 1
             done ;;
         mall_probe)  # each batch-256 decode projection (production route) with its weights cold (1.5 GB ring,
@@ -364,7 +364,7 @@ step() {
             local OB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256 --max-batch 256"
             OB="$OB --max-model-len 2048 --chunked-prefill 2048 --request-rate ${RATE:-32}"
             for r in 1 2; do
-                run online_seq_$r 300 $OB --no-overlap && run online_ovl_$r 300 $OB || return 1
+                run online_seq_$r 300 $OB --overlap off && run online_ovl_$r 300 $OB --overlap on || return 1
             done ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
