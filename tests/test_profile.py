@@ -52,3 +52,47 @@ def test_summarize_trace_and_counters(tmp_path):
     assert "1560 |" in md                              # 2*8192^3 / 0.705 ms
     assert "MFMA busy/SIMD vs GPU cycles 78.1%" in md  # 1e9 / 1024 / (1e7 / 8)
     assert "LDS conflict cycles 0.0% of LDS active" in md and "L2 hit 80.0%" in md
+
+
+def _trace(path, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for name, s, e in rows:
+            w.writerow({"Kernel_Name": name, "Start_Timestamp": s, "End_Timestamp": e})
+
+
+def test_step_idle_counts_only_gaps_no_kernel_covers(tmp_path):
+    """bench/step_idle.py: a step's idle time is its period minus the UNION
+    of kernel and copy intervals (overlapping kernels on two streams are not
+    counted twice, a gap between them is)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("step_idle", os.path.join(os.path.dirname(__file__), "..", "bench",
+                                                                            "step_idle.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    p = tmp_path / "t.csv"
+    # step 1 ends at 1000 ns; step 2: kernels [1500, 3000] and [2000, 4000] overlap, then a 1000 ns gap,
+    # then [5000, 6000], then its argmax [6000, 7000]
+    _trace(p, [("kgs::tfm::argmax_rows", 0, 1000), ("a", 1500, 3000), ("b", 2000, 4000), ("c", 5000, 6000),
+               ("kgs::tfm::argmax_rows", 6000, 7000)])
+    period, idle = mod.step_idle(str(p), 10)
+    assert period == [6.0] and idle == [1.5]  # 500 ns before "a" + 1000 ns between "b" and "c", in us
+
+
+def test_isa_diff_normalises_block_labels():
+    """bench/isa_diff.py: two assemblies that differ only in basic-block
+    label numbers (a kernel added before them renumbers the labels) compare
+    equal; a changed instruction does not."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("isa_diff", os.path.join(os.path.dirname(__file__), "..", "bench",
+                                                                           "isa_diff.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    a = "_Z1kv:  ; @k\n\ts_mov_b32 s0, 1\n.LBB0_2:\n\ts_cbranch_scc1 .LBB0_2 ; loop\n.Lfunc_end0:\n"
+    b = "_Z1kv:  ; @k\n\ts_mov_b32 s0, 1\n.LBB7_2:\n\ts_cbranch_scc1 .LBB7_2\n.Lfunc_end7:\n"
+    c = "_Z1kv:  ; @k\n\ts_mov_b32 s0, 2\n.LBB0_2:\n\ts_cbranch_scc1 .LBB0_2\n.Lfunc_end0:\n"
+    ka, kb, kc = mod.kernels(a), mod.kernels(b), mod.kernels(c)
+    assert list(ka) == ["_Z1kv"] and ka == kb and ka != kc
