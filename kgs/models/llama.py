@@ -143,11 +143,22 @@ class LlamaModel:
             qkv = L["qkv"](y)
             rope_qkv_(qkv, cos, sin, nh + nkv, hd, s)
             a = attention_qkv(qkv, b, s, nh, nkv, head_dim=hd, causal=True)
-            y = add_rmsnorm(x, L["o"](a), L["ln2"], cfg.eps)  # x += o-proj
+            y = self._add_norm(x, a, L["o"], L["ln2"])  # x += o-proj
             act = gemm_swiglu(y, L["gate_up"].w)  # SwiGLU in the GEMM epilogue
             nxt = self.layers[i + 1]["ln1"] if i + 1 < len(self.layers) else self.norm
-            y = add_rmsnorm(x, L["down"](act), nxt, cfg.eps)  # x += down-proj
+            y = self._add_norm(x, act, L["down"], nxt)  # x += down-proj
         return self.lm_head(y).reshape(b, s, cfg.vocab)
+
+    def _add_norm(self, x, a, proj, w):
+        """x += proj(a) and return rmsnorm(x) * w; on aligned operands the add
+        runs in the GEMM's store (kgs.ops.gemm.gemm_nt_add_, bitwise the same)."""
+        from kgs.ops.gemm import addc_ok, gemm_nt_add_
+        from kgs.ops.transformer import add_rmsnorm
+
+        if addc_ok(a, proj.w, x):
+            gemm_nt_add_(a, proj.w, x)
+            return add_rmsnorm(x, None, w, self.cfg.eps)
+        return add_rmsnorm(x, proj(a), w, self.cfg.eps)
 
     def _forward_fp8(self, x, b, s, cos, sin):
         """W8A8: every producer (norm, SwiGLU, attention-output quantiser) emits

@@ -36,6 +36,7 @@ _c_long = ctypes.c_long
 
 _SIGS = {
     "kgs_gemm_bf16_nt": ([_c_void_p, _c_void_p, _c_void_p, _c_void_p] + [_c_int] * 8 + [_c_void_p], _c_int),
+    "kgs_gemm_bf16_nt_addc": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [_c_void_p], _c_int),
     "kgs_tile_queue_stats": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
     "kgs_tile_queue_check": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
     "kgs_gemm_bf16_nt_fast_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),

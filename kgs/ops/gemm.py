@@ -11,6 +11,8 @@ in-pod workload runs on the hand-written MFMA kernel.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib
@@ -227,6 +229,39 @@ def gemm_nt_w4x(a: torch.Tensor, b, bn: int = 256, nslice: int = 1,
                                             _w4x_flags(packed, stages, nt_weights), _lib.stream_handle(a.device))
     _lib.check(rc, f"gemm_nt_w4x[{M}x{N}x{K} {bm}x{bn}/{nslice}]")
     return out
+
+
+def addc_ok(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> bool:
+    """Whether :func:`gemm_nt_add_` takes these operands: the aligned
+    four-wave path (M, N multiples of 256, K of 128, 16-B aligned rows).
+    ``KGS_PREFILL_ADDC=0`` says no to everything (A/B against the unfused pair)."""
+    if os.environ.get("KGS_PREFILL_ADDC", "1") != "1":
+        return False
+    if not (a.is_cuda and b.is_cuda and c.is_cuda) or any(t.dtype != torch.bfloat16 for t in (a, b, c)):
+        return False
+    if a.stride(1) != 1 or b.stride(1) != 1 or c.stride(1) != 1 or a.dim() != 2 or b.dim() != 2 or c.dim() != 2:
+        return False
+    M, K = a.shape
+    N = b.shape[0]
+    if b.shape[1] != K or tuple(c.shape) != (M, N):
+        return False
+    return bool(_lib.lib().kgs_gemm_bf16_nt_w4_ok(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0),
+                                                   b.stride(0), c.stride(0)))
+
+
+def gemm_nt_add_(a: torch.Tensor, b: torch.Tensor, c: torch.Tensor) -> torch.Tensor:
+    """In place ``c = bf16(c + bf16(a @ b.T))``: a projection whose residual add
+    runs in the GEMM's store (EPI_ADDC), with the roundings of ``gemm_nt`` followed
+    by ``add_rmsnorm``'s add. Aligned four-wave operands only (:func:`addc_ok`);
+    persistent above one tile per CU."""
+    if not addc_ok(a, b, c):
+        raise ValueError("gemm_nt_add_: operands outside the aligned four-wave path (see addc_ok)")
+    M, K = a.shape
+    N = b.shape[0]
+    rc = _lib.lib().kgs_gemm_bf16_nt_addc(a.data_ptr(), b.data_ptr(), c.data_ptr(), M, N, K, a.stride(0), b.stride(0),
+                                          c.stride(0), _lib.stream_handle(a.device))
+    _lib.check(rc, f"gemm_nt_add_[{M}x{N}x{K}]")
+    return c
 
 
 def gemm_nt_w4x_partials(a: torch.Tensor, b, bn: int, nslice: int, bm: int = 256, stages: int = 2,

@@ -237,6 +237,20 @@ class ServingModel:
 
         return add_rmsnorm(x, d, w, self.cfg.eps)
 
+    def _proj_add_norm(self, a, layer: int, name: str, x, w):
+        """Prompt pass: x += a @ W.T, return rmsnorm(x) * w. On kgs with aligned
+        operands the residual add runs in the GEMM's store (EPI_ADDC) and the
+        norm reads x once: bitwise the GEMM + add_rmsnorm pair, with one
+        [rows, hidden] tensor fewer through HBM (profiles/r5/prefill_swiglu)."""
+        if self.backend == "kgs":
+            from kgs.ops.gemm import addc_ok, gemm_nt_add_
+
+            wt = self.w[layer][name]
+            if addc_ok(a, wt, x):
+                gemm_nt_add_(a, wt, x)
+                return self._norm(x, None, w)
+        return self._norm(x, self._proj(a, layer, name, False), w)
+
     def _gate_up_act(self, y, layer):
         """Prompt-pass SwiGLU MLP input: fused into the GEMM epilogue on kgs."""
         if self.backend == "kgs" and self.fuse_splitk:
@@ -284,12 +298,12 @@ class ServingModel:
             T.op(f"prefill L{i} rope_cache")
             a = self._prefill_attention(qkv, seq_starts, seq_lens, padded_lens)
             T.op(f"prefill L{i} attention")
-            y = self._norm(x, self._proj(a, i, "o", False), self.ln2[i])
+            y = self._proj_add_norm(a, i, "o", x, self.ln2[i])
             T.op(f"prefill L{i} o+norm")
             act = self._gate_up_act(y, i)
             T.op(f"prefill L{i} gate_up")
             nxt = self.ln1[i + 1] if i + 1 < c.layers else self.norm
-            y = self._norm(x, self._proj(act, i, "down", False), nxt)
+            y = self._proj_add_norm(act, i, "down", x, nxt)
             T.op(f"prefill L{i} down+norm")
         last = torch.as_tensor([int(s) + int(n) - 1 for s, n in zip(seq_starts, seq_lens)], device=y.device)
         yl = y[last].contiguous()

@@ -281,6 +281,36 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
 // four-wave kernel on smaller tiles: 256x128 / 128x256 up to 128 tiles, 128x128
 // up to 64 -- 1.13-1.23x hipBLASLt there, where 256x256 tiles leave CUs idle
 // (profiles/r3/gemm_small_grid.json).
+// C[M, N] = bf16(C + bf16(A . B^T)): a projection with the residual add in its
+// epilogue (EPI_ADDC; the prompt pass's o / down, whose add_rmsnorm becomes a
+// plain rmsnorm -- same roundings, so bitwise the unfused pair). The aligned
+// four-wave path only (kgs_gemm_bf16_nt_w4_ok); persistent with more tiles
+// than CUs, else the one-shot grid (tall problems in the mirrored order).
+KGS_EXPORT int kgs_gemm_bf16_nt_addc(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                     int ldc, hipStream_t stream) {
+  using namespace kgs;
+  if (M <= 0 || N <= 0 || K <= 0 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (!kgs_gemm_bf16_nt_w4_ok(A, B, C, M, N, K, lda, ldb, ldc)) return KGS_ERR_ALIGN;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  const long tiles = (long)(M / 256) * (N / 256);
+  int* tq = (K >= 384 && tiles > cu_count()) ? tile_queue(stream) : nullptr;
+  if (tq) {
+    const hipError_t e = launch_w4p<EPI_ADDC>(a, b, c, nullptr, M, N, K, lda, ldb, ldc, cu_count(), tq, stream);
+    return e == hipSuccess ? 0 : (int)e;
+  }
+  using Kn = w4::Knobs<256, 256>;
+  const dim3 grid((unsigned)tiles);
+  if (M > N)
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_ADDC, 256, 0, Kn::B1, Kn::R, Kn::P, Kn::ORD, 140000000>), grid, dim3(256), 0,
+                       stream, a, b, c, nullptr, M, N, K, lda, ldb, ldc);
+  else
+    hipLaunchKernelGGL((w4::gemm_nt_w4<EPI_ADDC>), grid, dim3(256), 0, stream, a, b, c, nullptr, M, N, K, lda, ldb,
+                       ldc);
+  return (int)hipGetLastError();
+}
+
 KGS_EXPORT int kgs_gemm_bf16_nt(const void* A, const void* B, void* C, const void* bias, int M, int N, int K, int lda,
                                 int ldb, int ldc, int epi, int variant, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return KGS_ERR_SHAPE;

@@ -56,6 +56,7 @@ KGS_LAUNCH_W4P(EPI_BIAS)
 KGS_LAUNCH_W4P(EPI_BIAS_GELU)
 KGS_LAUNCH_W4P(EPI_BIAS_RELU)
 KGS_LAUNCH_W4P(EPI_BIAS_SILU)
+KGS_LAUNCH_W4P(EPI_ADDC)
 #undef KGS_LAUNCH_W4P
 
 // fp8 (e4m3): lengths and leading dimensions of A / B in 16-bit words

@@ -611,7 +611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int n = 0; n < NB; ++n) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[n][e] = 0.f;
-    if constexpr (EPI != EPI_NONE) {
+    if constexpr (epi_bias<EPI>()) {
       const bf16x4 bb = *(const bf16x4*)(bias + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[n][e] = bf2f((unsigned short)bb[e]);
@@ -622,6 +622,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
     unsigned short* crow = C + (long)row * ldc;
     const bool row_ok = !BNDM || row < M;
+    // EPI_ADDC: the row group's residual chunks are loaded together, before
+    // the first store (one memory latency per group, not one per store)
+    uint4 old[NB / 2];
+    if constexpr (EPI == EPI_ADDC) {
+#pragma unroll
+      for (int p = 0; p < NB / 2; ++p)
+        old[p] = row_ok ? *(const uint4*)(crow + tn * BN + c.wc * (BN / 2) + p * 32 + (fq & 1) * 16 + (fq >> 1) * 8)
+                        : make_uint4(0, 0, 0, 0);
+    }
     f32x4 vr[NB];
     read_row<NB, i>(vr);
 #pragma unroll
@@ -637,7 +646,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
       const uint4 qv = make_uint4(sx[0], sy[0], sx[1], sy[1]);
       const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
-      if (row_ok) *(uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8) = qv;
+      uint4* dst = (uint4*)(crow + col0 + (fq & 1) * 16 + (fq >> 1) * 8);
+      if constexpr (EPI == EPI_ADDC) {
+        if (row_ok) *dst = add_bf16x8(old[n / 2], qv);
+      } else {
+        if (row_ok) *dst = qv;
+      }
     }
   });
 }

@@ -256,6 +256,36 @@ __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ 
   }
 }
 
+// Residual-add epilogue (EPI_ADDC): row group I's four 16-B residual chunks
+// per lane (`old`) were loaded before its stores, and group I + 1's are issued
+// before group I's stores, so a tile's epilogue waits out about one memory
+// latency instead of one per store (32 per wave): +15 % on the prompt pass's o
+// projection when each store read its chunk itself.
+template <int I>
+__device__ __forceinline__ void pepi_addc(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn,
+                                          const uint4 (&old)[NB / 2]) {
+  if constexpr (I < MA) {
+    const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+    unsigned short* rowp = C + (long)(tm * BM + c.wr * (BM / 2) + I * 16 + fr) * ldc + tn * BN + c.wc * (BN / 2) +
+                           (fq & 1) * 16 + (fq >> 1) * 8;
+    uint4 nxt[NB / 2];
+    if constexpr (I + 1 < MA) {
+#pragma unroll
+      for (int p = 0; p < NB / 2; ++p) nxt[p] = *(const uint4*)(rowp + 16L * ldc + p * 32);
+    }
+    w4::static_for<0, NB / 2>([&](auto pc) {
+      constexpr int p = decltype(pc)::value, q = I * NB + 2 * p;
+      const f32x4 v0 = accr::read<q>(), v1 = accr::read<q + 1>();
+      const unsigned x0 = pack_bf16x2(v0[0], v0[1]), y0 = pack_bf16x2(v0[2], v0[3]);
+      const unsigned x1 = pack_bf16x2(v1[0], v1[1]), y1 = pack_bf16x2(v1[2], v1[3]);
+      auto sx = __builtin_amdgcn_permlane16_swap(x0, x1, false, false);
+      auto sy = __builtin_amdgcn_permlane16_swap(y0, y1, false, false);
+      *(uint4*)(rowp + p * 32) = add_bf16x8(old[p], make_uint4(sx[0], sy[0], sx[1], sy[1]));
+    });
+    pepi_addc<I + 1>(c, C, ldc, tm, tn, nxt);
+  }
+}
+
 // SwiGLU epilogue (X's SW digit, gemm_w4.h's one-shot SW epilogue on named
 // accumulators): B's 256 rows of a tile are 128 gate and 128 up rows staged in
 // alternating 32-row DMA groups, so a wave's fragment columns ng = 0, 1, 4, 5
@@ -351,6 +381,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // are 256 B rows = 128 gate + 128 up, ntn = N / 256
   constexpr bool SW = (X / 1000000) % 10 != 0;
   static_assert(!SW || (EPI == EPI_NONE && L == 0 && !NTST), "SwiGLU: no bias, production layout");
+  static_assert(EPI != EPI_ADDC || !NTST, "the residual add reads C");
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {
@@ -469,14 +500,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int n = 0; n < NB; ++n) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) bv[n][e] = 0.f;
-        if constexpr (EPI != EPI_NONE) {
+        if constexpr (epi_bias<EPI>()) {
           const bf16x4 bb = *(const bf16x4*)(bias + tn * BN + c.wc * (BN / 2) + n * 16 + fq * 4);
 #pragma unroll
           for (int e = 0; e < 4; ++e) bv[n][e] = bf2f((unsigned short)bb[e]);
         }
       }
     }
-    if constexpr (!SW) pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
+    if constexpr (EPI == EPI_ADDC) {
+      const int fr = lane & 15, fq = lane >> 4;
+      const unsigned short* r0 =
+          C + (long)(tm * BM + c.wr * (BM / 2) + fr) * ldc + tn * BN + c.wc * (BN / 2) + (fq & 1) * 16 + (fq >> 1) * 8;
+      uint4 old0[NB / 2];
+#pragma unroll
+      for (int p = 0; p < NB / 2; ++p) old0[p] = *(const uint4*)(r0 + p * 32);
+      pepi_addc<0>(c, C, ldc, tm, tn, old0);
+    } else if constexpr (!SW) {
+      pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
+    }
     if constexpr (TS) {
       const long long te = (long long)__builtin_amdgcn_s_memrealtime();
       if (threadIdx.x == 0 && ntile_done < 11) ts[2 + ntile_done] = te;

@@ -62,6 +62,20 @@ __device__ __forceinline__ unsigned pack_bf16x2(float lo, float hi) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2_t));
 }
 
+// 8 bf16 (one 16-B store's worth): bf16(x + d) per element, as add_rmsnorm rounds
+// the residual add (EPI_ADDC: x the stored residual, d the rounded product).
+__device__ __forceinline__ uint4 add_bf16x8(uint4 x, uint4 d) {
+  const unsigned xs[4] = {x.x, x.y, x.z, x.w}, ds[4] = {d.x, d.y, d.z, d.w};
+  unsigned o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float lo = bf2f((unsigned short)(xs[k] & 0xffff)) + bf2f((unsigned short)(ds[k] & 0xffff));
+    const float hi = bf2f((unsigned short)(xs[k] >> 16)) + bf2f((unsigned short)(ds[k] >> 16));
+    o[k] = pack_bf16x2(lo, hi);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 // s[base .. base + 7] -> a bf16x8 MFMA fragment, four v_cvt_pk_bf16_f32
 template <class V>
 __device__ __forceinline__ bf16x8 pack_bf16x8(const V& s, int base) {
@@ -114,7 +128,13 @@ __host__ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 }
 
 // Epilogue activations (fused into the GEMM store).
-enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_SILU = 4 };
+// EPI_ADDC: C = bf16(C + bf16(acc)), the residual add of a projection read and
+// written in the store (round 5, the prompt pass's o / down: add_rmsnorm's add
+// with the same two roundings, leaving it a plain rmsnorm). No bias.
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_SILU = 4, EPI_ADDC = 5 };
+
+template <int EPI>
+constexpr bool epi_bias() { return EPI != EPI_NONE && EPI != EPI_ADDC; }
 
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
@@ -128,7 +148,7 @@ __device__ __forceinline__ float gelu_tanh(float x) {
 
 template <int EPI>
 __device__ __forceinline__ float epilogue(float v, float b) {
-  if constexpr (EPI == EPI_NONE) return v;
+  if constexpr (EPI == EPI_NONE || EPI == EPI_ADDC) return v;
   v += b;
   if constexpr (EPI == EPI_BIAS_GELU) return gelu_tanh(v);
   if constexpr (EPI == EPI_BIAS_RELU) return v > 0.f ? v : 0.f;

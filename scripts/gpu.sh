@@ -169,6 +169,16 @@ step() {
             run prefill_head 300 python -u -m kgs.models.llama --backends kgs &&
             (export KGS_KERNELS_LIB=$LIB_B; run prefill_libb 300 python -u -m kgs.models.llama --backends kgs) ;;
         mall_prefetch) run mall_prefetch 300 python bench/mall_prefetch_probe.py --out "$O/mall_prefetch.json" ;;
+        addc_ab)  # prompt-pass residual add in the GEMM store (KGS_PREFILL_ADDC) on / off: serving b256 + prefill bench
+            local SB="python -u -m kgs.serve bench --requests 256 --input-len 512 --output-len 256"
+            SB="$SB --max-batch 256 --max-model-len 2048"
+            for r in 1 2; do
+                (export KGS_PREFILL_ADDC=1; run serve_addc1_$r 300 $SB) &&
+                (export KGS_PREFILL_ADDC=0; run serve_addc0_$r 300 $SB) &&
+                (export KGS_PREFILL_ADDC=1; run prefill_addc1_$r 300 python -u -m kgs.models.llama --backends kgs) &&
+                (export KGS_PREFILL_ADDC=0; run prefill_addc0_$r 300 python -u -m kgs.models.llama --backends kgs) ||
+                    return 1
+            done ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"

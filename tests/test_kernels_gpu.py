@@ -527,6 +527,33 @@ def test_gemm_w4x_swiglu_epilogue(M, I, K, bn, bm):
     assert ((fused.float() - r32).abs().max() / r32.abs().max()).item() < 2e-2
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 4096, 4096), (4096, 8192, 1024), (4096, 4096, 4096), (2048, 1024, 4096),
+                                   (1024, 512, 768), (16384, 4096, 1024)])
+def test_residual_add_epilogue_is_bitwise_gemm_then_add(M, N, K):
+    """Round 5: the prompt pass's o / down GEMM with the residual add in its
+    store (EPI_ADDC; persistent and one-shot grids, tall and wide) leaves x
+    bitwise where gemm_nt + add_rmsnorm's add leaves it, and the plain rmsnorm
+    after it gives add_rmsnorm's normalised rows."""
+    from kgs.ops import gemm_nt
+    from kgs.ops.gemm import addc_ok, gemm_nt_add_
+    from kgs.ops.transformer import add_rmsnorm
+
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    a = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b = ((torch.rand(N, K, device=DEV, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
+    x0 = (torch.rand(M, N, device=DEV, generator=g) * 4 - 2).bfloat16()
+    w = (torch.rand(N, device=DEV, generator=g) + 0.5).bfloat16()
+    x_ref = x0.clone()
+    y_ref = add_rmsnorm(x_ref, gemm_nt(a, b), w)
+    x = x0.clone()
+    assert addc_ok(a, b, x)
+    gemm_nt_add_(a, b, x)
+    torch.cuda.synchronize()
+    assert torch.equal(x, x_ref)
+    assert torch.equal(add_rmsnorm(x, None, w), y_ref)
+    assert not addc_ok(a[: M - 8], b, x[: M - 8])  # unaligned rows: the caller keeps the unfused pair
+
+
 @pytest.mark.parametrize("M,I,K", [(2048, 8192, 1024), (1024, 14336, 4096), (4096, 4096, 768)])
 def test_prompt_swiglu_on_the_persistent_kernel(M, I, K):
     """Round 5: the prompt pass's gate|up (256 x 256 tiles, aligned M, more tiles
