@@ -636,7 +636,9 @@ __global__ __launch_bounds__(256) void rope_cache(unsigned short* __restrict__ q
 // many bytes again as the qkv rows, all through L1 -- and the 8 heads' 16 row
 // loads are issued before the first rotation. Same arithmetic per element
 // (bitwise the per-head form's result).
-template <bool KV8>
+// VSEP: the v heads are left to v_cache_pages (below): this kernel neither
+// loads nor writes them.
+template <bool KV8, bool VSEP = false>
 __global__ __launch_bounds__(256) void rope_cache_g8(unsigned short* __restrict__ qkv, const float* __restrict__ cosv,
                                                      const float* __restrict__ sinv, const int* __restrict__ pos,
                                                      const int* __restrict__ slot, void* __restrict__ cache,
@@ -647,6 +649,7 @@ __global__ __launch_bounds__(256) void rope_cache_g8(unsigned short* __restrict_
   const long t = idx / (ng * 8);
   const int rem = (int)(idx - t * ng * 8);
   const int g = rem >> 3, c = rem & 7;
+  if (VSEP && g * 8 >= H + HKV) return;  // a group of v heads only
   const int p = pos[t];
   const int sl = slot[t];
   unsigned short* base = qkv + t * ld + (long)g * 8 * HD + 8 * c;
@@ -677,7 +680,56 @@ __global__ __launch_bounds__(256) void rope_cache_g8(unsigned short* __restrict_
       a[j] = o1;
       b[j] = o2;
     }
-    if (h >= H && sl >= 0) kv_write<KV8>(cache, sl, h, H, HKV, c, a[j], b[j]);
+    if (h >= H && sl >= 0 && !(VSEP && h >= H + HKV)) kv_write<KV8>(cache, sl, h, H, HKV, c, a[j], b[j]);
+  }
+}
+
+// The prompt pass's V rows into the paged bf16 cache, one (run of 32 tokens,
+// KV head) per workgroup. The V page layout is transposed (kv_v_index: a 16-B
+// chunk holds one dim of 8 tokens), so a per-token writer stores 2 bytes at a
+// time. Here the run's 32 x 128 values are staged in LDS and, when its slots
+// fill one page in order (a prompt written from a page boundary), written as
+// the page's 512 whole chunks; any other run goes element by element, exactly
+// as kv_write.
+__global__ __launch_bounds__(256) void v_cache_pages(const unsigned short* __restrict__ qkv,
+                                                     const int* __restrict__ slot, unsigned short* __restrict__ cache,
+                                                     long tokens, int H, int HKV, long ld) {
+  __shared__ unsigned short vs[PAGE][HD + 8];
+  __shared__ int sl[PAGE];
+  __shared__ int fast;
+  const long t0 = (long)blockIdx.x * PAGE;
+  const int kvh = blockIdx.y, tid = threadIdx.x;
+  if (tid < PAGE) sl[tid] = t0 + tid < tokens ? slot[t0 + tid] : -1;
+  for (int k = tid; k < PAGE * (HD / 8); k += 256) {
+    const int r = k / (HD / 8), ch = k % (HD / 8);
+    const long t = t0 + r;
+    const uint4 v = t < tokens ? *(const uint4*)(qkv + t * ld + (long)(H + HKV + kvh) * HD + ch * 8)
+                               : make_uint4(0, 0, 0, 0);
+    *(uint4*)&vs[r][ch * 8] = v;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int ok = sl[0] >= 0 && sl[0] % PAGE == 0;
+    for (int i = 1; i < PAGE && ok; ++i) ok = sl[i] == sl[0] + i;
+    fast = ok;
+  }
+  __syncthreads();
+  if (fast) {
+    unsigned short* pg = cache + (((long)(sl[0] / PAGE) * HKV + kvh) * 2 + 1) * PAGE_ELEMS;
+    for (int k = tid; k < PAGE_ELEMS / 8; k += 256) {  // chunk k = dt * 64 + g * 16 + m
+      const int d = (k >> 6) * 16 + (k & 15), g = (k >> 4) & 3;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (short)vs[4 * g + (j & 3) + 16 * (j >> 2)][d];
+      *(bf16x8*)(pg + k * 8) = o;
+    }
+  } else {
+    for (int k = tid; k < PAGE * HD; k += 256) {
+      const int r = k / HD, d = k % HD, s = sl[r];
+      if (s < 0) continue;
+      unsigned short* pg = cache + (((long)(s / PAGE) * HKV + kvh) * 2 + 1) * PAGE_ELEMS;
+      pg[kv_v_index(s % PAGE, d)] = vs[r][d];
+    }
   }
 }
 
@@ -1245,6 +1297,14 @@ KGS_EXPORT int kgs_rope_cache_bf16(void* qkv, const float* cosv, const float* si
     }
 #undef KGS_RCS_KV
 #undef KGS_RCS
+  } else if ((H + 2 * HKV) % 8 == 0 && !kv8 && tokens >= 1024) {
+    // prompt-sized: the v heads go through the page-run writer
+    const dim3 g8((unsigned)((n / 8 + 255) / 256));
+    hipLaunchKernelGGL((kgs::dec::rope_cache_g8<false, true>), g8, b, 0, s, q, cosv, sinv, pos, slot, cache, tokens, H,
+                       HKV, ld);
+    const dim3 gv((unsigned)((tokens + kgs::dec::PAGE - 1) / kgs::dec::PAGE), (unsigned)HKV);
+    hipLaunchKernelGGL(kgs::dec::v_cache_pages, gv, b, 0, s, (const unsigned short*)q, slot, (unsigned short*)cache,
+                       tokens, H, HKV, ld);
   } else if ((H + 2 * HKV) % 8 == 0) {
     const dim3 g8((unsigned)((n / 8 + 255) / 256));
     if (kv8)

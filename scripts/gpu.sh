@@ -179,6 +179,8 @@ step() {
                 (export KGS_PREFILL_ADDC=0; run prefill_addc0_$r 300 python -u -m kgs.models.llama --backends kgs) ||
                     return 1
             done ;;
+        rope_probe) run rope_probe 200 python bench/rope_cache_probe.py &&
+            (export KGS_KERNELS_LIB=$LIB_B; run rope_probe_libb 200 python bench/rope_cache_probe.py) ;;
         serve_nt_rep)  # the round-4 faulting configuration (batch $B, output 256, nt on) twice, nt off,
             # then nt on under a kernel trace (the last dispatches name a faulting kernel)
             local SB="python -u -m kgs.serve bench --requests ${B:-256} --input-len 512 --output-len 256"

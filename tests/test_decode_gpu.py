@@ -540,3 +540,51 @@ def test_nt_weight_loads_are_bitwise_the_default_policy(M):
     assert torch.equal(gemm_nt_w4x_swiglu(x, w, bn=128, nt_weights=True), gemm_nt_w4x_swiglu(x, w, bn=128))
     assert torch.equal(gemm_nt_w4x(x, w, bn=128, nt_weights=True), gemm_nt_w4x(x, w, bn=128))
     assert torch.equal(gemm_nt_w4x(x, w, bn=128, nslice=4, nt_weights=True), gemm_nt_w4x(x, w, bn=128, nslice=4))
+
+
+def test_prompt_rope_cache_v_page_runs():
+    """Round 5: at prompt sizes (>= 1024 rows) the v heads are written by
+    v_cache_pages -- whole 16-B chunks of the transposed V page when a 32-token
+    run fills one page in order, element by element otherwise. Runs from a
+    page boundary, a chunk starting mid-page, padding rows (slot -1) and a tail
+    shorter than a page: the cache equals the reference scatter of the
+    kernel's own rotated k and v, and the q / k rotation equals the short-input
+    (per-token) path's."""
+    from kgs.ops.decode import PAGE, PagedKVCache, ref_cache_write, rope_cache_
+    from kgs.ops.transformer import rope_tables
+
+    heads, hkv, hd = 32, 8, 128
+    width = (heads + 2 * hkv) * hd
+    cos, sin = rope_tables(4096, hd, 500000.0, DEV)
+    pos, slots = [], []
+    page = 1
+    for n, start in ((700, 0), (333, 0), (300, 40)):  # (tokens, context already cached)
+        off = start % PAGE  # 40: this chunk starts 8 tokens into its first page
+        for t in range(n):
+            pos.append(start + t)
+            slots.append(page * PAGE + off + t)
+        page += (off + n + PAGE - 1) // PAGE + 1
+        pos += [0] * 5  # padding rows between sequences
+        slots += [-1] * 5
+    T = len(pos)
+    assert T >= 1024
+    npages = page + 4
+    qkv = _bf(T, width)
+    pos_t = torch.tensor(pos, dtype=torch.int32, device=DEV)
+    slot_t = torch.tensor(slots, dtype=torch.int32, device=DEV)
+    cache = PagedKVCache(1, npages, hkv, DEV)
+    orig = qkv.clone()
+    rope_cache_(qkv, cos, sin, pos_t, slot_t, cache.layer(0), heads, hkv)
+    # the per-token path on the same rows, 1000 at a time (below the prompt threshold)
+    q2 = orig.clone()
+    cache2 = PagedKVCache(1, npages, hkv, DEV)
+    for s0 in range(0, T, 1000):
+        rope_cache_(q2[s0:s0 + 1000], cos, sin, pos_t[s0:s0 + 1000], slot_t[s0:s0 + 1000], cache2.layer(0), heads, hkv)
+    torch.cuda.synchronize()
+    assert torch.equal(qkv, q2)
+    assert torch.equal(cache.layer(0), cache2.layer(0))
+    ref = torch.zeros_like(cache.layer(0))
+    k = qkv[:, heads * hd:(heads + hkv) * hd].reshape(-1, hkv, hd)
+    v = qkv[:, (heads + hkv) * hd:].reshape(-1, hkv, hd)
+    ref_cache_write(ref, k, v, slot_t)
+    assert torch.equal(cache.layer(0), ref)
