@@ -385,8 +385,8 @@ def main(argv=None) -> int:
                     help="rows per mixed prompt-chunk + decode step (0 = whole-prompt prefill steps)")
     ap.add_argument("--prefix-caching", action="store_true", help="reuse cached pages of shared prompt prefixes")
     ap.add_argument("--overlap", action=argparse.BooleanOptionalAction, default=False,
-                    help="overlapped engine steps: ~5 %% lower TPOT, but a request arriving while a step is in "
-                         "flight waits one step more for its first token (profiles/r5/overlap/README.md)")
+                    help="overlapped engine steps: ~7 %% lower TPOT for a few ms more TTFT (a request arriving "
+                         "while a step is in flight misses that step; profiles/r5/overlap/README.md)")
     ap.add_argument("--kv-cache-dtype", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--decode-weights", choices=("bf16", "fp8"), default="bf16")
     ap.add_argument("--prefill-weights", choices=("bf16", "fp8"), default="bf16",

@@ -235,9 +235,8 @@ def main(argv=None) -> int:
                     help="gc.collect() + gc.freeze() after warm-up (A/B: collector pauses in the step loop)")
     ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
                     help="plan and launch step t+1 before step t's tokens are read back (EngineConfig.overlap). "
-                         "auto: on offline, off online -- a request arriving while a step is in flight then waits "
-                         "one more step for its first token (TTFT p50 +19 ms at 32 req/s) for a 5 %% lower TPOT "
-                         "(profiles/r5/overlap/README.md)")
+                         "auto: on offline, off online -- online it trades TTFT for TPOT (32 req/s: TTFT p50 "
+                         "+4 ms, TPOT -7 %%; profiles/r5/overlap/README.md)")
     ap.add_argument("--no-gate-up-panels", action="store_true",
                     help="unsplit SwiGLU decode routes read the row-major gate|up (A/B against the panel copies)")
     ap.add_argument("--fused-max-batch", type=int, default=48,

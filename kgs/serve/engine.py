@@ -134,6 +134,7 @@ class LLMEngine:
         # synchronise per step: those run one step at a time.
         self.overlap = cfg.overlap and not cfg.prefix_caching and not self.tq_check and not TRACE.sync_ops
         self._inflight: dict | None = None
+        self._arrived = False  # add_request since the last plan (see step())
         # KGS_HOST_PHASES=1: per step, the host time of each phase (host_phases()), to find host stalls
         self._phases = [] if os.environ.get("KGS_HOST_PHASES", "0") == "1" else None
         self._pinned = None  # two host buffers the in-flight tokens are copied into, alternately
@@ -176,6 +177,7 @@ class LLMEngine:
             self._seeded.add(rid)
         if not params.ignore_eos:
             self._watch_eos.add(rid)
+        self._arrived = True
         return rid
 
     def abort(self, rid: int) -> None:
@@ -216,9 +218,15 @@ class LLMEngine:
         ph = self._phases
         t = [time.perf_counter()] if ph is not None else None
         prev = self._inflight
-        if prev is not None and not self._overlap_now():
+        if prev is not None and (not self._overlap_now() or self._arrived):
+            # a request added since the step in flight was planned would only join
+            # the step after next (one more step to its first token): finish the
+            # step in flight first and plan the next one with it, as the
+            # sequential engine does; overlap resumes from there
             self._inflight = None
+            self._arrived = False
             return self._complete(prev, advanced=None)
+        self._arrived = False
         advanced = self.sched.update_pending(prev["ids"]) if prev is not None else None
         plan = self.sched.schedule()
         if t is not None:
