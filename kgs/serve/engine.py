@@ -129,10 +129,9 @@ class LLMEngine:
         self._seeded: set = set()
         self._watch_eos: set = set()  # requests whose tokens are checked for EOS / stop ids
         # Overlapped steps: step t+1 is planned and launched while step t runs,
-        # and step t's tokens are read back after that (see step()). Prefix
-        # caching hashes pages from token values, and the debug modes
-        # synchronise per step: those run one step at a time.
-        self.overlap = cfg.overlap and not cfg.prefix_caching and not self.tq_check and not TRACE.sync_ops
+        # and step t's tokens are read back after that (see step()). The debug
+        # modes synchronise per step: those run one step at a time.
+        self.overlap = cfg.overlap and not self.tq_check and not TRACE.sync_ops
         self._inflight: dict | None = None
         self._arrived = False  # add_request since the last plan (see step())
         # KGS_HOST_PHASES=1: per step, the host time of each phase (host_phases()), to find host stalls

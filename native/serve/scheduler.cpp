@@ -130,8 +130,12 @@ int Scheduler::match_prefix(Sequence& s) {
 
 void Scheduler::register_full_pages(Sequence& s) {
   const int ps = cfg_.page_size;
-  while ((s.hashed + 1) * ps <= s.cached && s.hashed < (int)s.pages.size()) {
+  while ((s.hashed + 1) * ps <= s.cached && s.hashed < (int)s.pages.size() &&
+         (s.hashed + 1) * ps <= (int)s.tokens.size()) {
     const int32_t* t = s.tokens.data() + s.hashed * ps;
+    // a page whose last generated token is still pending (overlapped engine
+    // steps) is registered by fill_pending, once the value is known
+    if (std::find(t, t + ps, kPendingToken) != t + ps) break;
     const uint64_t h = page_hash(s.tail_hash, t, ps);
     alloc_.register_page(s.pages[s.hashed], h, s.tail_hash, t, ps);
     s.tail_hash = h;
@@ -441,6 +445,7 @@ int Scheduler::fill_pending(const std::vector<int64_t>& ids, const std::vector<i
     if (!t.empty() && t.back() == kPendingToken) {
       t.back() = toks[i];
       ++n;
+      if (cfg_.prefix_caching && it->second.state == SeqState::kRunning) register_full_pages(it->second);
     }
   }
   return n;

@@ -133,7 +133,9 @@ class Scheduler {
   // lengths, page needs and length stops as update() with no eos), so the next
   // step can be scheduled before the sampled values are known; fill_pending()
   // writes the values in once they are (a sequence's pending token is always
-  // its last one: nothing else appends between the two calls). A stop on EOS,
+  // its last one: nothing else appends between the two calls). With prefix
+  // caching, a full page holding a pending token is registered by fill_pending
+  // (its hash needs the value). A stop on EOS,
   // seen one step late, goes through abort(). Returns the ids that finished /
   // the number of tokens filled.
   static constexpr int32_t kPendingToken = -1;

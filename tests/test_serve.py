@@ -964,3 +964,33 @@ def test_abort_while_a_step_is_in_flight():
         assert eng.sched.check_invariants() == "" and eng.sched.num_free_pages == 63
         res[ov] = [(x.output, x.finish_reason) for x in (r[0], r[2])]
     assert res[True] == res[False]
+
+
+def test_overlapped_steps_with_prefix_caching():
+    """Prefix caching under overlapped steps: a page completed by a generated
+    token that is still pending is registered once fill_pending knows the
+    token (its hash needs it). A follow-up turn whose prompt is an earlier
+    prompt + its answer hits the generated pages, and every generation equals
+    the sequential engine's."""
+    from kgs.serve import EngineConfig, LLMEngine, SamplingParams
+
+    rng = np.random.default_rng(17)
+    system = rng.integers(3, 512, size=300).tolist()
+    prompts = [system + rng.integers(3, 512, size=n).tolist() for n in (5, 40, 77)]
+    res = {}
+    for ov in (False, True):
+        eng = LLMEngine(_tiny(), EngineConfig(num_pages=128, max_batch=4, max_model_len=1024, cuda_graphs=False,
+                                              prefix_caching=True, chunked_prefill=256, overlap=ov),
+                        device="cpu", backend="ref")
+        assert eng.overlap == ov
+        p = SamplingParams(max_tokens=40, ignore_eos=True)
+        first = eng.generate(prompts, p)
+        # second turn: prompt + answer + a new question -> the answer's full pages are cached
+        turn2 = [q + r.output + [7, 8, 9] for q, r in zip(prompts, first)]
+        hits0 = eng.sched.prefix_hit_tokens
+        second = eng.generate(turn2, SamplingParams(max_tokens=6, ignore_eos=True))
+        hits = eng.sched.prefix_hit_tokens - hits0
+        assert eng.sched.check_invariants() == ""
+        res[ov] = ([r.output for r in first], [r.output for r in second], hits)
+    assert res[True][0] == res[False][0] and res[True][1] == res[False][1]
+    assert res[True][2] == res[False][2] and res[True][2] >= 3 * 320  # system prompt + generated pages
