@@ -994,3 +994,53 @@ def test_overlapped_steps_with_prefix_caching():
         res[ov] = ([r.output for r in first], [r.output for r in second], hits)
     assert res[True][0] == res[False][0] and res[True][1] == res[False][1]
     assert res[True][2] == res[False][2] and res[True][2] >= 3 * 320  # system prompt + generated pages
+
+
+@settings(max_examples=50, deadline=None)
+@given(st.lists(st.tuples(st.integers(0, 2), st.integers(1, 200), st.integers(1, 40)), min_size=1, max_size=20),
+       st.integers(12, 48), st.integers(1, 6), st.sampled_from([0, 128, 256]), st.booleans())
+def test_two_phase_random_traffic(reqs, pages, max_batch, chunk, prefix):
+    """The overlapped engine's scheduler protocol under random traffic: step
+    t+1 is planned after update_pending(t) and before fill_pending(t); late EOS
+    stops go through abort; preemption, chunking and prefix caching as they
+    come. Invariants hold every step, no pending token survives a fill, all
+    requests finish and no page leaks."""
+    c = _serve.SchedulerConfig()
+    c.num_pages, c.page_size, c.max_batch, c.max_model_len, c.pad_multiple = pages, 32, max_batch, 512, 128
+    c.max_prefill_tokens, c.chunk_tokens, c.prefix_caching = 1024, chunk, prefix
+    s = _serve.Scheduler(c)
+    P = _serve.Scheduler.PENDING
+    prefixes = [list(range(100 + 300 * k, 100 + 300 * k + 160)) for k in range(3)]
+    live = set()
+    for i, (k, extra, new) in enumerate(reqs):
+        if s.add(i, prefixes[k] + [3] * extra, new):
+            live.add(i)
+    rng = np.random.default_rng(0)
+    prev = None
+    for _ in range(4000):
+        if prev is not None:
+            for d in s.update_pending(prev):
+                live.discard(int(d))
+        p = s.schedule()
+        assert s.check_invariants() == "", s.check_invariants()
+        if prev is not None:  # step t's tokens arrive after step t+1 was planned
+            s.fill_pending(prev, np.full(len(prev), 4, np.int32))
+            for j in np.flatnonzero(rng.random(len(prev)) < 0.05):  # EOS seen one step late
+                if s.abort(int(prev[j])):
+                    live.discard(int(prev[j]))
+            for r in prev:
+                try:
+                    assert P not in s.tokens(int(r))
+                except KeyError:
+                    pass
+        if p.kind == 0:
+            prev = None
+            if not live:
+                break
+            continue
+        ids = p.seq_ids
+        if p.kind == 3:
+            ids = np.concatenate([ids[:p.n_prefill][p.last_chunk.astype(bool)], ids[p.n_prefill:]])
+        prev = np.asarray(ids, dtype=np.int64)
+    assert not live and s.num_running == 0 and s.num_waiting == 0
+    assert s.num_free_pages == pages - 1
