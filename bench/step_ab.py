@@ -79,9 +79,13 @@ def main(argv=None) -> int:
         return lambda i: gemm_nt(A, B, out=C[i & 1], variant=p)
 
     paths = {p: path(p) for p in a.paths.split(",")}
+    from kgs.ops.experiments import NO_OUTPUT
+
     for p, f in paths.items():  # numerics before timing
         f(0)
         torch.cuda.synchronize()
+        if p in NO_OUTPUT:  # a measurement build that does not write C
+            continue
         err = ((C[0][:256].float() - ref).abs().max() / ref.abs().max()).item()
         assert err < 1e-2, (p, err)
 

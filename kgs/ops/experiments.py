@@ -83,6 +83,12 @@ W4H.update({"w4pn_0": 131, "w4pn_140000008": 132, "w4pn_8": 133, "w4pn_140000000
 W4H.update({"w4pl_0": 135, "w4pl_140000008": 136, "w4pl_8": 137, "w4pl_140000000": 138})
 # round 4: MFMA order inside a k-sub: i-major (w4po0_X) / n-major (w4po2_X) instead of the growing square
 W4H.update({"w4po0_0": 139, "w4po2_0": 140, "w4po0_140000008": 141, "w4po2_140000008": 142})
+# round 5: C store measurement builds (gemm_w4p.h (L / 100) % 10): C not written (w4px_0, output
+# garbage) / s_waitcnt vmcnt(0) after each tile's stores (w4pd_0)
+W4H.update({"w4px_0": 143, "w4pd_0": 144})
+# ... and K-step 0 after an epilogue waiting vmcnt(ND + stores): w4pw_0
+W4H.update({"w4pw_0": 145})
+NO_OUTPUT = frozenset({"w4px_0"})  # timing only: C is not written
 
 
 @lru_cache(maxsize=1)

@@ -112,6 +112,19 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
         hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, false, 30>), pg, dim3(256), 0, s,
                            a, b, c, nullptr, M, N, K, lda, ldb, ldc, tq);
         break;
+      // round 5: C store measurement builds (gemm_w4p.h (L / 100) % 10): no store / drain after the stores
+      case 143:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 100>), pg, dim3(256), 0, s, a, b,
+                           c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 144:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 200>), pg, dim3(256), 0, s, a, b,
+                           c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
+      case 145:
+        hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 300>), pg, dim3(256), 0, s, a, b,
+                           c, nullptr, M, N, K, lda, ldb, ldc, tq);
+        break;
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)

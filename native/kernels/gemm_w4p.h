@@ -108,7 +108,7 @@ struct Lay<1> {
 
 // L / 10 (experiments): the MFMA order inside a k-sub, L / 10 - 1 (gemm_w4.h
 // make_order: 0 i-major, 1 growing square, 2 n-major); 0 = Knobs (growing square).
-constexpr int ord_of(int L) { return L / 10 ? L / 10 - 1 : Kn::ORD; }
+constexpr int ord_of(int L) { return (L / 10) % 10 ? (L / 10) % 10 - 1 : Kn::ORD; }
 
 template <int L>
 __device__ __forceinline__ const char* pabase(const Ctx& c, int st, int sub) {
@@ -164,7 +164,7 @@ struct Tick {
 // follows it. The DMA issues use `cd` (this tile's or the next tile's buffer
 // resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`. TK: 1 =
 // issue the ticket atomic after barrier 2, 2 = publish the ticket there.
-template <int ST, int X, bool ZERO, int TK, int K, int L = 0>
+template <int ST, int X, bool ZERO, int TK, int K, int L = 0, int WX = 0>
 __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
                                       Frag<MA, NB>& f1, Tick& tq) {
   constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = ord_of(L);
@@ -199,7 +199,7 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
       w4::bar();
     }
     if constexpr (K == KM - R - 1) {
-      w4::wait_vm<ND>();  // own DMA of the next K-tile landed
+      w4::wait_vm<ND + WX>();  // own DMA of the next K-tile landed (WX: younger stores, see the kernel)
       w4::bar();
       if constexpr (TK == 1) {
         if (threadIdx.x == 0) tq.tk = atomicAdd(tq.qx, 1);
@@ -207,12 +207,12 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
         if (threadIdx.x == 0) *tq.slot = tq.tk;
       }
     }
-    pbody<ST, X, ZERO, TK, K + 1, L>(c, cd, sp, f0, f1, tq);
+    pbody<ST, X, ZERO, TK, K + 1, L, WX>(c, cd, sp, f0, f1, tq);
   }
 }
 
 // One K-step on stage ST; its DMAs bring K-tile kd (of cd's tile) into ST.
-template <int ST, int X, bool ZERO, int TK = 0, int L = 0>
+template <int ST, int X, bool ZERO, int TK = 0, int L = 0, int WX = 0>
 __device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd,
                                       Tick& tq) {
   StepPtrs sp;
@@ -221,13 +221,13 @@ __device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>&
   sp.pa0 = pabase<L>(c, ST ^ 1, 0);
   sp.pb0 = pbbase<L>(c, ST ^ 1, 0);
   sp.k0 = kd * BK;
-  pbody<ST, X, ZERO, TK, 0, L>(c, cd, sp, f0, f1, tq);
+  pbody<ST, X, ZERO, TK, 0, L, WX>(c, cd, sp, f0, f1, tq);
 }
 
 // Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
 // bias + activation, pack to bf16, pair n-tiles with v_permlane16_swap -> one
 // 16-B store per lane (the one-shot kernel's epilogue, reading named AGPRs).
-template <int EPI, int Q, bool NTST = false>
+template <int EPI, int Q, bool NTST = false, int CST = 0>
 __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn,
                                      const float (&bv)[NB][4]) {
   if constexpr (Q < MA * NB) {
@@ -249,10 +249,12 @@ __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ 
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
       const u32x4 v = {qv.x, qv.y, qv.z, qv.w};
       __builtin_nontemporal_store(v, (u32x4*)dst);
+    } else if constexpr (CST == 1) {
+      if (ldc < 0) *dst = qv;  // measurement build: C is never written (ldc > 0), the packing stays
     } else {
       *dst = qv;
     }
-    pepi<EPI, Q + 2, NTST>(c, C, ldc, tm, tn, bv);
+    pepi<EPI, Q + 2, NTST, CST>(c, C, ldc, tm, tn, bv);
   }
 }
 
@@ -359,7 +361,12 @@ __device__ __forceinline__ void set_b(Ctx& c, const unsigned short* B, int tn, i
 // XCC_ID << 32, [2 + j] the end of its j-th tile's epilogue (j < 11), [13] its
 // exit (after the queue's exit counter / reset), [14] the end of its last tile,
 // [15] tiles.
-// L: LDS image layout (L % 10, Lay above) and MFMA order (L / 10, ord_of); 0 = production.
+// L: LDS image layout (L % 10, Lay above) and MFMA order ((L / 10) % 10, ord_of); 0 = production.
+// (L / 100) % 10, the C store (experiments only, EPI_NONE): 1 = no store (output not written),
+// 2 = s_waitcnt vmcnt(0) right after each tile's stores (measurement builds: how much of a tile
+// change waits on its stores -- gfx950 counts stores and loads in one vmcnt, so the next tile's
+// first DMA wait also covers them); 3 = that first wait counts the tile's stores as younger ops
+// (vmcnt(ND + stores)), so it waits for the next tile's K-tile 1 only.
 template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false, int L = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
@@ -382,6 +389,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr bool SW = (X / 1000000) % 10 != 0;
   static_assert(!SW || (EPI == EPI_NONE && L == 0 && !NTST), "SwiGLU: no bias, production layout");
   static_assert(EPI != EPI_ADDC || !NTST, "the residual add reads C");
+  constexpr int CST = (L / 100) % 10;
+  static_assert(CST == 0 || (EPI == EPI_NONE && !SW && !NTST && !TS), "store measurement builds: plain C only");
+  // CST 3: VMEM ops one epilogue issues per wave after the next tile's K-tile-1 DMAs (pepi: one
+  // 16-B store per accumulator pair). vmcnt completes in issue order, loads and stores alike (hipcc
+  // itself counts younger stores this way, e.g. vmcnt(3) over load, load, load, store); a count
+  // at most the true number keeps every K-tile-1 DMA outside the allowed ops.
+  constexpr int WXS = CST == 3 ? MA * NB / 2 : 0;
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {
@@ -449,7 +463,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   for (int st = 0; st < 2; ++st)
 #pragma unroll
     for (int j = 0; j < ND; ++j) pdma<L, X>(c, st, j, st * BK);
-  w4::wait_vm<ND>();
+  // CST 3: K-tile 1 too, so the first tile's K-step 0 (no epilogue before it) may wait vmcnt(ND + WXS)
+  if constexpr (WXS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else w4::wait_vm<ND>();
   w4::bar();
   Frag<MA, NB> f0, f1;
   {
@@ -474,7 +490,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   Tick tq{q + x + vzero, &tslot, 0};
   for (;;) {
-    pstep<0, X, true, DYN ? 1 : 0, L>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
+    pstep<0, X, true, DYN ? 1 : 0, L, WXS>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
     pstep<1, X, false, DYN ? 2 : 0, L>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
     for (int t = 2; t < nt - 2; t += 2) {
       pstep<0, X, false, 0, L>(c, c, f0, f1, t + 2, tq);
@@ -516,7 +532,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       for (int p = 0; p < NB / 2; ++p) old0[p] = *(const uint4*)(r0 + p * 32);
       pepi_addc<0>(c, C, ldc, tm, tn, old0);
     } else if constexpr (!SW) {
-      pepi<EPI, 0, NTST>(c, C, ldc, tm, tn, bv);
+      pepi<EPI, 0, NTST, CST>(c, C, ldc, tm, tn, bv);
+      if constexpr (CST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     if constexpr (TS) {
       const long long te = (long long)__builtin_amdgcn_s_memrealtime();
