@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   static_assert(CST == 0 || (EPI == EPI_NONE && !SW && !NTST && !TS), "store measurement builds: plain C only");
   // CST 3: VMEM ops one epilogue issues per wave after the next tile's K-tile-1 DMAs (pepi: one
   // 16-B store per accumulator pair). vmcnt completes in issue order, loads and stores alike (hipcc
-  // itself counts younger stores this way, e.g. vmcnt(3) over load, load, load, store); a count
+  // itself counts younger stores this way: vmcnt(3) for the first load of store, load, load, load, store); a count
   // at most the true number keeps every K-tile-1 DMA outside the allowed ops.
   constexpr int WXS = CST == 3 ? MA * NB / 2 : 0;
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
