@@ -205,3 +205,36 @@ def test_transposed_layout_tr_reads_are_waited_before_use(gemm_build):
     assert len(funcs) >= 8, len(funcs)  # A-, B- and AB-transposed layouts x epilogues
     for name, body in funcs.items():
         assert _tr_read_hazards(body) == [], name
+
+
+def test_counted_store_wait_allows_only_the_epilogue_stores_and_k_tile_2(tmp_path):
+    """gemm_w4p.h CST 3 (experiments `w4pw_0`): K-step 0 after an epilogue waits
+    vmcnt(ND + stores) = vmcnt(48) for the next tile's K-tile-1 DMAs. That is right
+    only if the 48 vector-memory ops issued just before the wait are this K-step's
+    16 DMAs and the epilogue's 32 stores, with the K-tile-1 DMAs before them, and
+    if the prologue drains both K-tiles (the first tile has no epilogue)."""
+    src = tmp_path / "w4pw.hip"
+    src.write_text('#include "gemm_w4p.h"\n'
+                   "void launch(hipStream_t s, const unsigned short* a, const unsigned short* b, unsigned short* c,"
+                   " int* q) {\n"
+                   "  hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 300>), dim3(256),"
+                   " dim3(256), 0, s, a, b, c, nullptr, 8192, 8192, 8192, 8192, 8192, 8192, q);\n}\n")
+    out = subprocess.run([HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17",
+                          "-I", str(ROOT / "native" / "kernels"), "-c", str(src), "-o", str(tmp_path / "w.o"),
+                          "-save-temps=obj"], capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    (s_file,) = list(tmp_path.glob("w4pw-hip-amdgcn-amd-amdhsa-gfx950.s"))
+    lines = [ln.split(";")[0].strip() for ln in s_file.read_text().splitlines()]
+    lines = [ln for ln in lines if ln]
+    vmem = re.compile(r"^(buffer_|global_|flat_)")
+    waits = [i for i, ln in enumerate(lines) if ln == "s_waitcnt vmcnt(48)"]
+    assert len(waits) == 1, waits
+    before = [ln for ln in lines[:waits[0]] if vmem.match(ln)]
+    youngest = before[-48:]
+    assert sum(ln.startswith("buffer_load_dwordx4") and ln.endswith(" lds") for ln in youngest) == 16
+    assert sum(ln.startswith("global_store_dwordx4") for ln in youngest) == 32
+    assert all(ln.startswith("buffer_load_dwordx4") and ln.endswith(" lds") for ln in before[-64:-48])  # K-tile 1
+    # prologue: the first full drain comes after the first 32 DMAs (K-tiles 0 and 1) and before any store
+    first_drain = lines.index("s_waitcnt vmcnt(0)", next(i for i, ln in enumerate(lines) if ln.endswith(" lds")))
+    pro = [ln for ln in lines[:first_drain] if vmem.match(ln)]
+    assert sum(ln.endswith(" lds") for ln in pro) == 32 and not any("store" in ln for ln in pro)
