@@ -31,6 +31,14 @@ hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned
                        tq);
   else if (longk)
     hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 8>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
+  else if (EPI == EPI_NONE && tiles > 2 * cus && tiles <= 8 * cus)
+    // 3-8 tiles per CU, plain C: stored non-temporally. Every tile change drains 32 MiB of C
+    // stores at once (4 MiB per XCD, the whole L2) and the step waits for it (3.4 % of the
+    // 8192^3 bench step); nt stores shorten the drain: 8192^3 +0.5 / +0.5 / +1.0 % on three
+    // boxes (profiles/r4/gemm/ntstore_sweep_boxD.json, profiles/r4/validate_b,
+    // profiles/r5/gemm/store_drain). At 16 tiles per CU (16384^2x8192) it measured -1.2 %.
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0, 1, EPI == EPI_NONE>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K,
+                       lda, ldb, ldc, tq);
   else
     hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
   return hipGetLastError();

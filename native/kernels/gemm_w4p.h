@@ -354,7 +354,7 @@ __device__ __forceinline__ void set_b(Ctx& c, const unsigned short* B, int tn, i
 // the first one too (a workgroup that starts late -- its CU held by a
 // collective launched just before -- takes only the tiles still left);
 // 0 = the static walk v, v + G, v + 2G (q unused), for measurements.
-// NTST: C stored non-temporally (measurement knob: the output is not re-read
+// NTST: C stored non-temporally (production at 3-8 tiles per CU, gemm_persistent.hip; the output is not re-read
 // by this launch, so it need not displace A / B lines in L2 / MALL).
 // TS: timing build (experiments only, EPI_NONE): `bias` is a long long[grid][16]
 // buffer; workgroup b writes [0] its start (s_memrealtime, 100 MHz), [1] HW_ID |

@@ -740,6 +740,19 @@ def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     assert torch.equal(_gemm_v(a2, b, variant), _gemm_v(a2, b, "w4h_1_24_20_1_0"))
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 8192, 384), (8192, 12288, 512), (8192, 8192, 2048)])
+def test_gemm_auto_nt_store_route_is_bitwise_the_one_shot_kernel(M, N, K):
+    """3-8 tiles per CU, plain C, not tall, K <= 8192: production stores C
+    non-temporally (gemm_persistent.hip); the image is the one-shot kernel's."""
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    one_shot = _gemm_v(a, b, "w4h_1_24_20_1_0")
+    assert torch.equal(gemm_nt(a, b), one_shot)
+    assert torch.equal(gemm_nt(a, b), _gemm_v(a, b, "w4pn_0"))
+
+
 def test_gemm_persistent_counted_store_wait_repeats_bitwise():
     """w4pw (gemm_w4p.h CST 3): K-step 0 after an epilogue waits vmcnt(ND + the
     epilogue's stores), i.e. only for the next tile's K-tile-1 DMAs. If vmcnt did
