@@ -18,6 +18,14 @@ value = aggregate GEMM TFLOP/s over all N GPUs (weak scaling: per-GPU work is
 fixed). Synthetic U[-1,1) operands (random data, not zeros: DVFS reads zeros
 fast, cdna_hip_programming.md rule 25).
 
+Self-normalising and self-checking (after the timed region, which alone gives
+``value`` and ``ms_per_step``): the last timed GEMM's whole output is compared
+with an fp32 reference (``rel_err``; the run fails above ``--max-rel-err``),
+and ``--yardstick-rounds`` interleaved rounds of S kgs steps and S steps of the
+same workload on the vendor GEMM (torch.matmul -> hipBLASLt) give
+``hipblaslt_tflops`` and ``ratio_vs_hipblaslt`` on the same box, so a change in
+``value`` between runs reads as box speed or kernel change.
+
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W]
         torchrun --nproc-per-node N bench.py --gpus N ...
 
@@ -62,6 +70,12 @@ def parse(argv=None):
     ap.add_argument("--allreduce-mb", type=float, default=64.0, help="gradient bucket all-reduced per step (MiB)")
     ap.add_argument("--no-overlap", action="store_true", help="run the all-reduce after the GEMMs, same stream")
     ap.add_argument("--compare-torch", action="store_true", help="also time torch.matmul (hipBLASLt), untimed part")
+    ap.add_argument("--yardstick-rounds", type=int, default=3,
+                    help="after the timed region: this many interleaved rounds of (S kgs steps, S vendor-GEMM "
+                         "steps) on the same operands, medians -> ratio_vs_hipblaslt (0 = off)")
+    ap.add_argument("--yardstick-steps", type=int, default=20, help="S, steps per yardstick block")
+    ap.add_argument("--max-rel-err", type=float, default=1e-2,
+                    help="the last timed GEMM's whole output is checked against fp32; above this the run fails")
     ap.add_argument("--verify", action="store_true", help="check one GEMM against fp32 torch before timing")
     ap.add_argument("--backend", choices=("kgs", "torch"), default="kgs",
                     help="kgs = hand-written gfx950 kernel (the benchmark); torch = reference / CPU test path")
@@ -136,6 +150,38 @@ def main(argv=None) -> int:
     return rc
 
 
+def yardstick(wl, ctx, sync, rounds: int, steps: int) -> dict:
+    """Interleaved medians of ``rounds`` x (``steps`` kgs steps, ``steps``
+    vendor-GEMM steps), each block bracketed like the timed region (barrier +
+    synchronize, max over ranks). Same operands, same all-reduce, same box."""
+    import statistics
+
+    from kgs.parallel import dist as kdist
+
+    for _ in range(min(3, steps)):  # the vendor path's first calls pick its kernel
+        wl.step(reference=True)
+
+    def block(reference: bool) -> float:
+        sync()
+        kdist.barrier(ctx)
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            wl.step(reference=reference)
+        sync()
+        kdist.barrier(ctx)
+        sync()
+        return kdist.max_over_ranks(ctx, time.perf_counter() - t0) / steps * 1e3
+
+    kgs, ref = [], []
+    for _ in range(rounds):
+        kgs.append(block(False))
+        ref.append(block(True))
+    return {"rounds": rounds, "steps": steps, "kgs_ms_per_step": round(statistics.median(kgs), 4),
+            "ref_ms_per_step": round(statistics.median(ref), 4), "kgs_ms": [round(t, 4) for t in kgs],
+            "ref_ms": [round(t, 4) for t in ref]}
+
+
 def run(args, wd) -> int:
     import torch
     from kgs.models.gemm_workload import GemmWorkload
@@ -197,9 +243,16 @@ def run(args, wd) -> int:
     kdist.barrier(ctx)
     sync()
     elapsed = time.perf_counter() - t0
+    elapsed_max = kdist.max_over_ranks(ctx, elapsed)
+    # --- untimed from here: the check and the same-box yardstick ---
+    wd.set_phase("check")
+    rel_err = kdist.max_over_ranks(ctx, wl.check_output())
+    ys = None
+    if args.yardstick_rounds > 0 and rel_err <= args.max_rel_err:
+        wd.set_phase("yardstick")
+        ys = yardstick(wl, ctx, sync, args.yardstick_rounds, args.yardstick_steps)
     wd.set_phase("report")
 
-    elapsed_max = kdist.max_over_ranks(ctx, elapsed)
     per_rank_ms = [round(t / max(1, args.steps) * 1e3, 4) for t in kdist.all_gather_object(ctx, elapsed)]
     ar_ms = wl.allreduce_ms()  # mean in-step all-reduce time over the timed steps (None at N=1)
     ms_per_step = elapsed_max / max(1, args.steps) * 1e3
@@ -215,6 +268,21 @@ def run(args, wd) -> int:
         extra["allreduce_busbw_gbs"] = round(ar_bytes / (ar_ms * 1e-3) * 2 * (world - 1) / world / 1e9, 2)
     if args.compare_torch:
         extra["torch_matmul_tflops_per_gpu"] = round(wl.torch_reference_tflops(), 1)
+    extra["rel_err"] = float(f"{rel_err:.3e}")
+    if ys is not None:
+        kgs_ms, ref_ms = ys["kgs_ms_per_step"], ys["ref_ms_per_step"]
+        extra["hipblaslt_tflops"] = round(flops_per_step / (ref_ms * 1e-3) / 1e12 * world, 2)
+        extra["ratio_vs_hipblaslt"] = round(ref_ms / kgs_ms, 4)  # > 1: the kgs step is faster
+        extra["yardstick"] = {**ys, "path": wl.reference_path_name(),
+                              "kgs_tflops": round(flops_per_step / (kgs_ms * 1e-3) / 1e12 * world, 2)}
+    if rel_err > args.max_rel_err:
+        if rank == 0:
+            launch.report_once({**error_report(args, world), "status": "error", "exit_code": 1, "phase": "check",
+                                "rel_err": rel_err, "reason": f"timed GEMM output rel err {rel_err:.3e} > "
+                                                              f"{args.max_rel_err:g} against fp32"})
+        wd.shutdown_bound(90.0)
+        kdist.shutdown(ctx)
+        return 1
 
     if rank == 0:
         out = {

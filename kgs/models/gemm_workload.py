@@ -63,6 +63,16 @@ class GemmWorkload:
             self._gemm = lambda i: gemm_nt(self.a, self.b, out=self.c[i & 1])
         else:
             self._gemm = lambda i: torch.matmul(self.a, self.b.T, out=self.c[i & 1])
+        # the yardstick: the vendor library (hipBLASLt behind torch) on the same
+        # operands, into its own outputs (the timed outputs stay checkable)
+        if dtype == "fp8":
+            ta = torch.tensor(self.sa, device=self.device)
+            tb = torch.tensor(self.sb, device=self.device)
+            self._ref_gemm = lambda i: torch._scaled_mm(self.qa, self.qb.T, scale_a=ta, scale_b=tb,
+                                                        out_dtype=torch.bfloat16, out=self._c_ref(i))
+        else:
+            self._ref_gemm = lambda i: torch.matmul(self.a, self.b.T, out=self._c_ref(i))
+        self._cref = None
 
     def flops_per_step(self) -> float:
         return 2.0 * self.m * self.n * self.k * self.g
@@ -76,6 +86,10 @@ class GemmWorkload:
 
         return "kgs gemm_nt_w4p (persistent 4-wave 256x256 LDS-DMA pipeline)" if fast_path_ok(self.a, self.b, self.c[0]) else \
             "kgs gemm_nt_generic"
+
+    def reference_path_name(self) -> str:
+        lib = "hipBLASLt" if self.cuda else "CPU BLAS"
+        return f"torch._scaled_mm ({lib})" if self.dtype == "fp8" else f"torch.matmul ({lib})"
 
     def _allreduce(self):
         import time
@@ -108,10 +122,19 @@ class GemmWorkload:
             ts = list(self._ar_wall)
         return sum(ts) / len(ts) if ts else None
 
-    def step(self) -> None:
+    def _c_ref(self, i):
+        if self._cref is None:
+            self._cref = [torch.empty_like(self.c[0]) for _ in range(2)]
+        return self._cref[i & 1]
+
+    def step(self, reference: bool = False) -> None:
+        """One workload step. ``reference``: the same step with the vendor GEMM
+        (torch.matmul -> hipBLASLt; torch._scaled_mm for fp8) in place of the
+        kgs kernel -- the same-box yardstick bench.py interleaves with it."""
+        gemm = self._ref_gemm if reference else self._gemm
         if not self.cuda:
             for i in range(self.g):
-                self._gemm(i)
+                gemm(i)
             if self.bucket is not None:
                 self._allreduce()
             return
@@ -121,7 +144,7 @@ class GemmWorkload:
             with torch.cuda.stream(self.comm_stream):
                 self._allreduce()
         for i in range(self.g):
-            self._gemm(i)
+            gemm(i)
         if self.bucket is not None:
             if self.overlap:
                 cur.wait_stream(self.comm_stream)
@@ -138,6 +161,33 @@ class GemmWorkload:
             ref = self.a[:rows].float() @ self.b.float().T
         got = self.c[0][:rows].float()
         return ((got - ref).abs().max() / ref.abs().max()).item()
+
+    @torch.no_grad()
+    def check_output(self, chunk_rows: int = 2048) -> float:
+        """Relative max error of the LAST timed GEMM's whole output (``C`` of
+        the step's final GEMM, as the timed loop left it) against an fp32
+        reference of the same operands: ``max|C - A.B^T| / max|A.B^T|``.
+        Row chunks keep the fp32 temporaries small; TF32 is off."""
+        got = self.c[(self.g - 1) & 1]
+        prev = torch.backends.cuda.matmul.allow_tf32 if self.cuda else None
+        if self.cuda:
+            torch.backends.cuda.matmul.allow_tf32 = False
+        try:
+            if self.dtype == "fp8":
+                bf = self.qb.float() * self.sb
+            else:
+                bf = self.b.float()
+            err = ref_max = 0.0
+            for r0 in range(0, self.m, chunk_rows):
+                a = self.qa[r0:r0 + chunk_rows].float() * self.sa if self.dtype == "fp8" else \
+                    self.a[r0:r0 + chunk_rows].float()
+                ref = a @ bf.T
+                err = max(err, (got[r0:r0 + chunk_rows].float() - ref).abs().max().item())
+                ref_max = max(ref_max, ref.abs().max().item())
+            return err / ref_max if ref_max > 0 else float(err)
+        finally:
+            if self.cuda:
+                torch.backends.cuda.matmul.allow_tf32 = prev
 
     def torch_reference_tflops(self, iters: int = 10) -> float:
         """hipBLASLt (torch.matmul) TFLOP/s on the same operands, for comparison."""

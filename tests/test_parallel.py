@@ -466,3 +466,61 @@ def test_watchdog_shutdown_bound_keeps_a_reported_result(tmp_path):
     assert r.returncode == 0, (r.returncode, r.stderr)
     assert time.monotonic() - t0 < 4.5
     assert "shutdown not done" in r.stderr and "watchdog: no completion" not in r.stderr
+
+
+def _bench_inproc(*extra):
+    import contextlib
+    import io
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from kgs.parallel import launch
+
+    launch._reported = False  # one JSON line per process; these tests call main() more than once
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.main(["--gpus", "1", "--steps", "2", "--warmup", "1", "--gemm-m", "128", "--gemm-n", "64",
+                         "--gemm-k", "96", "--backend", "torch", "--cpu", "--yardstick-steps", "2", *extra])
+    lines = [json.loads(ln) for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, buf.getvalue()
+    return rc, lines[0]
+
+
+def test_bench_line_carries_same_box_yardstick_and_full_check(monkeypatch):
+    """the default run checks the last timed output in full
+    against fp32 (rel_err) and times the vendor GEMM interleaved with the kgs
+    step (hipblaslt_tflops, ratio_vs_hipblaslt). value / ms_per_step stay the
+    timed region's: value = 4 GEMMs x 2MNK / ms_per_step."""
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    rc, j = _bench_inproc()
+    assert rc == 0 and "status" not in j
+    for key in ("rel_err", "hipblaslt_tflops", "ratio_vs_hipblaslt", "yardstick"):
+        assert key in j, key
+    assert 0 <= j["rel_err"] < 1e-2
+    ys = j["yardstick"]
+    assert ys["rounds"] == 3 and len(ys["kgs_ms"]) == 3 and len(ys["ref_ms"]) == 3
+    assert j["ratio_vs_hipblaslt"] == pytest.approx(ys["ref_ms_per_step"] / ys["kgs_ms_per_step"], rel=1e-3)
+    flops = 4 * 2.0 * 128 * 64 * 96
+    assert j["value"] == pytest.approx(flops / (j["ms_per_step"] * 1e-3) / 1e12, abs=0.011, rel=2e-3)
+    # the yardstick is untimed extra: its kgs median is not what value reports
+    assert j["ms_per_step"] == max(j["per_rank_ms_per_step"])
+    rc0, j0 = _bench_inproc("--yardstick-rounds", "0")
+    assert rc0 == 0 and "ratio_vs_hipblaslt" not in j0 and "rel_err" in j0
+
+
+def test_bench_fails_loudly_on_a_wrong_timed_output(monkeypatch):
+    from kgs.models.gemm_workload import GemmWorkload
+
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    real = GemmWorkload.step
+
+    def corrupt(self, reference=False):
+        real(self, reference)
+        if not reference:
+            self.c[(self.g - 1) & 1][3, 5] += 1e3  # one wrong element in the timed output
+    monkeypatch.setattr(GemmWorkload, "step", corrupt)
+    rc, j = _bench_inproc()
+    assert rc == 1
+    assert j["status"] == "error" and j["phase"] == "check" and j["rel_err"] > 1e-2 and j["value"] is None
