@@ -43,6 +43,9 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("src", help="file under native/kernels/")
     ap.add_argument("--rev", default="HEAD~1")
+    ap.add_argument("--rename", action="append", default=[], metavar="REGEX=REPL",
+                    help="rewrite this tree's kernel names before matching (a template that gained "
+                         "defaulted parameters mangles differently), e.g. 'ELi0ELi0ELi2EEEv=ELi0EEEv'")
     a = ap.parse_args(argv)
     with tempfile.TemporaryDirectory() as td:
         td = Path(td)
@@ -53,6 +56,9 @@ def main(argv=None) -> int:
         finally:
             subprocess.run(["git", "worktree", "remove", "--force", str(wt)], cwd=ROOT, capture_output=True)
         new = kernels(compile_asm(ROOT / "native" / "kernels" / a.src, td / "new"))
+        for rule in a.rename:
+            pat, repl = rule.split("=", 1)
+            new = {re.sub(pat, repl, k): v for k, v in new.items()}
     same = [n for n in old if old[n] == new.get(n)]
     changed = [n for n in old if n in new and old[n] != new[n]]
     print(f"{a.src} vs {a.rev}: {len(same)} kernels instruction-identical, {len(changed)} changed, "

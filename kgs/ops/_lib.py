@@ -164,9 +164,10 @@ def tile_queue_stats(device: int = 0) -> dict:
     """The persistent GEMMs' ticket-slot pool on ``device`` (tile_queue.h):
     slots allocated, owned by streams, owned by captured launches, and the
     launches that found no slot (they ran the one-shot grid)."""
-    out = (_c_long * 4)()
+    out = (_c_long * 5)()
     check(lib().kgs_tile_queue_stats(int(device), out), "kgs_tile_queue_stats")
-    return {"slots": out[0], "stream_slots": out[1], "capture_slots": out[2], "fallbacks": out[3]}
+    return {"slots": out[0], "stream_slots": out[1], "capture_slots": out[2], "fallbacks": out[3],
+            "grow_failures": out[4]}
 
 
 def tile_queue_check(device: int = 0) -> dict:
@@ -175,13 +176,16 @@ def tile_queue_check(device: int = 0) -> dict:
     the device first. ``dirty_slots`` > 0 means a launch left its tickets
     behind or something wrote into the pool (the next eager launch on that
     slot would take wrong tickets); ``slot_addr`` / ``words`` are the first
-    dirty slot's device address and its 16 words."""
+    dirty slot's device address and its 16 words. ``error_slots``: slots whose
+    error word a persistent GEMM set when it read a ticket no launch could
+    have issued (it stopped taking tiles: that launch's output is incomplete)."""
     import torch
 
     torch.cuda.synchronize(device)
-    out = (_c_long * 21)()
+    out = (_c_long * 22)()
     check(lib().kgs_tile_queue_check(int(device), out), "kgs_tile_queue_check")
-    r = {"dirty_slots": out[0], "dirty_words": out[1], "first_value": out[2], "first_word": out[3]}
+    r = {"dirty_slots": out[0], "dirty_words": out[1], "first_value": out[2], "first_word": out[3],
+         "error_slots": out[21]}
     if out[0]:
         r["slot_addr"] = hex(out[4])
         r["words"] = [f"{w & 0xffffffff:08x}" for w in out[5:21]]

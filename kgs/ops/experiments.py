@@ -88,6 +88,10 @@ W4H.update({"w4po0_0": 139, "w4po2_0": 140, "w4po0_140000008": 141, "w4po2_14000
 W4H.update({"w4px_0": 143, "w4pd_0": 144})
 # ... and K-step 0 after an epilogue waiting vmcnt(ND + stores): w4pw_0
 W4H.update({"w4pw_0": 145})
+# round 6: deferred C stores (gemm_w4p.h DD, SPS): w4pq<DD>x<SPS>[n]_<X> (n: non-temporal stores) -> 146..
+W4H.update({"w4pq8x2n_0": 146, "w4pq4x4n_0": 147, "w4pq8x1n_0": 148, "w4pq10x2n_0": 149, "w4pq16x1n_0": 150,
+            "w4pq8x2_0": 151, "w4pq8x2_140000008": 152, "w4pq12x1n_0": 153, "w4pq8x2n_140000008": 154,
+            "w4pq8x2n_8": 155})
 NO_OUTPUT = frozenset({"w4px_0"})  # timing only: C is not written
 
 

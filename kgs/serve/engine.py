@@ -124,6 +124,12 @@ class LLMEngine:
         self.validate = True  # host-side range checks of every step's device inputs (_check_plan)
         # KGS_TQ_CHECK=1: the persistent GEMMs' ticket pool checked after every step (kgs.ops._lib.tile_queue_check)
         self.tq_check = os.environ.get("KGS_TQ_CHECK", "0") == "1" and self.device.type == "cuda"
+        # KGS_GRAPH_AUDIT=1: keep each captured hipGraph and record its node types and memset nodes
+        # (kgs.utils.graph_audit; a memset node caused the round-5 serving fault)
+        from kgs.utils import graph_audit
+
+        self.graph_audit = graph_audit.enabled() and self.device.type == "cuda"
+        self.graph_audits: dict = {}
         self._want_lp: set = set()
         self._want_pen: set = set()
         self._seeded: set = set()
@@ -536,9 +542,14 @@ class LLMEngine:
             for _ in range(2):  # warm up: workspaces and allocator pools settle before capture
                 run()
         torch.cuda.current_stream(self.device).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
+        graph = torch.cuda.CUDAGraph(keep_graph=self.graph_audit)
         with torch.cuda.graph(graph):
             logits = run()
+        if self.graph_audit:
+            from kgs.utils.graph_audit import audit
+
+            self.graph_audits[(bb, wb)] = audit(graph)
+            graph.instantiate()
         host2 = {k: v.clone().pin_memory() for k, v in host.items()}
         g = {"graph": graph, "io": io, "host": [host, host2], "flip": 0,
              "host_np": [{k: v.numpy() for k, v in h.items()} for h in (host, host2)],

@@ -9,6 +9,8 @@ Builds, with the ROCm toolchain in ``/opt/rocm``:
 * ``kgs/_native/kgs-gpuprobe`` -- the pod's first-GEMM readiness probe: HIP
   host code linked against ``libkgs_kernels.so`` (no Python, no torch), one
   thread per visible GPU running the production GEMM with a sampled check.
+* ``kgs/_native/kgs-graph-memset-repro`` -- a pure-HIP check of hipGraph memset
+  nodes (native/probe/graph_memset_repro.hip), no torch, no kgs library.
 * ``kgs/_native/libkgs_experiments.so`` -- ``native/experiments/*.hip``, the
   measured GEMM alternatives and timing probes (some wrong by construction),
   opt-in through ``kgs.ops.experiments`` and never loaded by production code.
@@ -114,7 +116,7 @@ def _py_ext_suffix() -> str:
 # targets of the enumeration core) and nothing that needs hipcc.
 GROUPS = {
     "gpuinfo": ("gpuinfo-lib", "gpuinfo-py", "gpuinfo-cli"),
-    "gpu": ("kernels", "gpuprobe", "experiments", "rccl-bench"),
+    "gpu": ("kernels", "gpuprobe", "experiments", "rccl-bench", "memset-repro"),
 }
 
 
@@ -162,6 +164,15 @@ def targets(out: Path | None = None) -> list[Target]:
             HIPCC,
             flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-Wall"],
             link_flags=[f"-L{odir}", "-lkgs_kernels", "-Wl,-rpath,$ORIGIN", "-pthread"],
+            shared=False,
+        ),
+        Target(
+            "memset-repro",
+            odir / "kgs-graph-memset-repro",
+            [NATIVE / "probe" / "graph_memset_repro.hip"],
+            HIPCC,
+            flags=[f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-Wall"],
+            link_flags=[],
             shared=False,
         ),
         Target(

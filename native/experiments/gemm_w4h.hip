@@ -125,6 +125,25 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
         hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 300>), pg, dim3(256), 0, s, a, b,
                            c, nullptr, M, N, K, lda, ldb, ldc, tq);
         break;
+      // round 6: deferred C stores (gemm_w4p.h DD, SPS): SPS units per lane stored at the end of each of the
+      // next tile's first DD K-steps; ids and names in kgs/ops/experiments.py (w4pq_*)
+#define KGS_W4PQ(ID, X, NT, DD, SPS)                                                                          \
+  case ID:                                                                                                    \
+    if (K / 64 < ((DD + 2) & ~1) + 2) return KGS_ERR_SHAPE;                                                   \
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, X, 1, NT, false, 0, DD, SPS>), pg, dim3(256), 0, s, a, \
+                       b, c, nullptr, M, N, K, lda, ldb, ldc, tq);                                             \
+    break;
+      KGS_W4PQ(146, 0, true, 8, 2)
+      KGS_W4PQ(147, 0, true, 4, 4)
+      KGS_W4PQ(148, 0, true, 8, 1)
+      KGS_W4PQ(149, 0, true, 10, 2)
+      KGS_W4PQ(150, 0, true, 16, 1)
+      KGS_W4PQ(151, 0, false, 8, 2)
+      KGS_W4PQ(152, 140000008, false, 8, 2)
+      KGS_W4PQ(153, 0, true, 12, 1)
+      KGS_W4PQ(154, 140000008, true, 8, 2)
+      KGS_W4PQ(155, 8, true, 8, 2)
+#undef KGS_W4PQ
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)

@@ -84,13 +84,31 @@ __device__ __forceinline__ void commit_epoch(const Ptrs& P, const Who& me, unsig
 __device__ __forceinline__ unsigned long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
 // All NR ranks' block b meet; thread p < NR talks to peer p.
+//
+// The ordering across GPUs is spelled out in the ISA, not left to the atomic's
+// expansion (tests/test_kernel_resources.py pins it): a release-store
+// expansion emitted `buffer_wbl2 sc0 sc1` directly followed by the flag store
+// whenever an earlier s_waitcnt vmcnt(0) had already retired everything else
+// (the waitcnt pass dropped the wait after the write-back), so the flag could
+// overtake the L2 write-back of the data a peer reads over xGMI. Now:
+//   every wave   s_waitcnt vmcnt(0)           its own data stores reached L2
+//   s_barrier                                 all waves' stores are in L2
+//   flag thread  buffer_wbl2 sc0 sc1          write L2 back (system scope)
+//                s_waitcnt vmcnt(0)           ... and wait until it is done
+//                global_store flag sc0 sc1
+//   poll         global_load sc0 sc1; s_waitcnt vmcnt(0); buffer_inv sc0 sc1
+//                s_waitcnt vmcnt(0)           invalidate done before the barrier
+//   s_barrier                                 then any wave may read peer data
 template <int NR>
 __device__ __forceinline__ void block_barrier(const Ptrs& P, int rank, int b, int phase, unsigned epoch,
                                               unsigned long timeout, int* err) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x < NR) {
     const int p = threadIdx.x;
-    __hip_atomic_store(&P.sig[p]->flag[phase][b][rank], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2 sc0 sc1
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&P.sig[p]->flag[phase][b][rank], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     unsigned* mine = &P.sig[rank]->flag[phase][b][p];
     const unsigned long t0 = now_ticks();
     while (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != epoch) {
@@ -100,6 +118,7 @@ __device__ __forceinline__ void block_barrier(const Ptrs& P, int rank, int b, in
       }
       __builtin_amdgcn_s_sleep(1);
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }

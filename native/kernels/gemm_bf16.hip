@@ -61,6 +61,7 @@
 // the in-pod hot path required by BASELINE.json configs 3-4.
 #include "gemm_pipeline.h"
 #include "gemm_w4.h"
+#include "gemm_w4p.h"
 #include "tile_queue.h"
 #include "tile_queue_zero.h"
 
@@ -220,19 +221,24 @@ static hipError_t launch(int variant, const unsigned short* A, const unsigned sh
 
 }  // namespace kgs
 
+static_assert(kgs::w4p::TQ_ERR_WORD == kgs::TQ_ERR, "the kernels' error word is the pool's");
+
 // Ticket-slot pool of the persistent GEMMs on device `dev` (tile_queue.h):
-// out = {slots allocated, stream-owned, capture-owned, nullptr fallbacks}.
+// out = {slots allocated, stream-owned, capture-owned, nullptr fallbacks, failed growths}.
 KGS_EXPORT int kgs_tile_queue_stats(int dev, long* out) {
   const kgs::TileQueueStats st = kgs::tile_queue_stats(dev);
   out[0] = st.slots;
   out[1] = st.stream_slots;
   out[2] = st.capture_slots;
   out[3] = st.fallbacks;
+  out[4] = st.grow_failures;
   return 0;
 }
 
 // The quiescent-pool invariant (tile_queue.h tile_queue_check): out = {dirty
-// slots, dirty words, first dirty value, its word index}. No GEMM may be in flight.
+// slots, dirty words, first dirty value, its word index, the first dirty slot's
+// address, its 16 words, slots with the impossible-ticket error word set}. No
+// GEMM may be in flight.
 KGS_EXPORT int kgs_tile_queue_check(int dev, long* out) { return kgs::tile_queue_check(dev, out); }
 
 // Can the 256x256 pipelined kernel take this problem?
@@ -285,7 +291,8 @@ KGS_EXPORT int kgs_gemm_bf16_nt_w4x_ex(const void* A, const void* B, void* C, fl
 // epilogue (EPI_ADDC; the prompt pass's o / down, whose add_rmsnorm becomes a
 // plain rmsnorm -- same roundings, so bitwise the unfused pair). The aligned
 // four-wave path only (kgs_gemm_bf16_nt_w4_ok); persistent with more tiles
-// than CUs, else the one-shot grid (tall problems in the mirrored order).
+// than CUs on an eager stream, else (and in any hipGraph capture) the one-shot
+// grid (tall problems in the mirrored order).
 KGS_EXPORT int kgs_gemm_bf16_nt_addc(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                      int ldc, hipStream_t stream) {
   using namespace kgs;
@@ -295,7 +302,12 @@ KGS_EXPORT int kgs_gemm_bf16_nt_addc(const void* A, const void* B, void* C, int 
   auto b = (const unsigned short*)B;
   auto c = (unsigned short*)C;
   const long tiles = (long)(M / 256) * (N / 256);
-  int* tq = (K >= 384 && tiles > cu_count()) ? tile_queue(stream) : nullptr;
+  // A captured launch never takes a ticket slot: tile_queue.h lets one exec
+  // replayed concurrently with itself compute a tile twice, and this epilogue
+  // (C += A.B^T) would then add twice. Captures run the one-shot grid.
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &cs) != hipSuccess) return KGS_ERR_ARG;
+  int* tq = (K >= 384 && tiles > cu_count() && cs == hipStreamCaptureStatusNone) ? tile_queue(stream) : nullptr;
   if (tq) {
     const hipError_t e = launch_w4p<EPI_ADDC>(a, b, c, nullptr, M, N, K, lda, ldb, ldc, cu_count(), tq, stream);
     return e == hipSuccess ? 0 : (int)e;

@@ -225,7 +225,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       fstep<0, X, false, 0, KN>(c, c, f, k + 2, tq);
       fstep<1, X, false, 0, KN>(c, c, f, k + 3, tq);
     }
-    const int tnx = nwx + __builtin_amdgcn_readfirstlane(tslot);
+    const int raw = __builtin_amdgcn_readfirstlane(tslot);
+    w4p::mark_bad_ticket(q, raw, ntx);  // a corrupted slot is reported (gemm_w4p.h)
+    const int tnx = nwx + raw;
     const bool more = (unsigned)tnx < (unsigned)ntx;  // a ticket outside [0, ntx) never becomes a tile index
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(x + 8 * tnx, ntiles, ntm, ntn, sl, tmn, tnn);

@@ -258,6 +258,77 @@ __device__ __forceinline__ void pepi(const Ctx& c, unsigned short* __restrict__ 
   }
 }
 
+// Deferred C stores (kernel template DD > 0, round 6). At a tile change every
+// workgroup stores its 128 KiB of C at once: 32 MiB chip-wide, about 5.7 us of
+// HBM write time, and the next tile's first K-step waits for all of it (vmcnt
+// counts loads and stores in issue order, so a wait for a DMA issued after the
+// stores is a wait for the stores: 3.4 % of the 8192^3 bench step,
+// profiles/r5/gemm/store_drain/README.md). With DD > 0 the epilogue stores only
+// the first UI = 32 - DD * SPS 16-byte units per lane; the last DD * SPS are
+// packed into VGPRs (d[]) and stored SPS at a time at the end of the next
+// tile's K-steps 0 .. DD - 1, where they drain behind MFMA work. The K-step
+// after a storing one waits vmcnt(ND + SPS): the stores issued after the DMA it
+// waits for are younger, so they may still be in flight. On the first tile the
+// "deferred stores" go to a zero-size buffer (dropped by the range check, still
+// counted), so every K-step's wait count is a constant. The last tile's
+// deferred units are stored after the loop.
+template <int EPI, int Q>
+__device__ __forceinline__ uint4 punit(const float (&bv)[NB][4]) {
+  constexpr int n = Q % NB;
+  const f32x4 v0 = accr::read<Q>(), v1 = accr::read<Q + 1>();
+  uint2 o[2];
+  o[0].x = pack_bf16x2(epilogue<EPI>(v0[0], bv[n][0]), epilogue<EPI>(v0[1], bv[n][1]));
+  o[0].y = pack_bf16x2(epilogue<EPI>(v0[2], bv[n][2]), epilogue<EPI>(v0[3], bv[n][3]));
+  o[1].x = pack_bf16x2(epilogue<EPI>(v1[0], bv[n + 1][0]), epilogue<EPI>(v1[1], bv[n + 1][1]));
+  o[1].y = pack_bf16x2(epilogue<EPI>(v1[2], bv[n + 1][2]), epilogue<EPI>(v1[3], bv[n + 1][3]));
+  auto sx = __builtin_amdgcn_permlane16_swap(o[0].x, o[1].x, false, false);
+  auto sy = __builtin_amdgcn_permlane16_swap(o[0].y, o[1].y, false, false);
+  return make_uint4(sx[0], sy[0], sx[1], sy[1]);
+}
+
+typedef unsigned int w4p_u32x4 __attribute__((ext_vector_type(4)));
+
+// Epilogue with the last DEF units deferred into d[] (units Q / 2 >= UI).
+template <int EPI, int Q, int UI, int DEF, bool NTST>
+__device__ __forceinline__ void pepi_d(const Ctx& c, unsigned short* __restrict__ C, int ldc, int tm, int tn,
+                                       const float (&bv)[NB][4], uint4 (&d)[DEF]) {
+  if constexpr (Q < MA * NB) {
+    constexpr int i = Q / NB, n = Q % NB;
+    const uint4 qv = punit<EPI, Q>(bv);
+    if constexpr (Q / 2 < UI) {
+      const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+      const int row = tm * BM + c.wr * (BM / 2) + i * 16 + fr;
+      const int col0 = tn * BN + c.wc * (BN / 2) + n * 16;
+      uint4* dst = (uint4*)(C + (long)row * ldc + col0 + (fq & 1) * 16 + (fq >> 1) * 8);
+      if constexpr (NTST) {
+        const w4p_u32x4 v = {qv.x, qv.y, qv.z, qv.w};
+        __builtin_nontemporal_store(v, (w4p_u32x4*)dst);
+      } else {
+        *dst = qv;
+      }
+    } else {
+      d[Q / 2 - UI] = qv;
+    }
+    pepi_d<EPI, Q + 2, UI, DEF, NTST>(c, C, ldc, tm, tn, bv, d);
+  }
+}
+
+// Deferred units [U0, U0 + CNT) of the tile whose C block `rc` covers (rows at
+// stride ldc from the tile's corner); voff: this lane's byte offset in the block.
+template <int UI, int U0, int CNT, int DEF, bool NTST>
+__device__ __forceinline__ void dstore(const uint4 (&d)[DEF], __amdgpu_buffer_rsrc_t rc, int voff, int ldc) {
+  w4::static_for<0, CNT>([&](auto e) {
+    constexpr int u = U0 + decltype(e)::value, Q = 2 * (UI + u), i = Q / NB, n = Q % NB;
+    const w4p_u32x4 v = {d[u].x, d[u].y, d[u].z, d[u].w};
+    // column offset in the instruction's immediate, row group in soffset
+    __builtin_amdgcn_raw_buffer_store_b128(v, rc, voff + n * 32, i * 32 * ldc, NTST ? 2 : 0);
+  });
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_c(unsigned short* C, int tm, int tn, int ldc) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(C + (long)tm * BM * ldc + tn * BN), 0, BM * ldc * 2, 0x00020000);
+}
+
 // Residual-add epilogue (EPI_ADDC): row group I's four 16-B residual chunks
 // per lane (`old`) were loaded before its stores, and group I + 1's are issued
 // before group I's stores, so a tile's epilogue waits out about one memory
@@ -326,6 +397,19 @@ __device__ __forceinline__ void pepi_sw(const Ctx& c, unsigned short* __restrict
   }
 }
 
+// A ticket no launch could have issued. One launch hands label x at most ntx
+// queue tickets (raw values 0 .. ntx - 1); with 64 launches sharing a slot as
+// the bound, a raw value >= 64 ntx -- or a negative one -- means the slot was
+// corrupted. The workgroup then stops taking tiles (the callers' range checks:
+// no address is ever formed from it) and this marks the slot's error word,
+// which tile_queue_check reports, so the tiles it skipped never pass silently
+// (ADVICE r5). The word is not reset by the exit reset (words 0..8): sticky.
+constexpr int TQ_ERR_WORD = 15;  // tile_queue.h TQ_ERR
+__device__ __forceinline__ void mark_bad_ticket(int* q, int raw, int ntx) {
+  if ((unsigned)raw >= 64u * (unsigned)ntx && threadIdx.x == 0)
+    atomicExch(q + TQ_ERR_WORD, (int)(0x80000000u | ((unsigned)raw & 0x7fffffffu)));
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_a(const unsigned short* A, int tm, int lda) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(A + (long)tm * BM * lda), 0, BM * lda * 2, 0x00020000);
 }
@@ -367,7 +451,9 @@ __device__ __forceinline__ void set_b(Ctx& c, const unsigned short* B, int tn, i
 // change waits on its stores -- gfx950 counts stores and loads in one vmcnt, so the next tile's
 // first DMA wait also covers them); 3 = that first wait counts the tile's stores as younger ops
 // (vmcnt(ND + stores)), so it waits for the next tile's K-tile 1 only.
-template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false, int L = 0>
+// DD, SPS: deferred C stores (see pepi_d): SPS 16-B units per lane stored at the end of each of the next
+// tile's first DD K-steps (0 = off, the epilogue stores everything). Needs K / 64 >= PEEL + 2 (below).
+template <int EPI, int X = 0, int DYN = 1, bool NTST = false, bool TS = false, int L = 0, int DD = 0, int SPS = 2>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void gemm_nt_w4p(
     const unsigned short* __restrict__ A, const unsigned short* __restrict__ B, unsigned short* __restrict__ C,
     const unsigned short* __restrict__ bias, int M, int N, int K, int lda, int ldb, int ldc, int* __restrict__ q) {
@@ -396,6 +482,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // itself counts younger stores this way: vmcnt(3) for the first load of store, load, load, load, store); a count
   // at most the true number keeps every K-tile-1 DMA outside the allowed ops.
   constexpr int WXS = CST == 3 ? MA * NB / 2 : 0;
+  constexpr int DEF = DD * SPS, UI = MA * NB / 2 - DEF;  // deferred / immediate units per lane
+  // K-steps of a tile peeled out of the runtime loop: the storing ones, the one after them (its wait
+  // counts their stores), rounded up to a stage pair
+  constexpr int PEEL = DD ? ((DD + 2) & ~1) : 2;
+  static_assert(DD == 0 || (EPI != EPI_ADDC && !SW && CST == 0 && L % 10 == 0), "deferred stores: plain tiles");
+  static_assert(DEF >= 0 && UI >= 0 && (DD == 0 || SPS > 0), "deferred stores: at most a tile's units");
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {
@@ -448,6 +540,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
   // unsigned: a ticket outside [0, lim) -- a corrupted slot -- ends the
   // workgroup instead of becoming a tile index (no address from it, ever)
+  if constexpr (DYN == 2) mark_bad_ticket(q, t, ntx);
   if ((unsigned)t >= (unsigned)lim) {  // (DYN 2: queue empty when this workgroup started; DYN 0/1: never with grid <= tiles)
     if (DYN && threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)
       for (int i = 0; i <= 8; ++i) atomicExch(q + i, 0);
@@ -489,14 +582,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   int vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
   Tick tq{q + x + vzero, &tslot, 0};
+  // deferred stores: the previous tile's C block (first tile: zero-size, stores dropped)
+  uint4 dq[DEF > 0 ? DEF : 1];
+  __amdgpu_buffer_rsrc_t rprev = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, 0, 0x00020000);
+  int voffc = 0;
+  if constexpr (DEF > 0) {
+#pragma unroll
+    for (int u = 0; u < DEF; ++u) dq[u] = make_uint4(0, 0, 0, 0);
+    const int fr = lane & 15, fq = lane >> 4;
+    voffc = ((c.wr * (BM / 2) + fr) * ldc + c.wc * (BN / 2) + (fq & 1) * 16 + (fq >> 1) * 8) * 2;
+  }
   for (;;) {
-    pstep<0, X, true, DYN ? 1 : 0, L, WXS>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
-    pstep<1, X, false, DYN ? 2 : 0, L>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
-    for (int t = 2; t < nt - 2; t += 2) {
+    if constexpr (DD > 0) {
+      w4::static_for<0, PEEL>([&](auto jc) {
+        constexpr int J = decltype(jc)::value;
+        constexpr int TKJ = DYN ? (J == 0 ? 1 : J == 1 ? 2 : 0) : 0;
+        constexpr int WXJ = (J >= 1 && J <= DD) ? SPS : 0;
+        pstep<J & 1, X, J == 0, TKJ, L, WXJ>(c, c, f0, f1, J + 2, tq);
+        if constexpr (J < DD) dstore<UI, J * SPS, SPS, DEF, NTST>(dq, rprev, voffc, ldc);
+      });
+    } else {
+      pstep<0, X, true, DYN ? 1 : 0, L, WXS>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
+      pstep<1, X, false, DYN ? 2 : 0, L>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
+    }
+    for (int t = PEEL; t < nt - 2; t += 2) {
       pstep<0, X, false, 0, L>(c, c, f0, f1, t + 2, tq);
       pstep<1, X, false, 0, L>(c, c, f0, f1, t + 3, tq);
     }
-    const int tnx = DYN ? base + __builtin_amdgcn_readfirstlane(tslot) : t + (int)gridDim.x;
+    const int raw = DYN ? __builtin_amdgcn_readfirstlane(tslot) : 0;
+    if constexpr (DYN != 0) mark_bad_ticket(q, raw, ntx);
+    const int tnx = DYN ? base + raw : t + (int)gridDim.x;
     const bool more = (unsigned)tnx < (unsigned)lim;  // see the first ticket's check
     int tmn = tm, tnn = tn;
     if (more) w4::tile_of<X, false>(DYN ? x + 8 * tnx : tnx, ntiles, ntm, ntn, sl, tmn, tnn);
@@ -531,6 +646,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #pragma unroll
       for (int p = 0; p < NB / 2; ++p) old0[p] = *(const uint4*)(r0 + p * 32);
       pepi_addc<0>(c, C, ldc, tm, tn, old0);
+    } else if constexpr (DEF > 0) {
+      pepi_d<EPI, 0, UI, DEF, NTST>(c, C, ldc, tm, tn, bv, dq);
+      rprev = rsrc_c(C, tm, tn, ldc);
     } else if constexpr (!SW) {
       pepi<EPI, 0, NTST, CST>(c, C, ldc, tm, tn, bv);
       if constexpr (CST == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -552,6 +670,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     c.rb = cn.rb;
     c.rb2 = cn.rb2;
   }
+  if constexpr (DEF > 0) dstore<UI, 0, DEF, DEF, NTST>(dq, rprev, voffc, ldc);  // the last tile's deferred units
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before LDS is released
   if constexpr (DYN != 0) {
     if (threadIdx.x == 0 && atomicAdd(q + 8, 1) == (int)gridDim.x - 1)  // last one out resets the queue

@@ -21,7 +21,10 @@
 //    so every replay starts from zero whatever an earlier
 //    replay left (one exec replayed concurrently with itself -- HIP does not
 //    document that it serialises those -- can then only compute a tile twice,
-//    with identical inputs and output, never skip one).
+//    with identical inputs and output, never skip one). That holds for
+//    epilogues that only WRITE C. A read-modify-write epilogue (EPI_ADDC:
+//    C += A.B^T) computed twice adds twice, so kgs_gemm_bf16_nt_addc never
+//    takes a slot while its stream is capturing (it runs the one-shot grid).
 //  * no slot (reserve empty during a capture, allocation failure): nullptr and
 //    the caller runs the one-shot grid, which needs no counters.
 //
@@ -46,6 +49,7 @@
 namespace kgs {
 
 constexpr int TQ_INTS = 16;     // 8 tickets + exit counter, padded to 64 B
+constexpr int TQ_ERR = 15;      // padding word a kernel sets when it read an impossible ticket (sticky)
 constexpr int TQ_CHUNK = 256;   // slots per pool allocation (16 KiB)
 constexpr int TQ_RESERVE = 64;  // free slots kept for captures
 constexpr int TQ_DEVICES = 64;
@@ -55,6 +59,7 @@ struct TileQueueStats {
   long stream_slots;   // owned by a (stream[, thread])
   long capture_slots;  // owned by a captured launch
   long fallbacks;      // calls that returned nullptr
+  long grow_failures;  // pool growths that failed (each starts a backoff)
 };
 
 // Zero one 64-byte slot on `stream` with a KERNEL (tile_queue_zero.h; one
@@ -88,8 +93,9 @@ struct DevicePool {
   std::unordered_map<OwnerKey, int*, OwnerHash> owners;
   hipStream_t zero_stream = nullptr;  // private, non-blocking; touched only by the growing thread
   bool growing = false;               // one growth at a time per device
+  int grow_backoff = 0;               // eager calls to skip growing for after a failed growth
   bool warned = false;                // capture fallback reported once
-  long slots = 0, capture_slots = 0, fallbacks = 0;
+  long slots = 0, capture_slots = 0, fallbacks = 0, grow_failures = 0;
 };
 
 inline std::mutex& mu() {
@@ -125,14 +131,25 @@ inline int* new_chunk(DevicePool& P, int dev) {
 // Grow device `dev`'s pool by one chunk; called with `lock` held, releases it
 // around the allocation. Returns false if another thread is already growing
 // the pool or the allocation failed.
+// After a failure (memory nearly full, no stream) the next TQ_GROW_BACKOFF
+// eager calls do not retry: hipMalloc and stream creation stay off the hot path.
+constexpr int TQ_GROW_BACKOFF = 256;
 inline bool grow(DevicePool& P, int dev, std::unique_lock<std::mutex>& lock) {
   if (P.growing) return false;
+  if (P.grow_backoff > 0) {
+    --P.grow_backoff;
+    return false;
+  }
   P.growing = true;
   lock.unlock();
   int* p = new_chunk(P, dev);
   lock.lock();
   P.growing = false;
-  if (!p) return false;
+  if (!p) {
+    P.grow_backoff = TQ_GROW_BACKOFF;
+    ++P.grow_failures;
+    return false;
+  }
   for (int i = TQ_CHUNK - 1; i >= 0; --i) P.free_slots.push_back(p + i * TQ_INTS);
   P.chunks.push_back(p);
   P.slots += TQ_CHUNK;
@@ -192,9 +209,11 @@ inline int* tile_queue(hipStream_t stream) {
 // tickets. Copies the pool to the host (synchronous): the caller makes sure no
 // GEMM is in flight. out[0..3] = {dirty slots, dirty words, first dirty value,
 // its word index in the pool}; out[4] = the first dirty slot's device address,
-// out[5..20] its 16 words (what overwrote it names the writer). Returns 0 or a
-// hipError_t.
-constexpr int TQ_CHECK_OUT = 5 + TQ_INTS;
+// out[5..20] its 16 words (what overwrote it names the writer); out[21] = slots
+// whose error word (TQ_ERR) is set: a persistent GEMM read a ticket no launch
+// could have issued and stopped taking tiles, so its output is incomplete.
+// Returns 0 or a hipError_t.
+constexpr int TQ_CHECK_OUT = 5 + TQ_INTS + 1;
 inline int tile_queue_check(int dev, long* out) {
   using namespace tq_detail;
   for (int i = 0; i < TQ_CHECK_OUT; ++i) out[i] = 0;
@@ -221,6 +240,7 @@ inline int tile_queue_check(int dev, long* out) {
         }
       }
       out[0] += dirty;
+      out[5 + TQ_INTS] += h[sl * TQ_INTS + TQ_ERR] != 0;
     }
     base += TQ_INTS * TQ_CHUNK;
   }
@@ -229,7 +249,7 @@ inline int tile_queue_check(int dev, long* out) {
 
 inline TileQueueStats tile_queue_stats(int dev) {
   using namespace tq_detail;
-  TileQueueStats st{0, 0, 0, 0};
+  TileQueueStats st{0, 0, 0, 0, 0};
   if (dev < 0 || dev >= TQ_DEVICES) return st;
   std::lock_guard<std::mutex> lock(mu());
   const DevicePool& P = pools()[dev];
@@ -237,6 +257,7 @@ inline TileQueueStats tile_queue_stats(int dev) {
   st.stream_slots = (long)P.owners.size();
   st.capture_slots = P.capture_slots;
   st.fallbacks = P.fallbacks;
+  st.grow_failures = P.grow_failures;
   return st;
 }
 

@@ -54,6 +54,7 @@
 #   gemm_tail    per-workgroup start / per-tile end stamps of the persistent GEMM (head, tail, XCD spread)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
+#   memset_repro pure-HIP hipGraph memset-node check ($G graphs, $R replays, $P extra nodes; no torch)
 #   attn_bench   flash-attention forward vs SDPA
 #   serve_b16    batch-16 serving; skinny_tune: skinny GEMM variant x split-K tune at batches $MS
 #   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
@@ -378,6 +379,7 @@ step() {
             for r in 1 2; do
                 run online_seq_$r 300 $OB --overlap off && run online_ovl_$r 300 $OB --overlap on || return 1
             done ;;
+        memset_repro) run memset_repro 300 kgs/_native/kgs-graph-memset-repro ${G:-4} ${R:-200} ${P:-8} ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac

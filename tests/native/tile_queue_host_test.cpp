@@ -109,6 +109,21 @@ int main() {
   CHECK(chk[4] == (long)(uintptr_t)victim && chk[5 + 3] == 5 && chk[5 + 12] == -792735554 && chk[5] == 0);
   victim[12] = victim[3] = 0;
   CHECK(tile_queue_check(0, chk) == 0 && chk[1] == 0);
+  // 10. a kernel's impossible-ticket flag (padding word TQ_ERR) is counted separately
+  victim[TQ_ERR] = (int)0x80000123;
+  CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 1 && chk[5 + TQ_INTS] == 1);
+  victim[TQ_ERR] = 0;
+  CHECK(tile_queue_check(0, chk) == 0 && chk[0] == 0 && chk[5 + TQ_INTS] == 0);
+  // 11. a failed growth backs off: the next TQ_GROW_BACKOFF eager calls do not
+  // retry hipMalloc / stream creation, then it is tried again
+  fakehip::stream_dev()[S(4000)] = 3;
+  fakehip::malloc_budget() = 0;
+  CHECK(tile_queue(S(4000)) == nullptr && tile_queue_stats(3).grow_failures == 1);
+  fakehip::malloc_budget() = 1 << 30;
+  const int mallocs3 = fakehip::mallocs();
+  for (int i = 0; i < tq_detail::TQ_GROW_BACKOFF; ++i) CHECK(tile_queue(S(4000)) == nullptr);
+  CHECK(fakehip::mallocs() == mallocs3 && tile_queue_stats(3).fallbacks == 1 + tq_detail::TQ_GROW_BACKOFF);
+  CHECK(tile_queue(S(4000)) != nullptr && fakehip::mallocs() == mallocs3 + 1);
   std::printf("tile_queue host test: OK (%ld slots on device 0)\n", tile_queue_stats(0).slots);
   return 0;
 }

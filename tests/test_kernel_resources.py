@@ -16,10 +16,11 @@ pytestmark = pytest.mark.skipif(not Path(HIPCC).exists() and shutil.which("hipcc
                                 reason="hipcc not available")
 
 
-def _compile(src: str, odir: Path, save_temps: bool = False) -> tuple[dict, str]:
+def _compile(src: str, odir: Path, save_temps: bool = False, subdir: str = "kernels") -> tuple[dict, str]:
     """Resource remarks per kernel (and, with save_temps, the device assembly)."""
     cmd = [HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c",
-           str(ROOT / "native" / "kernels" / src), "-o", str(odir / (src + ".o")),
+           "-I", str(ROOT / "native" / "kernels"),
+           str(ROOT / "native" / subdir / src), "-o", str(odir / (src + ".o")),
            "-Rpass-analysis=kernel-resource-usage"]
     if save_temps:
         cmd.append("-save-temps=obj")
@@ -124,6 +125,42 @@ def test_persistent_gemm_k_loop_has_no_full_vmcnt_drain(gemm_build):
         full = [i for i, ln in enumerate(lines)
                 if re.search(r"s_waitcnt vmcnt\(0\)", ln) and "ASMSTART" not in lines[i - 1]]
         assert len(full) <= 3, (name, full)
+
+
+def _stray_agpr_lines(body: str) -> tuple[int, list]:
+    inside, stray, seen = False, [], 0
+    for ln in body.splitlines():
+        if "ASMSTART" in ln:
+            inside = True
+            continue
+        if "ASMEND" in ln:
+            inside = False
+            continue
+        code = ln.split(";")[0].strip()
+        if not code or code.startswith("."):
+            continue
+        if re.search(r"(?<![\w.])a\[?\d+", code):
+            if inside:
+                seen += 1
+            else:
+                stray.append(code)
+    return seen, stray
+
+
+def test_experiment_persistent_gemms_never_touch_agprs_outside_asm(tmp_path):
+    """Round 6: a deferred-store build (gemm_w4p.h DD 6, SPS 4: 24 units of C
+    held in VGPRs) reached 256 VGPRs and the allocator copied VGPRs into
+    accumulator AGPRs (v_accvgpr_write a5, v3 ...): the MFMAs then overwrote
+    them and the kernel faulted on the GPU (illegal address). Every persistent
+    instance of the experiments library is held to the production rule, so an
+    instance at the register limit fails here, on the CPU, not on a GPU box."""
+    _, asm = _compile("gemm_w4h.hip", tmp_path, save_temps=True, subdir="experiments")
+    funcs = _functions(asm, r"gemm_nt_w4pI|gemm_fp8_w4pI")
+    assert len(funcs) >= 40, len(funcs)
+    for name, body in funcs.items():
+        seen, stray = _stray_agpr_lines(body)
+        assert seen >= 256, (name, seen)
+        assert not stray, (name, stray[:5])
 
 
 def test_named_agpr_kernels_never_touch_agprs_outside_asm(gemm_build):
@@ -238,3 +275,117 @@ def test_counted_store_wait_allows_only_the_epilogue_stores_and_k_tile_2(tmp_pat
     first_drain = lines.index("s_waitcnt vmcnt(0)", next(i for i, ln in enumerate(lines) if ln.endswith(" lds")))
     pro = [ln for ln in lines[:first_drain] if vmem.match(ln)]
     assert sum(ln.endswith(" lds") for ln in pro) == 32 and not any("store" in ln for ln in pro)
+
+
+def _code_lines(body: str) -> list:
+    out = []
+    for ln in body.splitlines():
+        code = ln.split(";")[0].strip()
+        if code and not code.startswith(".") and not code.startswith("#"):
+            out.append(code)
+    return out
+
+
+def _ar_protocol_violations(body: str, n_barriers: int) -> list:
+    """Where the P2P all-reduce's cross-GPU ordering (allreduce_p2p.hip
+    block_barrier) is missing from one kernel's ISA:
+      * every flag store (system scope: ``global_store_dword ... sc0 sc1``) has
+        a ``buffer_wbl2 sc0 sc1`` before it, since the last s_barrier, and an
+        ``s_waitcnt vmcnt(0)`` between the two (the write-back finished), with
+        no other store in between;
+      * every flag poll (``global_load_dword ... sc0 sc1``) is followed by
+        ``s_waitcnt vmcnt(0)``, then ``buffer_inv sc0 sc1``, then another
+        ``s_waitcnt vmcnt(0)`` before the next s_barrier (no peer load first);
+      * before every s_barrier, the last vector store / atomic since the
+        previous one is retired by an ``s_waitcnt vmcnt(0)``."""
+    lines = _code_lines(body)
+    errs = []
+    is_flag_store = [bool(re.match(r"global_store_dword\s.*\bsc0 sc1\b", ln)) for ln in lines]
+    is_poll = [bool(re.match(r"global_load_dword\s.*\bsc0 sc1\b", ln)) for ln in lines]
+    vm0 = [bool(re.match(r"s_waitcnt\s.*vmcnt\(0\)", ln)) for ln in lines]
+    bar = [ln.startswith("s_barrier") for ln in lines]
+    if sum(is_flag_store) < n_barriers:
+        errs.append(f"{sum(is_flag_store)} system-scope flag stores < {n_barriers} barriers")
+    if sum(is_poll) < n_barriers:
+        errs.append(f"{sum(is_poll)} system-scope flag polls < {n_barriers} barriers")
+    for i in (i for i, f in enumerate(is_flag_store) if f):
+        j = i - 1
+        while j >= 0 and not bar[j] and not lines[j].startswith("buffer_wbl2"):
+            j -= 1
+        if j < 0 or bar[j] or not re.match(r"buffer_wbl2\s+sc0 sc1\b", lines[j]):
+            errs.append(f"flag store {i} ({lines[i]}): no buffer_wbl2 sc0 sc1 before it")
+            continue
+        mid = lines[j + 1:i]
+        if not any(vm0[j + 1:i]):
+            errs.append(f"flag store {i}: no s_waitcnt vmcnt(0) between buffer_wbl2 and the store")
+        if any(re.match(r"(global|buffer|flat)_(store|atomic)", ln) for ln in mid):
+            errs.append(f"flag store {i}: another store between buffer_wbl2 and the flag")
+    for i in (i for i, f in enumerate(is_poll) if f):
+        nb = next((k for k in range(i + 1, len(lines)) if bar[k]), len(lines))
+        seq = [k for k in range(i + 1, nb)]
+        w1 = next((k for k in seq if vm0[k]), None)
+        inv = next((k for k in seq if re.match(r"buffer_inv\s+sc0 sc1\b", lines[k])), None)
+        if w1 is None or inv is None or not w1 < inv:
+            errs.append(f"poll {i}: no s_waitcnt vmcnt(0) then buffer_inv sc0 sc1 before the next barrier")
+            continue
+        if not any(vm0[k] for k in range(inv + 1, nb)):
+            errs.append(f"poll {i}: buffer_inv not waited for before the barrier")
+        if any(re.match(r"global_load_dwordx", lines[k]) for k in range(i + 1, inv)):
+            errs.append(f"poll {i}: a data load before the invalidate")
+    prev = 0
+    for b in (k for k, f in enumerate(bar) if f):
+        last_vm = max((k for k in range(prev, b) if re.match(r"(global|buffer|flat)_(store|atomic)", lines[k])),
+                      default=None)
+        if last_vm is not None and not any(vm0[last_vm + 1:b]):
+            errs.append(f"barrier {b}: store {last_vm} ({lines[last_vm]}) not retired before it")
+        prev = b
+    return errs
+
+
+def _ar_build(tmp_path, source: str):
+    src = tmp_path / "allreduce_p2p.hip"
+    src.write_text(source)
+    cmd = [HIPCC if Path(HIPCC).exists() else "hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c",
+           "-I", str(ROOT / "native" / "kernels"), str(src), "-o", str(tmp_path / "ar.o"), "-save-temps=obj"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=900, cwd=tmp_path)
+    assert out.returncode == 0, out.stderr[-2000:]
+    (s_file,) = list(tmp_path.glob("allreduce_p2p-hip-amdgcn-amd-amdhsa-gfx950.s"))
+    funcs = _functions(s_file.read_text(), r"allreduce_(one|two)shotILb[01]ELi[2-8]E")
+    assert len(funcs) == 2 * 2 * 7, sorted(funcs)
+    return {n: _ar_protocol_violations(b, 2 if "oneshot" in n else 3) for n, b in funcs.items()}
+
+
+AR_SRC = ROOT / "native" / "kernels" / "allreduce_p2p.hip"
+
+
+def test_p2p_allreduce_orders_its_flags_for_xgmi_peers(tmp_path):
+    """cross-GPU correctness of the P2P all-reduce rests on
+    the flag protocol's system-scope release / acquire. Pinned in the compiled
+    ISA of every one- / two-shot instance with 2-8 ranks (both dtypes): L2
+    written back and the write-back waited for before each flag store, the
+    poll's invalidate waited for before any wave reads peer data, every wave's
+    stores retired before each barrier."""
+    bad = {n: e for n, e in _ar_build(tmp_path, AR_SRC.read_text()).items() if e}
+    assert not bad, {n: e[:3] for n, e in list(bad.items())[:3]}
+
+
+@pytest.mark.parametrize("mutation", ["agent_scope", "round5_release_store"])
+def test_p2p_allreduce_order_check_catches_weakened_builds(tmp_path, mutation):
+    """The checker above fails on builds whose ordering is too weak for xGMI
+    peers: the release / acquire at agent scope (no system write-back /
+    invalidate), and round 5's form -- the release store as one atomic, whose
+    expansion lost the wait between buffer_wbl2 and the flag store."""
+    src = AR_SRC.read_text()
+    if mutation == "agent_scope":
+        mutated = src.replace('__builtin_amdgcn_fence(__ATOMIC_RELEASE, "")', '__builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent")')
+        mutated = mutated.replace("__HIP_MEMORY_SCOPE_SYSTEM", "__HIP_MEMORY_SCOPE_AGENT")
+    else:
+        old = ('    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: buffer_wbl2 sc0 sc1\n'
+               '    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n'
+               '    __hip_atomic_store(&P.sig[p]->flag[phase][b][rank], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);\n')
+        new = '    __hip_atomic_store(&P.sig[p]->flag[phase][b][rank], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);\n'
+        assert old in src
+        mutated = src.replace(old, new)
+    assert mutated != src
+    bad = {n: e for n, e in _ar_build(tmp_path, mutated).items() if e}
+    assert bad, "the weakened build passed the ordering check"

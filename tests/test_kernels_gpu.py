@@ -530,13 +530,18 @@ def test_gemm_w4x_swiglu_epilogue(M, I, K, bn, bm):
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 4096, 4096), (4096, 8192, 1024), (4096, 4096, 4096), (2048, 1024, 4096),
-                                   (1024, 512, 768), (16384, 4096, 1024)])
+                                   (1024, 512, 768), (16384, 4096, 1024),
+                                   # the long-K persistent instances (tile groups of 8), tall and wide --
+                                   # Llama-8B's prompt-pass down projection is 8192 x 4096 x 14336
+                                   (8192, 4096, 14336), (4096, 8192, 14336)])
 def test_residual_add_epilogue_is_bitwise_gemm_then_add(M, N, K):
     """Round 5: the prompt pass's o / down GEMM with the residual add in its
     store (EPI_ADDC; persistent and one-shot grids, tall and wide) leaves x
     bitwise where gemm_nt + add_rmsnorm's add leaves it, and the plain rmsnorm
-    after it gives add_rmsnorm's normalised rows."""
+    after it gives add_rmsnorm's normalised rows. With more tiles than CUs the
+    launch is the persistent kernel: on a fresh stream it takes a ticket slot."""
     from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
     from kgs.ops.gemm import addc_ok, gemm_nt_add_
     from kgs.ops.transformer import add_rmsnorm
 
@@ -549,11 +554,46 @@ def test_residual_add_epilogue_is_bitwise_gemm_then_add(M, N, K):
     y_ref = add_rmsnorm(x_ref, gemm_nt(a, b), w)
     x = x0.clone()
     assert addc_ok(a, b, x)
-    gemm_nt_add_(a, b, x)
     torch.cuda.synchronize()
+    st0 = tile_queue_stats()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        gemm_nt_add_(a, b, x)
+    torch.cuda.synchronize()
+    persistent = (M // 256) * (N // 256) > torch.cuda.get_device_properties(DEV).multi_processor_count
+    assert tile_queue_stats()["stream_slots"] == st0["stream_slots"] + int(persistent)
     assert torch.equal(x, x_ref)
     assert torch.equal(add_rmsnorm(x, None, w), y_ref)
     assert not addc_ok(a[: M - 8], b, x[: M - 8])  # unaligned rows: the caller keeps the unfused pair
+    assert tile_queue_check()["dirty_slots"] == 0
+
+
+def test_residual_add_epilogue_in_a_graph_takes_no_ticket_slot():
+    """a captured EPI_ADDC launch runs the one-shot grid (a graph
+    exec replayed concurrently with itself may compute a persistent tile twice,
+    and C += A.B^T would add twice): no capture slot is taken, and one replay
+    adds exactly once, bitwise the eager launch."""
+    from kgs.ops._lib import tile_queue_stats
+    from kgs.ops.gemm import gemm_nt_add_
+
+    M, N, K = 8192, 4096, 4096
+    g = torch.Generator(device=DEV).manual_seed(11)
+    a = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b = ((torch.rand(N, K, device=DEV, generator=g) * 2 - 1) * K ** -0.5).bfloat16()
+    x0 = (torch.rand(M, N, device=DEV, generator=g) * 4 - 2).bfloat16()
+    want = gemm_nt_add_(a, b, x0.clone())
+    x = x0.clone()
+    st0 = tile_queue_stats()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gemm_nt_add_(a, b, x)
+    assert tile_queue_stats()["capture_slots"] == st0["capture_slots"]
+    x.copy_(x0)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(x, want)
+    del graph
 
 
 @pytest.mark.parametrize("M,I,K", [(2048, 8192, 1024), (1024, 14336, 4096), (4096, 4096, 768)])
@@ -721,7 +761,14 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
                                            (8192, 2304, 9216, "w4po2_140000008"),
                                            # round 5: drain after each tile's stores (measurement build)
                                            (8192, 8192, 384, "w4pd_0"), (8192, 8192, 384, "w4pw_0"),
-                                           (8192, 2304, 9216, "w4pw_0"), (4608, 4096, 384, "w4pw_0")])
+                                           (8192, 2304, 9216, "w4pw_0"), (4608, 4096, 384, "w4pw_0"),
+                                           # round 6: deferred C stores (gemm_w4p.h DD, SPS)
+                                           (8192, 8192, 1024, "w4pq8x2n_0"), (4608, 4096, 768, "w4pq8x2n_0"),
+                                           (1024, 768, 1024, "w4pq8x2n_0"), (8192, 8192, 2048, "w4pq4x4n_0"),
+                                           (8192, 8192, 1024, "w4pq8x1n_0"), (8192, 8192, 1024, "w4pq10x2n_0"),
+                                           (8192, 8192, 1280, "w4pq16x1n_0"), (8192, 8192, 1024, "w4pq12x1n_0"),
+                                           (8192, 8192, 1024, "w4pq8x2_0"), (8192, 2304, 9216, "w4pq8x2_140000008"),
+                                           (8192, 2304, 9216, "w4pq8x2n_140000008"), (4096, 4608, 8320, "w4pq8x2n_8")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
     tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
@@ -753,6 +800,44 @@ def test_gemm_auto_nt_store_route_is_bitwise_the_one_shot_kernel(M, N, K):
     assert torch.equal(gemm_nt(a, b), _gemm_v(a, b, "w4pn_0"))
 
 
+@pytest.mark.parametrize("M,N,K", [(8192, 8192, 8192), (8192, 4096, 14336), (16384, 16384, 8192)])
+def test_production_route_at_the_bench_shapes_in_full(M, N, K):
+    """gemm_nt's default route at the headline shapes (8192^3:
+    persistent, non-temporal C; 8192 x 4096 x 14336: tall, long-K mirrored
+    tile-group-8 map; 16384^2 x 8192: persistent, 16 tiles per CU) against an
+    fp32 reference over the WHOLE output, and bitwise the one-shot grid of the
+    same K-step. The route is the persistent kernel: on a fresh stream the
+    launch takes a ticket slot."""
+    from kgs.ops import gemm_nt
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
+
+    g = torch.Generator(device=DEV).manual_seed(M + 3 * N + 7 * K)
+    a = (torch.rand(M, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV, generator=g) * 2 - 1).bfloat16()
+    torch.cuda.synchronize()
+    st0 = tile_queue_stats()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        c = gemm_nt(a, b)
+    torch.cuda.synchronize()
+    assert tile_queue_stats()["stream_slots"] == st0["stream_slots"] + 1
+    assert tile_queue_check()["dirty_slots"] == 0
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        bf, err, amax = b.float(), 0.0, 0.0
+        for r0 in range(0, M, 2048):
+            ref = a[r0:r0 + 2048].float() @ bf.T
+            err = max(err, (c[r0:r0 + 2048].float() - ref).abs().max().item())
+            amax = max(amax, ref.abs().max().item())
+            del ref
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
+    assert err / amax < 1e-2, err / amax
+    assert torch.equal(c, gemm_nt(a, b, variant="w4_oneshot"))
+
+
 def test_gemm_persistent_counted_store_wait_repeats_bitwise():
     """w4pw (gemm_w4p.h CST 3): K-step 0 after an epilogue waits vmcnt(ND + the
     epilogue's stores), i.e. only for the next tile's K-tile-1 DMAs. If vmcnt did
@@ -764,6 +849,26 @@ def test_gemm_persistent_counted_store_wait_repeats_bitwise():
     one_shot = _gemm_v(a, b, "w4h_1_24_20_1_0")
     for i in range(24):
         assert torch.equal(_gemm_v(a, b, "w4pw_0"), one_shot), i
+
+
+def test_gemm_persistent_deferred_stores_repeat_bitwise_and_refuse_short_k():
+    """w4pq (gemm_w4p.h DD > 0): the next tile's K-steps 0 .. DD - 1 store the
+    previous tile's deferred C units and the K-step after each waits
+    vmcnt(ND + SPS), counting those stores as younger than the DMA it waits for.
+    If vmcnt did not complete in issue order, or a first tile's dropped stores
+    (zero-size buffer) were not counted, a K-step would read a K-tile still in
+    flight: 24 launches at 4 tiles per CU, every one bitwise the one-shot
+    kernel. K-steps fewer than the peeled ones + 2 are refused, not run."""
+    from kgs.ops import experiments as ex
+
+    a = (torch.rand(8192, 1024, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(8192, 1024, device=DEV) * 2 - 1).bfloat16()
+    one_shot = _gemm_v(a, b, "w4h_1_24_20_1_0")
+    for i in range(24):
+        assert torch.equal(_gemm_v(a, b, "w4pq8x2n_0" if i % 2 else "w4pq4x4n_0"), one_shot), i
+    short = (torch.rand(8192, 640, device=DEV) * 2 - 1).bfloat16()  # 10 K-steps < 10 peeled + 2
+    with pytest.raises(RuntimeError):
+        ex.gemm_nt(short, short, "w4pq8x2n_0")
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 512), (8192, 2304, 9216), (1024, 768, 1024)])
@@ -1063,6 +1168,10 @@ def test_first_persistent_gemm_on_a_busy_new_stream_returns_without_waiting():
 
     As, b = _queue_operands(1, seed=14)
     ref = gemm_nt(As[0], b, variant="w4_oneshot")
+    # the persistent instance launched once before the timed call: the first launch of a kernel loads
+    # its code object (lazy loading), which can wait for the device -- not what this test times
+    gemm_nt(As[0], b)
+    torch.cuda.synchronize()
     reserve = 64  # tile_queue.h TQ_RESERVE
 
     def free():

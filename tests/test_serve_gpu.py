@@ -332,6 +332,55 @@ def test_batch256_graph_decode_equals_eager_with_the_persistent_lm_head():
     assert toks[True] == toks[False]
 
 
+@pytest.mark.parametrize("kw", [{}, {"decode_weights": "fp8"}, {"kv_cache_dtype": "fp8"}], ids=["bf16", "fp8w", "fp8kv"])
+def test_serving_graphs_hold_no_memset_node(monkeypatch, kw):
+    """a memset node (captured hipMemsetAsync) is what left
+    garbage in a ticket slot in round 5. Every decode graph the engine captures
+    -- all batch / page-width buckets of warmup(), bf16, fp8 weights, fp8 KV --
+    is walked node by node through the HIP graph API (kgs.utils.graph_audit,
+    child graphs expanded): no memset node, and the kernels are there. The
+    audited graphs then serve: the tokens equal the eager engine's."""
+    from kgs.serve import SamplingParams
+
+    monkeypatch.setenv("KGS_GRAPH_AUDIT", "1")
+    eng = _engine(True, max_batch=16, **kw)
+    assert eng.graph_audit
+    eng.warmup()
+    assert len(eng.graph_audits) >= 5 * 3, sorted(eng.graph_audits)
+    for key, a in eng.graph_audits.items():
+        assert a["types"].get("kernel", 0) > 10, (key, a["types"])
+        assert a["types"].get("memset", 0) == 0 and not a["memsets"], (key, a["memsets"][:3])
+    rng = np.random.default_rng(9)
+    prompts = [rng.integers(3, 1024, size=n).tolist() for n in (21, 70, 5)]
+    p = SamplingParams(max_tokens=6, ignore_eos=True)
+    got = [r.output for r in eng.generate(prompts, p)]
+    assert eng.stats["graph_replays"] > 0
+    monkeypatch.setenv("KGS_GRAPH_AUDIT", "0")
+    assert got == [r.output for r in _engine(False, max_batch=16, **kw).generate(prompts, p)]
+
+
+def test_batch256_serving_graph_with_the_persistent_lm_head_holds_no_memset_node(monkeypatch):
+    """The graph that faulted in round 5 (batch 256, Llama-3 LM head on the
+    persistent GEMM, a captured ticket slot): its slot is now zeroed by a kernel
+    node, and the graph holds no memset node at all."""
+    from kgs.models.llama import LlamaConfig
+    from kgs.ops._lib import tile_queue_check, tile_queue_stats
+    from kgs.serve import EngineConfig, LLMEngine
+
+    monkeypatch.setenv("KGS_GRAPH_AUDIT", "1")
+    cfg = LlamaConfig(hidden=4096, intermediate=14336, heads=32, kv_heads=8, layers=1, vocab=128256)
+    eng = LLMEngine(cfg, EngineConfig(num_pages=1024, max_batch=256, max_model_len=256, cuda_graphs=True),
+                    device="cuda", backend="kgs")
+    st0 = tile_queue_stats()
+    eng.warmup(batches=[256], widths=[8])
+    assert tile_queue_stats()["capture_slots"] > st0["capture_slots"]  # the LM head is the persistent kernel
+    a = eng.graph_audits[(256, 8)]
+    assert a["types"].get("memset", 0) == 0 and a["types"]["kernel"] > 10, a["types"]
+    assert tile_queue_check()["dirty_slots"] == 0
+    del eng
+    torch.cuda.empty_cache()
+
+
 def test_nt_loads_and_gate_up_panels_keep_the_tokens(monkeypatch):
     """Round 5 made non-temporal decode weight loads and the SwiGLU gate|up
     tile-panel copies the default (profiles/r5/decode/README.md). Both only
