@@ -39,6 +39,7 @@ _SIGS = {
     "kgs_gemm_bf16_nt_addc": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6 + [_c_void_p], _c_int),
     "kgs_tile_queue_stats": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
     "kgs_tile_queue_check": ([_c_int, ctypes.POINTER(_c_long)], _c_int),
+    "kgs_tile_queue_slot": ([_c_void_p, ctypes.POINTER(_c_void_p)], _c_int),
     "kgs_gemm_bf16_nt_fast_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_bounded_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),
     "kgs_gemm_bf16_nt_w4_ok": ([_c_void_p, _c_void_p, _c_void_p] + [_c_int] * 6, _c_int),

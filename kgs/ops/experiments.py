@@ -91,7 +91,13 @@ W4H.update({"w4pw_0": 145})
 # round 6: deferred C stores (gemm_w4p.h DD, SPS): w4pq<DD>x<SPS>[n]_<X> (n: non-temporal stores) -> 146..
 W4H.update({"w4pq8x2n_0": 146, "w4pq4x4n_0": 147, "w4pq8x1n_0": 148, "w4pq10x2n_0": 149, "w4pq16x1n_0": 150,
             "w4pq8x2_0": 151, "w4pq8x2_140000008": 152, "w4pq12x1n_0": 153, "w4pq8x2n_140000008": 154,
-            "w4pq8x2n_8": 155})
+            "w4pq8x2n_8": 155, "w4pq1x16n_0": 156, "w4pq2x8n_0": 157, "w4pq3x6n_0": 158, "w4pq2x10n_0": 159,
+            "w4pq4x5n_0": 160, "w4pq4x4_140000008": 161, "w4pq4x4n_140000008": 162, "w4pq4x4_0": 163,
+            "w4pq4x4_8": 164, "w4pq2x8_140000008": 165, "w4pq2x8_0": 166})
+# round 6: one barrier per K-step (gemm_w4p.h OB), DMA window W MFMAs: w4pb[w<W>][q<DD>x<SPS>][t]_<X>
+# (nt C stores unless t) -> 167..
+W4H.update({"w4pb_0": 167, "w4pbw48_0": 168, "w4pbw32_0": 169, "w4pbq4x4_0": 170, "w4pbt_140000008": 171,
+            "w4pbt_8": 172, "w4pbt_0": 173, "w4pbw64_0": 174})
 NO_OUTPUT = frozenset({"w4px_0"})  # timing only: C is not written
 
 

@@ -143,7 +143,35 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
       KGS_W4PQ(153, 0, true, 12, 1)
       KGS_W4PQ(154, 140000008, true, 8, 2)
       KGS_W4PQ(155, 8, true, 8, 2)
+      // fewer storing K-steps, more stores each (4 x 4 led the first sweep)
+      KGS_W4PQ(156, 0, true, 1, 16)
+      KGS_W4PQ(157, 0, true, 2, 8)
+      KGS_W4PQ(158, 0, true, 3, 6)
+      KGS_W4PQ(159, 0, true, 2, 10)
+      KGS_W4PQ(160, 0, true, 4, 5)
+      KGS_W4PQ(161, 140000008, false, 4, 4)
+      KGS_W4PQ(162, 140000008, true, 4, 4)
+      KGS_W4PQ(163, 0, false, 4, 4)
+      KGS_W4PQ(164, 8, false, 4, 4)
+      KGS_W4PQ(165, 140000008, false, 2, 8)
+      KGS_W4PQ(166, 0, false, 2, 8)
 #undef KGS_W4PQ
+      // round 6: one barrier per K-step (gemm_w4p.h (L / 1000) % 10 == 1), DMA window W = (L / 10^4) % 100
+#define KGS_W4PB(ID, X, NT, L, DD, SPS)                                                                       \
+  case ID:                                                                                                    \
+    if (K / 64 < ((DD + 2) & ~1) + 2) return KGS_ERR_SHAPE;                                                   \
+    hipLaunchKernelGGL((kgs::w4p::gemm_nt_w4p<kgs::EPI_NONE, X, 1, NT, false, L, DD, SPS>), pg, dim3(256), 0, s, a, \
+                       b, c, nullptr, M, N, K, lda, ldb, ldc, tq);                                             \
+    break;
+      KGS_W4PB(167, 0, true, 1000, 0, 2)
+      KGS_W4PB(168, 0, true, 481000, 0, 2)
+      KGS_W4PB(169, 0, true, 321000, 0, 2)
+      KGS_W4PB(170, 0, true, 1000, 4, 4)
+      KGS_W4PB(171, 140000008, false, 1000, 0, 2)
+      KGS_W4PB(172, 8, false, 1000, 0, 2)
+      KGS_W4PB(173, 0, false, 1000, 0, 2)
+      KGS_W4PB(174, 0, true, 641000, 0, 2)
+#undef KGS_W4PB
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)
       KGS_W4P(122, 140000000, false)

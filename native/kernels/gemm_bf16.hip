@@ -235,6 +235,14 @@ KGS_EXPORT int kgs_tile_queue_stats(int dev, long* out) {
   return 0;
 }
 
+// Test hook: the ticket slot stream `s` owns (taken now if it has none), so a
+// GPU test can corrupt it and check that the persistent kernels report the
+// impossible tickets instead of faulting or skipping tiles silently.
+KGS_EXPORT int kgs_tile_queue_slot(hipStream_t s, void** out) {
+  *out = kgs::tile_queue(s);
+  return *out ? 0 : KGS_ERR_ARG;
+}
+
 // The quiescent-pool invariant (tile_queue.h tile_queue_check): out = {dirty
 // slots, dirty words, first dirty value, its word index, the first dirty slot's
 // address, its 16 words, slots with the impossible-ticket error word set}. No

@@ -31,12 +31,21 @@ hipError_t launch_w4p(const unsigned short* A, const unsigned short* B, unsigned
                        tq);
   else if (longk)
     hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 8>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
+  else if (EPI == EPI_NONE && tiles > 2 * cus && tiles <= 8 * cus && K / 64 >= 8)
+    // 3-8 tiles per CU, plain C: stored non-temporally, and half of each tile's C deferred
+    // (gemm_w4p.h DD 4, SPS 4: 16 of a lane's 32 units held in VGPRs and stored 4 at a time at
+    // the end of the next tile's K-steps 0-3). Every tile change drains 32 MiB of C stores at
+    // once (4 MiB per XCD, the whole L2) and the step waits for it (3.4 % of the 8192^3 bench
+    // step, profiles/r5/gemm/store_drain); nt stores shorten the drain: 8192^3 +0.5 / +0.5 /
+    // +1.0 % on three boxes (profiles/r4/gemm/ntstore_sweep_boxD.json, profiles/r4/validate_b,
+    // profiles/r5/gemm/store_drain); the deferral a further 0.41 / 0.40 / 0.46 % on three boxes
+    // (profiles/r6/gemm/deferred). At 16 tiles per CU (16384^2x8192) nt measured -1.2 % and
+    // the deferral nothing, and K < 512 has too few K-steps for the peeled ones.
+    // (DD / SPS spelled per EPI so the other epilogues reuse their one instance of the default)
+    hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0, 1, EPI == EPI_NONE, false, 0, EPI == EPI_NONE ? 4 : 0,
+                                         EPI == EPI_NONE ? 4 : 2>),
+                       pg, dim3(256), 0, s, A, B, C, bias, M, N, K, lda, ldb, ldc, tq);
   else if (EPI == EPI_NONE && tiles > 2 * cus && tiles <= 8 * cus)
-    // 3-8 tiles per CU, plain C: stored non-temporally. Every tile change drains 32 MiB of C
-    // stores at once (4 MiB per XCD, the whole L2) and the step waits for it (3.4 % of the
-    // 8192^3 bench step); nt stores shorten the drain: 8192^3 +0.5 / +0.5 / +1.0 % on three
-    // boxes (profiles/r4/gemm/ntstore_sweep_boxD.json, profiles/r4/validate_b,
-    // profiles/r5/gemm/store_drain). At 16 tiles per CU (16384^2x8192) it measured -1.2 %.
     hipLaunchKernelGGL((w4p::gemm_nt_w4p<EPI, 0, 1, EPI == EPI_NONE>), pg, dim3(256), 0, s, A, B, C, bias, M, N, K,
                        lda, ldb, ldc, tq);
   else

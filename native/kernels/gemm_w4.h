@@ -272,7 +272,7 @@ __device__ __forceinline__ void wait_vm() {
   else if constexpr (N == 32) asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
   else if constexpr (N == 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
   else if constexpr (N == 48) asm volatile("s_waitcnt vmcnt(48)" ::: "memory");
-  else if constexpr (N > 16 && N < 64) {
+  else if constexpr (N >= 0 && N < 64) {
     // other counts (gemm_w4p.h deferred C stores: ND + stores per K-step): the
     // gfx9 encoding vmcnt[3:0] | vmcnt[5:4] << 14, expcnt 7, lgkmcnt 15
     __builtin_amdgcn_sched_barrier(0);

@@ -178,7 +178,8 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
       else f1.b[x] = w4::frag(sp.pb1 + Lay<L % 10>::frag_off(x));
     }
     if constexpr (K >= B1 && K < KM - R) {
-      constexpr int NW = KM - R - B1;
+      // DMA window: the MFMAs [B1, KM - R), or the first W of them ((L / 10^4) % 100, experiments)
+      constexpr int NW = (L / 10000) % 100 ? (L / 10000) % 100 : KM - R - B1;
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
         if (B1 + (j * NW) / ND == K) pdma<L, X>(cd, ST, j, sp.k0);
@@ -194,11 +195,22 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
       }
     }
     w4::fence();
+    // OB ((L / 1000) % 10 == 1, experiments): ONE barrier per K-step. At MFMA B1 - 1 the wave waits for
+    // its own DMAs of K-tile t + 1 (issued by the previous K-step; nothing younger but WX stores) and
+    // for its reads of stage ST, then a barrier: stage ST is free for this step's DMAs AND K-tile t + 1
+    // is visible for the f0 reads of the last R MFMAs, so the barrier at KM - R - 1 goes.
+    constexpr bool OB = (L / 1000) % 10 == 1;
     if constexpr (K == B1 - 1) {
+      if constexpr (OB) w4::wait_vm<WX>();
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage ST retired
       w4::bar();
+      if constexpr (OB && TK == 1) {
+        if (threadIdx.x == 0) tq.tk = atomicAdd(tq.qx, 1);
+      } else if constexpr (OB && TK == 2) {
+        if (threadIdx.x == 0) *tq.slot = tq.tk;
+      }
     }
-    if constexpr (K == KM - R - 1) {
+    if constexpr (K == KM - R - 1 && !OB) {
       w4::wait_vm<ND + WX>();  // own DMA of the next K-tile landed (WX: younger stores, see the kernel)
       w4::bar();
       if constexpr (TK == 1) {
@@ -488,6 +500,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   constexpr int PEEL = DD ? ((DD + 2) & ~1) : 2;
   static_assert(DD == 0 || (EPI != EPI_ADDC && !SW && CST == 0 && L % 10 == 0), "deferred stores: plain tiles");
   static_assert(DEF >= 0 && UI >= 0 && (DD == 0 || SPS > 0), "deferred stores: at most a tile's units");
+  static_assert((L / 1000) % 10 == 0 || (CST == 0 && !TS), "one-barrier K-step: no store measurement builds");
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {

@@ -81,8 +81,11 @@ __global__ __launch_bounds__(THREADS) void quantize_kernel(const void* __restric
 }
 
 // the amax accumulator's reset, as a kernel: inside a hipGraph capture a
-// hipMemsetAsync becomes a memset node, which on this ROCm wrote garbage instead
-// of zeros (tile_queue.h tq_zero_slot, profiles/r5/fault/README.md)
+// hipMemsetAsync becomes a memset node, and in round 5 a memset node in the
+// captured serving graph left garbage instead of zeros (tile_queue.h
+// tq_zero_slot). A pure-HIP reproducer does not fail on its own, on ROCm 7.2 or
+// on torch's HIP 7.0 (profiles/r6/memset/README.md), so the trigger is in the
+// capture context, not isolated; captured paths use kernel nodes either way.
 __global__ __launch_bounds__(64) void zero_amax(unsigned* __restrict__ out2) {
   if (threadIdx.x == 0) out2[0] = 0u;
 }

@@ -64,12 +64,17 @@ struct TileQueueStats {
 
 // Zero one 64-byte slot on `stream` with a KERNEL (tile_queue_zero.h; one
 // definition per library). In a hipGraph capture it becomes a kernel node like
-// every other node. A captured hipMemsetAsync -- a memset node -- did not
-// zero the slot on this ROCm: after the decode graph's first replay the slot
-// held 64 bytes of host-pointer-like words (0x00005639_00004020,
-// 0x000073fd_988f2020, ...), i.e. garbage tickets; with a word whose high bit
-// was set the persistent GEMM turned it into a negative tile index and the
-// serving run died with hipErrorIllegalAddress (profiles/r5/fault/README.md).
+// every other node. In round 5 a captured hipMemsetAsync -- a memset node --
+// in the serving engine's decode graph did not zero the slot: after the
+// graph's first replay it held 64 bytes of host-pointer-like words
+// (0x00005639_00004020, 0x000073fd_988f2020, ...), i.e. garbage tickets; with a
+// word whose high bit was set the persistent GEMM turned it into a negative
+// tile index and the run died with hipErrorIllegalAddress
+// (profiles/r5/fault/README.md). A pure-HIP reproducer (memset node -> copy ->
+// dirty, 1600 replays, serial and concurrent) zeroes correctly on ROCm 7.2 and
+// on torch's HIP 7.0 (profiles/r6/memset/README.md): memset nodes do not fail
+// on their own; what in that capture made this one fail is not isolated.
+// tests/test_serve_gpu.py now asserts the serving graphs hold no memset node.
 hipError_t tq_zero_slot(int* slot, hipStream_t stream);
 
 namespace tq_detail {
@@ -115,8 +120,20 @@ inline int* new_chunk(DevicePool& P, int dev) {
   if (hipGetDevice(&cur) != hipSuccess) return nullptr;
   if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
   int* p = nullptr;
-  bool ok = P.zero_stream != nullptr ||
-            hipStreamCreateWithFlags(&P.zero_stream, hipStreamNonBlocking) == hipSuccess;
+  // The zeroing stream is HIGH priority. HIP multiplexes streams onto a few
+  // hardware queues per priority (GPU_MAX_HW_QUEUES, 4 here); a normal-priority
+  // private stream can share its hardware queue with a caller's stream, and
+  // then the chunk's memset -- and this thread's sync on it -- waits behind
+  // whatever that stream is running (measured: a 50 ms CU hold on the caller's
+  // stream made its first persistent GEMM call take 50 ms of host time). High
+  // priority streams come from their own queue pool.
+  bool ok = P.zero_stream != nullptr;
+  if (!ok) {
+    int least = 0, greatest = 0;
+    ok = (hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+          hipStreamCreateWithPriority(&P.zero_stream, hipStreamNonBlocking, greatest) == hipSuccess) ||
+         hipStreamCreateWithFlags(&P.zero_stream, hipStreamNonBlocking) == hipSuccess;
+  }
   ok = ok && hipMalloc(&p, sizeof(int) * TQ_INTS * TQ_CHUNK) == hipSuccess;
   ok = ok && hipMemsetAsync(p, 0, sizeof(int) * TQ_INTS * TQ_CHUNK, P.zero_stream) == hipSuccess &&
        hipStreamSynchronize(P.zero_stream) == hipSuccess;

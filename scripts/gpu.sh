@@ -38,6 +38,8 @@
 #   lib_ab       this tree's kernel library vs another build ($LIB_B), interleaved, five sweep shapes
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
+#   wait_split   SQ_WAIT_ANY vs K at 8192 x 8192 x K (persistent nt / deferred / one-shot / hipBLASLt): per-K-step
+#                and fixed (tile change + launch) parts (bench/wait_split.py)
 #   gemm_pmc2    kgs vs hipBLASLt at $MNK: SQ waits / MFMA busy, L2 hit-miss-DRAM, L1 latency / pending stalls
 #   bench_trace  kernel trace of bench.py (GEMM durations and the gaps between them)
 #   overlap_rccl GEMM first-ticket / grid policies vs an RCCL-shaped CU hold (normal and high-priority side stream)
@@ -54,7 +56,8 @@
 #   gemm_tail    per-workgroup start / per-tile end stamps of the persistent GEMM (head, tail, XCD spread)
 #   w4x_sweep    decode-batch GEMM sweep (four-wave tiles, slices, stages vs hipBLASLt)
 #   kt           GPU tests matching $KT (pytest -k)
-#   memset_repro pure-HIP hipGraph memset-node check ($G graphs, $R replays, $P extra nodes; no torch)
+#   memset_repro pure-HIP hipGraph memset-node check ($G graphs, $R replays, $P extra nodes; no torch);
+#                memset_repro_torch: the same binary on torch's bundled HIP runtime
 #   attn_bench   flash-attention forward vs SDPA
 #   serve_b16    batch-16 serving; skinny_tune: skinny GEMM variant x split-K tune at batches $MS
 #   online_sweep online serving (Poisson arrivals, 2048-row chunked steps) at 8-96 req/s
@@ -238,6 +241,13 @@ step() {
             run g2_tcp 120 timeout -s KILL 100 rocprofv3 --pmc TA_BUSY_avr TCP_TCC_READ_REQ_sum \
                 TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE \
                 --output-format csv -d "$O/g2_tcp_${MNK:-8192}" -o g -- $G ;;
+        wait_split)  # SQ waits of the persistent GEMM vs K at a fixed tile grid: steady K-loop vs tile change
+            local W="python3 bench/wait_split.py --plan $O/ws_plan.json"
+            run ws_sq 240 timeout -s KILL 230 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+                SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+                GRBM_COUNT --output-format csv -d "$O/ws_sq" -o w -- $W &&
+            run ws_sum 60 python3 bench/wait_split.py --summary "$O/ws_sq" --plan $O/ws_plan.json \
+                --json "$O/wait_split.json" ;;
         bench_trace) run bench_trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/btrace" -o b \
             -- python3 bench.py --steps 20 --warmup 5 ;;
         overlap_rccl) run overlap_rccl 300 python bench/overlap_rccl.py --out "$O/overlap_rccl_shape.json" &&
@@ -380,6 +390,11 @@ step() {
                 run online_seq_$r 300 $OB --overlap off && run online_ovl_$r 300 $OB --overlap on || return 1
             done ;;
         memset_repro) run memset_repro 300 kgs/_native/kgs-graph-memset-repro ${G:-4} ${R:-200} ${P:-8} ;;
+        memset_repro_torch)  # the same binary on torch's bundled HIP runtime (the one the serving engine used)
+            local th=/tmp/kgs_torchhip
+            mkdir -p $th && ln -sf "$(python3 -c 'import os, torch; print(os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so"))')" $th/libamdhip64.so.7 &&
+            LD_LIBRARY_PATH=$th${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} run memset_repro_torch 300 \
+                kgs/_native/kgs-graph-memset-repro ${G:-4} ${R:-200} ${P:-8} ;;
         kt) run kt 600 python -u -m pytest tests -x -v -m gpu -k "$KT" --timeout 120 --timeout-method thread ;;
         *) echo "unknown step $1" >&2; return 2 ;;
     esac

@@ -69,3 +69,18 @@ inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned flags) {
   fakehip::created().push_back(*s);
   return flags == hipStreamNonBlocking ? hipSuccess : 1;
 }
+namespace fakehip {
+inline std::vector<int>& priorities() {
+  static std::vector<int> v;
+  return v;
+}
+}  // namespace fakehip
+inline hipError_t hipDeviceGetStreamPriorityRange(int* least, int* greatest) {
+  *least = 0;
+  *greatest = -1;
+  return hipSuccess;
+}
+inline hipError_t hipStreamCreateWithPriority(hipStream_t* s, unsigned flags, int priority) {
+  fakehip::priorities().push_back(priority);
+  return hipStreamCreateWithFlags(s, flags);
+}

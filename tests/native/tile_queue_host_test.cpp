@@ -80,6 +80,9 @@ int main() {
   // sync went to a pool-private stream
   std::set<hipStream_t> priv(fakehip::created().begin(), fakehip::created().end());
   CHECK(priv.size() == 3);  // one per device that tried to grow (device 2: allocation then failed)
+  // ... each created at the highest priority: its own hardware-queue pool, never a caller's queue
+  CHECK(fakehip::priorities().size() == 3);
+  for (int pr : fakehip::priorities()) CHECK(pr == -1);
   for (const auto& m : fakehip::memsets())
     CHECK(m.n == 64 ? !priv.count(m.s) : (priv.count(m.s) && !m.captured));
   CHECK(!fakehip::syncs().empty());

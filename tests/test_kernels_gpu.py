@@ -768,7 +768,19 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
                                            (8192, 8192, 1024, "w4pq8x1n_0"), (8192, 8192, 1024, "w4pq10x2n_0"),
                                            (8192, 8192, 1280, "w4pq16x1n_0"), (8192, 8192, 1024, "w4pq12x1n_0"),
                                            (8192, 8192, 1024, "w4pq8x2_0"), (8192, 2304, 9216, "w4pq8x2_140000008"),
-                                           (8192, 2304, 9216, "w4pq8x2n_140000008"), (4096, 4608, 8320, "w4pq8x2n_8")])
+                                           (8192, 2304, 9216, "w4pq8x2n_140000008"), (4096, 4608, 8320, "w4pq8x2n_8"),
+                                           (8192, 8192, 1024, "w4pq1x16n_0"), (8192, 8192, 1024, "w4pq2x8n_0"),
+                                           (8192, 8192, 1024, "w4pq3x6n_0"), (8192, 8192, 1024, "w4pq2x10n_0"),
+                                           (8192, 8192, 1024, "w4pq4x5n_0"), (8192, 2304, 9216, "w4pq4x4_140000008"),
+                                           (8192, 2304, 9216, "w4pq4x4n_140000008"), (8192, 8192, 1024, "w4pq4x4_0"),
+                                           (4096, 4608, 8320, "w4pq4x4_8"), (8192, 2304, 9216, "w4pq2x8_140000008"),
+                                           (8192, 8192, 1024, "w4pq2x8_0"), (1024, 768, 1024, "w4pq1x16n_0"),
+                                           # round 6: one barrier per K-step
+                                           (8192, 8192, 1024, "w4pb_0"), (4608, 4096, 384, "w4pb_0"),
+                                           (1024, 768, 1024, "w4pb_0"), (8192, 8192, 1024, "w4pbw48_0"),
+                                           (8192, 8192, 1024, "w4pbw32_0"), (8192, 8192, 1024, "w4pbq4x4_0"),
+                                           (8192, 2304, 9216, "w4pbt_140000008"), (4096, 4608, 8320, "w4pbt_8"),
+                                           (8192, 8192, 1024, "w4pbt_0"), (8192, 8192, 1024, "w4pbw64_0")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
     tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
@@ -787,17 +799,21 @@ def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     assert torch.equal(_gemm_v(a2, b, variant), _gemm_v(a2, b, "w4h_1_24_20_1_0"))
 
 
-@pytest.mark.parametrize("M,N,K", [(8192, 8192, 384), (8192, 12288, 512), (8192, 8192, 2048)])
+@pytest.mark.parametrize("M,N,K", [(8192, 8192, 384), (8192, 12288, 512), (8192, 8192, 2048), (12288, 8192, 4096),
+                                   (8192, 8192, 8192)])
 def test_gemm_auto_nt_store_route_is_bitwise_the_one_shot_kernel(M, N, K):
     """3-8 tiles per CU, plain C, not tall, K <= 8192: production stores C
-    non-temporally (gemm_persistent.hip); the image is the one-shot kernel's."""
+    non-temporally, half of it deferred into the next tile's first K-steps
+    from K = 512 (gemm_persistent.hip); the image is the one-shot kernel's, and
+    repeated launches keep it (the deferred stores' counted waits)."""
     from kgs.ops import gemm_nt
 
     a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
     b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
     one_shot = _gemm_v(a, b, "w4h_1_24_20_1_0")
-    assert torch.equal(gemm_nt(a, b), one_shot)
-    assert torch.equal(gemm_nt(a, b), _gemm_v(a, b, "w4pn_0"))
+    for _ in range(3):
+        assert torch.equal(gemm_nt(a, b), one_shot)
+    assert torch.equal(gemm_nt(a, b), _gemm_v(a, b, "w4pn_0" if K < 512 else "w4pq4x4n_0"))
 
 
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 8192), (8192, 4096, 14336), (16384, 16384, 8192)])
@@ -1259,7 +1275,54 @@ def test_tile_queue_pool_is_clean_after_the_concurrency_tests():
 
     assert tile_queue_stats()["slots"] > 0
     tq = tile_queue_check()
-    assert tq == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1}, tq
+    assert tq == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1, "error_slots": 0}, tq
+
+
+def test_corrupted_ticket_slot_is_reported_not_faulted_or_silent():
+    """a slot whose tickets hold garbage (as the round-5 memset node
+    left one) must neither become an address nor pass silently. Tickets
+    0x40000000 (no launch could issue them) are written into a stream's slot;
+    the persistent GEMM on that stream ends cleanly, its workgroups stop at
+    their first queued ticket, and the slot's sticky error word reports it
+    (tile_queue_check error_slots). The slot is then repaired and the next
+    launch is exact again."""
+    import ctypes
+
+    from kgs.ops import gemm_nt
+    from kgs.ops import _lib
+    from kgs.utils.graph_audit import hip_runtime
+
+    a = (torch.rand(8192, 1024, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(8192, 1024, device=DEV) * 2 - 1).bfloat16()
+    ref = gemm_nt(a, b, variant="w4_oneshot")
+    s = torch.cuda.Stream()
+    slot = ctypes.c_void_p()
+    _lib.check(_lib.lib().kgs_tile_queue_slot(s.cuda_stream, ctypes.byref(slot)), "kgs_tile_queue_slot")
+    torch.cuda.synchronize()
+    hip = hip_runtime()
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    hip.hipMemcpy.restype = ctypes.c_int
+    words = (ctypes.c_int * 16)(*([0x40000000] * 8 + [0] * 8))
+    assert hip.hipMemcpy(slot, words, 64, 1) == 0  # host to device
+    assert _lib.tile_queue_check()["error_slots"] == 0
+    out = torch.zeros_like(ref)
+    with torch.cuda.stream(s):
+        gemm_nt(a, b, out=out)
+    torch.cuda.synchronize()
+    tq = _lib.tile_queue_check()
+    assert tq["error_slots"] == 1 and tq["dirty_slots"] == 1, tq
+    # each workgroup computed its static first tile and stopped at its first queued ticket
+    same = (out.view(32, 256, 32, 256) == ref.view(32, 256, 32, 256)).all(dim=3).all(dim=1)
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    assert int(same.sum()) == cus, int(same.sum())
+    zero = (ctypes.c_int * 16)()
+    assert hip.hipMemcpy(slot, zero, 64, 1) == 0
+    assert _lib.tile_queue_check() == {"dirty_slots": 0, "dirty_words": 0, "first_value": 0, "first_word": -1,
+                                       "error_slots": 0}
+    with torch.cuda.stream(s):
+        gemm_nt(a, b, out=out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
 
 
 @pytest.mark.parametrize("mode", [1, 2])
