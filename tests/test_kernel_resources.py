@@ -47,13 +47,31 @@ def _resources(src: str, tmp_path) -> dict:
     return _compile(src, tmp_path)[0]
 
 
+# The big translation units compile concurrently (one hipcc each, started together
+# by the first fixture that needs any of them): the module's wall time is the
+# slowest compile, not the sum.
+_BUILDS = {"gemm_bf16.hip": ("kernels", True), "gemm_persistent.hip": ("kernels", True),
+           "attention.hip": ("kernels", False), "gemm_w4h.hip": ("experiments", True)}
+
+
 @pytest.fixture(scope="module")
-def gemm_build(tmp_path_factory):
+def builds(tmp_path_factory):
+    from concurrent.futures import ThreadPoolExecutor
+
+    pool = ThreadPoolExecutor(len(_BUILDS))
+    futs = {src: pool.submit(_compile, src, tmp_path_factory.mktemp(Path(src).stem), temps, sub)
+            for src, (sub, temps) in _BUILDS.items()}
+    yield futs
+    pool.shutdown(wait=True)
+
+
+@pytest.fixture(scope="module")
+def gemm_build(builds):
     """gemm_bf16.hip (one-shot kernels) + gemm_persistent.hip (the persistent
     launcher), resources and assembly merged."""
     res, asm = {}, ""
     for src in ("gemm_bf16.hip", "gemm_persistent.hip"):
-        r, a = _compile(src, tmp_path_factory.mktemp(Path(src).stem), save_temps=True)
+        r, a = builds[src].result()
         res.update(r)
         asm += a
     return res, asm
@@ -102,8 +120,8 @@ def test_four_wave_gemms_touch_agprs_only_through_named_asm(gemm_build):
                 assert any(last_mfma < p < i for p in pads), (name, i, ln)
 
 
-def test_attention_fits_two_workgroups_per_cu(tmp_path):
-    res = _resources("attention.hip", tmp_path)
+def test_attention_fits_two_workgroups_per_cu(builds):
+    res = builds["attention.hip"].result()[0]
     (name, r), = [(n, r) for n, r in res.items() if "attn3fwd" in n]
     assert r.get("VGPRs Spill", 0) == 0
     assert r["VGPRs"] + r.get("AGPRs", 0) <= 256  # 2 waves / SIMD
@@ -147,14 +165,14 @@ def _stray_agpr_lines(body: str) -> tuple[int, list]:
     return seen, stray
 
 
-def test_experiment_persistent_gemms_never_touch_agprs_outside_asm(tmp_path):
+def test_experiment_persistent_gemms_never_touch_agprs_outside_asm(builds):
     """Round 6: a deferred-store build (gemm_w4p.h DD 6, SPS 4: 24 units of C
     held in VGPRs) reached 256 VGPRs and the allocator copied VGPRs into
     accumulator AGPRs (v_accvgpr_write a5, v3 ...): the MFMAs then overwrote
     them and the kernel faulted on the GPU (illegal address). Every persistent
     instance of the experiments library is held to the production rule, so an
     instance at the register limit fails here, on the CPU, not on a GPU box."""
-    _, asm = _compile("gemm_w4h.hip", tmp_path, save_temps=True, subdir="experiments")
+    _, asm = builds["gemm_w4h.hip"].result()
     funcs = _functions(asm, r"gemm_nt_w4pI|gemm_fp8_w4pI")
     assert len(funcs) >= 40, len(funcs)
     for name, body in funcs.items():
