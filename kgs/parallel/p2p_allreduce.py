@@ -63,7 +63,14 @@ class P2PAllReduce:
     """One-kernel all-reduce across the GPUs of a process group (<= 8 ranks)."""
 
     def __init__(self, group=None, max_bytes: int = 8 << 20, device=None, timeout_s: float = 10.0,
-                 oneshot_max_bytes: int | None = None, _local_world: int | None = None):
+                 oneshot_max_bytes: int | None = None, _local_world: int | None = None,
+                 staging_uncached: bool = False):
+        """``staging_uncached``: the staging (data) buffers from uncached device
+        memory, like the signal blocks. Off by default: the flag protocol writes
+        L2 back before a flag and invalidates after a poll (allreduce_p2p.hip
+        block_barrier, pinned by tests/test_kernel_resources.py), so cached
+        staging is correct, and the single-GPU A/B (bench/p2p_staging_ab.py,
+        profiles/r6/p2p/) measures what uncached costs."""
         so = _lib_checked()
         self.max_bytes = int(max_bytes)
         if self.max_bytes <= 0 or self.max_bytes % 16:
@@ -81,7 +88,7 @@ class P2PAllReduce:
             if _local_world is not None:
                 # N ranks in one process: all buffers local, one stream per rank
                 self.world, self.rank = int(_local_world), 0
-                self.data = [_alloc(self.max_bytes, False) for _ in range(self.world)]
+                self.data = [_alloc(self.max_bytes, staging_uncached) for _ in range(self.world)]
                 self.sigs = [_alloc(sig_bytes, True) for _ in range(self.world)]
                 self._owned += self.data + self.sigs
                 self.local = True
@@ -90,7 +97,7 @@ class P2PAllReduce:
 
                 self.world = dist.get_world_size(group)
                 self.rank = dist.get_rank(group)
-                my_data = _alloc(self.max_bytes, False)
+                my_data = _alloc(self.max_bytes, staging_uncached)
                 my_sig = _alloc(sig_bytes, True)
                 self._owned += [my_data, my_sig]
                 hbytes = so.kgs_ar_ipc_handle_bytes()

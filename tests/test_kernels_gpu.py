@@ -248,8 +248,9 @@ def test_gemm_auto_routes_aligned_to_four_wave_kernel():
     experiments library) compute the identical image."""
     from kgs.ops import experiments, gemm_nt
 
-    a = (torch.rand(2048, 1024, device=DEV) * 2 - 1).bfloat16()
-    b = (torch.rand(1536, 1024, device=DEV) * 2 - 1).bfloat16()
+    # K = 1280: 20 K-steps, enough for every variant's peeled ones (w4pq16x1n: 18 + 2)
+    a = (torch.rand(2048, 1280, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(1536, 1280, device=DEV) * 2 - 1).bfloat16()
     c = gemm_nt(a, b, variant="w4")
     assert _rel_err(c, _ref_nt(a, b)) < 1e-2
     assert torch.equal(gemm_nt(a, b), c)
