@@ -49,8 +49,12 @@ def main(argv=None) -> int:
                 for mode, ar in ars.items():  # numerics first
                     outs = ar.all_reduce_local(ins, algo=algo)
                     torch.cuda.synchronize()
-                    ar.check()
-                    assert all(bool(torch.all(o == want)) for o in outs), (world, kib, algo, mode)
+                    err = int(ar.err.item())
+                    wrong = [int((o != want).sum()) for o in outs]
+                    if err or any(wrong):
+                        raise SystemExit(json.dumps({"failure": {"world": world, "kib": kib, "algo": algo,
+                                                                 "mode": mode, "err": err, "wrong": wrong,
+                                                                 "at": "first call of the cell"}}))
                 for _ in range(a.rounds):
                     for mode, ar in ars.items():
                         outs = [torch.empty_like(x) for x in ins]
@@ -63,6 +67,14 @@ def main(argv=None) -> int:
                         e.record()
                         e.synchronize()
                         times[mode].append(s.elapsed_time(e) / a.iters * 1e3)
+                        # every timed block ends checked: the last call's outputs and the barrier error word
+                        # (a timed-out barrier in any call of the block sets it and stays set)
+                        err = int(ar.err.item())
+                        wrong = [int((o != want).sum()) for o in outs]
+                        if err or any(wrong):
+                            raise SystemExit(json.dumps({"failure": {"world": world, "kib": kib, "algo": algo,
+                                                                     "mode": mode, "err": err, "wrong": wrong,
+                                                                     "block_ms": times[mode][-1] / 1e3 * a.iters}}))
                 row = {"world": world, "kib": kib, "algo": algo,
                        **{f"{m}_us": round(statistics.median(v), 2) for m, v in times.items()}}
                 row["uncached_over_cached"] = round(row["uncached_us"] / row["cached_us"], 3)

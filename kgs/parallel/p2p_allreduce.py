@@ -64,13 +64,16 @@ class P2PAllReduce:
 
     def __init__(self, group=None, max_bytes: int = 8 << 20, device=None, timeout_s: float = 10.0,
                  oneshot_max_bytes: int | None = None, _local_world: int | None = None,
-                 staging_uncached: bool = False):
+                 staging_uncached: bool = True):
         """``staging_uncached``: the staging (data) buffers from uncached device
-        memory, like the signal blocks. Off by default: the flag protocol writes
-        L2 back before a flag and invalidates after a poll (allreduce_p2p.hip
-        block_barrier, pinned by tests/test_kernel_resources.py), so cached
-        staging is correct, and the single-GPU A/B (bench/p2p_staging_ab.py,
-        profiles/r6/p2p/) measures what uncached costs."""
+        memory, like the signal blocks (round 6 default). The flag protocol also
+        writes L2 back before a flag and invalidates after a poll
+        (allreduce_p2p.hip block_barrier, pinned by tests/test_kernel_resources.py),
+        but with uncached staging no peer's data ever waits in an L2. The
+        single-GPU A/B (bench/p2p_staging_ab.py, profiles/r6/p2p/README.md): equal
+        or faster in 16 of 18 cells, 0.79-0.90x the time at 4 MiB, at most
+        1.04x; and the one wrong result ever seen in local-rank runs came from a
+        cached-staging instance."""
         so = _lib_checked()
         self.max_bytes = int(max_bytes)
         if self.max_bytes <= 0 or self.max_bytes % 16:
