@@ -124,6 +124,8 @@ def lib() -> ctypes.CDLL:
     so.kgs_exp_attn4_fwd_bf16.restype = i
     so.kgs_exp_gemm_w4p_stamps.argtypes = [vp] * 3 + [i] * 7 + [vp] * 3
     so.kgs_exp_gemm_w4p_stamps.restype = i
+    so.kgs_exp_gemm_w4p_waits.argtypes = [vp] * 3 + [i] * 7 + [vp] * 3
+    so.kgs_exp_gemm_w4p_waits.restype = i
     so.kgs_exp_gemm_fp8_w4f8.argtypes = [vp] * 3 + [i] * 6 + [ctypes.c_float, i, vp]
     so.kgs_exp_gemm_fp8_w4f8.restype = i
     return so
@@ -256,3 +258,25 @@ def attention_qkv_w4(qkv: torch.Tensor, batch: int, seq: int, heads: int, kv_hea
                                       _lib.stream_handle(qkv.device))
     _lib.check(rc, "attention_qkv_w4")
     return out
+
+
+def gemm_w4p_waits(a, b, out, stamps: torch.Tensor, variant: int = 0) -> int:
+    """The persistent GEMM's wait-stamp build (gemm_w4p.h WSB): computes ``a @ b.T`` into ``out`` and
+    fills ``stamps`` (int64 ``[>= grid, 4, 16]``, per wave: s_memtime cycles of [category][lgkm wait,
+    barrier 1, vm wait, barrier 2] for category 0 = a tile's K-steps 0-1, 1 = the steady loop, 2 = the
+    last two, then start, end, tiles). Variant: 0 production nt + deferred 4 x 4, 1 nt only, 2 tall
+    long-K map, 3 map 0 temporal C. Returns the grid."""
+    import ctypes
+
+    M, K = a.shape
+    N = b.shape[0]
+    if stamps.dtype != torch.int64 or not stamps.is_contiguous() or stamps.dim() != 3 or tuple(stamps.shape[1:]) != (4, 16):
+        raise ValueError("stamps: contiguous int64 [grid, 4, 16]")
+    cus = torch.cuda.get_device_properties(a.device).multi_processor_count
+    if stamps.shape[0] < min((M // 256) * (N // 256), cus):
+        raise ValueError("stamps: fewer rows than the persistent grid")
+    g = ctypes.c_int(0)
+    _lib.check(lib().kgs_exp_gemm_w4p_waits(a.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, a.stride(0),
+                                            b.stride(0), out.stride(0), int(variant), stamps.data_ptr(),
+                                            ctypes.byref(g), _lib.stream_handle(a.device)), "kgs_exp_gemm_w4p_waits")
+    return g.value

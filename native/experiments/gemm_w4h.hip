@@ -240,6 +240,49 @@ KGS_EXPORT int kgs_exp_gemm_w4p_grid(const void* A, const void* B, void* C, int 
 
 // The persistent kernel's timing build (gemm_w4p.h TS) with tile map `map`
 // (table below; 0 and 1 are production's for square / tall long-K problems). `stamps`: long long[grid][16], grid = min(tiles, CUs) (returned in *grid_out).
+// Wait stamps of the persistent kernel (gemm_w4p.h WSB, round 6): s_memtime cycles every wave spent in
+// its lgkm wait, barrier 1, vm wait and barrier 2, per K-step category. stamps: long long[grid][4][16].
+// variant 0: production at 3-8 tiles per CU (nt C, deferred 4 x 4); 1: nt C, nothing deferred;
+// 2: the tall long-K map (mirrored G8, temporal C); 3: map 0, temporal C (16 tiles per CU).
+KGS_EXPORT int kgs_exp_gemm_w4p_waits(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
+                                      int ldc, int variant, void* stamps, int* grid_out, hipStream_t s) {
+  if (M <= 0 || N <= 0 || K < 768 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;
+  if (M % 256 || N % 256 || K % 128 || lda % 8 || ldb % 8 || ldc % 8) return KGS_ERR_ALIGN;
+  if ((uintptr_t)A % 16 || (uintptr_t)B % 16 || (uintptr_t)C % 16 || !stamps) return KGS_ERR_ALIGN;
+  if ((long)lda * 256 * 2 >= (1L << 31) || (long)ldb * 256 * 2 >= (1L << 31)) return KGS_ERR_SHAPE;
+  const int ntiles = (M / 256) * (N / 256);
+  const int grid = ntiles < cu_count() ? ntiles : cu_count();
+  if (grid_out) *grid_out = grid;
+  int* tq = kgs::tile_queue(s);
+  if (!tq) return KGS_ERR_ARG;
+  auto a = (const unsigned short*)A;
+  auto b = (const unsigned short*)B;
+  auto c = (unsigned short*)C;
+  auto ts = (const unsigned short*)stamps;
+  using namespace kgs::w4p;
+  switch (variant) {
+    case 0:
+      hipLaunchKernelGGL((gemm_nt_w4p<kgs::EPI_NONE, 0, 1, true, false, 1000000, 4, 4>), dim3(grid), dim3(256), 0, s,
+                         a, b, c, ts, M, N, K, lda, ldb, ldc, tq);
+      break;
+    case 1:
+      hipLaunchKernelGGL((gemm_nt_w4p<kgs::EPI_NONE, 0, 1, true, false, 1000000>), dim3(grid), dim3(256), 0, s, a, b,
+                         c, ts, M, N, K, lda, ldb, ldc, tq);
+      break;
+    case 2:
+      hipLaunchKernelGGL((gemm_nt_w4p<kgs::EPI_NONE, 140000008, 1, false, false, 1000000>), dim3(grid), dim3(256), 0,
+                         s, a, b, c, ts, M, N, K, lda, ldb, ldc, tq);
+      break;
+    case 3:
+      hipLaunchKernelGGL((gemm_nt_w4p<kgs::EPI_NONE, 0, 1, false, false, 1000000>), dim3(grid), dim3(256), 0, s, a,
+                         b, c, ts, M, N, K, lda, ldb, ldc, tq);
+      break;
+    default:
+      return KGS_ERR_ARG;
+  }
+  return (int)hipGetLastError();
+}
+
 KGS_EXPORT int kgs_exp_gemm_w4p_stamps(const void* A, const void* B, void* C, int M, int N, int K, int lda, int ldb,
                                        int ldc, int map, void* stamps, int* grid_out, hipStream_t s) {
   if (M <= 0 || N <= 0 || K < 384 || lda < K || ldb < K || ldc < N) return KGS_ERR_SHAPE;

@@ -159,14 +159,25 @@ struct Tick {
   int* slot;  // LDS
   int tk;
 };
+// The wait-stamp build's ticket ((L / 10^6) % 10 == 1, experiments): plus the s_memtime cycles this
+// wave spent in [category][lgkm wait, barrier 1, vm wait, barrier 2]; category 0 = a tile's K-steps
+// 0-1, 1 = the steady loop, 2 = the last two (the next tile's DMAs).
+struct TickW : Tick {
+  unsigned long long ws[12];
+};
+template <bool W>
+__device__ __forceinline__ auto make_tick(int* qx, int* slot) {
+  if constexpr (W) return TickW{{qx, slot, 0}, {}};
+  else return Tick{qx, slot, 0};
+}
 
 // gemm_w4.h's kbody with named accumulators: MFMA K of the K-step plus what
 // follows it. The DMA issues use `cd` (this tile's or the next tile's buffer
 // resources) and K-tile sp.k0 / BK; everything LDS-side uses `c`. TK: 1 =
 // issue the ticket atomic after barrier 2, 2 = publish the ticket there.
-template <int ST, int X, bool ZERO, int TK, int K, int L = 0, int WX = 0>
+template <int ST, int X, bool ZERO, int TK, int K, int L = 0, int WX = 0, int CAT = 1, class TQ = Tick>
 __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
-                                      Frag<MA, NB>& f1, Tick& tq) {
+                                      Frag<MA, NB>& f1, TQ& tq) {
   constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = ord_of(L);
   constexpr int KM = S::KM, HM = S::HM, NR = S::NR, ND = w4::dma_per_stage<BM, BN>();
   if constexpr (K < KM) {
@@ -200,10 +211,22 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
     // for its reads of stage ST, then a barrier: stage ST is free for this step's DMAs AND K-tile t + 1
     // is visible for the f0 reads of the last R MFMAs, so the barrier at KM - R - 1 goes.
     constexpr bool OB = (L / 1000) % 10 == 1;
+    // WSB ((L / 10^6) % 10 == 1, experiments): s_memtime around each wait and barrier (Tick::ws). A
+    // stamp's result is used right after the barrier it follows, before any LDS read is issued, so
+    // the lgkmcnt wait it needs costs only its own latency.
+    constexpr bool WSB = (L / 1000000) % 10 == 1;
     if constexpr (K == B1 - 1) {
+      unsigned long long t0 = 0, t1 = 0;
+      if constexpr (WSB) t0 = __builtin_amdgcn_s_memtime();
       if constexpr (OB) w4::wait_vm<WX>();
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's reads of stage ST retired
+      if constexpr (WSB) t1 = __builtin_amdgcn_s_memtime();
       w4::bar();
+      if constexpr (WSB) {
+        const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+        tq.ws[CAT * 4 + 0] += t1 - t0;
+        tq.ws[CAT * 4 + 1] += t2 - t1;
+      }
       if constexpr (OB && TK == 1) {
         if (threadIdx.x == 0) tq.tk = atomicAdd(tq.qx, 1);
       } else if constexpr (OB && TK == 2) {
@@ -211,29 +234,37 @@ __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtr
       }
     }
     if constexpr (K == KM - R - 1 && !OB) {
+      unsigned long long t3 = 0, t4 = 0;
+      if constexpr (WSB) t3 = __builtin_amdgcn_s_memtime();
       w4::wait_vm<ND + WX>();  // own DMA of the next K-tile landed (WX: younger stores, see the kernel)
+      if constexpr (WSB) t4 = __builtin_amdgcn_s_memtime();
       w4::bar();
+      if constexpr (WSB) {
+        const unsigned long long t5 = __builtin_amdgcn_s_memtime();
+        tq.ws[CAT * 4 + 2] += t4 - t3;
+        tq.ws[CAT * 4 + 3] += t5 - t4;
+      }
       if constexpr (TK == 1) {
         if (threadIdx.x == 0) tq.tk = atomicAdd(tq.qx, 1);
       } else if constexpr (TK == 2) {
         if (threadIdx.x == 0) *tq.slot = tq.tk;
       }
     }
-    pbody<ST, X, ZERO, TK, K + 1, L, WX>(c, cd, sp, f0, f1, tq);
+    pbody<ST, X, ZERO, TK, K + 1, L, WX, CAT, TQ>(c, cd, sp, f0, f1, tq);
   }
 }
 
 // One K-step on stage ST; its DMAs bring K-tile kd (of cd's tile) into ST.
-template <int ST, int X, bool ZERO, int TK = 0, int L = 0, int WX = 0>
+template <int ST, int X, bool ZERO, int TK = 0, int L = 0, int WX = 0, int CAT = 1, class TQ = Tick>
 __device__ __forceinline__ void pstep(const Ctx& c, const Ctx& cd, Frag<MA, NB>& f0, Frag<MA, NB>& f1, int kd,
-                                      Tick& tq) {
+                                      TQ& tq) {
   StepPtrs sp;
   sp.pa1 = pabase<L>(c, ST, 1);
   sp.pb1 = pbbase<L>(c, ST, 1);
   sp.pa0 = pabase<L>(c, ST ^ 1, 0);
   sp.pb0 = pbbase<L>(c, ST ^ 1, 0);
   sp.k0 = kd * BK;
-  pbody<ST, X, ZERO, TK, 0, L, WX>(c, cd, sp, f0, f1, tq);
+  pbody<ST, X, ZERO, TK, 0, L, WX, CAT, TQ>(c, cd, sp, f0, f1, tq);
 }
 
 // Epilogue of one tile, pairs of accumulators (q, q + 1) = (i, n), (i, n + 1):
@@ -501,6 +532,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   static_assert(DD == 0 || (EPI != EPI_ADDC && !SW && CST == 0 && L % 10 == 0), "deferred stores: plain tiles");
   static_assert(DEF >= 0 && UI >= 0 && (DD == 0 || SPS > 0), "deferred stores: at most a tile's units");
   static_assert((L / 1000) % 10 == 0 || (CST == 0 && !TS), "one-barrier K-step: no store measurement builds");
+  constexpr bool WSK = (L / 1000000) % 10 == 1;  // wait-stamp build (pbody WSB)
+  static_assert(!WSK || (EPI == EPI_NONE && !TS && !SW), "wait stamps: bias carries the stamp buffer");
+  const unsigned long long wst0 = WSK ? __builtin_amdgcn_s_memtime() : 0ull;
+  int wtiles = 0;
   long long* const ts = TS ? (long long*)bias + (long)blockIdx.x * 16 : nullptr;
   int ntile_done = 0;
   if constexpr (TS) {
@@ -594,7 +629,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // K-step 0, waits only for the atomic.
   int vzero;
   asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
-  Tick tq{q + x + vzero, &tslot, 0};
+  auto tq = make_tick<WSK>(q + x + vzero, &tslot);
   // deferred stores: the previous tile's C block (first tile: zero-size, stores dropped)
   uint4 dq[DEF > 0 ? DEF : 1];
   __amdgpu_buffer_rsrc_t rprev = __builtin_amdgcn_make_buffer_rsrc((void*)C, 0, 0, 0x00020000);
@@ -611,12 +646,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         constexpr int J = decltype(jc)::value;
         constexpr int TKJ = DYN ? (J == 0 ? 1 : J == 1 ? 2 : 0) : 0;
         constexpr int WXJ = (J >= 1 && J <= DD) ? SPS : 0;
-        pstep<J & 1, X, J == 0, TKJ, L, WXJ>(c, c, f0, f1, J + 2, tq);
+        pstep<J & 1, X, J == 0, TKJ, L, WXJ, J < 2 ? 0 : 1>(c, c, f0, f1, J + 2, tq);
         if constexpr (J < DD) dstore<UI, J * SPS, SPS, DEF, NTST>(dq, rprev, voffc, ldc);
       });
     } else {
-      pstep<0, X, true, DYN ? 1 : 0, L, WXS>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
-      pstep<1, X, false, DYN ? 2 : 0, L>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
+      pstep<0, X, true, DYN ? 1 : 0, L, WXS, 0>(c, c, f0, f1, 2, tq);   // ticket atomic after its barrier 2
+      pstep<1, X, false, DYN ? 2 : 0, L, 0, 0>(c, c, f0, f1, 3, tq);  // ticket to LDS after its barrier 2
     }
     for (int t = PEEL; t < nt - 2; t += 2) {
       pstep<0, X, false, 0, L>(c, c, f0, f1, t + 2, tq);
@@ -633,8 +668,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     set_b<SW>(cn, B, tnn, ldb, N);
     // the last two K-steps bring the next tile's K-tiles 0 and 1 (no next tile:
     // harmless re-loads of this tile's last K-tile into the freed stages)
-    pstep<0, X, false, 0, L>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
-    pstep<1, X, false, 0, L>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
+    pstep<0, X, false, 0, L, 0, 2>(c, cn, f0, f1, more ? 0 : nt - 1, tq);
+    pstep<1, X, false, 0, L, 0, 2>(c, cn, f0, f1, more ? 1 : nt - 1, tq);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // MFMA -> v_accvgpr_read
     if constexpr (SW) pepi_sw<0, 0>(c, C, ldc, tm, tn);
     float bv[NB][4];
@@ -675,6 +710,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         ts[15] = ntile_done;
       }
     }
+    if constexpr (WSK) ++wtiles;
     if (!more) break;
     t = tnx;
     tm = tmn;
@@ -693,6 +729,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     __syncthreads();
     const long long tx = (long long)__builtin_amdgcn_s_memrealtime();
     if (threadIdx.x == 0) ts[13] = tx;
+  }
+  if constexpr (WSK) {
+    // per wave: long long[grid][4][16] = ws[0..11], start, end (s_memtime), tiles
+    const unsigned long long wst1 = __builtin_amdgcn_s_memtime();
+    long long* const wb = (long long*)bias + ((long)blockIdx.x * 4 + w) * 16;
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < 12; ++j) wb[j] = (long long)tq.ws[j];
+      wb[12] = (long long)wst0;
+      wb[13] = (long long)wst1;
+      wb[14] = wtiles;
+    }
   }
 }
 

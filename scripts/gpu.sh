@@ -38,6 +38,7 @@
 #   lib_ab       this tree's kernel library vs another build ($LIB_B), interleaved, five sweep shapes
 #   fp8_sweep    kgs fp8 vs hipBLASLt fp8, N(0,1) operands ($SHAPES, $VARIANTS: e.g. w4f8_<X>_<B1>_<R>_<P> knobs)
 #   overlap_variants  bench/overlap.py for the persistent and one-shot grids, stand-in LDS 0 / 64 KiB
+#   gemm_waits   the persistent GEMM's wait-stamp build: lgkm / barrier / vm wait cycles per K-step category
 #   p2p_staging  P2P all-reduce with cached vs uncached staging buffers, local ranks on one GPU
 #   wait_split   SQ_WAIT_ANY vs K at 8192 x 8192 x K (persistent nt / deferred / one-shot / hipBLASLt): per-K-step
 #                and fixed (tile change + launch) parts (bench/wait_split.py)
@@ -242,6 +243,8 @@ step() {
             run g2_tcp 120 timeout -s KILL 100 rocprofv3 --pmc TA_BUSY_avr TCP_TCC_READ_REQ_sum \
                 TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE \
                 --output-format csv -d "$O/g2_tcp_${MNK:-8192}" -o g -- $G ;;
+        gemm_waits) run gemm_waits 300 python bench/gemm_waits.py --shapes ${SHAPES:-8192,8192x4096x14336,16384x16384x8192} \
+            --out "$O/gemm_waits.json" ;;
         p2p_staging) run p2p_staging 300 python bench/p2p_staging_ab.py --out "$O/p2p_staging_ab.json" ;;
         wait_split)  # SQ waits of the persistent GEMM vs K at a fixed tile grid: steady K-loop vs tile change
             local W="python3 bench/wait_split.py --plan $O/ws_plan.json"

@@ -888,6 +888,32 @@ def test_gemm_persistent_deferred_stores_repeat_bitwise_and_refuse_short_k():
         ex.gemm_nt(short, short, "w4pq8x2n_0")
 
 
+@pytest.mark.parametrize("M,N,K,variant", [(8192, 8192, 1024, 0), (8192, 8192, 1024, 1), (8192, 2304, 9216, 2),
+                                           (4096, 4608, 768, 3)])
+def test_gemm_persistent_wait_stamp_build(M, N, K, variant):
+    """bench/gemm_waits.py's source (gemm_w4p.h WSB): the wait-stamp build computes
+    the production image, and every wave reports each category's waits, a start
+    before its end and its tiles (which add up to the tile grid, 4 waves each)."""
+    from kgs.ops import experiments as ex
+    from kgs.ops import gemm_nt
+
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    ref = gemm_nt(a, b, variant="w4_oneshot")
+    out = torch.empty_like(ref)
+    cus = torch.cuda.get_device_properties(DEV).multi_processor_count
+    st = torch.zeros((cus, 4, 16), dtype=torch.int64, device=DEV)
+    grid = ex.gemm_w4p_waits(a, b, out, st, variant)
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    s = st[:grid].cpu()
+    assert int(s[:, :, 14].sum()) == 4 * (M // 256) * (N // 256)
+    assert bool((s[:, :, 13] > s[:, :, 12]).all()) and bool((s[:, :, :12] >= 0).all())
+    assert bool((s[:, :, 4:8].sum(-1) > 0).all())  # the steady loop's waits were stamped on every wave
+    total = (s[:, :, 13] - s[:, :, 12]).sum()
+    assert int(s[:, :, :12].sum()) < int(total)
+
+
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 512), (8192, 2304, 9216), (1024, 768, 1024)])
 def test_gemm_persistent_timing_build_stamps(M, N, K):
     """bench/gemm_tail.py's source: the timing build (gemm_w4p.h TS) computes
