@@ -817,6 +817,24 @@ def test_gemm_auto_nt_store_route_is_bitwise_the_one_shot_kernel(M, N, K):
     assert torch.equal(gemm_nt(a, b), _gemm_v(a, b, "w4pn_0" if K < 512 else "w4pq4x4n_0"))
 
 
+def test_deferred_store_route_with_a_strided_output():
+    """The deferred C units are stored through a buffer resource on the previous
+    tile's rows at stride ldc: with C a column slice of a wider matrix (ldc > N)
+    the image is the one-shot kernel's, and the columns outside the slice are
+    untouched (the resource's range covers only the tile's rows)."""
+    from kgs.ops import gemm_nt
+
+    M, N, K = 8192, 8192, 1024
+    a = (torch.rand(M, K, device=DEV) * 2 - 1).bfloat16()
+    b = (torch.rand(N, K, device=DEV) * 2 - 1).bfloat16()
+    wide = torch.full((M, N + 512), 7.0, device=DEV, dtype=torch.bfloat16)
+    out = wide[:, 256:256 + N]
+    assert out.stride(0) == N + 512
+    gemm_nt(a, b, out=out)
+    assert torch.equal(out, gemm_nt(a, b, variant="w4_oneshot"))
+    assert bool((wide[:, :256] == 7.0).all()) and bool((wide[:, 256 + N:] == 7.0).all())
+
+
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 8192), (8192, 4096, 14336), (16384, 16384, 8192)])
 def test_production_route_at_the_bench_shapes_in_full(M, N, K):
     """gemm_nt's default route at the headline shapes (8192^3:
