@@ -171,6 +171,14 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
       KGS_W4PB(172, 8, false, 1000, 0, 2)
       KGS_W4PB(173, 0, false, 1000, 0, 2)
       KGS_W4PB(174, 0, true, 641000, 0, 2)
+      // round 6: K-step schedule (gemm_w4p.h (L / 10^7) % 10: barrier 1 after MFMA B1, R MFMAs after
+      // barrier 2) on the production 3-8-tiles-per-CU route (nt C, deferred 4 x 4) and on the tall G8 map
+      KGS_W4PB(175, 0, true, 10000000, 4, 4)
+      KGS_W4PB(176, 0, true, 20000000, 4, 4)
+      KGS_W4PB(177, 0, true, 30000000, 4, 4)
+      KGS_W4PB(178, 0, true, 40000000, 4, 4)
+      KGS_W4PB(179, 140000008, false, 20000000, 0, 2)
+      KGS_W4PB(180, 140000008, false, 30000000, 0, 2)
 #undef KGS_W4PB
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)

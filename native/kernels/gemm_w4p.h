@@ -109,6 +109,13 @@ struct Lay<1> {
 // L / 10 (experiments): the MFMA order inside a k-sub, L / 10 - 1 (gemm_w4.h
 // make_order: 0 i-major, 1 growing square, 2 n-major); 0 = Knobs (growing square).
 constexpr int ord_of(int L) { return (L / 10) % 10 ? (L / 10) % 10 - 1 : Kn::ORD; }
+// (L / 10^7) % 10 (experiments): the K-step schedule, barrier 1 after MFMA B1 and R MFMAs after
+// barrier 2 (the DMA window is [B1, KM - R)); 0 = Knobs (B1 24, R 20). 1: 20 / 20, 2: 24 / 16,
+// 3: 20 / 16, 4: 18 / 16 (a wider DMA window; the f1 reads end at MFMA NR = 16).
+constexpr int b1_of(int L) {
+  return (L / 10000000) % 10 == 1 || (L / 10000000) % 10 == 3 ? 20 : (L / 10000000) % 10 == 4 ? 18 : Kn::B1;
+}
+constexpr int r_of(int L) { return (L / 10000000) % 10 >= 2 ? 16 : Kn::R; }
 
 template <int L>
 __device__ __forceinline__ const char* pabase(const Ctx& c, int st, int sub) {
@@ -178,8 +185,9 @@ __device__ __forceinline__ auto make_tick(int* qx, int* slot) {
 template <int ST, int X, bool ZERO, int TK, int K, int L = 0, int WX = 0, int CAT = 1, class TQ = Tick>
 __device__ __forceinline__ void pbody(const Ctx& c, const Ctx& cd, const StepPtrs& sp, Frag<MA, NB>& f0,
                                       Frag<MA, NB>& f1, TQ& tq) {
-  constexpr int B1 = Kn::B1, R = Kn::R, P = Kn::P, ORD = ord_of(L);
+  constexpr int B1 = b1_of(L), R = r_of(L), P = Kn::P, ORD = ord_of(L);
   constexpr int KM = S::KM, HM = S::HM, NR = S::NR, ND = w4::dma_per_stage<BM, BN>();
+  static_assert(B1 >= NR && B1 + ND <= KM - R && NR <= R * P, "bad K-step schedule");
   if constexpr (K < KM) {
     constexpr int mi = w4::Order<ORD, MA, NB>::o.i[K % HM], mn = w4::Order<ORD, MA, NB>::o.n[K % HM];
     if constexpr (K < HM) pmma<ZERO, mi, mn>(f0); else pmma<false, mi, mn>(f1);
