@@ -100,7 +100,8 @@ W4H.update({"w4pb_0": 167, "w4pbw48_0": 168, "w4pbw32_0": 169, "w4pbq4x4_0": 170
             "w4pbt_8": 172, "w4pbt_0": 173, "w4pbw64_0": 174})
 # round 6: K-step schedule (gemm_w4p.h (L / 10^7) % 10): w4pk<B1>r<R>[q4x4n]_<X> -> 175..
 W4H.update({"w4pk20r20q4x4n_0": 175, "w4pk24r16q4x4n_0": 176, "w4pk20r16q4x4n_0": 177, "w4pk18r16q4x4n_0": 178,
-            "w4pk24r16_140000008": 179, "w4pk20r16_140000008": 180})
+            "w4pk24r16_140000008": 179, "w4pk20r16_140000008": 180, "w4pk20r24q4x4n_0": 181,
+            "w4pk18r24q4x4n_0": 182, "w4pk24r24q4x4n_0": 183, "w4pk20r24_140000008": 184})
 NO_OUTPUT = frozenset({"w4px_0"})  # timing only: C is not written
 
 

@@ -179,6 +179,10 @@ KGS_EXPORT int kgs_exp_gemm_w4h(const void* A, const void* B, void* C, int M, in
       KGS_W4PB(178, 0, true, 40000000, 4, 4)
       KGS_W4PB(179, 140000008, false, 20000000, 0, 2)
       KGS_W4PB(180, 140000008, false, 30000000, 0, 2)
+      KGS_W4PB(181, 0, true, 50000000, 4, 4)
+      KGS_W4PB(182, 0, true, 60000000, 4, 4)
+      KGS_W4PB(183, 0, true, 70000000, 4, 4)
+      KGS_W4PB(184, 140000008, false, 50000000, 0, 2)
 #undef KGS_W4PB
       // the static walk (v, v + G, ...: no ticket atomics), default / mirror / G8 / mirror G8
       KGS_W4P(121, 0, false)

@@ -111,11 +111,16 @@ struct Lay<1> {
 constexpr int ord_of(int L) { return (L / 10) % 10 ? (L / 10) % 10 - 1 : Kn::ORD; }
 // (L / 10^7) % 10 (experiments): the K-step schedule, barrier 1 after MFMA B1 and R MFMAs after
 // barrier 2 (the DMA window is [B1, KM - R)); 0 = Knobs (B1 24, R 20). 1: 20 / 20, 2: 24 / 16,
-// 3: 20 / 16, 4: 18 / 16 (a wider DMA window; the f1 reads end at MFMA NR = 16).
+// 3: 20 / 16, 4: 18 / 16 (a wider DMA window; the f1 reads end at MFMA NR = 16); 5: 20 / 24,
+// 6: 18 / 24, 7: 24 / 24 (a longer read tail for the next K-step's first fragments).
 constexpr int b1_of(int L) {
-  return (L / 10000000) % 10 == 1 || (L / 10000000) % 10 == 3 ? 20 : (L / 10000000) % 10 == 4 ? 18 : Kn::B1;
+  constexpr int b1[8] = {Kn::B1, 20, 24, 20, 18, 20, 18, 24};
+  return b1[(L / 10000000) % 10 & 7];
 }
-constexpr int r_of(int L) { return (L / 10000000) % 10 >= 2 ? 16 : Kn::R; }
+constexpr int r_of(int L) {
+  constexpr int r[8] = {Kn::R, 20, 16, 16, 16, 24, 24, 24};
+  return r[(L / 10000000) % 10 & 7];
+}
 
 template <int L>
 __device__ __forceinline__ const char* pabase(const Ctx& c, int st, int sub) {

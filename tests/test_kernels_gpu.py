@@ -789,7 +789,11 @@ def test_gemm_small_grid_routing_is_bitwise_the_256_tile(M, N, K):
                                            (8192, 8192, 1024, "w4pk18r16q4x4n_0"),
                                            (4608, 4096, 768, "w4pk18r16q4x4n_0"),
                                            (8192, 2304, 9216, "w4pk24r16_140000008"),
-                                           (8192, 2304, 9216, "w4pk20r16_140000008")])
+                                           (8192, 2304, 9216, "w4pk20r16_140000008"),
+                                           (8192, 8192, 1024, "w4pk20r24q4x4n_0"),
+                                           (8192, 8192, 1024, "w4pk18r24q4x4n_0"),
+                                           (8192, 8192, 1024, "w4pk24r24q4x4n_0"),
+                                           (8192, 2304, 9216, "w4pk20r24_140000008")])
 def test_gemm_persistent_is_bitwise_the_one_shot_kernel(M, N, K, variant):
     """The persistent four-wave kernel (gemm_w4p.h: one workgroup per CU walking
     tiles, named accumulator AGPRs, the next tile's K-tiles loaded by the last
